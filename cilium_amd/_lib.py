@@ -1,0 +1,77 @@
+"""ctypes binding of include/l7gpu.h (the product's C-ABI).
+
+The shared library is built in-tree by cilium_amd/build.py.  There is no
+fallback: if libl7gpu.so is missing or fails to load, importing the engine
+raises, so nothing can silently classify on the CPU.
+"""
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libl7gpu.so")
+
+DENY, ALLOW, PARSE_ERROR, INCOMPLETE, UNSUPPORTED = 0, 1, 2, 3, 4
+PROTO_HTTP, PROTO_KAFKA, PROTO_MEMCACHE = 1, 2, 3
+VERDICT_NAMES = {DENY: "DENY", ALLOW: "ALLOW", PARSE_ERROR: "PARSE_ERROR",
+                 INCOMPLETE: "INCOMPLETE", UNSUPPORTED: "UNSUPPORTED"}
+
+
+class Conn(C.Structure):
+    """l7g_conn_t (20 bytes; same layout as the oracle's ref_conn_t)."""
+    _fields_ = [("policy", C.c_int32), ("port", C.c_uint32), ("ingress", C.c_uint8),
+                ("proto", C.c_uint8), ("_pad", C.c_uint16), ("src_id", C.c_uint32),
+                ("dst_id", C.c_uint32)]
+
+
+class Stats(C.Structure):
+    _fields_ = [(n, C.c_uint32) for n in (
+        "policies", "rules", "http_rulesets", "http_chunks", "http_dfas", "http_dfa_states",
+        "kafka_rulesets", "kafka_rules", "kafka_topics")] + [("table_bytes", C.c_uint64)]
+
+
+EXPORTS = (
+    "l7g_engine_create", "l7g_engine_destroy", "l7g_policy_update", "l7g_policy_index",
+    "l7g_policy_nrules", "l7g_conns_set", "l7g_classify", "l7g_classify_host", "l7g_stats",
+    "l7g_debug_regex",
+)
+
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} is missing: run python -m cilium_amd.build (no CPU fallback exists)")
+    lib = C.CDLL(LIB_PATH)
+    vp, sz, cp = C.c_void_p, C.c_size_t, C.c_char_p
+    lib.l7g_engine_create.restype = vp
+    lib.l7g_engine_create.argtypes = [C.c_int, cp, sz]
+    lib.l7g_engine_destroy.argtypes = [vp]
+    lib.l7g_policy_update.argtypes = [vp, cp, sz, cp, sz]
+    lib.l7g_policy_index.restype = C.c_int32
+    lib.l7g_policy_index.argtypes = [vp, cp, sz]
+    lib.l7g_policy_nrules.restype = C.c_int32
+    lib.l7g_policy_nrules.argtypes = [vp]
+    lib.l7g_conns_set.argtypes = [vp, vp, C.c_uint32, cp, sz]
+    lib.l7g_classify.argtypes = [vp, vp, vp, vp, vp, C.c_uint32, vp, vp, vp, vp, vp]
+    lib.l7g_classify_host.argtypes = [vp, vp, C.c_uint64, vp, vp, vp, C.c_uint32, vp, vp, vp]
+    lib.l7g_stats.argtypes = [vp, C.POINTER(Stats)]
+    lib.l7g_debug_regex.argtypes = [cp, sz, C.c_int, cp, sz, cp, sz]
+    _lib = lib
+    return lib
+
+
+def debug_regex(pattern, data, anchored=True):
+    """Compile `pattern` with the product's Go-regexp DFA compiler and run the
+    compiled tables on `data` (host walk of the device tables; test hook).
+    Returns True/False, or raises ValueError with Go's compile error text."""
+    lib = load()
+    p = pattern.encode() if isinstance(pattern, str) else pattern
+    d = data.encode() if isinstance(data, str) else data
+    err = C.create_string_buffer(512)
+    r = lib.l7g_debug_regex(p, len(p), 1 if anchored else 0, d, len(d), err, 512)
+    if r < 0:
+        raise ValueError(err.value.decode(errors="replace"))
+    return bool(r)

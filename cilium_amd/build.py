@@ -1,0 +1,84 @@
+"""Build cilium_amd/libl7gpu.so (HIP kernels for gfx950 + C++ host code).
+
+Every translation unit is compiled with hipcc; the shared object is linked
+against the libamdhip64.so that PyTorch-ROCm loads (torch/lib), so a process
+that uses both torch (device memory, streams, torch.distributed/RCCL) and this
+library runs exactly one HIP runtime.  Output stays in-tree so it travels to
+the GPU box with the repo snapshot.
+"""
+import concurrent.futures as cf
+import glob
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+BUILD = os.path.join(HERE, "build")
+LIB = os.path.join(HERE, "libl7gpu.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("L7G_ARCH", "gfx950")
+
+COMMON = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", "-Wno-sign-compare"]
+HIP_FLAGS = [f"--offload-arch={ARCH}", "-mcode-object-version=5", "-munsafe-fp-atomics"]
+
+
+def torch_libdir():
+    import importlib.util
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.submodule_search_locations:
+        return None
+    d = os.path.join(list(spec.submodule_search_locations)[0], "lib")
+    return d if os.path.exists(os.path.join(d, "libamdhip64.so")) else None
+
+
+def sources():
+    return sorted(glob.glob(os.path.join(CSRC, "**", "*.cc"), recursive=True) +
+                  glob.glob(os.path.join(CSRC, "**", "*.hip"), recursive=True))
+
+
+def headers():
+    return glob.glob(os.path.join(CSRC, "**", "*.h"), recursive=True) + \
+        glob.glob(os.path.join(HERE, "..", "include", "*.h"))
+
+
+def _compile(src, obj, newest_header):
+    if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), newest_header):
+        return None
+    os.makedirs(os.path.dirname(obj), exist_ok=True)
+    if src.endswith(".hip"):
+        cmd = [HIPCC] + COMMON + HIP_FLAGS + ["-c", src, "-o", obj]
+    else:  # host-only C++: plain g++ against the HIP runtime headers
+        cmd = ["g++"] + COMMON + ["-I/opt/rocm/include", "-D__HIP_PLATFORM_AMD__", "-c", src, "-o", obj]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return src
+
+
+def build(verbose=False, jobs=8):
+    srcs = sources()
+    newest_header = max([os.path.getmtime(h) for h in headers()] + [0])
+    objs = [os.path.join(BUILD, os.path.relpath(s, CSRC)) + ".o" for s in srcs]
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        done = list(ex.map(lambda so: _compile(so[0], so[1], newest_header), zip(srcs, objs)))
+    rebuilt = [d for d in done if d]
+    if verbose and rebuilt:
+        print("compiled:", *[os.path.relpath(r, HERE) for r in rebuilt], file=sys.stderr)
+    if rebuilt or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(o) for o in objs):
+        tl = torch_libdir()
+        link = ["g++", "-shared", "-o", LIB + ".tmp"] + objs
+        if tl:
+            link += [f"-L{tl}", "-l:libamdhip64.so", f"-Wl,-rpath,{tl}"]
+        else:
+            link += ["-L/opt/rocm/lib", "-lamdhip64", "-Wl,-rpath,/opt/rocm/lib"]
+        link += ["-pthread"]
+        r = subprocess.run(link, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed: {' '.join(link)}\n{r.stdout}\n{r.stderr}")
+        os.replace(LIB + ".tmp", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(verbose=True))

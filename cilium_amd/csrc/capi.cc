@@ -1,0 +1,296 @@
+// C-ABI implementation (include/l7gpu.h): engine state, policy versions,
+// connection table, table upload and kernel dispatch (product code).
+#include <hip/hip_runtime_api.h>
+
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/l7gpu.h"
+#include "device_tables.h"
+#include "engine/http_compile.h"
+#include "engine/kafka_compile.h"
+#include "policy/policy.h"
+#include "regex/re_dfa.h"
+
+namespace l7 {
+hipError_t LaunchHttpClassify(const uint8_t *arena, const uint64_t *offs, const uint32_t *lens, const uint32_t *conn_ids,
+                              uint32_t n, const DevConn *conns, uint32_t nconns, const HttpTables &T,
+                              uint8_t *verdict, int32_t *rule, uint32_t *consumed, uint64_t *counters,
+                              uint32_t ncounters, hipStream_t stream);
+hipError_t LaunchKafkaClassify(const uint8_t *arena, const uint64_t *offs, const uint32_t *lens, const uint32_t *conn_ids,
+                               uint32_t n, const DevConn *conns, uint32_t nconns, const KafkaTables &T,
+                               uint8_t *verdict, int32_t *rule, uint32_t *consumed, uint64_t *counters,
+                               uint32_t ncounters, hipStream_t stream);
+}  // namespace l7
+
+using namespace l7;
+
+struct l7g_engine {
+    int device = 0;
+    std::mutex mu;
+    std::unique_ptr<PolicySet> ps;
+    std::unique_ptr<HttpCompiler> hc;
+    std::unique_ptr<KafkaCompiler> kc;
+    std::vector<l7g_conn_t> attrs;
+    std::vector<DevConn> conns;
+    uint8_t *d_blob = nullptr;
+    size_t blob_bytes = 0;
+    DevConn *d_conns = nullptr;
+    size_t conns_cap = 0;
+    HttpTables ht{};
+    KafkaTables kt{};
+    bool tables_dirty = true, conns_dirty = true;
+    bool has_http = false, has_kafka = false;
+};
+
+static void set_err(char *err, size_t errlen, const std::string &m) {
+    if (!err || errlen == 0) return;
+    size_t n = std::min(errlen - 1, m.size());
+    memcpy(err, m.data(), n);
+    err[n] = 0;
+}
+
+namespace {
+
+template <class T>
+size_t Put(std::vector<uint8_t> &blob, const std::vector<T> &v) {
+    size_t off = (blob.size() + 255) & ~(size_t)255;
+    blob.resize(off + v.size() * sizeof(T) + 16);  // +16: aligned 16-byte reads may run past the end
+    if (!v.empty()) memcpy(blob.data() + off, v.data(), v.size() * sizeof(T));
+    return off;
+}
+
+// Resolve every connection to its rule set (once per connection / policy version).
+bool ResolveConns(l7g_engine *e, std::string *err) {
+    e->conns.assign(e->attrs.size(), DevConn{-1, PROTO_NONE, {0, 0, 0}});
+    e->has_http = e->has_kafka = false;
+    for (size_t i = 0; i < e->attrs.size(); i++) {
+        const l7g_conn_t &a = e->attrs[i];
+        DevConn &c = e->conns[i];
+        c.proto = a.proto;
+        if (a.proto == PROTO_HTTP) {
+            // remote identity: ingress = source, egress = destination (cilium_l7policy.cc:144-150)
+            uint64_t remote = a.ingress ? a.src_id : a.dst_id;
+            c.ruleset = e->hc->RulesetFor(a.policy, a.ingress != 0, a.port, remote, err);
+            if (c.ruleset < 0) return false;
+            e->has_http = true;
+        } else if (a.proto == PROTO_KAFKA) {
+            // Kafka rules are selected by the source identity in both directions
+            // (pkg/proxy/kafka.go:327,357)
+            c.ruleset = e->kc->RulesetFor(a.policy, a.ingress != 0, a.port, a.src_id, err);
+            if (c.ruleset < 0) return false;
+            e->has_kafka = true;
+        }
+    }
+    e->tables_dirty = e->conns_dirty = true;
+    return true;
+}
+
+hipError_t Upload(l7g_engine *e) {
+    hipError_t rc;
+    if (e->tables_dirty) {
+        std::vector<uint8_t> blob;
+        const HttpImage &H = e->hc->image();
+        size_t o_rs = Put(blob, H.rulesets), o_ch = Put(blob, H.chunks), o_f = Put(blob, H.fields),
+               o_d = Put(blob, H.dfas), o_tr = Put(blob, H.trans), o_m = Put(blob, H.masks), o_c = Put(blob, H.cls),
+               o_r = Put(blob, H.rule_ids), o_h = Put(blob, H.hdrs), o_n = Put(blob, H.names);
+        const KafkaImage &K = e->kc->image();
+        size_t k_rs = Put(blob, K.rulesets), k_r = Put(blob, K.rules), k_idx = Put(blob, K.index),
+               k_th = Put(blob, K.topic_hash), k_ch = Put(blob, K.client_hash), k_s = Put(blob, K.strings);
+        uint8_t *d = nullptr;
+        if ((rc = hipMalloc(&d, blob.size())) != hipSuccess) return rc;
+        if ((rc = hipMemcpy(d, blob.data(), blob.size(), hipMemcpyHostToDevice)) != hipSuccess) { hipFree(d); return rc; }
+        if (e->d_blob) { hipDeviceSynchronize(); hipFree(e->d_blob); }
+        e->d_blob = d;
+        e->blob_bytes = blob.size();
+        HttpTables &T = e->ht;
+        T.rulesets = (const DevRuleset *)(d + o_rs);
+        T.chunks = (const DevChunk *)(d + o_ch);
+        T.fields = (const DevField *)(d + o_f);
+        T.dfas = (const DevDfa *)(d + o_d);
+        T.trans = (const uint16_t *)(d + o_tr);
+        T.masks = (const uint64_t *)(d + o_m);
+        T.cls = (const uint8_t *)(d + o_c);
+        T.rule_ids = (const int32_t *)(d + o_r);
+        T.hdrs = (const DevHdrName *)(d + o_h);
+        T.names = (const uint8_t *)(d + o_n);
+        T.nrulesets = (uint32_t)H.rulesets.size();
+        KafkaTables &KT = e->kt;
+        KT.rulesets = (const DevKafkaRuleset *)(d + k_rs);
+        KT.rules = (const DevKafkaRule *)(d + k_r);
+        KT.index = (const uint32_t *)(d + k_idx);
+        KT.topic_hash = (const DevStrSlot *)(d + k_th);
+        KT.client_hash = (const DevStrSlot *)(d + k_ch);
+        KT.strings = (const uint8_t *)(d + k_s);
+        KT.nrulesets = (uint32_t)K.rulesets.size();
+        KT.topic_mask = K.topic_mask;
+        KT.client_mask = K.client_mask;
+        e->tables_dirty = false;
+    }
+    if (e->conns_dirty) {
+        size_t need = std::max<size_t>(e->conns.size(), 1);
+        if (need > e->conns_cap) {
+            if (e->d_conns) { hipDeviceSynchronize(); hipFree(e->d_conns); e->d_conns = nullptr; }
+            if ((rc = hipMalloc(&e->d_conns, need * sizeof(DevConn))) != hipSuccess) return rc;
+            e->conns_cap = need;
+        }
+        if (!e->conns.empty() &&
+            (rc = hipMemcpy(e->d_conns, e->conns.data(), e->conns.size() * sizeof(DevConn), hipMemcpyHostToDevice)) != hipSuccess)
+            return rc;
+        e->conns_dirty = false;
+    }
+    return hipSuccess;
+}
+
+}  // namespace
+
+extern "C" {
+
+l7g_engine *l7g_engine_create(int device, char *err, size_t errlen) {
+    int ndev = 0;
+    hipError_t rc = hipGetDeviceCount(&ndev);
+    if (rc != hipSuccess || device < 0 || device >= ndev) {
+        set_err(err, errlen, std::string("no such HIP device: ") + std::to_string(device) + " (" + hipGetErrorString(rc) + ")");
+        return nullptr;
+    }
+    if ((rc = hipSetDevice(device)) != hipSuccess) { set_err(err, errlen, hipGetErrorString(rc)); return nullptr; }
+    auto *e = new l7g_engine();
+    e->device = device;
+    e->ps = std::make_unique<PolicySet>();
+    e->hc = std::make_unique<HttpCompiler>(e->ps.get());
+    e->kc = std::make_unique<KafkaCompiler>(e->ps.get());
+    return e;
+}
+
+void l7g_engine_destroy(l7g_engine *e) {
+    if (!e) return;
+    hipSetDevice(e->device);
+    hipDeviceSynchronize();
+    if (e->d_blob) hipFree(e->d_blob);
+    if (e->d_conns) hipFree(e->d_conns);
+    delete e;
+}
+
+int l7g_policy_update(l7g_engine *e, const char *json, size_t len, char *err, size_t errlen) {
+    std::lock_guard<std::mutex> g(e->mu);
+    auto ps = std::make_unique<PolicySet>();
+    std::string m;
+    if (!LoadPolicySet(json, len, ps.get(), &m)) { set_err(err, errlen, m); return -1; }
+    auto hc = std::make_unique<HttpCompiler>(ps.get());
+    auto kc = std::make_unique<KafkaCompiler>(ps.get());
+    std::swap(e->ps, ps);
+    std::swap(e->hc, hc);
+    std::swap(e->kc, kc);
+    if (!ResolveConns(e, &m)) {  // roll back: previous version stays in force
+        std::swap(e->ps, ps);
+        std::swap(e->hc, hc);
+        std::swap(e->kc, kc);
+        std::string m2;
+        ResolveConns(e, &m2);
+        set_err(err, errlen, m);
+        return -1;
+    }
+    return 0;
+}
+
+int32_t l7g_policy_index(l7g_engine *e, const char *name, size_t len) {
+    std::lock_guard<std::mutex> g(e->mu);
+    auto it = e->ps->by_name.find(std::string(name, len));
+    return it == e->ps->by_name.end() ? -1 : it->second;
+}
+
+int32_t l7g_policy_nrules(l7g_engine *e) {
+    std::lock_guard<std::mutex> g(e->mu);
+    return e->ps->nrules;
+}
+
+int l7g_conns_set(l7g_engine *e, const l7g_conn_t *conns, uint32_t n, char *err, size_t errlen) {
+    std::lock_guard<std::mutex> g(e->mu);
+    e->attrs.assign(conns, conns + n);
+    std::string m;
+    if (!ResolveConns(e, &m)) { set_err(err, errlen, m); return -1; }
+    return 0;
+}
+
+int l7g_classify(l7g_engine *e, const uint8_t *arena, const uint64_t *off, const uint32_t *len, const uint32_t *conn,
+                 uint32_t n, uint8_t *verdict, int32_t *rule, uint32_t *consumed, uint64_t *counters, void *stream) {
+    std::lock_guard<std::mutex> g(e->mu);
+    hipError_t rc = hipSetDevice(e->device);
+    if (rc == hipSuccess) rc = Upload(e);
+    if (rc != hipSuccess) return (int)rc;
+    hipStream_t s = (hipStream_t)stream;
+    const uint32_t ncounters = counters ? (uint32_t)e->ps->nrules + 8 : 0;
+    // The kernels each classify only their own protocol's requests and skip
+    // the rest, so a mixed batch needs one launch per protocol present.
+    if (e->has_http || !e->has_kafka)
+        rc = LaunchHttpClassify(arena, off, len, conn, n, e->d_conns, (uint32_t)e->conns.size(), e->ht, verdict, rule,
+                                consumed, counters, ncounters, s);
+    if (rc == hipSuccess && e->has_kafka)
+        rc = LaunchKafkaClassify(arena, off, len, conn, n, e->d_conns, (uint32_t)e->conns.size(), e->kt, verdict, rule,
+                                 consumed, counters, ncounters, s);
+    return (int)rc;
+}
+
+int l7g_classify_host(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const uint64_t *off, const uint32_t *len,
+                      const uint32_t *conn, uint32_t n, uint8_t *verdict, int32_t *rule, uint32_t *consumed) {
+    hipError_t rc = hipSetDevice(e->device);
+    if (rc != hipSuccess) return (int)rc;
+    uint8_t *d_a = nullptr, *d_v = nullptr;
+    uint64_t *d_o = nullptr;
+    uint32_t *d_l = nullptr, *d_c = nullptr, *d_cons = nullptr;
+    int32_t *d_r = nullptr;
+    size_t nn = std::max<uint32_t>(n, 1);
+    rc = hipMalloc(&d_a, arena_len + 64);
+    if (rc == hipSuccess) rc = hipMalloc(&d_o, nn * 8);
+    if (rc == hipSuccess) rc = hipMalloc(&d_l, nn * 4);
+    if (rc == hipSuccess) rc = hipMalloc(&d_c, nn * 4);
+    if (rc == hipSuccess) rc = hipMalloc(&d_v, nn);
+    if (rc == hipSuccess) rc = hipMalloc(&d_r, nn * 4);
+    if (rc == hipSuccess) rc = hipMalloc(&d_cons, nn * 4);
+    if (rc == hipSuccess && arena_len) rc = hipMemcpy(d_a, arena, arena_len, hipMemcpyHostToDevice);
+    if (rc == hipSuccess && n) rc = hipMemcpy(d_o, off, n * 8, hipMemcpyHostToDevice);
+    if (rc == hipSuccess && n) rc = hipMemcpy(d_l, len, n * 4, hipMemcpyHostToDevice);
+    if (rc == hipSuccess && n) rc = hipMemcpy(d_c, conn, n * 4, hipMemcpyHostToDevice);
+    if (rc == hipSuccess) rc = (hipError_t)l7g_classify(e, d_a, d_o, d_l, d_c, n, d_v, d_r, d_cons, nullptr, nullptr);
+    if (rc == hipSuccess) rc = hipDeviceSynchronize();
+    if (rc == hipSuccess && n) rc = hipMemcpy(verdict, d_v, n, hipMemcpyDeviceToHost);
+    if (rc == hipSuccess && n) rc = hipMemcpy(rule, d_r, n * 4, hipMemcpyDeviceToHost);
+    if (rc == hipSuccess && n) rc = hipMemcpy(consumed, d_cons, n * 4, hipMemcpyDeviceToHost);
+    hipFree(d_a); hipFree(d_o); hipFree(d_l); hipFree(d_c); hipFree(d_v); hipFree(d_r); hipFree(d_cons);
+    return (int)rc;
+}
+
+int l7g_stats(l7g_engine *e, l7g_stats_t *out) {
+    std::lock_guard<std::mutex> g(e->mu);
+    memset(out, 0, sizeof *out);
+    out->policies = (uint32_t)e->ps->policies.size();
+    out->rules = (uint32_t)e->ps->nrules;
+    const HttpImage &H = e->hc->image();
+    out->http_rulesets = (uint32_t)H.rulesets.size();
+    out->http_chunks = (uint32_t)H.chunks.size();
+    out->http_dfas = (uint32_t)H.dfas.size();
+    out->http_dfa_states = (uint32_t)H.dfa_states;
+    const KafkaImage &K = e->kc->image();
+    out->kafka_rulesets = (uint32_t)K.rulesets.size();
+    out->kafka_rules = (uint32_t)K.rules.size();
+    out->kafka_topics = (uint32_t)K.ntopics;
+    out->table_bytes = e->blob_bytes;
+    return 0;
+}
+
+int l7g_debug_regex(const char *pat, size_t patlen, int anchored, const uint8_t *s, size_t slen, char *err,
+                    size_t errlen) {
+    std::string m;
+    auto ast = re::Parse(std::string(pat, patlen), &m);
+    if (!ast) { set_err(err, errlen, m); return -1; }
+    re::DFA d;
+    std::vector<re::Pattern> ps{{ast.get(), anchored != 0}};
+    if (!re::BuildDFA(ps, 1 << 16, &d, &m)) { set_err(err, errlen, m); return -1; }
+    auto acc = re::RunDFA(d, s, slen);
+    return (int)(acc[0] & 1);
+}
+
+}  // extern "C"

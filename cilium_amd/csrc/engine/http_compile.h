@@ -1,0 +1,52 @@
+// HTTP rule-set compiler (product code): Envoy HTTP policy semantics
+// (envoy/cilium_network_policy.h:50-237) lowered to device tables.
+//
+// For a connection (policy, direction, port, remote identity) the verdict is
+// the first HTTP rule, in PortNetworkPolicy evaluation order, whose header
+// matchers all match; the order is fixed per connection, so it is resolved
+// here once into a "rule set": an ordered rule list + a terminal verdict.
+// Each rule set is split into chunks of <= 64 rules; per chunk and header
+// field, the field's matchers are compiled into byte DFAs whose states carry
+// the 64-bit mask of rules satisfied on that field if the value ends there.
+#pragma once
+#include <cstdint>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../device_tables.h"
+#include "../policy/policy.h"
+
+namespace l7 {
+
+struct HttpImage {
+    std::vector<DevRuleset> rulesets;
+    std::vector<DevChunk> chunks;
+    std::vector<DevField> fields;
+    std::vector<DevDfa> dfas;
+    std::vector<uint16_t> trans;
+    std::vector<uint64_t> masks;
+    std::vector<uint8_t> cls;
+    std::vector<int32_t> rule_ids;
+    std::vector<DevHdrName> hdrs;
+    std::vector<uint8_t> names;
+    size_t dfa_states = 0;
+};
+
+class HttpCompiler {
+public:
+    explicit HttpCompiler(const PolicySet *ps) : ps_(ps) {}
+    // Returns the rule set index for a connection, compiling it on first use.
+    // policy < 0: unknown policy (NetworkPolicyMap::Allowed => deny).
+    int RulesetFor(int policy, bool ingress, uint32_t port, uint64_t remote, std::string *err);
+    const HttpImage &image() const { return img_; }
+    int max_dfa_states = 4096;
+
+private:
+    const PolicySet *ps_;
+    HttpImage img_;
+    std::map<std::pair<std::vector<int>, int>, int> cache_;  // (rule ids, terminal) -> ruleset
+    int Compile(const std::vector<const HttpRule *> &rules, uint8_t terminal, std::string *err);
+};
+
+}  // namespace l7

@@ -1,0 +1,392 @@
+// Kafka request classification on gfx950 (product code).
+//
+// One lane per request frame.  Each lane restates, sequentially over its own
+// bytes, the reference's decode path: proto.ReadReq framing
+// (vendor/github.com/optiopay/kafka/proto/messages.go:124-165), the typed
+// decoders (:504-537, :767-824, :1033-1054, :1173-1228, :1389-1430,
+// :1591-1647, :1810-1858) with io.ReadFull / LimitReader semantics
+// (serialization.go:19-203), readMessageSet with CRC32-IEEE per message and
+// stop-without-drain (:363-494), then MatchesRule (pkg/kafka/policy.go:200-225)
+// against the connection's rule set using the precomputed topic / key views
+// (engine/kafka_compile.h).  Compressed message sets => L7_UNSUPPORTED.
+#include <hip/hip_runtime.h>
+
+#include "../device_tables.h"
+
+namespace l7 {
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr uint32_t kMaxParseBuf = 6553500;
+constexpr uint32_t kInf = 0xFFFFFFFFu;
+
+struct KDec {
+    const uint8_t *b;
+    uint32_t pos, end;
+    int64_t limit;  // LimitReader remaining, -1 = none
+    int err;        // 0 ok, 1 EOF, 2 ErrUnexpectedEOF, 3 other
+};
+
+__device__ __forceinline__ uint32_t kavail(const KDec &d) {
+    uint32_t a = d.end - d.pos;
+    if (d.limit >= 0 && (uint64_t)d.limit < a) a = (uint32_t)d.limit;
+    return a;
+}
+// io.ReadFull(r, buf[:n]); returns start offset, sets d.err on a short read
+__device__ __forceinline__ uint32_t kread(KDec &d, uint32_t n) {
+    uint32_t at = d.pos;
+    if (n == 0) return at;
+    uint32_t a = kavail(d);
+    if (a == 0) { d.err = 1; return at; }
+    uint32_t take = a < n ? a : n;
+    d.pos += take;
+    if (d.limit >= 0) d.limit -= take;
+    if (take < n) d.err = 2;
+    return at;
+}
+__device__ __forceinline__ uint64_t be_load(const uint8_t *p, int n) {
+    uint64_t v = 0;
+    for (int i = 0; i < n; i++) v = (v << 8) | p[i];
+    return v;
+}
+__device__ __forceinline__ int64_t dec_int(KDec &d, int n) {
+    if (d.err) return 0;
+    uint32_t at = kread(d, (uint32_t)n);
+    if (d.err) return 0;
+    uint64_t v = be_load(d.b + at, n);
+    return n == 1 ? (int64_t)(int8_t)v : n == 2 ? (int64_t)(int16_t)v : n == 4 ? (int64_t)(int32_t)v : (int64_t)v;
+}
+// DecodeString -> (off, len); len < 1 => ""
+__device__ __forceinline__ void dec_string(KDec &d, uint32_t &off, uint32_t &len) {
+    off = 0; len = 0;
+    if (d.err) return;
+    int16_t sl = (int16_t)dec_int(d, 2);
+    if (d.err || sl < 1) return;
+    uint32_t at = kread(d, (uint32_t)sl);
+    if (d.err) return;
+    off = at; len = (uint32_t)sl;
+}
+// DecodeArrayLen(nullable): -1 null; sets bad on ErrInvalidArrayLen
+__device__ __forceinline__ int64_t dec_arraylen(KDec &d, bool nullable, bool &bad) {
+    int64_t l = (int32_t)dec_int(d, 4);
+    bad = false;
+    if (l < 0) { if (nullable) return -1; bad = true; return 0; }
+    if (l > kMaxParseBuf) { bad = true; return 0; }
+    return l;
+}
+__device__ __forceinline__ void dec_bytes(KDec &d) {
+    if (d.err) return;
+    int32_t sl = (int32_t)dec_int(d, 4);
+    if (d.err || sl < 1) return;
+    if ((uint32_t)sl > kMaxParseBuf) { d.err = 3; return; }
+    kread(d, (uint32_t)sl);
+}
+
+__device__ uint32_t crc32_ieee(const uint32_t *tab, const uint8_t *p, uint32_t n) {
+    uint32_t c = 0xFFFFFFFFu;
+    for (uint32_t i = 0; i < n; i++) c = tab[(c ^ p[i]) & 0xFF] ^ (c >> 8);
+    return ~c;
+}
+
+// readMessageSet on the shared position; 0 ok, -1 error, -2 compressed
+__device__ int read_message_set(const uint8_t *b, uint32_t &pos, uint32_t end, int32_t size, int16_t version,
+                                const uint32_t *crctab) {
+    if (size < 0) return 0;
+    if ((uint32_t)size > kMaxParseBuf) return -1;
+    KDec dec{b, pos, end, size, 0};
+    int rc = 0;
+    for (;;) {
+        (void)dec_int(dec, 8);
+        if (dec.err) break;
+        int32_t msize = (int32_t)dec_int(dec, 4);
+        if (dec.err || msize <= 0) break;
+        if ((uint32_t)msize > kMaxParseBuf) { rc = -1; break; }
+        uint32_t at = kread(dec, (uint32_t)msize);
+        if (dec.err) break;
+        KDec md{b, at, at + (uint32_t)msize, -1, 0};
+        uint32_t crc = (uint32_t)dec_int(md, 4);
+        if (msize <= 4) break;
+        if (crc != crc32_ieee(crctab, b + at + 4, (uint32_t)msize - 4)) break;  // stop, no drain
+        (void)dec_int(md, 1);
+        int8_t attr = (int8_t)dec_int(md, 1);
+        if (version >= 1) (void)dec_int(md, 8);
+        int codec = attr & 3;
+        if (codec == 3) break;  // `return nil, err` with err == nil
+        dec_bytes(md);
+        dec_bytes(md);
+        if (md.err) { rc = -1; break; }
+        if (codec != 0) { rc = -2; break; }
+    }
+    pos = dec.pos;
+    return rc;
+}
+
+__device__ int32_t str_lookup(const DevStrSlot *tab, uint32_t mask, const uint8_t *strings, const uint8_t *s,
+                              uint32_t n) {
+    uint32_t h = kFnvBasis;
+    for (uint32_t i = 0; i < n; i++) h = (h ^ s[i]) * 16777619u;
+    for (uint32_t slot = h & mask;; slot = (slot + 1) & mask) {
+        const DevStrSlot e = tab[slot];
+        if (!e.used) return -1;
+        if (e.hash == h && e.len == n) {
+            bool eq = true;
+            for (uint32_t i = 0; i < n && eq; i++) eq = strings[e.str_off + i] == s[i];
+            if (eq) return e.id;
+        }
+    }
+}
+
+__device__ __forceinline__ bool is_topic_api_key(int k) {
+    // 0 1 2 3 4 5 6 8 9 19 20 21 23 24 27 28 34 35 37
+    if (k < 0 || k > 37) return false;
+    const uint64_t m = (1ull << 0) | (1ull << 1) | (1ull << 2) | (1ull << 3) | (1ull << 4) | (1ull << 5) | (1ull << 6) |
+                       (1ull << 8) | (1ull << 9) | (1ull << 19) | (1ull << 20) | (1ull << 21) | (1ull << 23) |
+                       (1ull << 24) | (1ull << 27) | (1ull << 28) | (1ull << 34) | (1ull << 35) | (1ull << 37);
+    return (m >> k) & 1;
+}
+
+struct ReqInfo {
+    int kind;
+    int version;
+    int typed;      // 0 nil request, 1 typed with topics/ClientID, 2 ConsumerMetadata
+    int32_t client; // interned id, -2 unknown / empty
+};
+
+__device__ __forceinline__ bool rule_matches(const DevKafkaRule &r, const ReqInfo &q) {
+    if (!r.any_key && (q.kind < 0 || q.kind > 63 || !((r.keymask >> q.kind) & 1))) return false;
+    if (r.has_version && r.version != q.version) return false;
+    if (!r.has_topic && r.client < 0) return true;
+    if (q.typed == 1) return r.client < 0 || r.client == q.client;
+    if (q.typed == 2) return true;
+    return !(r.has_topic && is_topic_api_key(q.kind));
+}
+
+// first position of topic `tid`'s rule list that matches, kInf if none
+__device__ uint32_t topic_first(const KafkaTables &T, const DevKafkaRuleset &rs, const ReqInfo &q, int32_t tid) {
+    if (tid < 0 || rs.ntopics == 0) return kInf;
+    const uint32_t *dir = T.index + rs.topics_off;
+    uint32_t lo = 0, hi = rs.ntopics;
+    while (lo < hi) {
+        uint32_t m = (lo + hi) >> 1;
+        if (dir[3 * m] < (uint32_t)tid) lo = m + 1; else hi = m;
+    }
+    if (lo >= rs.ntopics || dir[3 * lo] != (uint32_t)tid) return kInf;
+    const uint32_t off = dir[3 * lo + 1], cnt = dir[3 * lo + 2];
+    for (uint32_t i = 0; i < cnt; i++) {
+        uint32_t p = T.index[off + i];
+        if (rule_matches(T.rules[rs.rule_first + p], q)) return p;
+    }
+    return kInf;
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(kBlock) void kafka_classify_kernel(
+    const uint8_t *__restrict__ arena, const uint64_t *__restrict__ offs, const uint32_t *__restrict__ lens,
+    const uint32_t *__restrict__ conn_ids, uint32_t n, const DevConn *__restrict__ conns, uint32_t nconns,
+    KafkaTables T, uint8_t *__restrict__ out_verdict, int32_t *__restrict__ out_rule, uint32_t *__restrict__ out_consumed,
+    uint64_t *__restrict__ counters, uint32_t ncounters) {
+    __shared__ uint32_t crctab[256];
+    for (uint32_t i = threadIdx.x; i < 256; i += kBlock) {
+        uint32_t c = i;
+        for (int k = 0; k < 8; k++) c = (c & 1) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
+        crctab[i] = c;
+    }
+    __syncthreads();
+    for (uint32_t idx = blockIdx.x * kBlock + threadIdx.x; idx < n; idx += gridDim.x * kBlock) {
+        const uint32_t ci = conn_ids[idx];
+        if (ci >= nconns) continue;
+        const DevConn conn = conns[ci];
+        if (conn.proto != PROTO_KAFKA) continue;
+        const uint8_t *b = arena + offs[idx];
+        const uint32_t len = lens[idx];
+        uint8_t verdict = V_PARSE_ERROR;
+        int32_t rule = -1;
+        uint32_t consumed = 0;
+        // ---- proto.ReadReq
+        do {
+            if (len < 4) { verdict = V_INCOMPLETE; break; }
+            const int32_t size = (int32_t)be_load(b, 4);
+            if (size <= 0) { verdict = V_PARSE_ERROR; break; }
+            if (len < 6) { verdict = V_INCOMPLETE; break; }
+            if ((uint64_t)(uint32_t)size + 4 > kMaxParseBuf) { verdict = V_PARSE_ERROR; break; }
+            const uint32_t rawlen = (uint32_t)size + 4;
+            if (rawlen > len) { verdict = V_INCOMPLETE; break; }
+            if (rawlen < 12) { verdict = V_PARSE_ERROR; break; }
+            ReqInfo q;
+            q.kind = (int16_t)be_load(b + 4, 2);
+            q.version = (int16_t)be_load(b + 6, 2);
+            q.typed = (q.kind == 0 || q.kind == 1 || q.kind == 2 || q.kind == 3 || q.kind == 8 || q.kind == 9) ? 1
+                    : (q.kind == 10 ? 2 : 0);
+            q.client = -2;
+            const DevKafkaRuleset rs = T.rulesets[conn.ruleset];
+            uint32_t ntopics = 0, cmax = 0;  // raw topic count; max over topics of first matching rule
+            int rc = 0;
+            if (q.typed) {
+                KDec d{b, 0, rawlen, -1, 0};
+                bool bad = false;
+                (void)dec_int(d, 4); (void)dec_int(d, 2);
+                const int16_t ver = (int16_t)dec_int(d, 2);
+                (void)dec_int(d, 4);
+                uint32_t co, cl;
+                dec_string(d, co, cl);
+                if (!d.err && cl > 0) q.client = str_lookup(T.client_hash, T.client_mask, T.strings, b + co, cl);
+                if (q.client < 0) q.client = -2;
+                const bool topics_on = q.typed == 1;
+                auto on_topic = [&](uint32_t to, uint32_t tl) {
+                    if (!topics_on) return;
+                    ntopics++;
+                    int32_t tid = tl > 0 ? str_lookup(T.topic_hash, T.topic_mask, T.strings, b + to, tl) : -1;
+                    uint32_t e = topic_first(T, rs, q, tid);
+                    cmax = cmax > e ? cmax : e;
+                };
+                int64_t nt, np;
+                uint32_t o, l;
+                switch (q.kind) {
+                case 0:  // Produce
+                    if (ver >= 3) dec_string(d, o, l);
+                    (void)dec_int(d, 2); (void)dec_int(d, 4);
+                    nt = dec_arraylen(d, false, bad);
+                    if (bad) { rc = -1; break; }
+                    for (int64_t t = 0; t < nt && rc == 0; t++) {
+                        dec_string(d, o, l);
+                        if (d.err) break;
+                        on_topic(o, l);
+                        np = dec_arraylen(d, false, bad);
+                        if (bad) { rc = -1; break; }
+                        for (int64_t p = 0; p < np; p++) {
+                            (void)dec_int(d, 4);
+                            if (d.err) { rc = -1; break; }
+                            const int32_t ss = (int32_t)dec_int(d, 4);
+                            if (d.err) { rc = -1; break; }
+                            rc = read_message_set(b, d.pos, d.end, ss, ver, crctab);
+                            if (rc) break;
+                        }
+                    }
+                    break;
+                case 1:  // Fetch
+                    (void)dec_int(d, 4); (void)dec_int(d, 4); (void)dec_int(d, 4);
+                    if (ver >= 3) (void)dec_int(d, 4);
+                    if (ver >= 4) (void)dec_int(d, 1);
+                    nt = dec_arraylen(d, false, bad);
+                    if (bad) { rc = -1; break; }
+                    for (int64_t t = 0; t < nt && !d.err; t++) {
+                        dec_string(d, o, l);
+                        on_topic(o, l);
+                        np = dec_arraylen(d, false, bad);
+                        if (bad) { rc = -1; break; }
+                        for (int64_t p = 0; p < np && !d.err; p++) {
+                            (void)dec_int(d, 4); (void)dec_int(d, 8);
+                            if (ver >= 5) (void)dec_int(d, 8);
+                            (void)dec_int(d, 4);
+                        }
+                    }
+                    break;
+                case 2:  // Offset
+                    (void)dec_int(d, 4);
+                    if (ver >= 2) (void)dec_int(d, 1);
+                    nt = dec_arraylen(d, false, bad);
+                    if (bad) { rc = -1; break; }
+                    for (int64_t t = 0; t < nt && !d.err; t++) {
+                        dec_string(d, o, l);
+                        on_topic(o, l);
+                        np = dec_arraylen(d, false, bad);
+                        if (bad) { rc = -1; break; }
+                        for (int64_t p = 0; p < np && !d.err; p++) {
+                            (void)dec_int(d, 4); (void)dec_int(d, 8);
+                            if (ver == 0) (void)dec_int(d, 4);
+                        }
+                    }
+                    break;
+                case 3:  // Metadata
+                    nt = dec_arraylen(d, true, bad);
+                    if (bad) { rc = -1; break; }
+                    for (int64_t t = 0; t < nt && !d.err; t++) { dec_string(d, o, l); if (!d.err) on_topic(o, l); }
+                    if (ver >= 4) (void)dec_int(d, 1);
+                    break;
+                case 8:  // OffsetCommit
+                    dec_string(d, o, l);
+                    if (ver >= 1) { (void)dec_int(d, 4); dec_string(d, o, l); }
+                    if (ver >= 2) (void)dec_int(d, 8);
+                    nt = dec_arraylen(d, false, bad);
+                    if (bad) { rc = -1; break; }
+                    for (int64_t t = 0; t < nt && !d.err; t++) {
+                        dec_string(d, o, l);
+                        on_topic(o, l);
+                        np = dec_arraylen(d, false, bad);
+                        if (bad) { rc = -1; break; }
+                        for (int64_t p = 0; p < np && !d.err; p++) {
+                            (void)dec_int(d, 4); (void)dec_int(d, 8);
+                            if (ver == 1) (void)dec_int(d, 8);
+                            uint32_t o2, l2;
+                            dec_string(d, o2, l2);
+                        }
+                    }
+                    break;
+                case 9:  // OffsetFetch
+                    dec_string(d, o, l);
+                    nt = dec_arraylen(d, true, bad);
+                    if (bad) { rc = -1; break; }
+                    for (int64_t t = 0; t < nt && !d.err; t++) {
+                        dec_string(d, o, l);
+                        on_topic(o, l);
+                        np = dec_arraylen(d, false, bad);
+                        if (bad) { rc = -1; break; }
+                        for (int64_t p = 0; p < np && !d.err; p++) (void)dec_int(d, 4);
+                    }
+                    break;
+                case 10:  // ConsumerMetadata
+                    dec_string(d, o, l);
+                    if (ver >= 1) (void)dec_int(d, 1);
+                    break;
+                }
+                if (rc == 0 && d.err) rc = -1;
+            }
+            if (rc == -1) { verdict = V_PARSE_ERROR; break; }
+            if (rc == -2) { verdict = V_UNSUPPORTED; break; }
+            consumed = rawlen;
+            verdict = V_DENY;
+            if (!rs.any) break;
+            // ---- MatchesRule
+            uint32_t best = kInf;
+            if (ntopics == 0) {
+                const int key = (q.kind >= 0 && q.kind < 64) ? q.kind : 64;
+                const uint32_t off = T.index[rs.bykey_off + 2 * key], cnt = T.index[rs.bykey_off + 2 * key + 1];
+                for (uint32_t i = 0; i < cnt; i++) {
+                    uint32_t p = T.index[off + i];
+                    if (rule_matches(T.rules[rs.rule_first + p], q)) { best = p; break; }
+                }
+            } else {
+                for (uint32_t i = 0; i < rs.ntopicless; i++) {
+                    uint32_t p = T.index[rs.topicless_off + i];
+                    if (p >= cmax) break;  // cannot beat topic completion
+                    if (rule_matches(T.rules[rs.rule_first + p], q)) { best = p; break; }
+                }
+                if (best == kInf) best = cmax;
+            }
+            if (best != kInf) { verdict = V_ALLOW; rule = T.rules[rs.rule_first + best].gid; }
+        } while (false);
+        out_verdict[idx] = verdict;
+        out_rule[idx] = rule;
+        out_consumed[idx] = consumed;
+        if (counters) {
+            atomicAdd((unsigned long long *)&counters[ncounters - 8 + verdict], 1ull);
+            if (rule >= 0 && (uint32_t)rule < ncounters - 8) atomicAdd((unsigned long long *)&counters[rule], 1ull);
+        }
+    }
+}
+
+hipError_t LaunchKafkaClassify(const uint8_t *arena, const uint64_t *offs, const uint32_t *lens, const uint32_t *conn_ids,
+                               uint32_t n, const DevConn *conns, uint32_t nconns, const KafkaTables &T,
+                               uint8_t *verdict, int32_t *rule, uint32_t *consumed, uint64_t *counters,
+                               uint32_t ncounters, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    uint32_t blocks = (n + kBlock - 1) / kBlock;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(kafka_classify_kernel, dim3(blocks), dim3(kBlock), 0, stream, arena, offs, lens, conn_ids, n,
+                       conns, nconns, T, verdict, rule, consumed, counters, ncounters);
+    return hipGetLastError();
+}
+
+}  // namespace l7

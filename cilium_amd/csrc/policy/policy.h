@@ -1,0 +1,71 @@
+// L7 policy model (product code): the NPDS cilium.NetworkPolicy shape
+// (envoy/cilium/npds.proto:31-182) with the reference's rule types:
+//   HTTP  : HttpNetworkPolicyRule = AND of Envoy HeaderMatchers, produced from
+//           api.PortRuleHTTP by getHTTPRule (pkg/envoy/server.go:336-399)
+//   Kafka : api.PortRuleKafka + Sanitize (pkg/policy/api/kafka.go:26-293,
+//           rule_validation.go:232-275)
+//   L7    : generic key/value rules for proxylib parsers (npds.proto:179-182)
+#pragma once
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../regex/re_ast.h"
+
+namespace l7 {
+
+enum class HM : uint8_t { Exact, Regex, Present, Prefix, Suffix, Range };
+
+struct HeaderMatcher {
+    std::string name;   // lower-cased (Envoy LowerCaseString)
+    HM type = HM::Exact;
+    std::string value;
+    bool invert = false;
+    int64_t rstart = 0, rend = 0;
+    std::shared_ptr<re::Node> ast;  // HM::Regex
+};
+
+struct HttpRule { std::vector<HeaderMatcher> m; int id = -1; };
+
+struct KafkaRule {
+    uint64_t keymask = 0;  // api keys 0..63
+    bool any_key = true;   // apiKeyInt empty (CheckAPIKeyRole wildcard)
+    bool has_version = false;
+    int16_t version = 0;
+    std::string topic, client;
+    int id = -1;
+};
+
+struct L7Rule { std::vector<std::pair<std::string, std::string>> kv; int id = -1; };
+
+struct PortRule {
+    std::vector<uint64_t> remotes;  // empty = any remote
+    enum Type { None, Http, Kafka, L7 } type = None;
+    std::vector<HttpRule> http;
+    std::vector<KafkaRule> kafka;
+    std::string l7proto;
+    std::vector<L7Rule> l7;
+    bool RemoteOk(uint64_t id) const;
+};
+
+struct PortPolicy { uint32_t port = 0; bool tcp = true; std::vector<PortRule> rules; bool has_http = false; };
+
+struct NetworkPolicy {
+    std::string name;
+    uint64_t id = 0;
+    std::vector<PortPolicy> ingress, egress;
+    // exact-port entry then port-0 entry (envoy/cilium_network_policy.h:169-192)
+    void Lookup(bool ingress, uint32_t port, const PortPolicy **exact, const PortPolicy **wild) const;
+};
+
+struct PolicySet {
+    std::vector<NetworkPolicy> policies;
+    std::map<std::string, int> by_name;
+    int nrules = 0;  // global rule ids are 0..nrules-1 in document order
+};
+
+bool LoadPolicySet(const char *json, size_t n, PolicySet *out, std::string *err);
+
+}  // namespace l7

@@ -1,0 +1,116 @@
+"""Host-side engine: the Python face of the C-ABI (include/l7gpu.h).
+
+Mirrors the reference's per-request verdict interface for this path:
+policies in (NPDS cilium.NetworkPolicy shape), connections opened with their
+(policy, port, direction, identities) as in proxylib OnNewConnection
+(proxylib/proxylib.go:57-74), then batches of requests classified into
+(verdict, matched rule, consumed bytes).
+"""
+import ctypes as C
+import json
+
+import numpy as np
+
+from . import _lib
+from ._lib import Conn
+
+
+class PolicyError(ValueError):
+    """The policy set was rejected (the reference would NACK it)."""
+
+
+class Engine:
+    def __init__(self, device=0):
+        self._lib = _lib.load()
+        err = C.create_string_buffer(512)
+        h = self._lib.l7g_engine_create(device, err, 512)
+        if not h:
+            raise RuntimeError("l7g_engine_create: " + err.value.decode(errors="replace"))
+        self._h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.l7g_engine_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---------------------------------------------------------------- policy
+    def update_policy(self, policy):
+        js = policy if isinstance(policy, (str, bytes)) else json.dumps(policy)
+        b = js.encode() if isinstance(js, str) else js
+        err = C.create_string_buffer(1024)
+        if self._lib.l7g_policy_update(self._h, b, len(b), err, 1024) != 0:
+            raise PolicyError(err.value.decode(errors="replace"))
+
+    def policy_index(self, name):
+        b = name.encode()
+        return self._lib.l7g_policy_index(self._h, b, len(b))
+
+    @property
+    def nrules(self):
+        return self._lib.l7g_policy_nrules(self._h)
+
+    # ----------------------------------------------------------- connections
+    def set_connections(self, conns):
+        """conns: sequence of dicts/tuples (policy, port, ingress, proto, src_id, dst_id)
+        or a numpy structured array with those fields."""
+        arr = conns_array(conns)
+        err = C.create_string_buffer(1024)
+        if self._lib.l7g_conns_set(self._h, arr.ctypes.data, len(arr), err, 1024) != 0:
+            raise PolicyError(err.value.decode(errors="replace"))
+        self._conns = arr
+
+    # --------------------------------------------------------- classification
+    def classify_device(self, arena_ptr, off_ptr, len_ptr, conn_ptr, n, verdict_ptr, rule_ptr,
+                        consumed_ptr, counters_ptr=0, stream=0):
+        """All pointers are device addresses (e.g. torch tensor .data_ptr())."""
+        rc = self._lib.l7g_classify(self._h, arena_ptr, off_ptr, len_ptr, conn_ptr, n, verdict_ptr,
+                                    rule_ptr, consumed_ptr, counters_ptr or None, stream or None)
+        if rc != 0:
+            raise RuntimeError(f"l7g_classify failed: HIP error {rc}")
+
+    def classify(self, arena, offsets, lengths, conn_ids):
+        """Host-buffer convenience: copies to the device, classifies, copies back."""
+        arena = np.ascontiguousarray(arena, dtype=np.uint8)
+        off = np.ascontiguousarray(offsets, dtype=np.uint64)
+        ln = np.ascontiguousarray(lengths, dtype=np.uint32)
+        cid = np.ascontiguousarray(conn_ids, dtype=np.uint32)
+        n = len(off)
+        v = np.zeros(n, np.uint8)
+        r = np.zeros(n, np.int32)
+        c = np.zeros(n, np.uint32)
+        rc = self._lib.l7g_classify_host(self._h, arena.ctypes.data, arena.nbytes, off.ctypes.data,
+                                         ln.ctypes.data, cid.ctypes.data, n, v.ctypes.data,
+                                         r.ctypes.data, c.ctypes.data)
+        if rc != 0:
+            raise RuntimeError(f"l7g_classify_host failed: HIP error {rc}")
+        return v, r, c
+
+    def stats(self):
+        s = _lib.Stats()
+        self._lib.l7g_stats(self._h, C.byref(s))
+        return {k: getattr(s, k) for k, _ in s._fields_}
+
+
+CONN_DTYPE = np.dtype([("policy", "<i4"), ("port", "<u4"), ("ingress", "u1"), ("proto", "u1"),
+                       ("_pad", "<u2"), ("src_id", "<u4"), ("dst_id", "<u4")])
+assert CONN_DTYPE.itemsize == C.sizeof(Conn)
+
+
+def conns_array(conns):
+    if isinstance(conns, np.ndarray) and conns.dtype == CONN_DTYPE:
+        return np.ascontiguousarray(conns)
+    arr = np.zeros(len(conns), CONN_DTYPE)
+    for i, c in enumerate(conns):
+        if isinstance(c, dict):
+            for k in ("policy", "port", "ingress", "proto", "src_id", "dst_id"):
+                arr[i][k] = c.get(k, 0)
+        else:
+            arr[i] = (c[0], c[1], c[2], c[3], 0, c[4], c[5])
+    return arr

@@ -1,0 +1,395 @@
+"""Deterministic synthetic workloads.
+
+Every generator returns a Workload: one packed payload arena, per-request
+(offset, length, connection) arrays, the connection table and the policy set
+(cilium.NetworkPolicy JSON).  Seeds are 0x1C1D0000 + config number.
+
+cfg1  1 rule  {Method:"GET", Path:"/public/.*"}                  (HTTP)
+cfg2  64 HTTP rules over Method/Path/Host + literal X-Token header  (HTTP, bench)
+cfg3  Kafka produce/fetch/metadata stream, ~1k PortRuleKafka rules  (Kafka)
+cfg4  10k HTTP rules across 512 identities                          (HTTP)
+"""
+import struct
+import zlib
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import api
+from ._lib import PROTO_HTTP, PROTO_KAFKA
+from .engine import CONN_DTYPE
+
+SEED_BASE = 0x1C1D0000
+
+
+@dataclass
+class Workload:
+    name: str
+    arena: np.ndarray            # uint8
+    offsets: np.ndarray          # uint64
+    lengths: np.ndarray          # uint32
+    conn_ids: np.ndarray         # uint32
+    conns: np.ndarray            # CONN_DTYPE
+    policy: dict                 # policy set JSON (dict)
+    meta: dict = field(default_factory=dict)
+
+    @property
+    def n(self):
+        return len(self.offsets)
+
+    def subset(self, idx):
+        idx = np.asarray(idx)
+        return Workload(self.name + "[sub]", self.arena, self.offsets[idx], self.lengths[idx],
+                        self.conn_ids[idx], self.conns, self.policy, self.meta)
+
+    def algorithmic_bytes(self):
+        """B_i = len_i + 16 (offset u64 + len u32 + meta u32) + 9 (verdict u8 + rule i32 + consumed u32)."""
+        return int(self.lengths.astype(np.int64).sum()) + 25 * self.n
+
+
+def pack(reqs):
+    lens = np.fromiter((len(r) for r in reqs), dtype=np.uint32, count=len(reqs))
+    offs = np.zeros(len(reqs), dtype=np.uint64)
+    if len(reqs) > 1:
+        offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    arena = np.frombuffer(b"".join(reqs), dtype=np.uint8).copy()
+    return arena, offs, lens
+
+
+def make_conns(n, policy, port, ingress, proto, src_ids, dst_id=7):
+    c = np.zeros(n, CONN_DTYPE)
+    c["policy"] = policy
+    c["port"] = port
+    c["ingress"] = 1 if ingress else 0
+    c["proto"] = proto
+    c["src_id"] = src_ids
+    c["dst_id"] = dst_id
+    return c
+
+
+# ------------------------------------------------------------------ HTTP
+_ALNUM = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz0123456789", dtype=np.uint8)
+_PATHCH = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz0123456789/_-", dtype=np.uint8)
+_LOWER = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz", dtype=np.uint8)
+_PAD = bytes((b"abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789" * 40)[:2100])
+_METHODS = [b"GET", b"POST", b"PUT", b"DELETE", b"PATCH"]
+
+
+def _rand_str(rng, alphabet, lo, hi, n):
+    lens = rng.integers(lo, hi + 1, size=n)
+    buf = alphabet[rng.integers(0, len(alphabet), size=int(lens.sum()))].tobytes()
+    out, p = [], 0
+    for L in lens:
+        out.append(buf[p:p + L])
+        p += L
+    return out
+
+
+def http_requests(n, seed, with_token=True):
+    """The §8(d) HTTP template; total length uniform in [256, 2048]."""
+    rng = np.random.default_rng(seed)
+    meth = rng.choice(5, p=[0.6, 0.2, 0.1, 0.05, 0.05], size=n)
+    kind = rng.choice(3, p=[0.5, 0.3, 0.2], size=n)
+    words = _rand_str(rng, _LOWER, 3, 8, n)
+    nums = rng.integers(0, 100, size=n)
+    tails = _rand_str(rng, _PATHCH, 0, 40, n)
+    svc = rng.integers(0, 64, size=n)
+    ver = rng.integers(1, 4, size=n)
+    host = rng.integers(0, 64, size=n)
+    tok_kind = rng.choice(4, p=[0.5, 0.25, 0.24, 0.01], size=n)  # digits / alnum / absent / literal
+    tok_digits = _rand_str(rng, np.frombuffer(b"0123456789", np.uint8), 8, 16, n)
+    tok_alnum = _rand_str(rng, _ALNUM, 8, 16, n)
+    total = rng.integers(256, 2049, size=n)
+    padoff = rng.integers(0, 40, size=n)
+    reqs = []
+    for i in range(n):
+        k = kind[i]
+        if k == 0:
+            path = b"/public/%s/%d/%s" % (words[i], nums[i], tails[i])
+        elif k == 1:
+            path = b"/private/" + tails[i]
+        else:
+            path = b"/api/v%d/svc%d/%s" % (ver[i], svc[i], tails[i])
+        head = b"%s %s HTTP/1.1\r\nHost: svc-%d.ns.svc.cluster.local\r\nUser-Agent: l7bench/1\r\nAccept: */*\r\n" % (
+            _METHODS[meth[i]], path, host[i])
+        if with_token:
+            t = tok_kind[i]
+            if t == 0:
+                head += b"X-Token: " + tok_digits[i] + b"\r\n"
+            elif t == 1:
+                head += b"X-Token: " + tok_alnum[i] + b"\r\n"
+            elif t == 3:
+                head += b"X-Token: [0-9]+\r\n"
+        padlen = max(0, int(total[i]) - len(head) - 11)
+        reqs.append(head + b"X-Pad: " + _PAD[padoff[i]:padoff[i] + padlen] + b"\r\n\r\n")
+    return reqs
+
+
+def cfg1_policy():
+    rules = api.http_rules_from_api([api.PortRuleHTTP(method="GET", path="/public/.*")])
+    return api.policy_set(api.network_policy("10.0.0.1", 3, ingress=[(80, [api.port_rule(http=rules)])]))
+
+
+def cfg2_rules(k0=0, count=64):
+    out = []
+    for k in range(k0, k0 + count):
+        method = ["GET", "POST", "PUT|PATCH", "(GET|HEAD)"][k % 4]
+        path = f"/api/v{k % 3 + 1}/svc{k % 64}/.*" if k % 2 == 0 else f"/public/[a-z]+/{k % 100}/.*"
+        host = f"svc-{k % 64}\\..*"
+        headers = ["X-Token: [0-9]+"] if k % 4 == 3 else []
+        out.append(api.PortRuleHTTP(method=method, path=path, host=host, headers=headers))
+    return out
+
+
+def cfg2_policy():
+    rules = api.http_rules_from_api(cfg2_rules())
+    return api.policy_set(api.network_policy("10.0.0.1", 3, ingress=[(80, [api.port_rule(http=rules)])]))
+
+
+def http_workload(cfg, n, nconns=1024, seed=None):
+    seed = SEED_BASE + cfg if seed is None else seed
+    reqs = http_requests(n, seed, with_token=(cfg != 1))
+    arena, offs, lens = pack(reqs)
+    rng = np.random.default_rng(seed + 1)
+    conn_ids = rng.integers(0, nconns, size=n).astype(np.uint32)
+    conns = make_conns(nconns, 0, 80, True, PROTO_HTTP, 1000 + np.arange(nconns))
+    pol = cfg1_policy() if cfg == 1 else cfg2_policy()
+    return Workload(f"cfg{cfg}", arena, offs, lens, conn_ids, conns, pol)
+
+
+def cfg4_workload(n, nids=512, rules_total=10000, seed=None, unknown_frac=0.02):
+    """10k HTTP rules across 512 identities (ids 256..767), ~20 rules each as
+    separate PortNetworkPolicyRule groups; requests from connections whose
+    source identity is uniform over the 512 (+2% unknown => deny)."""
+    seed = SEED_BASE + 4 if seed is None else seed
+    rng = np.random.default_rng(seed)
+    per = rules_total // nids
+    groups = []
+    for g in range(nids):
+        ks = rng.integers(0, 4096, size=per)
+        rules = [cfg2_rules(int(k), 1)[0] for k in ks]
+        groups.append(api.port_rule(remote_policies=[256 + g], http=api.http_rules_from_api(rules)))
+    pol = api.policy_set(api.network_policy("10.0.0.1", 3, ingress=[(80, groups)]))
+    reqs = http_requests(n, seed + 7)
+    arena, offs, lens = pack(reqs)
+    nconns = nids * 4 + 64
+    ids = np.concatenate([256 + np.repeat(np.arange(nids), 4), 5000 + np.arange(64)])
+    conns = make_conns(nconns, 0, 80, True, PROTO_HTTP, ids)
+    known = rng.random(n) >= unknown_frac
+    conn_ids = np.where(known, rng.integers(0, nids * 4, size=n), nids * 4 + rng.integers(0, 64, size=n))
+    return Workload("cfg4", arena, offs, lens, conn_ids.astype(np.uint32), conns, pol)
+
+
+# ------------------------------------------------------------------ adversarial HTTP
+_SPECIALS = [b" ", b"\r", b"\n", b"\t", b":", b"\x00", b"\x7f", b"\xff", b"\xc3\xa9", b"\r\n", b"\r\n\r\n",
+             b"Content-Length: 5\r\n", b"Transfer-Encoding: chunked\r\n", b"Host: evil\r\n", b" x", b"HTTP/1.1"]
+
+
+def http_adversarial(n, seed):
+    """Valid template requests with random mutations (substitute / insert /
+    delete / truncate / duplicate headers) to exercise framing precedence."""
+    base = http_requests(n, seed)
+    rng = np.random.default_rng(seed + 99)
+    out = []
+    for i, r in enumerate(base):
+        r = bytearray(r[: int(rng.integers(64, 400))] + b"X-Pad: q\r\n\r\n") if rng.random() < 0.5 else bytearray(r)
+        for _ in range(int(rng.integers(0, 4))):
+            op = rng.integers(0, 5)
+            p = int(rng.integers(0, max(1, len(r))))
+            if op == 0:
+                s = _SPECIALS[int(rng.integers(0, len(_SPECIALS)))]
+                r[p:p + len(s)] = s
+            elif op == 1:
+                r[p:p] = _SPECIALS[int(rng.integers(0, len(_SPECIALS)))]
+            elif op == 2:
+                del r[p:p + int(rng.integers(1, 4))]
+            elif op == 3:
+                r = r[:p]
+            else:
+                r = r + b"GET / HTTP/1.1\r\n\r\n"
+        if rng.random() < 0.1 and r.endswith(b"\r\n\r\n"):
+            r = r[:-2] + b"Content-Length: %d\r\n\r\n" % int(rng.integers(0, 20)) + bytes(int(rng.integers(0, 25)))
+        out.append(bytes(r))
+    return out
+
+
+# ------------------------------------------------------------------ Kafka wire encoder
+# Restates the optiopay/kafka proto encoders the reference's decoders expect
+# (vendor/github.com/optiopay/kafka/proto/messages.go: *Req.Bytes).
+
+def k_str(s):
+    if s is None:
+        return struct.pack(">h", -1)
+    b = s.encode() if isinstance(s, str) else s
+    return struct.pack(">h", len(b)) + b
+
+
+def k_bytes(b):
+    if b is None:
+        return struct.pack(">i", -1)
+    return struct.pack(">i", len(b)) + b
+
+
+def k_message(value, key=None, version=0, attributes=0, timestamp=0, bad_crc=False):
+    """One message-set entry: offset i64, size i32, crc u32, magic, attributes,
+    [timestamp i64 when the *API version* >= 1 (readMessageSet quirk)], key, value."""
+    body = struct.pack(">bb", 1 if version >= 1 else 0, attributes)
+    if version >= 1:
+        body += struct.pack(">q", timestamp)
+    body += k_bytes(key) + k_bytes(value)
+    crc = zlib.crc32(body) & 0xFFFFFFFF
+    if bad_crc:
+        crc ^= 0x5A5A5A5A
+    msg = struct.pack(">I", crc) + body
+    return struct.pack(">qi", 0, len(msg)) + msg
+
+
+def k_request(kind, version, corr, client, body):
+    payload = struct.pack(">hhi", kind, version, corr) + k_str(client) + body
+    return struct.pack(">i", len(payload)) + payload
+
+
+def k_produce(version, corr, client, topics, acks=-1, timeout=1000, txn=None):
+    """topics: list of (name, [(partition, [message bytes...]), ...])"""
+    b = b""
+    if version >= 3:
+        b += k_str(txn)
+    b += struct.pack(">hi", acks, timeout) + struct.pack(">i", len(topics))
+    for name, parts in topics:
+        b += k_str(name) + struct.pack(">i", len(parts))
+        for pid, msgs in parts:
+            ms = b"".join(msgs)
+            b += struct.pack(">ii", pid, len(ms)) + ms
+    return k_request(0, version, corr, client, b)
+
+
+def k_fetch(version, corr, client, topics):
+    """topics: list of (name, [partition ids])"""
+    b = struct.pack(">iii", -1, 100, 1)
+    if version >= 3:
+        b += struct.pack(">i", 1 << 20)
+    if version >= 4:
+        b += struct.pack(">b", 0)
+    b += struct.pack(">i", len(topics))
+    for name, parts in topics:
+        b += k_str(name) + struct.pack(">i", len(parts))
+        for pid in parts:
+            b += struct.pack(">iq", pid, 0)
+            if version >= 5:
+                b += struct.pack(">q", 0)
+            b += struct.pack(">i", 1 << 16)
+    return k_request(1, version, corr, client, b)
+
+
+def k_metadata(version, corr, client, topics):
+    b = struct.pack(">i", -1) if topics is None else struct.pack(">i", len(topics)) + b"".join(k_str(t) for t in topics)
+    if version >= 4:
+        b += b"\x01"
+    return k_request(3, version, corr, client, b)
+
+
+def kafka_topics():
+    return [f"topic-{i:04d}" for i in range(1000)]
+
+
+def cfg3_rules():
+    topics = kafka_topics()
+    rules = [api.PortRuleKafka(role="produce", topic=topics[i]) for i in range(500)]
+    rules += [api.PortRuleKafka(api_key="fetch", topic=topics[500 + j], client_id=f"client-{j % 16:02d}")
+              for j in range(500)]
+    rules += [api.PortRuleKafka(api_key="metadata"), api.PortRuleKafka(api_key="apiversions")]
+    return rules
+
+
+def cfg3_policy():
+    return api.policy_set(api.network_policy("10.0.0.1", 3, ingress=[(9092, [api.port_rule(kafka=cfg3_rules())])]))
+
+
+def kafka_requests(n, seed):
+    rng = np.random.default_rng(seed)
+    topics = kafka_topics()
+    kind = rng.choice(3, p=[0.5, 0.4, 0.1], size=n)
+    out = []
+
+    def pick_topic():
+        if rng.random() < 0.9:
+            return topics[int(rng.integers(0, 1000))]
+        return f"other-{int(rng.integers(0, 1000)):04d}"
+
+    for i in range(n):
+        client = f"client-{int(rng.integers(0, 16)):02d}"
+        if kind[i] == 0:
+            v = int(rng.integers(0, 3))
+            tps = []
+            for _ in range(int(rng.integers(1, 4))):
+                msgs = [k_message(bytes(rng.integers(0, 256, size=int(rng.integers(64, 513)), dtype=np.uint8)),
+                                  key=None if rng.random() < 0.5 else b"k%d" % i, version=v)
+                        for _ in range(int(rng.integers(1, 5)))]
+                tps.append((pick_topic(), [(0, msgs)]))
+            out.append(k_produce(v, i, client, tps))
+        elif kind[i] == 1:
+            v = int(rng.integers(0, 6))
+            tps = [(pick_topic(), [int(rng.integers(0, 8))]) for _ in range(int(rng.integers(1, 5)))]
+            out.append(k_fetch(v, i, client, tps))
+        else:
+            sub = int(rng.integers(0, 3))
+            if sub == 0:
+                tl = None if rng.random() < 0.3 else [pick_topic() for _ in range(int(rng.integers(0, 4)))]
+                out.append(k_metadata(int(rng.integers(0, 6)), i, client, tl))
+            elif sub == 1:
+                out.append(k_request(18, 0, i, client, b""))  # ApiVersions
+            else:
+                out.append(k_request(12, 0, i, client, k_str("group") + struct.pack(">i", 1) + k_str("m")))  # Heartbeat
+    return out
+
+
+def kafka_adversarial(n, seed):
+    """Mutated Kafka frames: bad CRCs, truncation, size/array-length edits,
+    compressed sets, unknown kinds, negative string lengths."""
+    rng = np.random.default_rng(seed)
+    base = kafka_requests(n, seed + 5)
+    out = []
+    for r in base:
+        r = bytearray(r)
+        op = int(rng.integers(0, 10))
+        if op == 0 and len(r) > 40:  # flip a byte somewhere in the body
+            p = int(rng.integers(12, len(r)))
+            r[p] ^= int(rng.integers(1, 256))
+        elif op == 1:  # truncate the frame but keep the declared size
+            r = r[: int(rng.integers(0, len(r)))]
+        elif op == 2:  # declared size smaller than the body (trailing bytes ignored / short reads)
+            newsize = int(rng.integers(0, max(1, len(r) - 4)))
+            r[0:4] = struct.pack(">i", newsize)
+        elif op == 3:  # negative or huge sizes
+            r[0:4] = struct.pack(">i", int(rng.choice([-1, 0, 3, 7, 6553500, 6553497])))
+        elif op == 4:  # unknown / odd kinds
+            r[4:6] = struct.pack(">h", int(rng.choice([-1, 7, 19, 33, 64, 1000, 10])))
+        elif op == 5:  # version edits
+            r[6:8] = struct.pack(">h", int(rng.integers(-2, 8)))
+        elif op == 6:  # produce with a corrupt CRC in the middle message / compressed set
+            v = int(rng.integers(0, 3))
+            msgs = [k_message(b"x" * 70, version=v), k_message(b"y" * 70, version=v, bad_crc=True),
+                    k_message(b"z" * 70, version=v)]
+            tps = [("topic-0001", [(0, msgs)]), ("topic-0002", [(0, [k_message(b"w" * 80, version=v)])])]
+            if rng.random() < 0.3:
+                tps = [("topic-0003", [(0, [k_message(b"c" * 90, version=v, attributes=int(rng.integers(1, 4)))])])]
+            r = bytearray(k_produce(v, 7, "client-01", tps))
+        elif op == 7:  # negative array length
+            p = 14 + int.from_bytes(r[12:14], "big", signed=True) if len(r) > 14 else 12
+            if 0 < p < len(r) - 4:
+                r[p:p + 4] = struct.pack(">i", -int(rng.integers(1, 3)))
+        elif op == 8:  # negative string length for the client id
+            if len(r) > 14:
+                r[12:14] = struct.pack(">h", -int(rng.integers(1, 5)))
+        out.append(bytes(r))
+    return out
+
+
+def kafka_workload(n, nconns=256, seed=None, adversarial=False):
+    seed = SEED_BASE + 3 if seed is None else seed
+    reqs = kafka_adversarial(n, seed) if adversarial else kafka_requests(n, seed)
+    arena, offs, lens = pack(reqs)
+    rng = np.random.default_rng(seed + 1)
+    conn_ids = rng.integers(0, nconns, size=n).astype(np.uint32)
+    conns = make_conns(nconns, 0, 9092, True, PROTO_KAFKA, 2000 + np.arange(nconns))
+    return Workload("cfg3", arena, offs, lens, conn_ids, conns, cfg3_policy())

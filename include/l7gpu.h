@@ -1,0 +1,104 @@
+/*
+ * l7gpu.h — C-ABI of the MI355X-native batched L7 policy classifier.
+ *
+ * This is the drop-in boundary for the reference's L7 verdict path.  Every
+ * entry point is plain C (pointers + sizes, no C++/torch types) so a Go cgo
+ * package, Envoy's dlopen loader, or ctypes can bind it.  What each entry
+ * replaces in the reference (file:line):
+ *
+ *   l7g_policy_update   proxylib Instance.PolicyUpdate            proxylib/proxylib/instance.go:168-219
+ *                       Envoy NetworkPolicyMap::onConfigUpdate     envoy/cilium_network_policy.h:240-250
+ *                       (policies in the cilium.NetworkPolicy shape, envoy/cilium/npds.proto:31-182,
+ *                        as JSON; see DESIGN.md §Policy JSON)
+ *   l7g_policy_index    NetworkPolicyMap::GetPolicyInstance        envoy/cilium_network_policy.h:213-221
+ *   l7g_conns_set       proxylib OnNewConnection / Close           proxylib/proxylib.go:57-74,112-116
+ *                       Cilium::SocketOption (identity, port, dir) envoy/cilium_l7policy.cc:133-150
+ *   l7g_classify        per request: AccessFilter::decodeHeaders -> NetworkPolicyMap::Allowed
+ *                                                                  envoy/cilium_l7policy.cc:127-182,
+ *                                                                  envoy/cilium_network_policy.h:223-237
+ *                       kafka.ReadRequest + canAccess/MatchesRule  pkg/kafka/request.go:186-229,
+ *                                                                  pkg/proxy/kafka.go:117-153,
+ *                                                                  pkg/kafka/policy.go:200-225
+ *   l7g_counters        Endpoint.UpdateProxyStatistics counters    pkg/endpoint/endpoint.go:2207-2233
+ *
+ * Verdict codes match the oracle (oracle/l7ref.h) and DESIGN.md.
+ */
+#ifndef L7GPU_H
+#define L7GPU_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct l7g_engine l7g_engine;
+
+enum { L7G_PROTO_HTTP = 1, L7G_PROTO_KAFKA = 2, L7G_PROTO_MEMCACHE = 3 };
+enum {
+    L7G_DENY = 0,        /* policy denies (HTTP 403 / Kafka ErrTopicAuthorizationFailed) */
+    L7G_ALLOW = 1,       /* policy allows; rule = matched global rule id or -1 */
+    L7G_PARSE_ERROR = 2, /* malformed request (connection is closed by the caller) */
+    L7G_INCOMPLETE = 3,  /* more bytes are needed (proxylib MORE) */
+    L7G_UNSUPPORTED = 4, /* framing not handled on the device (chunked body, compressed Kafka set) */
+};
+
+/* Connection attributes (20 bytes; identical layout to the oracle's ref_conn_t). */
+typedef struct {
+    int32_t policy;   /* l7g_policy_index(name), -1 = no policy for this endpoint (deny) */
+    uint32_t port;    /* destination port */
+    uint8_t ingress;  /* 1 = ingress */
+    uint8_t proto;    /* L7G_PROTO_* */
+    uint16_t _pad;
+    uint32_t src_id;  /* source security identity */
+    uint32_t dst_id;  /* destination security identity */
+} l7g_conn_t;
+
+typedef struct {
+    uint32_t policies, rules, http_rulesets, http_chunks, http_dfas, http_dfa_states;
+    uint32_t kafka_rulesets, kafka_rules, kafka_topics;
+    uint64_t table_bytes;
+} l7g_stats_t;
+
+/* Engine bound to one HIP device.  err receives a message on failure. */
+l7g_engine *l7g_engine_create(int device, char *err, size_t errlen);
+void l7g_engine_destroy(l7g_engine *e);
+
+/* Atomically replaces the policy set (0 = ok).  On error the previous policy
+ * set stays in force (like an NPDS NACK).  Existing connections are re-resolved. */
+int l7g_policy_update(l7g_engine *e, const char *json, size_t len, char *err, size_t errlen);
+int32_t l7g_policy_index(l7g_engine *e, const char *name, size_t len);
+int32_t l7g_policy_nrules(l7g_engine *e);
+
+/* Replaces the connection table (connection i = conns[i]); compiles the rule
+ * sets the connections need.  0 = ok. */
+int l7g_conns_set(l7g_engine *e, const l7g_conn_t *conns, uint32_t n, char *err, size_t errlen);
+
+/* Classifies n requests resident in device memory: request i is
+ * arena[off[i] .. off[i]+len[i]) on connection conn[i].  Writes verdict[i],
+ * rule[i] (global rule id, -1 = none) and consumed[i] (bytes of the first
+ * complete request; 0 unless ALLOW/DENY).  Asynchronous on `stream`
+ * (a hipStream_t, NULL = default stream).  counters may be NULL, else a
+ * device array of (rules + 8) uint64 that accumulates per-rule allow hits
+ * followed by per-verdict totals.  Returns 0 or a HIP error code. */
+int l7g_classify(l7g_engine *e, const uint8_t *arena, const uint64_t *off, const uint32_t *len,
+                 const uint32_t *conn, uint32_t n, uint8_t *verdict, int32_t *rule, uint32_t *consumed,
+                 uint64_t *counters, void *stream);
+
+/* Same with host buffers: copies in, classifies, copies out, synchronises. */
+int l7g_classify_host(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const uint64_t *off,
+                      const uint32_t *len, const uint32_t *conn, uint32_t n, uint8_t *verdict, int32_t *rule,
+                      uint32_t *consumed);
+
+int l7g_stats(l7g_engine *e, l7g_stats_t *out);
+
+/* Test hook: compile one Go regexp with the product's DFA compiler and run
+ * the compiled tables on the host.  Returns 1 match, 0 no match, -1 compile
+ * error (err set).  anchored: 1 = full match, 0 = Go regexp.Match. */
+int l7g_debug_regex(const char *pat, size_t patlen, int anchored, const uint8_t *s, size_t slen, char *err,
+                    size_t errlen);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,70 @@
+/* ref_internal.h — TEST INFRASTRUCTURE ONLY (parity oracle internals). */
+#ifndef REF_INTERNAL_H
+#define REF_INTERNAL_H
+#include <stddef.h>
+#include <stdint.h>
+#include "l7ref.h"
+
+/* ---------------- minimal JSON ---------------- */
+enum { JN_NULL, JN_BOOL, JN_NUM, JN_STR, JN_ARR, JN_OBJ };
+typedef struct jnode {
+    int type;
+    double num; int64_t inum; int is_int;
+    char *str; size_t slen;        /* JN_STR (UTF-8, NUL-terminated) */
+    struct jnode **items; char **keys; size_t *keylens; int n, cap; /* ARR/OBJ */
+    int b;
+} jnode;
+jnode *jparse(const char *s, size_t n, char *err, size_t errlen);
+void jfree(jnode *j);
+jnode *jget(const jnode *obj, const char *key);
+
+/* ---------------- policy model (NPDS NetworkPolicy, envoy/cilium/npds.proto) ---- */
+enum { HM_EXACT, HM_REGEX, HM_PRESENT, HM_PREFIX, HM_SUFFIX, HM_RANGE };
+typedef struct {
+    char *name; size_t namelen;   /* lower-cased (Envoy LowerCaseString) */
+    int type;
+    char *value; size_t vlen;
+    ref_re *re;
+    int invert;
+    int64_t rstart, rend;
+} ref_hmatch;
+
+typedef struct { ref_hmatch *m; int n; int id; } ref_http_rule;
+
+typedef struct {
+    uint64_t keymask;       /* api keys 0..63 allowed; 0 = any (apiKeyInt empty) */
+    int any_key;
+    int has_version; int16_t version;
+    char *topic; size_t topiclen;
+    char *client; size_t clientlen;
+    int id;
+} ref_kafka_rule;
+
+typedef struct {
+    char *command; char *key_exact; char *key_prefix; ref_re *key_re;
+    int empty; int id;
+} ref_mc_rule;
+
+enum { L7T_NONE = 0, L7T_HTTP, L7T_KAFKA, L7T_L7 };
+typedef struct {
+    uint64_t *remotes; int nremotes;
+    int l7type;
+    ref_http_rule *http; int nhttp;
+    ref_kafka_rule *kafka; int nkafka;
+    char *l7proto;
+    ref_mc_rule *l7; int nl7;
+} ref_pnp_rule;
+
+typedef struct { uint32_t port; int tcp; ref_pnp_rule *rules; int nrules; int has_http; } ref_port;
+typedef struct { char *name; uint64_t id; ref_port *in; int nin; ref_port *eg; int neg; } ref_netpolicy;
+struct ref_policy { ref_netpolicy *p; int np; int nrules_total; };
+
+/* ---------------- per-protocol verdict functions ---------------- */
+typedef struct { uint8_t verdict; int32_t rule; uint32_t consumed; } ref_out_t;
+void ref_http_verdict(const ref_policy *pol, const ref_conn_t *c, const uint8_t *buf, uint32_t len, ref_out_t *o);
+void ref_kafka_verdict(const ref_policy *pol, const ref_conn_t *c, const uint8_t *buf, uint32_t len, ref_out_t *o);
+
+int ref_port_lookup(const ref_netpolicy *np, int ingress, uint32_t port, const ref_port **exact, const ref_port **wild);
+int ref_remote_ok(const ref_pnp_rule *r, uint64_t id);
+
+#endif

@@ -1,0 +1,177 @@
+#!/usr/bin/env python3
+"""Writes tests/golden/reference_kats.json: the known-answer tests the
+reference's own test-suite asserts for this path, transcribed as data
+(inputs + the reference's expected outcomes; no reference code).
+
+Sources (file:line in the reference):
+  regex      pkg/policy/api/rule_validation_test.go:155-205  (Path/Method "*" rejected)
+             proxylib/proxylib_memcached_test.go:626-640     (keyRegex ^.el.o$ on key Hello)
+             proxylib/r2d2/r2d2parser_test.go:150-178         (file s.* : ssss PASS, yyyyy DROP)
+  http       envoy/cilium_integration_test.cc:165-199 (BASIC_POLICY), :738-856 (verdicts),
+             :224-234 (SocketOption: ingress remote 1, egress dst identity 1 via host map)
+  http_xlate pkg/envoy/server_test.go:38-96 (getHTTPRule expected HeaderMatchers)
+  kafka      pkg/kafka/policy_test.go:52-127 (MatchesRule assertions)
+             pkg/proxy/kafka_test.go:167-258 (produce allowedTopic ok / disallowedTopic denied)
+Kafka requests are encoded to wire bytes with cilium_amd.gen's restatement of
+the optiopay encoders (valid CRCs), exactly what the reference decoder reads.
+"""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", ".."))
+from cilium_amd import gen  # noqa: E402
+
+OUT = os.path.join(os.path.dirname(__file__), "reference_kats.json")
+
+BASIC_POLICY = {
+    "name": "173", "policy": 3,
+    "ingress_per_port_policies": [{"port": 80, "rules": [
+        {"remote_policies": [1], "http_rules": {"http_rules": [
+            {"headers": [{"name": ":path", "exact_match": "/allowed"}]},
+            {"headers": [{"name": ":path", "regex_match": ".*public$"}]},
+            {"headers": [{"name": ":authority", "exact_match": "allowedHOST"}]},
+            {"headers": [{"name": ":authority", "regex_match": ".*REGEX.*"}]},
+            {"headers": [{"name": ":method", "exact_match": "PUT"}, {"name": ":path", "exact_match": "/public/opinions"}]},
+        ]}},
+        {"remote_policies": [2], "http_rules": {"http_rules": [
+            {"headers": [{"name": ":path", "exact_match": "/only-2-allowed"}]}]}},
+    ]}],
+}
+BASIC_POLICY["egress_per_port_policies"] = json.loads(json.dumps(BASIC_POLICY["ingress_per_port_policies"]))
+
+HTTP_CASES = [  # (test name, method, path, authority, extra headers, expected)
+    ("DeniedPathPrefix", "GET", "/prefix", "host", [], "DENY"),
+    ("AllowedPathPrefix", "GET", "/allowed", "host", [], "ALLOW"),
+    ("AllowedPathPrefixStrippedHeader", "GET", "/allowed", "host", [("x-envoy-original-dst-host", "1.1.1.1:9999")], "ALLOW"),
+    ("AllowedPathRegex", "GET", "/maybe/public", "host", [], "ALLOW"),
+    ("DeniedPath", "GET", "/maybe/private", "host", [], "DENY"),
+    ("AllowedHostString", "GET", "/maybe/private", "allowedHOST", [], "ALLOW"),
+    ("AllowedHostRegex", "GET", "/maybe/private", "hostREGEXname", [], "ALLOW"),
+    ("DeniedMethod", "POST", "/maybe/private", "host", [], "DENY"),
+    ("AcceptedMethod", "PUT", "/public/opinions", "host", [], "ALLOW"),
+    ("L3DeniedPath", "GET", "/only-2-allowed", "host", [], "DENY"),
+]
+EGRESS_SKIP = {"AllowedPathPrefixStrippedHeader"}  # CiliumIntegrationEgressTest has 9 cases
+
+
+def http_section():
+    cases = []
+    for ingress in (True, False):
+        for name, m, p, a, extra, exp in HTTP_CASES:
+            if not ingress and name in EGRESS_SKIP:
+                continue
+            req = f"{m} {p} HTTP/1.1\r\nHost: {a}\r\n" + "".join(f"{k}: {v}\r\n" for k, v in extra) + "\r\n"
+            cases.append({
+                "name": ("Ingress" if ingress else "Egress") + name,
+                "request": req,
+                # ingress: SocketOption(maps_, 1, 173, true, 80, ..): identity 1 is the source
+                # egress:  SocketOption(maps_, 173, 1 (host map 127.0.0.0/8 -> 1), false, 80, ..)
+                "conn": {"policy_name": "173", "port": 80, "ingress": ingress,
+                         "src_id": 1 if ingress else 173, "dst_id": 173 if ingress else 1},
+                "expect": exp,
+            })
+    dup = json.loads(json.dumps(BASIC_POLICY))
+    dup["ingress_per_port_policies"].append(
+        {"port": 80, "rules": [{"remote_policies": [2], "http_rules": {"http_rules": [
+            {"headers": [{"name": ":path", "value": "/only-2-allowed", "regex": False}]}]}}]})
+    return {
+        "ref": "envoy/cilium_integration_test.cc:165-199,738-856",
+        "policy": {"policies": [BASIC_POLICY]},
+        "cases": cases,
+        "duplicate_port": {"ref": "envoy/cilium_integration_test.cc:779-797", "policy": {"policies": [dup]},
+                           "request": "GET /allowed HTTP/1.1\r\nHost: host\r\n\r\n", "expect": "DENY"},
+    }
+
+
+def regex_section():
+    return [
+        {"pattern": "*", "compile_error": True, "ref": "pkg/policy/api/rule_validation_test.go:155-178 (Path)"},
+        {"pattern": "*", "compile_error": True, "ref": "pkg/policy/api/rule_validation_test.go:180-204 (Method)"},
+        {"pattern": "GET", "compile_error": False, "ref": "pkg/policy/api/rule_validation_test.go:180-204"},
+        {"pattern": "/", "compile_error": False, "ref": "pkg/policy/api/rule_validation_test.go:180-204"},
+        {"pattern": "^.el.o$", "input": "Hello", "anchored": False, "match": True,
+         "ref": "proxylib/proxylib_memcached_test.go:626-640"},
+        {"pattern": "s.*", "input": "ssss", "anchored": False, "match": True, "ref": "proxylib/r2d2/r2d2parser_test.go:150-178"},
+        {"pattern": "s.*", "input": "yyyyy", "anchored": False, "match": False, "ref": "proxylib/r2d2/r2d2parser_test.go:150-178"},
+        {"pattern": ".*public$", "input": "/maybe/public", "anchored": True, "match": True,
+         "ref": "envoy/cilium_integration_test.cc:176,767-769"},
+        {"pattern": ".*public$", "input": "/maybe/private", "anchored": True, "match": False,
+         "ref": "envoy/cilium_integration_test.cc:176,771-773"},
+        {"pattern": ".*REGEX.*", "input": "hostREGEXname", "anchored": True, "match": True,
+         "ref": "envoy/cilium_integration_test.cc:178,779-781"},
+    ]
+
+
+def xlate_section():
+    return {
+        "ref": "pkg/envoy/server_test.go:38-96",
+        "cases": [
+            {"rule": {"path": "/foo", "method": "GET", "host": "foo.cilium.io", "headers": ["header2 value", "header1"]},
+             "expected": [
+                 {"name": ":authority", "regex_match": "foo.cilium.io"},
+                 {"name": ":method", "regex_match": "GET"},
+                 {"name": ":path", "regex_match": "/foo"},
+                 {"name": "header1", "present_match": True},
+                 {"name": "header2", "exact_match": "value"}]},
+            {"rule": {"path": "/bar", "method": "PUT"},
+             "expected": [{"name": ":method", "regex_match": "PUT"}, {"name": ":path", "regex_match": "/bar"}]},
+            {"rule": {"path": "/bar", "method": "GET"},
+             "expected": [{"name": ":method", "regex_match": "GET"}, {"name": ":path", "regex_match": "/bar"}]},
+        ],
+    }
+
+
+LOREM = ("Lorem ipsum dolor sit amet, consectetur adipiscing elit. Donec a diam lectus. Sed sit amet ipsum mauris. "
+         "Maecenas congue ligula ac quam viverra nec consectetur ante hendrerit. Donec et mollis dolor. Praesent et "
+         "diam eget libero egestas mattis sit amet vitae augue. Nam tincidunt congue enim, ut porta lorem lacinia "
+         "consectetur.").encode()
+
+
+def kafka_section():
+    msgs = [gen.k_message(LOREM, version=0) for _ in range(100)]
+    produce = gen.k_produce(0, 241, "test", [("foo", [(0, msgs)]), ("bar", [(0, msgs)])], acks=-1, timeout=1000)
+    T = lambda t: {"topic": t}  # noqa: E731
+    policy_cases = [  # pkg/kafka/policy_test.go:85-108
+        ([], False), ([{}], True), ([T("foo")], False), ([T("foo"), T("bar")], True),
+        ([T("foo"), T("baz")], False), ([T("baz"), T("foo2")], False), ([T("bar"), T("foo")], True),
+        ([T("bar"), T("foo"), T("baz")], True),
+    ]
+    reqs = {"produce_foo_bar": produce.hex()}
+    cases = [{"request": "produce_foo_bar", "rules": r, "expect": "ALLOW" if e else "DENY",
+              "ref": "pkg/kafka/policy_test.go:85-108"} for r, e in policy_cases]
+    reqs["apiversions"] = gen.k_request(18, 0, 1, "test", b"").hex()
+    r12 = [{"apiKey": "metadata"}, {"apiKey": "apiversions"}]
+    cases.append({"request": "apiversions", "rules": [], "expect": "DENY", "ref": "pkg/kafka/policy_test.go:113-114"})
+    cases.append({"request": "apiversions", "rules": r12, "expect": "ALLOW", "ref": "pkg/kafka/policy_test.go:117-122"})
+    reqs["kind19"] = gen.k_request(19, 0, 1, "test", b"").hex()
+    cases.append({"request": "kind19", "rules": r12, "expect": "DENY", "ref": "pkg/kafka/policy_test.go:124-126"})
+    proxy_rules = [{"apiKey": "metadata", "apiVersion": "0"}, {"apiKey": "produce", "apiVersion": "0", "topic": "allowedTopic"}]
+    two = [gen.k_message(b"first"), gen.k_message(b"second")]
+    for name, req, exp in (
+        ("metadata all topics", gen.k_metadata(0, 1, "tester", []), "ALLOW"),
+        ("metadata allowedTopic", gen.k_metadata(0, 2, "tester", ["allowedTopic"]), "ALLOW"),
+        ("produce allowedTopic", gen.k_produce(0, 3, "tester", [("allowedTopic", [(0, two)])]), "ALLOW"),
+        ("produce disallowedTopic", gen.k_produce(0, 4, "tester", [("disallowedTopic", [(0, two)])]), "DENY"),
+    ):
+        reqs[name] = req.hex()
+        cases.append({"name": name, "request": name, "rules": proxy_rules, "expect": exp, "src_id": 200,
+                      "ref": "pkg/proxy/kafka_test.go:184-258"})
+    return {"requests": reqs, "cases": cases}
+
+
+def main():
+    data = {
+        "note": "Known-answer tests transcribed from the reference's own tests; 'expect' is the reference's asserted outcome.",
+        "regex": regex_section(),
+        "http": http_section(),
+        "http_translation": xlate_section(),
+        "kafka": kafka_section(),
+    }
+    with open(OUT, "w") as f:
+        json.dump(data, f, indent=1, sort_keys=True)
+    print(OUT, os.path.getsize(OUT), "bytes")
+
+
+if __name__ == "__main__":
+    main()
