@@ -150,6 +150,14 @@ hipError_t Upload(l7g_engine *e) {
 extern "C" {
 
 l7g_engine *l7g_engine_create(int device, char *err, size_t errlen) {
+    if (device == L7G_HOST_ONLY) {  // rule compiler only: no HIP calls, classify unavailable
+        auto *e = new l7g_engine();
+        e->device = -1;
+        e->ps = std::make_unique<PolicySet>();
+        e->hc = std::make_unique<HttpCompiler>(e->ps.get());
+        e->kc = std::make_unique<KafkaCompiler>(e->ps.get());
+        return e;
+    }
     int ndev = 0;
     hipError_t rc = hipGetDeviceCount(&ndev);
     if (rc != hipSuccess || device < 0 || device >= ndev) {
@@ -167,6 +175,7 @@ l7g_engine *l7g_engine_create(int device, char *err, size_t errlen) {
 
 void l7g_engine_destroy(l7g_engine *e) {
     if (!e) return;
+    if (e->device < 0) { delete e; return; }
     hipSetDevice(e->device);
     hipDeviceSynchronize();
     if (e->d_blob) hipFree(e->d_blob);
@@ -218,6 +227,7 @@ int l7g_conns_set(l7g_engine *e, const l7g_conn_t *conns, uint32_t n, char *err,
 int l7g_classify(l7g_engine *e, const uint8_t *arena, const uint64_t *off, const uint32_t *len, const uint32_t *conn,
                  uint32_t n, uint8_t *verdict, int32_t *rule, uint32_t *consumed, uint64_t *counters, void *stream) {
     std::lock_guard<std::mutex> g(e->mu);
+    if (e->device < 0) return (int)hipErrorNoDevice;
     hipError_t rc = hipSetDevice(e->device);
     if (rc == hipSuccess) rc = Upload(e);
     if (rc != hipSuccess) return (int)rc;
@@ -236,6 +246,7 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, const uint64_t *off, const
 
 int l7g_classify_host(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const uint64_t *off, const uint32_t *len,
                       const uint32_t *conn, uint32_t n, uint8_t *verdict, int32_t *rule, uint32_t *consumed) {
+    if (e->device < 0) return (int)hipErrorNoDevice;
     hipError_t rc = hipSetDevice(e->device);
     if (rc != hipSuccess) return (int)rc;
     uint8_t *d_a = nullptr, *d_v = nullptr;

@@ -131,7 +131,7 @@ __global__ __launch_bounds__(kBlock) void http_classify_kernel(
         uint32_t hash = kFnvBasis;
         int hk = HK_NONE, hslot = 0;
         bool have_cl = false, have_te = false, cl_bad = false, cl_ws = false;
-        uint64_t cl = 0;
+        uint64_t cl = 0, clv = 0;  // committed Content-Length / value of the current line
         uint32_t ndig = 0, hdr_end = 0;
         uint32_t pos = 0;
         const uintptr_t base = (uintptr_t)req;
@@ -196,7 +196,7 @@ __global__ __launch_bounds__(kBlock) void http_classify_kernel(
                                 }
                             }
                         }
-                        st = ST_OWS; cl = 0; ndig = 0; cl_bad = false; cl_ws = false;
+                        st = ST_OWS; clv = 0; ndig = 0; cl_bad = false; cl_ws = false;
                         break;
                     }
                     if (!is_tchar(c)) { st = ST_ERR; break; }
@@ -212,7 +212,7 @@ __global__ __launch_bounds__(kBlock) void http_classify_kernel(
                     if (c != ' ' && c != '\t') {
                         vend = pos + 1;
                         if (hk == HK_CL) {
-                            if (c >= '0' && c <= '9' && !cl_ws) { cl = cl * 10 + (c - '0'); ndig++; }
+                            if (c >= '0' && c <= '9' && !cl_ws) { clv = clv * 10 + (c - '0'); ndig++; }
                             else cl_bad = true;
                         }
                     } else if (hk == HK_CL) cl_ws = true;
@@ -225,6 +225,7 @@ __global__ __launch_bounds__(kBlock) void http_classify_kernel(
                     } else if (hk == HK_CL) {
                         if (have_cl || ndig == 0 || ndig > 10 || cl_bad) { st = ST_ERR; break; }
                         have_cl = true;
+                        cl = clv;
                     } else if (hk == HK_TE) {
                         have_te = true;
                     }

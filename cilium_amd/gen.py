@@ -91,11 +91,15 @@ def http_requests(n, seed, with_token=True):
     meth = rng.choice(5, p=[0.6, 0.2, 0.1, 0.05, 0.05], size=n)
     kind = rng.choice(3, p=[0.5, 0.3, 0.2], size=n)
     words = _rand_str(rng, _LOWER, 3, 8, n)
-    nums = rng.integers(0, 100, size=n)
+    # paths and hosts are correlated the way a real client population targets
+    # services, so the cfg2/cfg4 rules (which pin service, version and host
+    # together) match a realistic share of requests instead of ~0
+    nums = np.where(rng.random(n) < 0.6, 2 * rng.integers(0, 32, size=n) + 1, rng.integers(0, 100, size=n))
     tails = _rand_str(rng, _PATHCH, 0, 40, n)
     svc = rng.integers(0, 64, size=n)
-    ver = rng.integers(1, 4, size=n)
-    host = rng.integers(0, 64, size=n)
+    ver = np.where(rng.random(n) < 0.8, svc % 3 + 1, rng.integers(1, 4, size=n))
+    target = np.where(kind == 0, nums % 64, svc)
+    host = np.where(rng.random(n) < 0.8, target, rng.integers(0, 64, size=n))
     tok_kind = rng.choice(4, p=[0.5, 0.25, 0.24, 0.01], size=n)  # digits / alnum / absent / literal
     tok_digits = _rand_str(rng, np.frombuffer(b"0123456789", np.uint8), 8, 16, n)
     tok_alnum = _rand_str(rng, _ALNUM, 8, 16, n)

@@ -60,7 +60,10 @@ typedef struct {
     uint64_t table_bytes;
 } l7g_stats_t;
 
-/* Engine bound to one HIP device.  err receives a message on failure. */
+/* Engine bound to one HIP device.  err receives a message on failure.
+ * device == L7G_HOST_ONLY creates a compile-only engine (policy validation and
+ * rule-table statistics; classification returns hipErrorNoDevice). */
+#define L7G_HOST_ONLY (-1)
 l7g_engine *l7g_engine_create(int device, char *err, size_t errlen);
 void l7g_engine_destroy(l7g_engine *e);
 

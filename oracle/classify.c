@@ -310,7 +310,7 @@ typedef struct {
 static void *run(void *arg) {
     job_t *j = arg;
     for (uint32_t i = j->lo; i < j->hi; i++) {
-        ref_out_t o = {L7_PARSE_ERROR, -1, 0};
+        ref_out_t o = {L7_UNSUPPORTED, -1, 0}; /* unknown connection / no parser */
         uint32_t ci = j->conn[i];
         if (ci < j->nconns) {
             const ref_conn_t *c = &j->conns[ci];

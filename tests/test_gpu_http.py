@@ -1,0 +1,154 @@
+"""HTTP parity on the GPU: the product (HIP kernels via the C-ABI) vs the oracle,
+bit-exact on verdict, matched rule id and consumed bytes."""
+import numpy as np
+import pytest
+
+from cilium_amd import gen
+from cilium_amd._lib import ALLOW, DENY, INCOMPLETE, PARSE_ERROR, PROTO_HTTP, UNSUPPORTED
+
+pytestmark = pytest.mark.gpu
+
+
+def both(engine, oracle, w, nthreads=8):
+    engine.update_policy(w.policy)
+    engine.set_connections(w.conns)
+    got = engine.classify(w.arena, w.offsets, w.lengths, w.conn_ids)
+    ref = oracle.classify_workload(w, nthreads)
+    return got, ref
+
+
+def assert_same(got, ref, w=None):
+    for name, a, b in zip(("verdict", "rule", "consumed"), got, ref):
+        bad = np.nonzero(a != b)[0]
+        if len(bad):
+            i = int(bad[0])
+            ctx = ""
+            if w is not None:
+                o, L = int(w.offsets[i]), int(w.lengths[i])
+                ctx = bytes(w.arena[o:o + min(L, 300)])
+            raise AssertionError(f"{name} mismatch at {i} ({len(bad)} total): got {a[i]} ref {b[i]}; "
+                                 f"all got=({got[0][i]},{got[1][i]},{got[2][i]}) ref=({ref[0][i]},{ref[1][i]},{ref[2][i]}) {ctx!r}")
+
+
+def wl_from_reqs(reqs, policy, conns, conn_ids=None):
+    arena, offs, lens = gen.pack(reqs)
+    if conn_ids is None:
+        conn_ids = np.zeros(len(reqs), np.uint32)
+    return gen.Workload("t", arena, offs, lens, np.asarray(conn_ids, np.uint32), conns, policy)
+
+
+def test_http_kats(engine, oracle, kats):
+    h = kats["http"]
+    engine.update_policy(h["policy"])
+    reqs, conns = [], []
+    for case in h["cases"]:
+        c = case["conn"]
+        conns.append({"policy": engine.policy_index(c["policy_name"]), "port": c["port"], "ingress": int(c["ingress"]),
+                      "proto": PROTO_HTTP, "src_id": c["src_id"], "dst_id": c["dst_id"]})
+        reqs.append(case["request"].encode())
+    engine.set_connections(conns)
+    arena, offs, lens = gen.pack(reqs)
+    v, r, c = engine.classify(arena, offs, lens, np.arange(len(reqs), dtype=np.uint32))
+    want = [ALLOW if case["expect"] == "ALLOW" else DENY for case in h["cases"]]
+    assert list(v) == want
+    assert list(c) == [len(x) for x in reqs]
+    # the matched rule is the one the Envoy evaluation order reaches first
+    ref = oracle.Policy(h["policy"]).classify(conns, arena, offs, lens, np.arange(len(reqs), dtype=np.uint32))
+    assert_same((v, r, c), ref)
+
+
+def test_http_duplicate_port_keeps_previous(engine, kats):
+    from cilium_amd import PolicyError
+    d = kats["http"]["duplicate_port"]
+    engine.update_policy({"policies": []})
+    with pytest.raises(PolicyError):
+        engine.update_policy(d["policy"])
+    conns = [{"policy": engine.policy_index("173"), "port": 80, "ingress": 1, "proto": PROTO_HTTP, "src_id": 1, "dst_id": 173}]
+    engine.set_connections(conns)
+    b = d["request"].encode()
+    v, _, _ = engine.classify(np.frombuffer(b, np.uint8), [0], [len(b)], [0])
+    assert v[0] == DENY  # no policy named 173 => NetworkPolicyMap::Allowed denies
+
+
+@pytest.mark.parametrize("cfg", [1, 2])
+def test_cfg_parity(engine, oracle, cfg):
+    w = gen.http_workload(cfg, 30000)
+    got, ref = both(engine, oracle, w)
+    assert_same(got, ref, w)
+    v = got[0]
+    assert (v == ALLOW).mean() > 0.05 and (v == DENY).mean() > 0.05
+
+
+def test_cfg4_small_parity(engine, oracle):
+    w = gen.cfg4_workload(20000, nids=64, rules_total=64 * 20)
+    got, ref = both(engine, oracle, w)
+    assert_same(got, ref, w)
+    st = engine.stats()
+    assert st["http_rulesets"] >= 64
+
+
+def test_adversarial_parity(engine, oracle):
+    reqs = gen.http_adversarial(20000, 4242)
+    base = gen.http_workload(2, 1)
+    rng = np.random.default_rng(5)
+    w = wl_from_reqs(reqs, base.policy, base.conns, rng.integers(0, len(base.conns), len(reqs)))
+    got, ref = both(engine, oracle, w)
+    assert_same(got, ref, w)
+    v = got[0]
+    for code in (ALLOW, DENY, PARSE_ERROR, INCOMPLETE, UNSUPPORTED):
+        assert (v == code).any(), code
+
+
+def test_edge_cases(engine, oracle):
+    pol = gen.cfg2_policy()
+    long_path = b"/public/abc/7/" + b"x" * 1900
+    reqs = [
+        b"", b"G", b"GET", b"GET ", b"GET /", b"GET / HTTP/1.1", b"GET / HTTP/1.1\r", b"GET / HTTP/1.1\r\n",
+        b"GET / HTTP/1.1\r\n\r\n", b" GET / HTTP/1.1\r\n\r\n", b"GET  / HTTP/1.1\r\n\r\n", b"GET / HTTP/1.1\n\r\n",
+        b"GET / HTTP/1.1\r\nHost: svc-7.x\r\n\r\n", b"GET / HTTP/1.1\r\nHost:svc-7.x\r\n\r\n",
+        b"GET / HTTP/1.1\r\nHost: \r\n\r\n", b"GET / HTTP/1.1\r\n Host: a\r\n\r\n", b"GET / HTTP/1.1\r\nHost : a\r\n\r\n",
+        b"GET / HTTP/1.1\r\nHost: a\r\nHost: svc-1.x\r\n\r\n", b"GET / HTTP/2.0\r\n\r\n", b"GET / HTTP/1.x\r\n\r\n",
+        b"GET " + long_path + b" HTTP/1.1\r\nHost: svc-7.q\r\nX-Token: [0-9]+\r\n\r\n",
+        b"POST /api/v1/svc0/x HTTP/1.1\r\nHost: svc-0.a\r\nContent-Length: 3\r\n\r\nabc",
+        b"POST /api/v1/svc0/x HTTP/1.1\r\nHost: svc-0.a\r\nContent-Length: 4\r\n\r\nabc",
+        b"POST /api/v1/svc0/x HTTP/1.1\r\nContent-Length: 1\r\nContent-Length: 1\r\n\r\nx",
+        b"POST /api/v1/svc0/x HTTP/1.1\r\nContent-Length: 1 2\r\n\r\nx",
+        b"POST /api/v1/svc0/x HTTP/1.1\r\nContent-Length:  007  \r\n\r\n1234567",
+        b"POST /api/v1/svc0/x HTTP/1.1\r\nContent-Length: 99999999999\r\n\r\n",
+        b"POST /x HTTP/1.1\r\nTransfer-Encoding: chunked\r\n\r\n",
+        b"GET /\xc3\xa9 HTTP/1.1\r\nHost: svc-3.\xff\r\n\r\n", b"GET /a\x7f HTTP/1.1\r\n\r\n",
+        b"GET / HTTP/1.1\r\nX-Token: 123\t \r\nHost: svc-3.z\r\n\r\n", b"GET / HTTP/1.1\r\nX-Token:\t123\r\n\r\n",
+        b"GET / HTTP/1.1\r\nx-token: [0-9]+\r\nHOST: svc-3.z\r\n\r\n", b"GET / HTTP/1.1\r\nX-Bad\x01: 1\r\n\r\n",
+        b"GET / HTTP/1.1\r\nX-V: a\x00b\r\n\r\n", b"(GET) / HTTP/1.1\r\n\r\n", b"GET / HTTP/1.1\r\n\r\nGET / HTTP/1.1\r\n\r\n",
+    ]
+    conns = gen.make_conns(4, 0, 80, True, PROTO_HTTP, [1, 2, 3, 4])
+    conns[2]["proto"] = 0       # connection without a parser
+    conns[3]["policy"] = -1     # endpoint without policy
+    ids = np.arange(len(reqs)) % 4
+    w = wl_from_reqs(reqs, pol, conns, ids)
+    got, ref = both(engine, oracle, w, 1)
+    assert_same(got, ref, w)
+    # unknown connection index
+    w2 = wl_from_reqs(reqs[:4], pol, conns, [99, 100, 101, 4])
+    got, ref = both(engine, oracle, w2, 1)
+    assert_same(got, ref, w2)
+
+
+def test_unaligned_offsets_and_tail(engine, oracle):
+    """Requests at every offset modulo 16, the last one ending at the arena's end."""
+    base = gen.http_requests(64, 77)
+    pad = []
+    for i, r in enumerate(base):
+        pad.append(b"#" * (i % 16))
+        pad.append(r)
+    blob = b"".join(pad)
+    offs, p = [], 0
+    for i, r in enumerate(base):
+        p += i % 16
+        offs.append(p)
+        p += len(r)
+    w = gen.Workload("t", np.frombuffer(blob, np.uint8).copy(), np.array(offs, np.uint64),
+                     np.array([len(r) for r in base], np.uint32), np.zeros(64, np.uint32),
+                     gen.make_conns(1, 0, 80, True, PROTO_HTTP, [5]), gen.cfg2_policy())
+    got, ref = both(engine, oracle, w, 1)
+    assert_same(got, ref, w)
