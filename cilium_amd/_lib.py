@@ -26,7 +26,9 @@ class Conn(C.Structure):
 class Stats(C.Structure):
     _fields_ = [(n, C.c_uint32) for n in (
         "policies", "rules", "http_rulesets", "http_chunks", "http_dfas", "http_dfa_states",
-        "kafka_rulesets", "kafka_rules", "kafka_topics")] + [("table_bytes", C.c_uint64)]
+        "kafka_rulesets", "kafka_rules", "kafka_topics")] + [
+        ("table_bytes", C.c_uint64), ("http_image_bytes", C.c_uint64), ("hot_ruleset", C.c_int32),
+        ("hot_image_bytes", C.c_uint32)]
 
 
 EXPORTS = (

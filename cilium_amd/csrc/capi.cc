@@ -44,6 +44,7 @@ struct l7g_engine {
     KafkaTables kt{};
     bool tables_dirty = true, conns_dirty = true;
     bool has_http = false, has_kafka = false;
+    int32_t hot_ruleset = -1;  // HTTP rule set staged in LDS (most connections)
 };
 
 static void set_err(char *err, size_t errlen, const std::string &m) {
@@ -85,6 +86,15 @@ bool ResolveConns(l7g_engine *e, std::string *err) {
             e->has_kafka = true;
         }
     }
+    // The rule set serving the most connections has its image staged in LDS
+    // by every workgroup (if it fits); the others are read from HBM/L2.
+    std::vector<uint32_t> uses(e->hc->image().rulesets.size(), 0);
+    for (size_t i = 0; i < e->attrs.size(); i++)
+        if (e->attrs[i].proto == PROTO_HTTP && e->conns[i].ruleset >= 0) uses[e->conns[i].ruleset]++;
+    e->hot_ruleset = -1;
+    uint32_t best = 0;
+    for (size_t r = 0; r < uses.size(); r++)
+        if (uses[r] > best && e->hc->image().rulesets[r].image_len <= kLdsImageBytes) { best = uses[r]; e->hot_ruleset = (int32_t)r; }
     e->tables_dirty = e->conns_dirty = true;
     return true;
 }
@@ -94,9 +104,7 @@ hipError_t Upload(l7g_engine *e) {
     if (e->tables_dirty) {
         std::vector<uint8_t> blob;
         const HttpImage &H = e->hc->image();
-        size_t o_rs = Put(blob, H.rulesets), o_ch = Put(blob, H.chunks), o_f = Put(blob, H.fields),
-               o_d = Put(blob, H.dfas), o_tr = Put(blob, H.trans), o_m = Put(blob, H.masks), o_c = Put(blob, H.cls),
-               o_r = Put(blob, H.rule_ids), o_h = Put(blob, H.hdrs), o_n = Put(blob, H.names);
+        size_t o_rs = Put(blob, H.rulesets), o_img = Put(blob, H.images);
         const KafkaImage &K = e->kc->image();
         size_t k_rs = Put(blob, K.rulesets), k_r = Put(blob, K.rules), k_idx = Put(blob, K.index),
                k_th = Put(blob, K.topic_hash), k_ch = Put(blob, K.client_hash), k_s = Put(blob, K.strings);
@@ -108,16 +116,9 @@ hipError_t Upload(l7g_engine *e) {
         e->blob_bytes = blob.size();
         HttpTables &T = e->ht;
         T.rulesets = (const DevRuleset *)(d + o_rs);
-        T.chunks = (const DevChunk *)(d + o_ch);
-        T.fields = (const DevField *)(d + o_f);
-        T.dfas = (const DevDfa *)(d + o_d);
-        T.trans = (const uint16_t *)(d + o_tr);
-        T.masks = (const uint64_t *)(d + o_m);
-        T.cls = (const uint8_t *)(d + o_c);
-        T.rule_ids = (const int32_t *)(d + o_r);
-        T.hdrs = (const DevHdrName *)(d + o_h);
-        T.names = (const uint8_t *)(d + o_n);
+        T.images = d + o_img;
         T.nrulesets = (uint32_t)H.rulesets.size();
+        T.hot_ruleset = e->hot_ruleset;
         KafkaTables &KT = e->kt;
         KT.rulesets = (const DevKafkaRuleset *)(d + k_rs);
         KT.rules = (const DevKafkaRule *)(d + k_r);
@@ -281,14 +282,17 @@ int l7g_stats(l7g_engine *e, l7g_stats_t *out) {
     out->rules = (uint32_t)e->ps->nrules;
     const HttpImage &H = e->hc->image();
     out->http_rulesets = (uint32_t)H.rulesets.size();
-    out->http_chunks = (uint32_t)H.chunks.size();
-    out->http_dfas = (uint32_t)H.dfas.size();
+    out->http_chunks = (uint32_t)H.chunks;
+    out->http_dfas = (uint32_t)H.dfas;
     out->http_dfa_states = (uint32_t)H.dfa_states;
     const KafkaImage &K = e->kc->image();
     out->kafka_rulesets = (uint32_t)K.rulesets.size();
     out->kafka_rules = (uint32_t)K.rules.size();
     out->kafka_topics = (uint32_t)K.ntopics;
     out->table_bytes = e->blob_bytes;
+    out->http_image_bytes = H.images.size();
+    out->hot_ruleset = e->hot_ruleset;
+    out->hot_image_bytes = e->hot_ruleset >= 0 ? H.rulesets[e->hot_ruleset].image_len : 0;
     return 0;
 }
 

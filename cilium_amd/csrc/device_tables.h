@@ -26,56 +26,64 @@ struct DevConn {
 };
 
 // ---------------- HTTP ----------------
+// Every HTTP rule set is one self-contained, 16-byte aligned "image": a
+// header, DFA descriptors, per-chunk masks, rule ids, custom header names,
+// and the DFA tables themselves.  All offsets are bytes from the image start,
+// so the kernel can stage the image of the hottest rule set in LDS and
+// address it with the same offsets it uses for images left in HBM.
+//
+// A rule set's rules are split into chunks of <= 64 rules (u64 masks, bit b
+// of chunk c = rule 64c+b in evaluation order).  The patterns of each header
+// slot, over all rules of the rule set, are compiled into one DFA (several if
+// the state budget is exceeded); a DFA state carries, per chunk, the mask of
+// rules whose matcher on that slot holds if the value ends in that state.
+constexpr int kChunksPerPass = 4;       // chunk accumulators the kernel keeps in registers
+constexpr int kDfasPerPass = 2;         // DFAs per slot walked in one framing pass
+constexpr uint32_t kLdsImageBytes = 40 * 1024;
+
 struct DevDfa {            // 16 B
-    uint32_t trans_off;    // u16 units into HttpTables::trans ([nstates][ncls])
-    uint32_t mask_off;     // u64 units into HttpTables::masks ([nstates], rule-chunk mask at EOF)
-    uint32_t cls_off;      // byte offset into HttpTables::cls (256 B byte->class map)
+    uint32_t cls_off;      // u8[256]: byte -> class
+    uint32_t trans_off;    // u16[nstates][ncls]; state 0 = dead
+    uint32_t mask_off;     // u64[nstates][nchunks]
     uint16_t ncls;
     uint16_t start;
 };
-struct DevField {          // 16 B: one header field of one rule chunk
-    uint8_t slot;          // SLOT_*
-    uint8_t ndfa;
-    uint16_t pad;
-    uint32_t dfa_first;
-    uint64_t absent_mask;  // rules of the chunk satisfied when the header is absent
-};
-struct DevChunk {          // 32 B: <= 64 rules evaluated with one u64 mask
-    uint64_t all_mask;
-    uint32_t field_first;
-    uint16_t nfields;
-    uint16_t nrules;
-    uint32_t rule_id_off;  // int32 global rule ids, in evaluation order
-    uint32_t pad[3];
-};
-struct DevHdrName {        // 12 B: custom header names a rule set looks at
+struct DevHdrName {        // 12 B: a custom header name the rule set looks at
     uint32_t hash;         // FNV-1a of the lower-cased name
     uint16_t len;
     uint16_t pad;
-    uint32_t name_off;     // byte offset into HttpTables::names
+    uint32_t name_off;     // lower-cased bytes
 };
-struct DevRuleset {        // 16 B
-    uint32_t chunk_first;
-    uint16_t nchunks;
+struct ImgHeader {         // 64 B, at offset 0 of every image
+    uint8_t nchunks;
     uint8_t nhdr;
     uint8_t terminal;      // verdict when no rule matches (V_ALLOW => rule -1)
-    uint32_t hdr_first;
-    uint32_t pad;
+    uint8_t ndfa;
+    uint8_t slot_dfa[kNumSlots + 1];  // DFAs of slot s: [slot_dfa[s], slot_dfa[s+1])
+    uint8_t max_slot_dfas; // most DFAs on one slot (framing passes = ceil(/kDfasPerPass))
+    uint8_t pad0[3];
+    uint16_t ref_slots;    // slots some rule constrains
+    uint16_t pad1;
+    uint32_t dfa_off;      // DevDfa[ndfa]
+    uint32_t init_off;     // u64[nchunks]: rules of the chunk (minus those on never-present headers)
+    uint32_t absent_off;   // u64[kNumSlots][nchunks]: rules satisfied when the slot is absent
+    uint32_t rule_off;     // i32[nchunks * 64]: global rule ids
+    uint32_t hdr_off;      // DevHdrName[nhdr]
+    uint32_t total_states;
+    uint32_t pad2[4];
+};
+static_assert(sizeof(ImgHeader) == 64, "ImgHeader layout");
+
+struct DevRuleset {        // 8 B
+    uint32_t image_off;    // into HttpTables::images (16-byte aligned)
+    uint32_t image_len;
 };
 
 struct HttpTables {
     const DevRuleset *rulesets;
-    const DevChunk *chunks;
-    const DevField *fields;
-    const DevDfa *dfas;
-    const uint16_t *trans;
-    const uint64_t *masks;
-    const uint8_t *cls;
-    const int32_t *rule_ids;
-    const DevHdrName *hdrs;
-    const uint8_t *names;
+    const uint8_t *images;
     uint32_t nrulesets;
-    uint32_t pad;
+    int32_t hot_ruleset;   // rule set whose image is staged in LDS (-1: none)
 };
 
 // ---------------- Kafka ----------------

@@ -1,6 +1,7 @@
 #include "http_compile.h"
 
 #include <algorithm>
+#include <cstring>
 #include <functional>
 #include <memory>
 
@@ -101,8 +102,19 @@ int HttpCompiler::RulesetFor(int policy, bool ingress, uint32_t port, uint64_t r
     return rs;
 }
 
+namespace {
+
+template <class T>
+uint32_t Append(std::vector<uint8_t> &img, const T *p, size_t n) {
+    size_t off = (img.size() + 15) & ~(size_t)15;
+    img.resize(off + n * sizeof(T));
+    if (n) memcpy(img.data() + off, p, n * sizeof(T));
+    return (uint32_t)off;
+}
+
+}  // namespace
+
 int HttpCompiler::Compile(const std::vector<const HttpRule *> &rules, uint8_t terminal, std::string *err) {
-    HttpImage &I = img_;
     // custom header names used anywhere in the rule set
     std::vector<std::string> custom;
     for (auto *r : rules)
@@ -117,118 +129,150 @@ int HttpCompiler::Compile(const std::vector<const HttpRule *> &rules, uint8_t te
         if (s >= 0) return s;
         return SLOT_CUSTOM0 + (int)(std::find(custom.begin(), custom.end(), name) - custom.begin());
     };
+    const size_t nr = rules.size();
+    const size_t nchunks = (nr + 63) / 64;
+    if (nchunks > 255) { *err = "rule set has more than 16320 HTTP rules"; return -1; }
+    auto bit = [](size_t r) { return 1ull << (r & 63); };
+    std::vector<uint64_t> all(nchunks, 0), init(nchunks, 0);
+    for (size_t r = 0; r < nr; r++) all[r >> 6] |= bit(r);
+    init = all;
+    // absent[s][c]: rules of chunk c not constrained on slot s.  A matcher on
+    // a missing header never holds (HeaderUtility::matchHeaders returns false
+    // before invert_match applies), so constrained rules drop out.
+    std::vector<uint64_t> absent((size_t)kNumSlots * nchunks);
+    for (int s = 0; s < kNumSlots; s++)
+        for (size_t c = 0; c < nchunks; c++) absent[s * nchunks + c] = all[c];
+    // matchers per slot: (rule index, matcher)
+    std::map<int, std::vector<std::pair<size_t, const HeaderMatcher *>>> by_slot;
+    for (size_t r = 0; r < nr; r++)
+        for (auto &m : rules[r]->m) {
+            int s = slot_of(m.name);
+            if (s == kSlotNever) { init[r >> 6] &= ~bit(r); continue; }
+            by_slot[s].emplace_back(r, &m);
+            absent[s * nchunks + (r >> 6)] &= ~bit(r);
+        }
 
-    DevRuleset rs{};
-    rs.terminal = terminal;
-    rs.nhdr = (uint8_t)custom.size();
-    rs.hdr_first = (uint32_t)I.hdrs.size();
+    ImgHeader H{};
+    H.nchunks = (uint8_t)nchunks;
+    H.nhdr = (uint8_t)custom.size();
+    H.terminal = terminal;
+    struct Built { int slot; re::DFA d; std::vector<uint64_t> masks; };
+    std::vector<Built> built;
+    for (auto &kv : by_slot) {
+        const int slot = kv.first;
+        H.ref_slots |= (uint16_t)(1u << slot);
+        // distinct patterns of this slot
+        std::vector<Pat> pats;
+        std::vector<std::pair<size_t, int>> rm_pat;  // (rule, pattern)
+        for (auto &rm : kv.second) {
+            const HeaderMatcher *m = rm.second;
+            int idx = -1;
+            for (size_t p = 0; p < pats.size(); p++)
+                if (pats[p].type == m->type && pats[p].value == m->value && pats[p].invert == m->invert) { idx = (int)p; break; }
+            if (idx < 0) { idx = (int)pats.size(); pats.push_back({m->type, m->value, m->invert, m->ast}); }
+            rm_pat.emplace_back(rm.first, idx);
+        }
+        std::vector<std::unique_ptr<re::Node>> owned;
+        std::vector<const re::Node *> asts;
+        for (auto &p : pats) {
+            if (p.type == HM::Regex) { asts.push_back(p.ast.get()); continue; }
+            auto a = PatternAst(p, err);
+            if (!a) return -1;
+            asts.push_back(a.get());
+            owned.push_back(std::move(a));
+        }
+        // build DFAs, halving the pattern set until each fits the budget
+        std::vector<std::vector<int>> groups;
+        std::vector<re::DFA> dfas;
+        std::function<bool(std::vector<int>)> build = [&](std::vector<int> sub) -> bool {
+            std::vector<re::Pattern> ps;
+            for (int p : sub) ps.push_back({asts[p], true});
+            re::DFA d;
+            std::string e;
+            if (re::BuildDFA(ps, max_dfa_states, &d, &e)) { groups.push_back(sub); dfas.push_back(std::move(d)); return true; }
+            if (sub.size() == 1) { *err = "regex too complex for the DFA budget: " + pats[sub[0]].value; return false; }
+            std::vector<int> a(sub.begin(), sub.begin() + sub.size() / 2), b(sub.begin() + sub.size() / 2, sub.end());
+            return build(a) && build(b);
+        };
+        std::vector<int> allp;
+        for (size_t p = 0; p < pats.size(); p++) allp.push_back((int)p);
+        if (!build(allp)) return -1;
+        H.max_slot_dfas = (uint8_t)std::max<size_t>(H.max_slot_dfas, dfas.size());
+        for (size_t g = 0; g < dfas.size(); g++) {
+            Built b{slot, std::move(dfas[g]), {}};
+            const std::vector<int> &sub = groups[g];
+            std::vector<int> local(pats.size(), -1);
+            for (size_t q = 0; q < sub.size(); q++) local[sub[q]] = (int)q;
+            b.masks.resize((size_t)b.d.nstates * nchunks);
+            for (int s = 0; s < b.d.nstates; s++) {
+                uint64_t *m = &b.masks[(size_t)s * nchunks];
+                for (size_t c = 0; c < nchunks; c++) m[c] = all[c];
+                for (auto &rp : rm_pat) {
+                    int q = local[rp.second];
+                    if (q < 0) continue;  // checked by another DFA of this slot
+                    bool acc = (b.d.accept[s][q >> 6] >> (q & 63)) & 1;
+                    if (acc == pats[rp.second].invert) m[rp.first >> 6] &= ~bit(rp.first);
+                }
+            }
+            built.push_back(std::move(b));
+        }
+    }
+    if (built.size() > 255) { *err = "rule set needs more than 255 DFAs"; return -1; }
+    H.ndfa = (uint8_t)built.size();
+    // slot directory (built is ordered by slot)
+    for (int s = 0, k = 0; s <= kNumSlots; s++) {
+        while (k < (int)built.size() && built[k].slot < s) k++;
+        H.slot_dfa[s] = (uint8_t)k;
+    }
+
+    // ---- assemble the image
+    std::vector<uint8_t> img(sizeof(ImgHeader));
+    std::vector<DevDfa> dd(built.size());
+    H.dfa_off = Append(img, dd.data(), dd.size());
+    H.init_off = Append(img, init.data(), init.size());
+    H.absent_off = Append(img, absent.data(), absent.size());
+    std::vector<int32_t> ids(nchunks * 64, -1);
+    for (size_t r = 0; r < nr; r++) ids[r] = rules[r]->id;
+    H.rule_off = Append(img, ids.data(), ids.size());
+    std::vector<DevHdrName> hn;
+    std::vector<uint8_t> names;
     for (auto &nm : custom) {
         DevHdrName h{};
         uint32_t hash = kFnvBasis;
         for (char c : nm) hash = l7_fnv_step(hash, (uint8_t)c);
         h.hash = hash;
         h.len = (uint16_t)nm.size();
-        h.name_off = (uint32_t)I.names.size();
-        I.names.insert(I.names.end(), nm.begin(), nm.end());
-        I.hdrs.push_back(h);
+        h.name_off = (uint32_t)names.size();
+        names.insert(names.end(), nm.begin(), nm.end());
+        hn.push_back(h);
     }
-    rs.chunk_first = (uint32_t)I.chunks.size();
-
-    for (size_t c0 = 0; c0 < rules.size() || (c0 == 0 && rules.empty()); c0 += 64) {
-        if (rules.empty()) break;
-        size_t c1 = std::min(rules.size(), c0 + 64);
-        int nr = (int)(c1 - c0);
-        DevChunk ch{};
-        ch.nrules = (uint16_t)nr;
-        ch.all_mask = nr == 64 ? ~0ull : ((1ull << nr) - 1);
-        ch.rule_id_off = (uint32_t)I.rule_ids.size();
-        for (size_t i = c0; i < c1; i++) I.rule_ids.push_back(rules[i]->id);
-        ch.field_first = (uint32_t)I.fields.size();
-
-        // matchers grouped by slot: (rule index in chunk, matcher)
-        std::map<int, std::vector<std::pair<int, const HeaderMatcher *>>> by_slot;
-        for (size_t i = c0; i < c1; i++)
-            for (auto &m : rules[i]->m) by_slot[slot_of(m.name)].emplace_back((int)(i - c0), &m);
-
-        for (auto &kv : by_slot) {
-            DevField f{};
-            f.slot = (uint8_t)kv.first;
-            uint64_t constrained = 0;
-            for (auto &rm : kv.second) constrained |= 1ull << rm.first;
-            f.absent_mask = ch.all_mask & ~constrained;
-            f.dfa_first = (uint32_t)I.dfas.size();
-            if (kv.first == kSlotNever) { f.ndfa = 0; I.fields.push_back(f); continue; }
-
-            // distinct patterns of this field
-            std::vector<Pat> pats;
-            std::vector<std::pair<int, int>> rm_pat;  // (rule, pattern)
-            for (auto &rm : kv.second) {
-                const HeaderMatcher *m = rm.second;
-                int idx = -1;
-                for (size_t p = 0; p < pats.size(); p++)
-                    if (pats[p].type == m->type && pats[p].value == m->value && pats[p].invert == m->invert) { idx = (int)p; break; }
-                if (idx < 0) { idx = (int)pats.size(); pats.push_back({m->type, m->value, m->invert, m->ast}); }
-                rm_pat.emplace_back(rm.first, idx);
-            }
-            std::vector<std::unique_ptr<re::Node>> owned;
-            std::vector<const re::Node *> asts;
-            for (auto &p : pats) {
-                if (p.type == HM::Regex) { asts.push_back(p.ast.get()); continue; }
-                auto a = PatternAst(p, err);
-                if (!a) return -1;
-                asts.push_back(a.get());
-                owned.push_back(std::move(a));
-            }
-            // build DFAs, halving the pattern set until each fits the budget
-            std::vector<std::vector<int>> groups;
-            std::vector<re::DFA> dfas;
-            std::function<bool(std::vector<int>)> build = [&](std::vector<int> sub) -> bool {
-                std::vector<re::Pattern> ps;
-                for (int p : sub) ps.push_back({asts[p], true});
-                re::DFA d;
-                std::string e;
-                if (re::BuildDFA(ps, max_dfa_states, &d, &e)) { groups.push_back(sub); dfas.push_back(std::move(d)); return true; }
-                if (sub.size() == 1) { *err = "regex too complex for the DFA budget: " + pats[sub[0]].value; return false; }
-                std::vector<int> a(sub.begin(), sub.begin() + sub.size() / 2), b(sub.begin() + sub.size() / 2, sub.end());
-                return build(a) && build(b);
-            };
-            std::vector<int> all;
-            for (size_t p = 0; p < pats.size(); p++) all.push_back((int)p);
-            if (!build(all)) return -1;
-            if (dfas.size() > 255) { *err = "too many DFAs for one header field"; return -1; }
-            f.ndfa = (uint8_t)dfas.size();
-            for (size_t g = 0; g < dfas.size(); g++) {
-                const re::DFA &d = dfas[g];
-                const std::vector<int> &sub = groups[g];
-                DevDfa dd{};
-                dd.trans_off = (uint32_t)I.trans.size();
-                dd.mask_off = (uint32_t)I.masks.size();
-                dd.cls_off = (uint32_t)I.cls.size();
-                dd.ncls = (uint16_t)d.ncls;
-                dd.start = (uint16_t)d.start;
-                I.cls.insert(I.cls.end(), d.cls, d.cls + 256);
-                I.trans.insert(I.trans.end(), d.next.begin(), d.next.end());
-                for (int s = 0; s < d.nstates; s++) {
-                    uint64_t mask = ch.all_mask;
-                    for (auto &rp : rm_pat) {
-                        auto pos = std::find(sub.begin(), sub.end(), rp.second);
-                        if (pos == sub.end()) continue;  // checked by another DFA of this field
-                        int local = (int)(pos - sub.begin());
-                        bool acc = (d.accept[s][local >> 6] >> (local & 63)) & 1;
-                        if (acc == pats[rp.second].invert) mask &= ~(1ull << rp.first);
-                    }
-                    I.masks.push_back(mask);
-                }
-                I.dfa_states += d.nstates;
-                I.dfas.push_back(dd);
-            }
-            I.fields.push_back(f);
-        }
-        ch.nfields = (uint16_t)(I.fields.size() - ch.field_first);
-        I.chunks.push_back(ch);
+    H.hdr_off = Append(img, hn.data(), hn.size());
+    uint32_t names_off = Append(img, names.data(), names.size());
+    for (auto &h : hn) h.name_off += names_off;
+    if (!hn.empty()) memcpy(img.data() + H.hdr_off, hn.data(), hn.size() * sizeof(DevHdrName));
+    for (size_t k = 0; k < built.size(); k++) {
+        const re::DFA &d = built[k].d;
+        dd[k].ncls = (uint16_t)d.ncls;
+        dd[k].start = (uint16_t)d.start;
+        dd[k].cls_off = Append(img, d.cls, 256);
+        dd[k].trans_off = Append(img, d.next.data(), d.next.size());
+        dd[k].mask_off = Append(img, built[k].masks.data(), built[k].masks.size());
+        H.total_states += (uint32_t)d.nstates;
     }
-    rs.nchunks = (uint16_t)(I.chunks.size() - rs.chunk_first);
+    memcpy(img.data() + H.dfa_off, dd.data(), dd.size() * sizeof(DevDfa));
+    memcpy(img.data(), &H, sizeof H);
+    img.resize((img.size() + 15) & ~(size_t)15);
+
+    HttpImage &I = img_;
+    DevRuleset rs{};
+    rs.image_off = (uint32_t)I.images.size();
+    rs.image_len = (uint32_t)img.size();
+    if ((uint64_t)rs.image_off + img.size() > 0xFFFFFFFFull) { *err = "HTTP rule tables exceed 4 GiB"; return -1; }
+    I.images.insert(I.images.end(), img.begin(), img.end());
     I.rulesets.push_back(rs);
+    I.chunks += nchunks;
+    I.dfas += built.size();
+    I.dfa_states += H.total_states;
     return (int)I.rulesets.size() - 1;
 }
 

@@ -5,9 +5,11 @@
 // the first HTTP rule, in PortNetworkPolicy evaluation order, whose header
 // matchers all match; the order is fixed per connection, so it is resolved
 // here once into a "rule set": an ordered rule list + a terminal verdict.
-// Each rule set is split into chunks of <= 64 rules; per chunk and header
-// field, the field's matchers are compiled into byte DFAs whose states carry
-// the 64-bit mask of rules satisfied on that field if the value ends there.
+// Each rule set becomes one self-contained image (device_tables.h): rules in
+// chunks of <= 64, and per header slot the matchers of ALL rules compiled
+// into byte DFAs whose states carry, per chunk, the mask of rules satisfied
+// on that slot if the value ends there.  The kernel walks these DFAs while it
+// frames the request, so every request byte is read once.
 #pragma once
 #include <cstdint>
 #include <map>
@@ -21,16 +23,8 @@ namespace l7 {
 
 struct HttpImage {
     std::vector<DevRuleset> rulesets;
-    std::vector<DevChunk> chunks;
-    std::vector<DevField> fields;
-    std::vector<DevDfa> dfas;
-    std::vector<uint16_t> trans;
-    std::vector<uint64_t> masks;
-    std::vector<uint8_t> cls;
-    std::vector<int32_t> rule_ids;
-    std::vector<DevHdrName> hdrs;
-    std::vector<uint8_t> names;
-    size_t dfa_states = 0;
+    std::vector<uint8_t> images;
+    size_t chunks = 0, dfas = 0, dfa_states = 0;
 };
 
 class HttpCompiler {

@@ -57,7 +57,10 @@ typedef struct {
 typedef struct {
     uint32_t policies, rules, http_rulesets, http_chunks, http_dfas, http_dfa_states;
     uint32_t kafka_rulesets, kafka_rules, kafka_topics;
-    uint64_t table_bytes;
+    uint64_t table_bytes;       /* device table blob (0 until first upload) */
+    uint64_t http_image_bytes;  /* all HTTP rule-set images */
+    int32_t hot_ruleset;        /* HTTP rule set staged in LDS, -1 none */
+    uint32_t hot_image_bytes;
 } l7g_stats_t;
 
 /* Engine bound to one HIP device.  err receives a message on failure.
