@@ -17,7 +17,7 @@
 
 namespace l7 {
 hipError_t LaunchHttpClassify(const uint8_t *arena, const uint64_t *offs, const uint32_t *lens, const uint32_t *conn_ids,
-                              uint32_t n, const DevConn *conns, uint32_t nconns, const HttpTables &T,
+                              uint32_t n, const DevConn *conns, uint32_t nconns, const HttpTables &T, bool any_cold,
                               uint8_t *verdict, int32_t *rule, uint32_t *consumed, uint64_t *counters,
                               uint32_t ncounters, hipStream_t stream);
 hipError_t LaunchKafkaClassify(const uint8_t *arena, const uint64_t *offs, const uint32_t *lens, const uint32_t *conn_ids,
@@ -45,6 +45,7 @@ struct l7g_engine {
     bool tables_dirty = true, conns_dirty = true;
     bool has_http = false, has_kafka = false;
     int32_t hot_ruleset = -1;  // HTTP rule set staged in LDS (most connections)
+    bool any_cold = false;     // some HTTP connection uses another rule set
 };
 
 static void set_err(char *err, size_t errlen, const std::string &m) {
@@ -95,6 +96,9 @@ bool ResolveConns(l7g_engine *e, std::string *err) {
     uint32_t best = 0;
     for (size_t r = 0; r < uses.size(); r++)
         if (uses[r] > best && e->hc->image().rulesets[r].image_len <= kLdsImageBytes) { best = uses[r]; e->hot_ruleset = (int32_t)r; }
+    e->any_cold = false;
+    for (size_t i = 0; i < e->attrs.size(); i++)
+        if (e->attrs[i].proto == PROTO_HTTP && e->conns[i].ruleset != e->hot_ruleset) e->any_cold = true;
     e->tables_dirty = e->conns_dirty = true;
     return true;
 }
@@ -237,7 +241,8 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, const uint64_t *off, const
     // The kernels each classify only their own protocol's requests and skip
     // the rest, so a mixed batch needs one launch per protocol present.
     if (e->has_http || !e->has_kafka)
-        rc = LaunchHttpClassify(arena, off, len, conn, n, e->d_conns, (uint32_t)e->conns.size(), e->ht, verdict, rule,
+        rc = LaunchHttpClassify(arena, off, len, conn, n, e->d_conns, (uint32_t)e->conns.size(), e->ht, e->any_cold,
+                                verdict, rule,
                                 consumed, counters, ncounters, s);
     if (rc == hipSuccess && e->has_kafka)
         rc = LaunchKafkaClassify(arena, off, len, conn, n, e->d_conns, (uint32_t)e->conns.size(), e->kt, verdict, rule,

@@ -37,9 +37,17 @@ struct DevConn {
 // slot, over all rules of the rule set, are compiled into one DFA (several if
 // the state budget is exceeded); a DFA state carries, per chunk, the mask of
 // rules whose matcher on that slot holds if the value ends in that state.
-constexpr int kChunksPerPass = 4;       // chunk accumulators the kernel keeps in registers
-constexpr int kDfasPerPass = 2;         // DFAs per slot walked in one framing pass
-constexpr uint32_t kLdsImageBytes = 40 * 1024;
+constexpr int kChunksPerPass = 2;       // chunk accumulators the kernel keeps in registers
+constexpr int kDfasPerPass = 1;         // DFAs per slot walked in one framing pass
+constexpr uint32_t kLdsImageBytes = 28 * 1024;  // LDS budget for the hot rule-set image
+
+// Header-name recognition: every image carries a small DFA over the
+// lower-cased name bytes that spells out the names the framer must know
+// (host, content-length, transfer-encoding and the rule set's custom header
+// names).  State 0 = a non-tchar byte was seen, 1 = valid name that is none
+// of them, 2 = start.  name_info[state] = NI_* flags of the name ending there.
+enum : uint8_t { NI_CUSTOM = 0x0F /* custom index + 1 */, NI_HOST = 0x10, NI_CL = 0x20, NI_TE = 0x40 };
+constexpr uint16_t kNameBad = 0, kNameOther = 1, kNameStart = 2;
 
 struct DevDfa {            // 16 B
     uint32_t cls_off;      // u8[256]: byte -> class
@@ -70,7 +78,11 @@ struct ImgHeader {         // 64 B, at offset 0 of every image
     uint32_t rule_off;     // i32[nchunks * 64]: global rule ids
     uint32_t hdr_off;      // DevHdrName[nhdr]
     uint32_t total_states;
-    uint32_t pad2[4];
+    uint32_t name_cls_off;    // u8[256]: byte -> class (0 = not a tchar; case folded)
+    uint32_t name_trans_off;  // u16[name_states][name_ncls]
+    uint32_t name_info_off;   // u8[name_states]: NI_* flags
+    uint16_t name_ncls;
+    uint16_t name_states;
 };
 static_assert(sizeof(ImgHeader) == 64, "ImgHeader layout");
 

@@ -104,6 +104,83 @@ int HttpCompiler::RulesetFor(int policy, bool ingress, uint32_t port, uint64_t r
 
 namespace {
 
+bool IsTchar(uint8_t c) {
+    if ((c >= '0' && c <= '9') || (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z')) return true;
+    return c && strchr("!#$%&'*+-.^_`|~", c) != nullptr;
+}
+
+// Trie automaton over lower-cased header-name bytes (device_tables.h, NI_*).
+struct NameDfa {
+    uint8_t cls[256] = {0};
+    int ncls = 2;
+    std::vector<uint16_t> trans;  // [state][class]
+    std::vector<uint8_t> info;    // [state]
+};
+
+NameDfa BuildNameDfa(const std::vector<std::string> &custom) {
+    std::vector<std::pair<std::string, uint8_t>> cands = {
+        {"host", NI_HOST}, {"content-length", NI_CL}, {"transfer-encoding", NI_TE}};
+    for (size_t q = 0; q < custom.size(); q++) {
+        bool merged = false;
+        for (auto &c : cands)
+            if (c.first == custom[q]) { c.second |= (uint8_t)(q + 1); merged = true; }
+        if (!merged) cands.emplace_back(custom[q], (uint8_t)(q + 1));
+    }
+    NameDfa d;
+    // classes: 0 = not a tchar, 1 = tchar spelling none of the names, 2.. = name bytes
+    int byte_cls[256];
+    for (int c = 0; c < 256; c++) byte_cls[c] = -1;
+    for (auto &cd : cands) {
+        bool ok = !cd.first.empty();
+        for (unsigned char ch : cd.first) ok = ok && IsTchar(ch) && !(ch >= 'A' && ch <= 'Z');
+        if (!ok) continue;  // a name no valid header line can carry: never present
+        for (unsigned char ch : cd.first)
+            if (byte_cls[ch] < 0) byte_cls[ch] = d.ncls++;
+    }
+    for (int c = 0; c < 256; c++) {
+        if (!IsTchar((uint8_t)c)) { d.cls[c] = 0; continue; }
+        int lc = (c >= 'A' && c <= 'Z') ? c + 32 : c;
+        d.cls[c] = (uint8_t)(byte_cls[lc] >= 0 ? byte_cls[lc] : 1);
+    }
+    // trie: 0 bad, 1 other, 2 root
+    std::vector<std::map<int, int>> kids(3);
+    std::vector<uint8_t> info(3, 0);
+    for (auto &cd : cands) {
+        bool ok = !cd.first.empty();
+        for (unsigned char ch : cd.first) ok = ok && IsTchar(ch) && !(ch >= 'A' && ch <= 'Z');
+        if (!ok) continue;
+        int s = kNameStart;
+        for (unsigned char ch : cd.first) {
+            int k = d.cls[ch];
+            auto it = kids[s].find(k);
+            if (it == kids[s].end()) {
+                kids.emplace_back();
+                info.push_back(0);
+                int ns = (int)kids.size() - 1;
+                kids[s][k] = ns;
+                s = ns;
+            } else {
+                s = it->second;
+            }
+        }
+        info[s] |= cd.second;
+    }
+    const int ns = (int)kids.size();
+    d.trans.assign((size_t)ns * d.ncls, kNameOther);
+    for (int s = 0; s < ns; s++)
+        for (int k = 0; k < d.ncls; k++) {
+            uint16_t to = kNameOther;
+            if (s == kNameBad || k == 0) to = kNameBad;
+            else if (s != kNameOther) {
+                auto it = kids[s].find(k);
+                if (it != kids[s].end()) to = (uint16_t)it->second;
+            }
+            d.trans[(size_t)s * d.ncls + k] = to;
+        }
+    d.info = info;
+    return d;
+}
+
 template <class T>
 uint32_t Append(std::vector<uint8_t> &img, const T *p, size_t n) {
     size_t off = (img.size() + 15) & ~(size_t)15;
@@ -250,6 +327,14 @@ int HttpCompiler::Compile(const std::vector<const HttpRule *> &rules, uint8_t te
     uint32_t names_off = Append(img, names.data(), names.size());
     for (auto &h : hn) h.name_off += names_off;
     if (!hn.empty()) memcpy(img.data() + H.hdr_off, hn.data(), hn.size() * sizeof(DevHdrName));
+    {
+        NameDfa nd = BuildNameDfa(custom);
+        H.name_ncls = (uint16_t)nd.ncls;
+        H.name_states = (uint16_t)nd.info.size();
+        H.name_cls_off = Append(img, nd.cls, 256);
+        H.name_trans_off = Append(img, nd.trans.data(), nd.trans.size());
+        H.name_info_off = Append(img, nd.info.data(), nd.info.size());
+    }
     for (size_t k = 0; k < built.size(); k++) {
         const re::DFA &d = built[k].d;
         dd[k].ncls = (uint16_t)d.ncls;

@@ -1,28 +1,32 @@
-// HTTP/1 request classification on gfx950 (product code).
+// HTTP/1 request classification on gfx950 (product code), v3.
 //
-// One lane per request, one forward pass over its bytes.  The request is
-// read as 64-byte windows (four 16-byte loads, the next window prefetched
-// into registers while the current one is consumed); a window is copied to
-// the lane's LDS slot only when bytes in it are looked at one by one.
+// Work split: one wave owns a tile of 64 consecutive requests, one lane per
+// request.  The requests' bytes reach the lanes through LDS in rounds:
 //
-//   * request line and header names are framed byte by byte (the grammar and
-//     error precedence are DESIGN.md §HTTP framing, restating what Envoy's
-//     HTTP/1 codec enforces before cilium.l7policy's decodeHeaders,
-//     envoy/cilium_l7policy.cc:127-182);
-//   * the values of header slots the connection's rule set constrains
-//     (:method, :path, :authority, <= 8 custom headers) are fed through the
-//     slot's DFAs while they are framed, and the end state's per-chunk rule
-//     masks are AND-ed into <= 4 register accumulators;
-//   * every other header value is skipped 64 bytes per step with a SWAR scan
-//     for the bytes that end or invalidate it (CTLs, DEL);
-//   * at the end, the first rule whose accumulator bit survives wins
-//     (envoy/cilium_network_policy.h:50-237 lowered by engine/http_compile.cc).
-// Rule sets larger than 4 chunks x 4 DFAs per slot re-frame the request once
-// per group (results identical; only the cost grows).
+//   * DMA: each round the wave copies, for every lane still working, the next
+//     128-byte window of its request (one cache line: windows are 128-byte
+//     aligned in memory) into the lane's LDS slot with global_load_lds_dwordx4.
+//     Eight lanes cooperate per window, so one wave-instruction moves eight
+//     full cache lines (coalesced) and a round is eight instructions for the
+//     whole wave.  Chunks outside [current position, request end) are not read.
+//     The chunk order inside a slot is XOR-swizzled by the lane index, so the
+//     lanes' later ds_read_b128 of "their chunk k" hit 64 distinct banks.
+//   * parse: every lane then consumes its window from LDS with the resumable
+//     framer below: the request line, header names (through the rule set's
+//     name DFA), and the values of header slots the rule set constrains (fed
+//     through the slot's DFAs, end-state rule masks AND-ed into <= 4 u64
+//     accumulators).  Values nobody constrains are skipped 16 bytes per step
+//     with a SWAR test for CTL/DEL.
 //
-// The image of the rule set serving most connections is staged in LDS by each
-// workgroup; waves whose lanes all use it read tables from LDS, others from
-// HBM/L2 through the same offsets.
+// Sixteen waves per CU (one 1024-thread workgroup, all 160 KiB of LDS: 16 x
+// 8 KiB windows + the hot rule-set image + rule counters) keep ~100 KiB of DMA
+// in flight per CU while other waves parse.
+//
+// The grammar, error precedence and policy semantics restate Envoy's HTTP/1
+// codec + cilium.l7policy (envoy/cilium_l7policy.cc:127-182,
+// envoy/cilium_network_policy.h:50-237); the oracle is
+// oracle/http_ref.c.  Rule sets larger than 4 chunks x 2 DFAs per slot are
+// evaluated in several framing passes (results identical; only cost grows).
 #include <hip/hip_runtime.h>
 
 #include <cstddef>
@@ -33,40 +37,24 @@ namespace l7 {
 
 namespace {
 
-constexpr int kBlock = 512;
-constexpr int kLdsRuleCounters = 1024;
-constexpr uint32_t kNoChunk = 0xFFFFFFF0u;  // cursor holds no chunk (never k or k - 1)
-constexpr uint32_t kEnd = 0x100;   // "byte" returned past the end of the request
+constexpr int kWaves = 16;
+constexpr int kBlock = 64 * kWaves;
+constexpr uint32_t kWin = 128;                 // bytes per lane per round (one cache line)
+constexpr uint32_t kWaveLds = 64 * kWin;       // 8 KiB per wave
+constexpr int kLdsRuleCounters = 1016;
+constexpr uint32_t kOffImg = kWaves * kWaveLds;
+constexpr uint32_t kOffCnt = kOffImg + kLdsImageBytes;
+constexpr uint32_t kLdsBytes = kOffCnt + (8 + kLdsRuleCounters) * 4;
+static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
 
-__device__ __forceinline__ bool is_tchar(uint32_t c) {
-    // tchar = "!#$%&'*+-.^_`|~" / DIGIT / ALPHA  (bitmap over 0x20..0x7F)
-    const uint32_t m1 = 0x03FF6CFAu;  // 0x20-0x3F: ! # $ % & ' * + - . 0-9
-    const uint32_t m2 = 0xC7FFFFFEu;  // 0x40-0x5F: A-Z ^ _
-    const uint32_t m3 = 0x57FFFFFFu;  // 0x60-0x7F: ` a-z | ~
-    uint32_t w = c < 0x40 ? m1 : (c < 0x60 ? m2 : m3);
-    return (c - 0x20u < 0x60u) && ((w >> (c & 31)) & 1);
-}
+enum : uint32_t {
+    M_METHOD, M_TARGET, M_VERSION, M_LINE, M_NAME, M_OWS, M_VALUE, M_SKIP, M_LF, M_ENDLF, M_DONE
+};
+constexpr uint32_t kNoSlot = 0xFF;
 
-__device__ __forceinline__ uint32_t fnv_step(uint32_t h, uint32_t c) {  // == l7_fnv_step (host)
-    c += (c - 'A' < 26u) ? 32u : 0u;
-    return (h ^ c) * 16777619u;
-}
-
-constexpr uint32_t fnv_const(const char *s, int n) {
-    uint32_t h = kFnvBasis;
-    for (int i = 0; i < n; i++) h = (h ^ (uint8_t)s[i]) * 16777619u;
-    return h;
-}
-constexpr uint32_t kHashHost = fnv_const("host", 4);
-constexpr uint32_t kHashCL = fnv_const("content-length", 14);
-constexpr uint32_t kHashTE = fnv_const("transfer-encoding", 17);
 __constant__ uint32_t kVer[10] = {'H', 'T', 'T', 'P', '/', 0x100, '.', 0x100, '\r', '\n'};
-__constant__ uint8_t kHost[4] = {'h', 'o', 's', 't'};
-__constant__ uint8_t kCL[14] = {'c', 'o', 'n', 't', 'e', 'n', 't', '-', 'l', 'e', 'n', 'g', 't', 'h'};
-__constant__ uint8_t kTE[17] = {'t', 'r', 'a', 'n', 's', 'f', 'e', 'r', '-', 'e', 'n', 'c', 'o', 'd', 'i', 'n', 'g'};
 
-// Per-dword SWAR: bit 7 of byte i set iff byte i < 0x20 or == 0x7F (exact, no
-// carries between bytes).  HT is reported too and skipped by the caller.
+// Per-dword SWAR: bit 7 of byte i set iff byte i < 0x20 or == 0x7F (exact).
 __device__ __forceinline__ uint32_t stop_bits(uint32_t x) {
     const uint32_t t = x & 0x7F7F7F7Fu;
     return (~(t + 0x60606060u) | (t + 0x01010101u)) & ~x & 0x80808080u;
@@ -74,7 +62,6 @@ __device__ __forceinline__ uint32_t stop_bits(uint32_t x) {
 // bit 7 of each byte -> 4-bit nibble
 __device__ __forceinline__ uint32_t nib(uint32_t s) { return __builtin_amdgcn_ubfe((s >> 7) * 0x204081u, 21, 4); }
 
-// ---------------------------------------------------------------- tables
 // Rule-set image accessor: LDS (hot rule set) or global memory.
 template <bool kLds>
 struct Img {
@@ -85,433 +72,534 @@ struct Img {
     __device__ __forceinline__ uint64_t u64(uint32_t o) const { return *(const uint64_t *)(p + o); }
 };
 
-// ---------------------------------------------------------------- cursor
-// Byte-wise reads: the 16-byte chunk holding the current position plus the
-// next chunk, prefetched.  Positions are relative to the request start
-// rounded down to 64 bytes, so chunks and windows are aligned in memory.
-// Loads are never predicated: a chunk past the request end is read from the
-// request's last chunk instead (its bytes are never consumed), so every load
-// stays inside the request's own 16-byte chunks.
-struct Cursor {
-    const uint8_t *abase;  // request start rounded down to 64 B
-    uint32_t lena;         // request end, relative to abase (> 0)
-    uint32_t last;         // offset of the chunk holding the request's last byte
-    uint32_t ck;           // chunk index held in cw
-    uint4 cw, nw;
-};
-
-__device__ __forceinline__ uint4 load16(const Cursor &C, uint32_t k) {
-    return *(const uint4 *)(C.abase + min(k * 16, C.last));
-}
-
-__device__ __forceinline__ void cursor_init(Cursor &C, const uint8_t *req, uint32_t len) {  // len > 0
-    const uint32_t a = (uint32_t)((uintptr_t)req & 63);
-    C.abase = req - a;
-    C.lena = len + a;
-    C.last = (C.lena - 1) & ~15u;
-    C.ck = a >> 4;
-    C.cw = load16(C, C.ck);
-    C.nw = load16(C, C.ck + 1);
-}
-
-// Byte at aligned position pa (kEnd past the request).  Positions only move
-// forward: usually into the prefetched chunk, after a skip anywhere ahead.
-__device__ __forceinline__ uint32_t rd(Cursor &C, uint32_t pa) {
-    if (pa >= C.lena) return kEnd;
-    const uint32_t k = pa >> 4;
-    if (k != C.ck) {
-        C.cw = k == C.ck + 1 ? C.nw : load16(C, k);
-        C.ck = k;
-        C.nw = load16(C, k + 1);
-    }
-    // two selects + v_perm_b32 (selector 0x0C yields a zero byte); an indexed
-    // select over the four dwords would be lowered to a scratch array
-    const uint32_t q = pa & 15;
-    const bool upper = (q & 8) != 0;
-    const uint32_t lo = upper ? C.cw.z : C.cw.x, hi = upper ? C.cw.w : C.cw.y;
-    return __builtin_amdgcn_perm(hi, lo, (q & 7) | 0x0C0C0C00u);
-}
-
-__device__ __forceinline__ void load64(const Cursor &C, uint32_t k, uint4 &w0, uint4 &w1, uint4 &w2, uint4 &w3) {
-    const uint32_t o = k * 64;
-    w0 = *(const uint4 *)(C.abase + min(o, C.last));
-    w1 = *(const uint4 *)(C.abase + min(o + 16, C.last));
-    w2 = *(const uint4 *)(C.abase + min(o + 32, C.last));
-    w3 = *(const uint4 *)(C.abase + min(o + 48, C.last));
-}
-
-// 64-bit mask of the stop bytes of a window (bit i = byte i).
-__device__ __forceinline__ uint32_t mask32(uint4 w) {
-    return nib(stop_bits(w.x)) | nib(stop_bits(w.y)) << 4 | nib(stop_bits(w.z)) << 8 | nib(stop_bits(w.w)) << 12;
-}
-__device__ __forceinline__ uint64_t window_mask(uint4 a0, uint4 a1, uint4 a2, uint4 a3) {
-    return (uint64_t)(mask32(a0) | mask32(a1) << 16) | (uint64_t)(mask32(a2) | mask32(a3) << 16) << 32;
-}
-
-// First position >= pa whose byte ends or invalidates a header value (CTL,
-// DEL, or the request end); HT is reported as well.  Reads 64-byte windows
-// (the next one in flight while the current one is tested); windows without
-// such a byte cost only the SWAR test.
-__device__ __forceinline__ uint32_t skip_value(const Cursor &C, uint32_t pa) {
-    if (pa >= C.lena) return C.lena;
-    uint32_t k = pa >> 6;
-    uint4 a0, a1, a2, a3, b0, b1, b2, b3;
-    load64(C, k, a0, a1, a2, a3);
-    load64(C, k + 1, b0, b1, b2, b3);
-    for (;;) {
-        const uint32_t any = stop_bits(a0.x) | stop_bits(a0.y) | stop_bits(a0.z) | stop_bits(a0.w) |
-                             stop_bits(a1.x) | stop_bits(a1.y) | stop_bits(a1.z) | stop_bits(a1.w) |
-                             stop_bits(a2.x) | stop_bits(a2.y) | stop_bits(a2.z) | stop_bits(a2.w) |
-                             stop_bits(a3.x) | stop_bits(a3.y) | stop_bits(a3.z) | stop_bits(a3.w);
-        const uint32_t wend = k * 64 + 64;
-        if (any != 0 || wend > C.lena) {
-            uint64_t m = window_mask(a0, a1, a2, a3);
-            if (wend > C.lena) m |= ~0ull << (C.lena & 63);  // request end inside this window
-            if (pa > k * 64) m &= ~0ull << (pa & 63);
-            if (m) return k * 64 + (uint32_t)__builtin_ctzll(m);
-        }
-        k++;
-        a0 = b0; a1 = b1; a2 = b2; a3 = b3;
-        load64(C, k + 1, b0, b1, b2, b3);
-    }
-}
-
-// Lower-cased comparison of request bytes (global memory) with a table name.
-__device__ bool name_eq(const uint8_t *a, const uint8_t *b, uint32_t n) {
-    for (uint32_t i = 0; i < n; i++) {
-        uint32_t c = a[i];
-        if (c - 'A' < 26u) c += 32;
-        if (c != b[i]) return false;
-    }
-    return true;
-}
-
-// Image header fields (ImgHeader), read when needed rather than held in
-// registers; wave-uniform in the LDS path, so moved to SGPRs there.
+// Header fields: wave-uniform in the LDS path (kept in SGPRs there).
 template <bool kLds>
 __device__ __forceinline__ uint32_t uni(uint32_t v) {
     return kLds ? (uint32_t)__builtin_amdgcn_readfirstlane((int)v) : v;
 }
 #define HDR_U32(I, field) uni<kLds>((I).u32(offsetof(ImgHeader, field)))
+#define HDR_U16(I, field) uni<kLds>((I).u16(offsetof(ImgHeader, field)))
 #define HDR_U8(I, field) uni<kLds>((I).u8(offsetof(ImgHeader, field)))
 
-// DFAs of one slot for the current pass.
-struct SlotDfas {
-    uint32_t nd;
-    uint32_t cls[kDfasPerPass], trans[kDfasPerPass], mask[kDfasPerPass], ncls[kDfasPerPass];
-    uint32_t st[kDfasPerPass];
-};
-
-template <bool kLds>
-__device__ __forceinline__ void slot_begin(const Img<kLds> &I, uint32_t slot, uint32_t dgroup,
-                                           SlotDfas &S) {
-    const uint32_t lo = I.u8(offsetof(ImgHeader, slot_dfa) + slot) + dgroup * kDfasPerPass;
-    const uint32_t hi = I.u8(offsetof(ImgHeader, slot_dfa) + slot + 1);
-    S.nd = hi > lo ? min(hi - lo, (uint32_t)kDfasPerPass) : 0;
-#pragma unroll
-    for (int k = 0; k < kDfasPerPass; k++) {
-        S.st[k] = 0;
-        if ((uint32_t)k < S.nd) {
-            const uint32_t d = HDR_U32(I, dfa_off) + (lo + k) * sizeof(DevDfa);
-            S.cls[k] = I.u32(d + 0);
-            S.trans[k] = I.u32(d + 4);
-            S.mask[k] = I.u32(d + 8);
-            const uint32_t nc_st = I.u32(d + 12);
-            S.ncls[k] = nc_st & 0xFFFF;
-            S.st[k] = nc_st >> 16;
-        }
-    }
-}
-
-template <bool kLds>
-__device__ __forceinline__ void slot_step(const Img<kLds> &I, SlotDfas &S, uint32_t c) {
-#pragma unroll
-    for (int k = 0; k < kDfasPerPass; k++)
-        if (S.st[k] != 0) S.st[k] = I.u16(S.trans[k] + 2 * (S.st[k] * S.ncls[k] + I.u8(S.cls[k] + c)));
-}
-
-// AND the end states' masks of chunks [cg, cg + nc) into acc.
-template <bool kLds>
-__device__ __forceinline__ void slot_end(const Img<kLds> &I, const SlotDfas &S, uint32_t nchunks, uint32_t cg,
-                                         uint32_t nc, uint64_t *acc) {
-#pragma unroll
-    for (int k = 0; k < kDfasPerPass; k++) {
-        if ((uint32_t)k >= S.nd) break;
-        const uint32_t base = S.mask[k] + 8 * (S.st[k] * nchunks + cg);
-#pragma unroll
-        for (int c = 0; c < kChunksPerPass; c++)
-            if ((uint32_t)c < nc) acc[c] &= I.u64(base + 8 * c);
-    }
-}
-
-struct Result {
+// ---------------------------------------------------------------- lane state
+struct Lane {
+    uint64_t wb;        // request start rounded down to 128 B (absolute)
+    uint32_t a0;        // position of request byte 0 relative to wb
+    uint32_t lena;      // a0 + len
+    uint32_t pa;        // next position to look at
+    uint32_t mode;
+    uint32_t mark;      // token start (method/target/name) or version index
+    uint32_t idx;       // request index
+    bool done;
     uint8_t verdict;
     int32_t rule;
     uint32_t consumed;
+    // framing
+    uint32_t present;   // slots seen (first occurrence)
+    uint32_t slot;      // slot of the current header value (kNoSlot: none)
+    uint32_t nstate;    // name DFA state
+    uint32_t ninfo;     // NI_* flags of the current header name
+    bool have_cl, have_te, cl_bad, cl_ws, in_ows;
+    uint32_t ndig;
+    uint64_t clv, cl;
+    // DFAs of the current slot
+    uint32_t nd;
+    uint32_t dcls[kDfasPerPass], dtrans[kDfasPerPass], dmask[kDfasPerPass], dncls[kDfasPerPass];
+    uint32_t st[kDfasPerPass], saved[kDfasPerPass];
+    // rule accumulators for the current chunk group
+    uint64_t acc[kChunksPerPass];
+    uint32_t cg, dg;    // chunk group, DFA group of this pass
 };
 
-// One framing pass over the request; on success the accumulators hold the
-// chunk group's slot masks and *hdr_end / *cl the framing results.
 template <bool kLds>
-__device__ __forceinline__ uint8_t frame_pass(const Img<kLds> &I, const uint8_t *names_g, const uint8_t *req,
-                              uint32_t len, uint32_t cg, uint32_t nc, uint32_t dgroup, uint64_t *acc,
-                              uint32_t *present_out, uint32_t *consumed_out) {
-    Cursor C;
-    cursor_init(C, req, len);
-    const uint32_t a0 = (uint32_t)((uintptr_t)req & 63);  // aligned position of byte 0
-    const uint32_t nchunks = HDR_U8(I, nchunks);
-    uint32_t present = 0;
-    uint32_t pa = a0;
-    uint32_t c;
-    SlotDfas S;
-
-    // ---- method: 1*tchar SP
-    slot_begin(I, SLOT_METHOD, dgroup, S);
-    for (;;) {
-        c = rd(C, pa);
-        if (c == ' ') break;
-        if (!is_tchar(c)) return c == kEnd ? V_INCOMPLETE : V_PARSE_ERROR;
-        slot_step(I, S, c);
-        pa++;
-    }
-    if (pa == a0) return V_PARSE_ERROR;
-    slot_end(I, S, nchunks, cg, nc, acc);
-    present |= 1u << SLOT_METHOD;
-    pa++;
-    // ---- request target: 1*(VCHAR / obs-text) SP
-    slot_begin(I, SLOT_PATH, dgroup, S);
-    const uint32_t ps = pa;
-    for (;;) {
-        c = rd(C, pa);
-        if (c == ' ') break;
-        if (c <= 0x20 || c == 0x7F || c == kEnd) return c == kEnd ? V_INCOMPLETE : V_PARSE_ERROR;
-        slot_step(I, S, c);
-        pa++;
-    }
-    if (pa == ps) return V_PARSE_ERROR;
-    slot_end(I, S, nchunks, cg, nc, acc);
-    present |= 1u << SLOT_PATH;
-    pa++;
-    // ---- "HTTP/" DIGIT "." DIGIT CRLF
-#pragma unroll 1
-    for (uint32_t i = 0; i < 10; i++) {
-        c = rd(C, pa);
-        const uint32_t want = kVer[i];
-        if (want == 0x100 ? c - '0' >= 10u : c != want) return c == kEnd ? V_INCOMPLETE : V_PARSE_ERROR;
-        pa++;
-    }
-    // ---- header lines
-    bool have_cl = false, have_te = false;
-    uint64_t cl = 0;
-    const uint8_t *abase = C.abase;
-    for (;;) {
-        c = rd(C, pa);
-        if (c == '\r') {
-            c = rd(C, pa + 1);
-            if (c != '\n') return c == kEnd ? V_INCOMPLETE : V_PARSE_ERROR;
-            pa += 2;
-            break;
-        }
-        // field-name: 1*tchar ":"  (a line starting with SP/HT is obs-fold: error)
-        const uint32_t ns = pa;
-        uint32_t hash = kFnvBasis;
-        for (;;) {
-            c = rd(C, pa);
-            if (c == ':') break;
-            if (!is_tchar(c)) return c == kEnd ? V_INCOMPLETE : V_PARSE_ERROR;
-            hash = fnv_step(hash, c);
-            pa++;
-        }
-        const uint32_t nl = pa - ns;
-        if (nl == 0) return V_PARSE_ERROR;
-        pa++;
-        uint32_t slot = ~0u;
-        bool is_cl = false, is_te = false;
-        if (nl == 4 && hash == kHashHost && name_eq(abase + ns, kHost, 4)) {
-            if (!(present & (1u << SLOT_AUTHORITY))) slot = SLOT_AUTHORITY;
-        } else {
-            if (nl == 14 && hash == kHashCL && name_eq(abase + ns, kCL, 14)) is_cl = true;
-            else if (nl == 17 && hash == kHashTE && name_eq(abase + ns, kTE, 17)) is_te = true;
-            const uint32_t nhdr = HDR_U8(I, nhdr);
-            for (uint32_t q = 0; q < nhdr; q++) {
-                const uint32_t ho = HDR_U32(I, hdr_off) + q * sizeof(DevHdrName);
-                if (I.u32(ho) == hash && (I.u32(ho + 4) & 0xFFFF) == nl && name_eq(abase + ns, names_g + I.u32(ho + 8), nl)) {
-                    if (!(present & (1u << (SLOT_CUSTOM0 + q)))) slot = SLOT_CUSTOM0 + q;
-                    break;
-                }
-            }
-        }
-        if (slot != ~0u && !((HDR_U32(I, ref_slots) >> slot) & 1)) slot = ~0u;
-        // OWS
-        for (;;) {
-            c = rd(C, pa);
-            if (c != ' ' && c != '\t') break;
-            pa++;
-        }
-        uint64_t clv = 0;
-        uint32_t ndig = 0;
-        bool cl_bad = false, cl_ws = false;
-        if (slot == ~0u && !is_cl) {
-            // value nobody looks at: SWAR skip to CR, CTL or DEL
-            C.ck = kNoChunk;  // the byte cursor's chunks are dead across the skip
-            for (;;) {
-                pa = skip_value(C, pa);
-                c = rd(C, pa);
-                if (c != '\t') break;
-                pa++;
-            }
-            if (c != '\r') return c == kEnd ? V_INCOMPLETE : V_PARSE_ERROR;
-        } else {
-            if (slot != ~0u) slot_begin(I, slot, dgroup, S);
-            else {
-                S.nd = 0;
+__device__ __forceinline__ void slot_begin(const Img<kLds> &I, Lane &L, uint32_t slot) {
+    const uint32_t lo = I.u8(offsetof(ImgHeader, slot_dfa) + slot) + L.dg * kDfasPerPass;
+    const uint32_t hi = I.u8(offsetof(ImgHeader, slot_dfa) + slot + 1);
+    L.nd = hi > lo ? min(hi - lo, (uint32_t)kDfasPerPass) : 0;
 #pragma unroll
-                for (int k = 0; k < kDfasPerPass; k++) S.st[k] = 0;
-            }
-            uint32_t saved[kDfasPerPass];
-            bool in_ows = false;
-            for (;;) {
-                c = rd(C, pa);
-                if (c == '\r') break;
-                if ((c < 0x20 && c != '\t') || c == 0x7F || c == kEnd) return c == kEnd ? V_INCOMPLETE : V_PARSE_ERROR;
-                if (c == ' ' || c == '\t') {
-                    if (!in_ows) {
-#pragma unroll
-                        for (int k = 0; k < kDfasPerPass; k++) saved[k] = S.st[k];
-                        in_ows = true;
-                    }
-                    cl_ws = true;
-                } else {
-                    in_ows = false;
-                    if (c - '0' < 10u && !cl_ws) { clv = clv * 10 + (c - '0'); ndig++; }
-                    else cl_bad = true;
-                }
-                if (S.nd) slot_step(I, S, c);
-                pa++;
-            }
-            if (in_ows) {
-#pragma unroll
-                for (int k = 0; k < kDfasPerPass; k++) S.st[k] = saved[k];
-            }
-        }
-        // CR LF
-        c = rd(C, pa + 1);
-        if (c != '\n') return c == kEnd ? V_INCOMPLETE : V_PARSE_ERROR;
-        pa += 2;
-        if (is_cl) {
-            if (have_cl || ndig == 0 || ndig > 10 || cl_bad) return V_PARSE_ERROR;
-            have_cl = true;
-            cl = clv;
-        }
-        if (is_te) have_te = true;
-        if (slot != ~0u) {
-            slot_end(I, S, nchunks, cg, nc, acc);
-            present |= 1u << slot;
+    for (int k = 0; k < kDfasPerPass; k++) {
+        L.st[k] = 0;
+        if ((uint32_t)k < L.nd) {
+            const uint32_t d = HDR_U32(I, dfa_off) + (lo + k) * sizeof(DevDfa);
+            L.dcls[k] = I.u32(d + 0);
+            L.dtrans[k] = I.u32(d + 4);
+            L.dmask[k] = I.u32(d + 8);
+            const uint32_t nc_st = I.u32(d + 12);
+            L.dncls[k] = nc_st & 0xFFFF;
+            L.st[k] = nc_st >> 16;
         }
     }
-    if (have_te) return V_UNSUPPORTED;
-    const uint64_t total = (uint64_t)(pa - a0) + cl;
-    if (total > 0xFFFFFFFFull) return V_PARSE_ERROR;
-    if (total > len) return V_INCOMPLETE;
-    *consumed_out = (uint32_t)total;
-    *present_out = present;
-    return V_ALLOW;  // framing ok
 }
 
 template <bool kLds>
-__device__ __forceinline__ Result classify(const Img<kLds> &I, const uint8_t *names_g, const uint8_t *req, uint32_t len) {
-    if (len == 0) return Result{V_INCOMPLETE, -1, 0};
-    Result R{V_PARSE_ERROR, -1, 0};
+__device__ __forceinline__ void slot_step(const Img<kLds> &I, Lane &L, uint32_t c) {
+#pragma unroll
+    for (int k = 0; k < kDfasPerPass; k++)
+        if (L.st[k] != 0) L.st[k] = I.u16(L.dtrans[k] + 2 * (L.st[k] * L.dncls[k] + I.u8(L.dcls[k] + c)));
+}
+
+// AND the end states' masks of the pass's chunks into the accumulators.
+template <bool kLds>
+__device__ __forceinline__ void slot_end(const Img<kLds> &I, Lane &L) {
     const uint32_t nchunks = HDR_U8(I, nchunks);
-    const uint32_t max_dfas = HDR_U8(I, max_slot_dfas);
-    const uint32_t ngroups = nchunks ? (nchunks + kChunksPerPass - 1) / kChunksPerPass : 1;
-    const uint32_t ndg = max_dfas ? (max_dfas + kDfasPerPass - 1) / kDfasPerPass : 1;
-    for (uint32_t g = 0; g < ngroups; g++) {
-        const uint32_t cg = g * kChunksPerPass;
-        const uint32_t nc = nchunks > cg ? min(nchunks - cg, (uint32_t)kChunksPerPass) : 0;
-        uint64_t acc[kChunksPerPass];
+    const uint32_t nc = nchunks > L.cg ? min(nchunks - L.cg, (uint32_t)kChunksPerPass) : 0;
 #pragma unroll
-        for (int c = 0; c < kChunksPerPass; c++) acc[c] = (uint32_t)c < nc ? I.u64(HDR_U32(I, init_off) + 8 * (cg + c)) : 0;
-        uint32_t present = 0, consumed = 0;
-        for (uint32_t dg = 0; dg < ndg; dg++) {
-            const uint8_t v = frame_pass(I, names_g, req, len, cg, nc, dg, acc, &present, &consumed);
-            if (v != V_ALLOW) { R.verdict = v; return R; }
-        }
-        R.consumed = consumed;
-        // headers the rule set constrains but the request lacks
-        uint32_t missing = HDR_U32(I, ref_slots) & 0xFFFF & ~present;
-        while (missing) {
-            const uint32_t s = __builtin_ctz(missing);
-            missing &= missing - 1;
+    for (int k = 0; k < kDfasPerPass; k++) {
+        if ((uint32_t)k >= L.nd) break;
+        const uint32_t base = L.dmask[k] + 8 * (L.st[k] * nchunks + L.cg);
 #pragma unroll
-            for (int c = 0; c < kChunksPerPass; c++)
-                if ((uint32_t)c < nc) acc[c] &= I.u64(HDR_U32(I, absent_off) + 8 * (s * nchunks + cg + c));
-        }
+        for (int c = 0; c < kChunksPerPass; c++)
+            if ((uint32_t)c < nc) L.acc[c] &= I.u64(base + 8 * c);
+    }
+}
+
+template <bool kLds>
+__device__ __forceinline__ void acc_init(const Img<kLds> &I, Lane &L) {
+    const uint32_t nchunks = HDR_U8(I, nchunks);
 #pragma unroll
-        for (int c = 0; c < kChunksPerPass; c++) {
-            if ((uint32_t)c < nc && acc[c]) {
-                R.verdict = V_ALLOW;
-                R.rule = (int32_t)I.u32(HDR_U32(I, rule_off) + 4 * (64 * (cg + c) + (uint32_t)__builtin_ctzll(acc[c])));
-                return R;
+    for (int c = 0; c < kChunksPerPass; c++)
+        L.acc[c] = L.cg + c < nchunks ? I.u64(HDR_U32(I, init_off) + 8 * (L.cg + c)) : 0;
+}
+
+template <bool kLds>
+__device__ __forceinline__ void frame_reset(const Img<kLds> &I, Lane &L) {
+    L.pa = L.a0;
+    L.mode = M_METHOD;
+    L.mark = L.a0;
+    L.present = 0;
+    L.have_cl = L.have_te = false;
+    L.cl = 0;
+    slot_begin(I, L, SLOT_METHOD);
+}
+
+__device__ __forceinline__ void finish(Lane &L, uint8_t v, int32_t rule = -1) {
+    L.done = true;
+    L.mode = M_DONE;
+    L.verdict = v;
+    L.rule = rule;
+    if (v != V_ALLOW && v != V_DENY) L.consumed = 0;
+}
+
+// Headers complete (framing succeeded for this pass): next pass or verdict.
+template <bool kLds>
+__device__ __forceinline__ void headers_done(const Img<kLds> &I, Lane &L) {
+    const uint64_t total = (uint64_t)(L.pa - L.a0) + L.cl;
+    if (L.have_te) {
+        finish(L, V_UNSUPPORTED);
+    } else if (total > 0xFFFFFFFFull) {
+        finish(L, V_PARSE_ERROR);
+    } else if (total > (uint64_t)(L.lena - L.a0)) {
+        finish(L, V_INCOMPLETE);
+    } else {
+        L.consumed = (uint32_t)total;
+        const uint32_t max_dfas = HDR_U8(I, max_slot_dfas);
+        const uint32_t ndg = max_dfas ? (max_dfas + kDfasPerPass - 1) / kDfasPerPass : 1;
+        const uint32_t nchunks = HDR_U8(I, nchunks);
+        if (L.dg + 1 < ndg) {  // more DFAs of this chunk group: frame again
+            L.dg++;
+            frame_reset(I, L);
+        } else {
+            const uint32_t nc = nchunks > L.cg ? min(nchunks - L.cg, (uint32_t)kChunksPerPass) : 0;
+            // headers the rule set constrains but the request lacks
+            uint32_t missing = HDR_U32(I, ref_slots) & 0xFFFF & ~L.present;
+            while (missing) {
+                const uint32_t s = __builtin_ctz(missing);
+                missing &= missing - 1;
+#pragma unroll
+                for (int c = 0; c < kChunksPerPass; c++)
+                    if ((uint32_t)c < nc) L.acc[c] &= I.u64(HDR_U32(I, absent_off) + 8 * (s * nchunks + L.cg + c));
+            }
+            int32_t hit = -1;
+#pragma unroll
+            for (int c = kChunksPerPass - 1; c >= 0; c--)
+                if ((uint32_t)c < nc && L.acc[c]) hit = (int32_t)(64 * (L.cg + c) + (uint32_t)__builtin_ctzll(L.acc[c]));
+            if (hit >= 0) {
+                finish(L, V_ALLOW, (int32_t)I.u32(HDR_U32(I, rule_off) + 4 * (uint32_t)hit));
+            } else if (L.cg + kChunksPerPass < nchunks) {  // next chunk group
+                L.cg += kChunksPerPass;
+                L.dg = 0;
+                acc_init(I, L);
+                frame_reset(I, L);
+            } else {
+                finish(L, (uint8_t)HDR_U8(I, terminal));
             }
         }
     }
-    R.verdict = (uint8_t)HDR_U8(I, terminal);
-    return R;
+}
+
+// Header line complete (CRLF seen); false = Content-Length framing error.
+template <bool kLds>
+__device__ __forceinline__ bool line_done(const Img<kLds> &I, Lane &L) {
+    bool ok = true;
+    if (L.ninfo & NI_CL) {
+        ok = !(L.have_cl || L.ndig == 0 || L.ndig > 10 || L.cl_bad);
+        L.have_cl = true;
+        L.cl = L.clv;
+    }
+    if (L.ninfo & NI_TE) L.have_te = true;
+    if (L.slot != kNoSlot) {
+        slot_end(I, L);
+        L.present |= 1u << L.slot;
+    }
+    return ok;
+}
+
+// ---------------------------------------------------------------- parse one window
+// Consumes [L.pa, min(window end, request end)) from the lane's LDS slot.
+// Every loop has a single exit; errors set the mode to M_DONE, so later
+// blocks fall through (keeps the control flow shallow for the register
+// allocator).
+template <bool kLds>
+__device__ __forceinline__ void parse_window(const Img<kLds> &I, Lane &L, const uint8_t *slot, uint32_t swz) {
+    const uint32_t lim = min((L.pa & ~(kWin - 1)) + kWin, L.lena);
+    // byte at p (p < lim): chunk (p >> 4) & 7 sits at position ((p >> 4) & 7) ^ sw
+    auto B = [&](uint32_t p) -> uint32_t { return slot[(p & (kWin - 1)) ^ swz]; };
+    const uint32_t ncls_name = HDR_U16(I, name_ncls);
+    const uint32_t name_cls = HDR_U32(I, name_cls_off), name_trans = HDR_U32(I, name_trans_off);
+
+    // ---- request line
+    if (L.mode == M_METHOD) {  // 1*tchar SP
+        uint32_t c = 0;
+        for (; L.pa < lim; L.pa++) {
+            c = B(L.pa);
+            if (I.u8(name_cls + c) == 0) break;  // not a tchar (SP included)
+            slot_step(I, L, c);
+        }
+        if (L.pa < lim) {
+            if (c != ' ' || L.pa == L.mark) {
+                finish(L, V_PARSE_ERROR);
+            } else {
+                slot_end(I, L);
+                L.present |= 1u << SLOT_METHOD;
+                L.pa++;
+                L.mark = L.pa;
+                L.mode = M_TARGET;
+                slot_begin(I, L, SLOT_PATH);
+            }
+        }
+    }
+    if (L.mode == M_TARGET) {  // 1*(VCHAR / obs-text) SP
+        uint32_t c = 0;
+        for (; L.pa < lim; L.pa++) {
+            c = B(L.pa);
+            if (c <= 0x20 || c == 0x7F) break;
+            slot_step(I, L, c);
+        }
+        if (L.pa < lim) {
+            if (c != ' ' || L.pa == L.mark) {
+                finish(L, V_PARSE_ERROR);
+            } else {
+                slot_end(I, L);
+                L.present |= 1u << SLOT_PATH;
+                L.pa++;
+                L.mark = 0;
+                L.mode = M_VERSION;
+            }
+        }
+    }
+    if (L.mode == M_VERSION) {  // "HTTP/" DIGIT "." DIGIT CRLF
+        for (; L.pa < lim && L.mark < 10; L.pa++, L.mark++) {
+            const uint32_t c = B(L.pa);
+            const uint32_t want = kVer[L.mark];
+            if (want == 0x100 ? c - '0' >= 10u : c != want) break;
+        }
+        if (L.mark == 10) L.mode = M_LINE;
+        else if (L.pa < lim) finish(L, V_PARSE_ERROR);
+    }
+    // ---- header lines
+    while (L.mode >= M_LINE && L.mode < M_DONE && L.pa < lim) {
+        if (L.mode == M_LINE) {
+            if (B(L.pa) == '\r') {
+                L.pa++;
+                L.mode = M_ENDLF;
+            } else {
+                L.mode = M_NAME;
+                L.mark = L.pa;
+                L.nstate = kNameStart;
+            }
+        }
+        if (L.mode == M_ENDLF && L.pa < lim) {
+            if (B(L.pa) != '\n') {
+                finish(L, V_PARSE_ERROR);
+            } else {
+                L.pa++;
+                headers_done(I, L);  // done, or a new pass from the request start
+            }
+        }
+        if (L.mode == M_NAME) {  // 1*tchar ":"  (obs-fold SP/HT is not a tchar)
+            uint32_t c = 0;
+            for (; L.pa < lim; L.pa++) {
+                c = B(L.pa);
+                const uint32_t k = I.u8(name_cls + c);
+                if (k == 0) break;
+                L.nstate = I.u16(name_trans + 2 * (L.nstate * ncls_name + k));
+            }
+            if (L.pa < lim) {
+                if (c != ':' || L.pa == L.mark) {
+                    finish(L, V_PARSE_ERROR);
+                } else {
+                    L.pa++;
+                    L.ninfo = L.nstate >= kNameStart ? I.u8(HDR_U32(I, name_info_off) + L.nstate) : 0;
+                    uint32_t s = kNoSlot;
+                    if (L.ninfo & NI_HOST) s = SLOT_AUTHORITY;
+                    else if (L.ninfo & NI_CUSTOM) s = SLOT_CUSTOM0 + (L.ninfo & NI_CUSTOM) - 1;
+                    if (s != kNoSlot && ((L.present >> s) & 1)) s = kNoSlot;                // first occurrence only
+                    if (s != kNoSlot && !((HDR_U32(I, ref_slots) >> s) & 1)) s = kNoSlot;  // nobody looks at it
+                    L.slot = s;
+                    L.mode = M_OWS;
+                }
+            }
+        }
+        if (L.mode == M_OWS) {
+            for (; L.pa < lim; L.pa++) {
+                const uint32_t c = B(L.pa);
+                if (c != ' ' && c != '\t') break;
+            }
+            if (L.pa < lim) {
+                if (L.slot == kNoSlot && !(L.ninfo & NI_CL)) {
+                    L.mode = M_SKIP;
+                } else {
+                    L.mode = M_VALUE;
+                    if (L.slot != kNoSlot) {
+                        slot_begin(I, L, L.slot);
+                    } else {
+                        L.nd = 0;
+#pragma unroll
+                        for (int k = 0; k < kDfasPerPass; k++) L.st[k] = 0;
+                    }
+                    L.in_ows = false;
+                    L.clv = 0;
+                    L.ndig = 0;
+                    L.cl_bad = L.cl_ws = false;
+                }
+            }
+        }
+        if (L.mode == M_VALUE) {  // a value some rule (or Content-Length framing) looks at
+            uint32_t c = 0;
+            for (; L.pa < lim; L.pa++) {
+                c = B(L.pa);
+                if ((c < 0x20 && c != '\t') || c == 0x7F) break;  // CR ends it; other CTLs are errors
+                const bool ws = c == ' ' || c == '\t';
+                if (ws && !L.in_ows) {
+#pragma unroll
+                    for (int k = 0; k < kDfasPerPass; k++) L.saved[k] = L.st[k];
+                }
+                L.in_ows = ws;
+                L.cl_ws |= ws;
+                if (!ws) {
+                    if (c - '0' < 10u && !L.cl_ws) {
+                        L.clv = L.clv * 10 + (c - '0');
+                        L.ndig++;
+                    } else {
+                        L.cl_bad = true;
+                    }
+                }
+                slot_step(I, L, c);
+            }
+            if (L.pa < lim) {
+                if (c != '\r') {
+                    finish(L, V_PARSE_ERROR);
+                } else {
+                    if (L.in_ows) {  // trailing OWS is not part of the value
+#pragma unroll
+                        for (int k = 0; k < kDfasPerPass; k++) L.st[k] = L.saved[k];
+                    }
+                    L.pa++;
+                    L.mode = M_LF;
+                }
+            }
+        }
+        if (L.mode == M_SKIP) {  // a value nobody looks at: find CR (or a CTL / DEL) 16 bytes a step
+            uint32_t stop = 0;
+            while (L.pa < lim) {
+                const uint32_t k = L.pa >> 4;
+                const uint4 w = *(const uint4 *)(slot + ((L.pa & (kWin - 16)) ^ swz));
+                uint32_t m = nib(stop_bits(w.x)) | nib(stop_bits(w.y)) << 4 | nib(stop_bits(w.z)) << 8 |
+                             nib(stop_bits(w.w)) << 12;
+                m &= 0xFFFFu << (L.pa & 15);
+                const uint32_t cend = (k + 1) * 16;
+                if (cend > lim) m &= (1u << (lim & 15)) - 1u;  // lim inside this chunk
+                const uint32_t p = k * 16 + (uint32_t)__builtin_ctz(m | 0x10000u);
+                L.pa = min(p, lim);
+                if (p < cend) {
+                    const uint32_t c = B(p);
+                    if (c != '\t') {
+                        stop = c | 0x100;
+                        break;
+                    }
+                    L.pa++;
+                }
+            }
+            if (stop) {
+                if (stop != ('\r' | 0x100)) {
+                    finish(L, V_PARSE_ERROR);
+                } else {
+                    L.pa++;
+                    L.mode = M_LF;
+                }
+            }
+        }
+        if (L.mode == M_LF && L.pa < lim) {
+            if (B(L.pa) != '\n') {
+                finish(L, V_PARSE_ERROR);
+            } else {
+                L.pa++;
+                if (line_done(I, L)) L.mode = M_LINE;
+                else finish(L, V_PARSE_ERROR);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------- DMA
+// Copies, for every working lane t, chunks [lo, hi] of the 128-byte window at
+// `win` into LDS slot t (chunk c stored at position c ^ s(t)).  packed =
+// window address | hi << 4 | lo << 1 | 1 (addresses are 128-byte aligned).
+__device__ __forceinline__ void dma_windows(uint8_t *wave_lds, uint64_t packed, uint32_t lane) {
+    const uint32_t plo = (uint32_t)packed, phi = (uint32_t)(packed >> 32);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's earlier LDS reads have landed
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        const int t = 8 * j + (int)(lane >> 3);
+        const uint32_t tlo = __shfl(plo, t), thi = __shfl(phi, t);
+        const uint32_t c = (lane & 7) ^ (((uint32_t)t >> 1) & 7);
+        const uint32_t clo = (tlo >> 1) & 7, chi = (tlo >> 4) & 7;
+        if ((tlo & 1) && c >= clo && c <= chi) {
+            const uint8_t *src = (const uint8_t *)((((uint64_t)thi) << 32) | (tlo & ~127u)) + 16 * c;
+            __builtin_amdgcn_global_load_lds((const void *)src,
+                                             (__attribute__((address_space(3))) void *)(wave_lds + j * 1024), 16, 0, 0);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+struct Out {
+    uint8_t *verdict;
+    int32_t *rule;
+    uint32_t *consumed;
+    uint32_t *s_cnt;
+    uint64_t *counters;
+    uint32_t nrules;
+};
+
+__device__ __forceinline__ void emit(const Lane &L, const Out &O) {
+    O.verdict[L.idx] = L.verdict;
+    O.rule[L.idx] = L.rule;
+    O.consumed[L.idx] = L.consumed;
+    if (O.counters) {
+        atomicAdd(&O.s_cnt[L.verdict], 1u);
+        if (L.rule >= 0 && (uint32_t)L.rule < O.nrules) {
+            if (L.rule < kLdsRuleCounters) atomicAdd(&O.s_cnt[8 + L.rule], 1u);
+            else atomicAdd((unsigned long long *)&O.counters[L.rule], 1ull);
+        }
+    }
+}
+
+// All rounds of one tile.
+template <bool kLds>
+__device__ __forceinline__ void run_tile(Lane &L, const uint8_t *img, uint8_t *wave_lds, uint32_t lane, const Out &O) {
+    const Img<kLds> I{img};
+    if (!L.done) {
+        L.cg = 0;
+        L.dg = 0;
+        acc_init(I, L);
+        frame_reset(I, L);
+        if (L.lena == L.a0) {
+            finish(L, V_INCOMPLETE);
+            emit(L, O);
+        }
+    }
+    const uint8_t *slot = wave_lds + lane * kWin;
+    const uint32_t swz = ((lane >> 1) & 7) << 4;
+    while (__any(!L.done)) {
+        uint64_t packed = 0;
+        if (!L.done) {
+            const uint32_t w = L.pa & ~(kWin - 1);
+            const uint32_t lo = (L.pa - w) >> 4;
+            const uint32_t hi = min(L.lena - 1 - w, kWin - 1) >> 4;
+            packed = (L.wb + w) | (hi << 4) | (lo << 1) | 1u;
+        }
+        dma_windows(wave_lds, packed, lane);
+        if (!L.done) {
+            parse_window(I, L, slot, swz);
+            if (!L.done && L.pa >= L.lena) finish(L, V_INCOMPLETE);
+            if (L.done) emit(L, O);
+        }
+    }
 }
 
 }  // namespace
 
+// kHot = true : requests whose connection uses the hot rule set (image in LDS),
+//               plus entries on connections without an HTTP parser.
+// kHot = false: every other HTTP request (images read through L2); all of
+//               them when no hot kernel runs (T.hot_ruleset < 0).
+template <bool kHot>
 __global__ __launch_bounds__(kBlock) void http_classify_kernel(
     const uint8_t *__restrict__ arena, const uint64_t *__restrict__ offs, const uint32_t *__restrict__ lens,
     const uint32_t *__restrict__ conn_ids, uint32_t n, const DevConn *__restrict__ conns, uint32_t nconns,
     HttpTables T, uint8_t *__restrict__ out_verdict, int32_t *__restrict__ out_rule, uint32_t *__restrict__ out_consumed,
     uint64_t *__restrict__ counters, uint32_t ncounters) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_img[kLdsImageBytes];
-    __shared__ uint32_t s_cnt[8 + kLdsRuleCounters];
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
     const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63, wave = tid >> 6;
+    uint8_t *s_img = lds + kOffImg;
+    uint32_t *s_cnt = (uint32_t *)(lds + kOffCnt);
 
-    // stage the hot rule set's image; zero the counters
     const int32_t hot = T.hot_ruleset;
-    if (hot >= 0 && (uint32_t)hot < T.nrulesets) {
+    const bool hot_ok = hot >= 0 && (uint32_t)hot < T.nrulesets && T.rulesets[hot].image_len <= kLdsImageBytes;
+    if (kHot && !hot_ok) return;
+    // stage the hot rule set's image; zero the counters
+    if (kHot) {
         const DevRuleset r = T.rulesets[hot];
         const uint4 *src = (const uint4 *)(T.images + r.image_off);
-        const uint32_t n16 = min(r.image_len, kLdsImageBytes) / 16;
+        const uint32_t n16 = (r.image_len + 15) / 16;
         for (uint32_t i = tid; i < n16; i += kBlock) ((uint4 *)s_img)[i] = src[i];
     }
     if (counters)
         for (uint32_t i = tid; i < 8 + kLdsRuleCounters; i += kBlock) s_cnt[i] = 0;
     __syncthreads();
 
-    const uint32_t nrules = ncounters > 8 ? ncounters - 8 : 0;
-    for (uint32_t idx = blockIdx.x * kBlock + tid; idx < n; idx += gridDim.x * kBlock) {
-        const uint32_t ci = conn_ids[idx];
-        const DevConn conn = ci < nconns ? conns[ci] : DevConn{-1, PROTO_NONE, {0, 0, 0}};
-        // entries of other protocols belong to their own kernels; this kernel
-        // also answers entries whose connection is unknown or has no parser
-        if (conn.proto == PROTO_KAFKA || conn.proto == PROTO_MEMCACHE) continue;
-        Result R{V_UNSUPPORTED, -1, 0};
-        if (conn.proto == PROTO_HTTP && conn.ruleset >= 0 && (uint32_t)conn.ruleset < T.nrulesets) {
-            const uint8_t *req = arena + offs[idx];
-            const uint32_t len = lens[idx];
-            const DevRuleset rs = T.rulesets[conn.ruleset];
-            const uint8_t *gimg = T.images + rs.image_off;
-            if (__all(conn.ruleset == hot)) R = classify(Img<true>{s_img}, gimg, req, len);
-            else R = classify(Img<false>{gimg}, gimg, req, len);
-        }
-        out_verdict[idx] = R.verdict;
-        out_rule[idx] = R.rule;
-        out_consumed[idx] = R.consumed;
-        if (counters) {
-            atomicAdd(&s_cnt[R.verdict], 1u);
-            if (R.rule >= 0 && (uint32_t)R.rule < nrules) {
-                if (R.rule < kLdsRuleCounters) atomicAdd(&s_cnt[8 + R.rule], 1u);
-                else atomicAdd((unsigned long long *)&counters[R.rule], 1ull);
+    const Out O{out_verdict, out_rule, out_consumed, s_cnt, counters, ncounters > 8 ? ncounters - 8 : 0};
+    uint8_t *wave_lds = lds + wave * kWaveLds;
+    const uint32_t ntiles = (n + 63) / 64;
+    for (uint32_t tile = blockIdx.x * kWaves + wave; tile < ntiles; tile += gridDim.x * kWaves) {
+        Lane L;
+        L.idx = tile * 64 + lane;
+        L.done = true;
+        L.verdict = V_UNSUPPORTED;
+        L.rule = -1;
+        L.consumed = 0;
+        L.mode = M_DONE;
+        L.wb = 0;
+        L.a0 = L.lena = L.pa = 0;
+        const uint8_t *img = kHot ? s_img : nullptr;
+        if (L.idx < n) {
+            const uint32_t ci = conn_ids[L.idx];
+            const DevConn conn = ci < nconns ? conns[ci] : DevConn{-1, PROTO_NONE, {0, 0, 0}};
+            // entries of other protocols belong to their own kernels; the HTTP
+            // kernel answers entries whose connection is unknown or has no parser
+            const bool mine = !(conn.proto == PROTO_KAFKA || conn.proto == PROTO_MEMCACHE);
+            const bool http = mine && conn.proto == PROTO_HTTP && conn.ruleset >= 0 && (uint32_t)conn.ruleset < T.nrulesets;
+            const bool is_hot = http && hot_ok && conn.ruleset == hot;
+            if (mine && !http && (kHot || !hot_ok)) emit(L, O);  // unsupported connection: answered now
+            if (http && is_hot == kHot) {
+                const uint64_t off = offs[L.idx];
+                const uint32_t len = lens[L.idx];
+                const uint64_t a = (uint64_t)(arena + off);
+                L.wb = a & ~(uint64_t)127;
+                L.a0 = (uint32_t)(a & 127);
+                L.lena = L.a0 + len;
+                if (L.lena < L.a0) L.lena = 0xFFFFFFFFu;  // len > 4 GiB - 128: framing stops there
+                if (!kHot) img = T.images + T.rulesets[conn.ruleset].image_off;
+                L.done = false;
             }
         }
+        run_tile<kHot>(L, img, wave_lds, lane, O);
     }
     if (counters) {
         __syncthreads();
+        const uint32_t nrules = O.nrules;
         for (uint32_t i = tid; i < 8 + kLdsRuleCounters; i += kBlock) {
             const uint32_t v = s_cnt[i];
             if (!v) continue;
@@ -521,10 +609,11 @@ __global__ __launch_bounds__(kBlock) void http_classify_kernel(
     }
 }
 
-// Host-side launcher (called from the C-ABI): a persistent grid of two
-// workgroups per CU (LDS: 40 KiB image + 4 KiB counters each).
+// Host-side launcher (called from the C-ABI): persistent grids of one
+// 1024-thread workgroup per CU; the hot-rule-set kernel, then (only if some
+// HTTP connection uses another rule set) the general one.
 hipError_t LaunchHttpClassify(const uint8_t *arena, const uint64_t *offs, const uint32_t *lens, const uint32_t *conn_ids,
-                              uint32_t n, const DevConn *conns, uint32_t nconns, const HttpTables &T,
+                              uint32_t n, const DevConn *conns, uint32_t nconns, const HttpTables &T, bool any_cold,
                               uint8_t *verdict, int32_t *rule, uint32_t *consumed, uint64_t *counters,
                               uint32_t ncounters, hipStream_t stream) {
     if (n == 0) return hipSuccess;
@@ -535,10 +624,16 @@ hipError_t LaunchHttpClassify(const uint8_t *arena, const uint64_t *offs, const 
             hipDeviceGetAttribute(&num_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || num_cus <= 0)
             num_cus = 256;
     }
-    uint32_t blocks = (n + kBlock - 1) / kBlock;
-    blocks = min(blocks, (uint32_t)num_cus * 2);
-    hipLaunchKernelGGL(http_classify_kernel, dim3(blocks), dim3(kBlock), 0, stream, arena, offs, lens, conn_ids, n,
-                       conns, nconns, T, verdict, rule, consumed, counters, ncounters);
+    const uint32_t ntiles = (n + 63) / 64;
+    uint32_t blocks = (ntiles + kWaves - 1) / kWaves;
+    blocks = min(blocks, (uint32_t)num_cus);
+    const bool hot = T.hot_ruleset >= 0;
+    if (hot)
+        hipLaunchKernelGGL(http_classify_kernel<true>, dim3(blocks), dim3(kBlock), 0, stream, arena, offs, lens, conn_ids,
+                           n, conns, nconns, T, verdict, rule, consumed, counters, ncounters);
+    if (!hot || any_cold)
+        hipLaunchKernelGGL(http_classify_kernel<false>, dim3(blocks), dim3(kBlock), 0, stream, arena, offs, lens,
+                           conn_ids, n, conns, nconns, T, verdict, rule, consumed, counters, ncounters);
     return hipGetLastError();
 }
 

@@ -29,7 +29,7 @@ for step in "$@"; do
     pmc)
         i=0
         for ctrs in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY" \
-                    "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE" \
+                    "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE SQ_WAIT_INST_LDS SQ_INST_CYCLES_VMEM" \
                     "FETCH_SIZE" "WRITE_SIZE" "TA_BUSY_avr TA_BUSY_max TCP_TCC_READ_REQ_sum"; do
             i=$((i+1))
             run pmc$i 180 rocprofv3 --pmc $ctrs -d "$OUT/pmc$i" -o pmc --output-format csv -- python3 -u bench.py --steps 3 --warmup 1 --no-cpu-baseline
