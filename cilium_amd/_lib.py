@@ -8,7 +8,8 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libl7gpu.so")
+# L7G_LIB may name the profiling build (libl7gpu_timing.so) for experiments
+LIB_PATH = os.environ.get("L7G_LIB") or os.path.join(HERE, "libl7gpu.so")
 
 DENY, ALLOW, PARSE_ERROR, INCOMPLETE, UNSUPPORTED = 0, 1, 2, 3, 4
 PROTO_HTTP, PROTO_KAFKA, PROTO_MEMCACHE = 1, 2, 3
@@ -34,7 +35,7 @@ class Stats(C.Structure):
 EXPORTS = (
     "l7g_engine_create", "l7g_engine_destroy", "l7g_policy_update", "l7g_policy_index",
     "l7g_policy_nrules", "l7g_conns_set", "l7g_classify", "l7g_classify_host", "l7g_stats",
-    "l7g_debug_regex",
+    "l7g_debug_regex", "l7g_debug_phase_times",
 )
 
 _lib = None
@@ -61,6 +62,7 @@ def load():
     lib.l7g_classify_host.argtypes = [vp, vp, C.c_uint64, vp, vp, vp, C.c_uint32, vp, vp, vp]
     lib.l7g_stats.argtypes = [vp, C.POINTER(Stats)]
     lib.l7g_debug_regex.argtypes = [cp, sz, C.c_int, cp, sz, cp, sz]
+    lib.l7g_debug_phase_times.argtypes = [vp, vp, C.c_int]
     _lib = lib
     return lib
 

@@ -16,6 +16,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 BUILD = os.path.join(HERE, "build")
 LIB = os.path.join(HERE, "libl7gpu.so")
+LIB_TIMING = os.path.join(HERE, "libl7gpu_timing.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("L7G_ARCH", "gfx950")
 
@@ -42,12 +43,12 @@ def headers():
         glob.glob(os.path.join(HERE, "..", "include", "*.h"))
 
 
-def _compile(src, obj, newest_header):
+def _compile(src, obj, newest_header, defines=()):
     if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), newest_header):
         return None
     os.makedirs(os.path.dirname(obj), exist_ok=True)
     if src.endswith(".hip"):
-        cmd = [HIPCC] + COMMON + HIP_FLAGS + ["-c", src, "-o", obj]
+        cmd = [HIPCC] + COMMON + HIP_FLAGS + list(defines) + ["-c", src, "-o", obj]
     else:  # host-only C++: plain g++ against the HIP runtime headers
         cmd = ["g++"] + COMMON + ["-I/opt/rocm/include", "-D__HIP_PLATFORM_AMD__", "-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
@@ -56,18 +57,28 @@ def _compile(src, obj, newest_header):
     return src
 
 
-def build(verbose=False, jobs=8):
+def build(verbose=False, jobs=8, timing=False, variant=None, defines=()):
+    """timing=True builds the profiling variant libl7gpu_timing.so (kernels
+    compiled with -DL7G_PHASE_TIMING; see l7g_debug_phase_times).  variant=NAME
+    builds libl7gpu_NAME.so with extra -D defines (kernel experiments only;
+    the product is always libl7gpu.so)."""
     srcs = sources()
     newest_header = max([os.path.getmtime(h) for h in headers()] + [0])
-    objs = [os.path.join(BUILD, os.path.relpath(s, CSRC)) + ".o" for s in srcs]
+    if timing:
+        variant, defines = "timing", ("-DL7G_PHASE_TIMING",) + tuple(defines)
+    bdir = BUILD + ("_" + variant if variant else "")
+    lib = os.path.join(HERE, f"libl7gpu_{variant}.so") if variant else LIB
+    defines = tuple(defines)
+    objs = [os.path.join(bdir, os.path.relpath(s, CSRC)) + ".o" for s in srcs]
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-        done = list(ex.map(lambda so: _compile(so[0], so[1], newest_header), zip(srcs, objs)))
+        done = list(ex.map(lambda so: _compile(so[0], so[1], newest_header, defines), zip(srcs, objs)))
     rebuilt = [d for d in done if d]
     if verbose and rebuilt:
         print("compiled:", *[os.path.relpath(r, HERE) for r in rebuilt], file=sys.stderr)
-    if rebuilt or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(o) for o in objs):
+    LIB_OUT = lib
+    if rebuilt or not os.path.exists(LIB_OUT) or os.path.getmtime(LIB_OUT) < max(os.path.getmtime(o) for o in objs):
         tl = torch_libdir()
-        link = ["g++", "-shared", "-o", LIB + ".tmp"] + objs
+        link = ["g++", "-shared", "-o", LIB_OUT + ".tmp"] + objs
         if tl:
             link += [f"-L{tl}", "-l:libamdhip64.so", f"-Wl,-rpath,{tl}"]
         else:
@@ -76,9 +87,12 @@ def build(verbose=False, jobs=8):
         r = subprocess.run(link, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed: {' '.join(link)}\n{r.stdout}\n{r.stderr}")
-        os.replace(LIB + ".tmp", LIB)
-    return LIB
+        os.replace(LIB_OUT + ".tmp", LIB_OUT)
+    return LIB_OUT
 
 
 if __name__ == "__main__":
-    print(build(verbose=True))
+    # python -m cilium_amd.build [--timing] [--variant NAME -DX=Y ...]
+    argv = sys.argv[1:]
+    var = argv[argv.index("--variant") + 1] if "--variant" in argv else None
+    print(build(verbose=True, timing="--timing" in argv, variant=var, defines=[a for a in argv if a.startswith("-D")]))

@@ -24,6 +24,7 @@ hipError_t LaunchKafkaClassify(const uint8_t *arena, const uint64_t *offs, const
                                uint32_t n, const DevConn *conns, uint32_t nconns, const KafkaTables &T,
                                uint8_t *verdict, int32_t *rule, uint32_t *consumed, uint64_t *counters,
                                uint32_t ncounters, hipStream_t stream);
+hipError_t HttpPhaseTimes(uint64_t *out, bool reset);
 }  // namespace l7
 
 using namespace l7;
@@ -299,6 +300,12 @@ int l7g_stats(l7g_engine *e, l7g_stats_t *out) {
     out->hot_ruleset = e->hot_ruleset;
     out->hot_image_bytes = e->hot_ruleset >= 0 ? H.rulesets[e->hot_ruleset].image_len : 0;
     return 0;
+}
+
+int l7g_debug_phase_times(l7g_engine *e, uint64_t *out8, int reset) {
+    if (!e || e->device < 0) return (int)hipErrorNoDevice;
+    hipSetDevice(e->device);
+    return (int)HttpPhaseTimes(out8, reset != 0);
 }
 
 int l7g_debug_regex(const char *pat, size_t patlen, int anchored, const uint8_t *s, size_t slen, char *err,

@@ -37,7 +37,7 @@ struct DevConn {
 // slot, over all rules of the rule set, are compiled into one DFA (several if
 // the state budget is exceeded); a DFA state carries, per chunk, the mask of
 // rules whose matcher on that slot holds if the value ends in that state.
-constexpr int kChunksPerPass = 2;       // chunk accumulators the kernel keeps in registers
+constexpr int kChunksPerPass = 4;       // chunk accumulators the kernel keeps in registers
 constexpr int kDfasPerPass = 1;         // DFAs per slot walked in one framing pass
 constexpr uint32_t kLdsImageBytes = 28 * 1024;  // LDS budget for the hot rule-set image
 

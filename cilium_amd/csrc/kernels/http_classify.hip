@@ -1,32 +1,43 @@
-// HTTP/1 request classification on gfx950 (product code), v3.
+// HTTP/1 request classification on gfx950 (product code), v4.
 //
-// Work split: one wave owns a tile of 64 consecutive requests, one lane per
-// request.  The requests' bytes reach the lanes through LDS in rounds:
+// One wave owns a tile of 64 consecutive requests, one lane per request.
+// Work proceeds in rounds, each made of three wave-wide steps:
 //
-//   * DMA: each round the wave copies, for every lane still working, the next
-//     128-byte window of its request (one cache line: windows are 128-byte
-//     aligned in memory) into the lane's LDS slot with global_load_lds_dwordx4.
-//     Eight lanes cooperate per window, so one wave-instruction moves eight
-//     full cache lines (coalesced) and a round is eight instructions for the
-//     whole wave.  Chunks outside [current position, request end) are not read.
-//     The chunk order inside a slot is XOR-swizzled by the lane index, so the
-//     lanes' later ds_read_b128 of "their chunk k" hit 64 distinct banks.
-//   * parse: every lane then consumes its window from LDS with the resumable
-//     framer below: the request line, header names (through the rule set's
-//     name DFA), and the values of header slots the rule set constrains (fed
-//     through the slot's DFAs, end-state rule masks AND-ed into <= 4 u64
-//     accumulators).  Values nobody constrains are skipped 16 bytes per step
-//     with a SWAR test for CTL/DEL.
+//   1. window DMA: for every lane that needs bytes, the wave copies the next
+//      256-byte window of the lane's request (16-byte aligned, clipped to the
+//      request) into the lane's LDS slot with global_load_lds_dwordx4.
+//      Sixteen lanes cooperate per window (one wave-instruction moves four
+//      windows); chunk c of lane t's window is stored at position c ^ (t & 15)
+//      so the lanes' later ds_read_b128 of "their chunk k" hit 64 distinct
+//      banks.
+//   2. parse: each lane runs the resumable framer over its window: request
+//      line, header names (name DFA), header values of slots the rule set
+//      constrains (slot DFAs; end-state rule masks AND-ed into u64
+//      accumulators), Content-Length digits.  Bytes come from a two-chunk
+//      register cursor (16-byte LDS reads, next chunk prefetched); tchar and
+//      CTL tests are ALU; on the long tokens the DFA class of the next byte is
+//      fetched while the current transition is in flight, so a byte costs one
+//      dependent LDS round trip.  Values nobody constrains are skipped 16
+//      bytes a step (SWAR CTL/DEL test).
+//   3. scan: a lane whose unconstrained value runs past its window hands the
+//      rest to the wave: for up to 16 such lanes at a time the wave reads 1 KiB
+//      pieces of each lane's request with coalesced 16-byte-per-lane loads
+//      (all pieces in flight together) and finds the value's end (first byte
+//      < 0x20 other than HT, or DEL) by ballot.  The lane's next window starts
+//      there.
 //
-// Sixteen waves per CU (one 1024-thread workgroup, all 160 KiB of LDS: 16 x
-// 8 KiB windows + the hot rule-set image + rule counters) keep ~100 KiB of DMA
-// in flight per CU while other waves parse.
+// For the benchmark stream a tile takes two windows per request (head, then
+// the end of the header block) and one scan (the long pad header), so the pad
+// bytes are read once, by coalesced loads.
 //
-// The grammar, error precedence and policy semantics restate Envoy's HTTP/1
-// codec + cilium.l7policy (envoy/cilium_l7policy.cc:127-182,
+// One 512-thread workgroup per CU: 8 waves x 16 KiB windows + the hot rule
+// set's image (<= 28 KiB) + rule counters = 160 KiB of LDS.
+//
+// Grammar, error precedence and policy semantics: Envoy's HTTP/1 codec +
+// cilium.l7policy (envoy/cilium_l7policy.cc:127-182,
 // envoy/cilium_network_policy.h:50-237); the oracle is
-// oracle/http_ref.c.  Rule sets larger than 4 chunks x 2 DFAs per slot are
-// evaluated in several framing passes (results identical; only cost grows).
+// oracle/http_ref.c.  Rule sets larger than kChunksPerPass chunks x
+// kDfasPerPass DFAs per slot are evaluated in several framing passes.
 #include <hip/hip_runtime.h>
 
 #include <cstddef>
@@ -37,15 +48,47 @@ namespace l7 {
 
 namespace {
 
-constexpr int kWaves = 16;
+#ifndef L7G_HTTP_WAVES  // experiment knobs (tools/exp_http.py builds); defaults are the product's
+#define L7G_HTTP_WAVES 8
+#endif
+#ifndef L7G_HTTP_WIN
+#define L7G_HTTP_WIN 256
+#endif
+constexpr int kWaves = L7G_HTTP_WAVES;
 constexpr int kBlock = 64 * kWaves;
-constexpr uint32_t kWin = 128;                 // bytes per lane per round (one cache line)
-constexpr uint32_t kWaveLds = 64 * kWin;       // 8 KiB per wave
+constexpr uint32_t kWin = L7G_HTTP_WIN;        // bytes per lane window
+constexpr uint32_t kWinChunks = kWin / 16;
+constexpr uint32_t kWaveLds = 64 * kWin;       // 16 KiB per wave
 constexpr int kLdsRuleCounters = 1016;
 constexpr uint32_t kOffImg = kWaves * kWaveLds;
 constexpr uint32_t kOffCnt = kOffImg + kLdsImageBytes;
 constexpr uint32_t kLdsBytes = kOffCnt + (8 + kLdsRuleCounters) * 4;
 static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
+constexpr int kScanBatch = kWaveLds / 1024;    // lanes whose long values are scanned together
+constexpr uint32_t kLanesPerWin = kWinChunks;  // DMA: one lane per 16-byte chunk of a window
+constexpr uint32_t kWinPerInst = 64 / kLanesPerWin;
+static_assert(kWinChunks == 8 || kWinChunks == 16, "window size");
+// Chunk swizzle of lane t's slot, chosen so that the 16 lanes of each
+// ds_read_b128 bank group reading "their chunk k" cover all 64 banks.
+__device__ __forceinline__ uint32_t win_swizzle(uint32_t t) {
+    return kWinChunks == 16 ? (t & 15) : ((t >> 1) & 7);
+}
+
+// Optional per-phase cycle accounting (debug builds with -DL7G_PHASE_TIMING:
+// libl7gpu_timing.so, used by tools/exp_http.py).  Slots: 0 dma, 1 parse,
+// 2 scan, 3 emit/other, 4 rounds, 5 scan batches, 6 tiles.
+#ifdef L7G_PHASE_TIMING
+__device__ unsigned long long g_phase[8];
+#define PH_DECL uint64_t ph_t = __builtin_amdgcn_s_memtime(); uint64_t ph_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define PH_MARK(slot) do { const uint64_t ph_n = __builtin_amdgcn_s_memtime(); ph_acc[slot] += ph_n - ph_t; ph_t = ph_n; } while (0)
+#define PH_COUNT(slot, v) (ph_acc[slot] += (v))
+#define PH_FLUSH(lane) do { if ((lane) == 0) for (int ph_i = 0; ph_i < 8; ph_i++) atomicAdd(&g_phase[ph_i], (unsigned long long)ph_acc[ph_i]); } while (0)
+#else
+#define PH_DECL
+#define PH_MARK(slot) do {} while (0)
+#define PH_COUNT(slot, v) do {} while (0)
+#define PH_FLUSH(lane) do {} while (0)
+#endif
 
 enum : uint32_t {
     M_METHOD, M_TARGET, M_VERSION, M_LINE, M_NAME, M_OWS, M_VALUE, M_SKIP, M_LF, M_ENDLF, M_DONE
@@ -54,6 +97,15 @@ constexpr uint32_t kNoSlot = 0xFF;
 
 __constant__ uint32_t kVer[10] = {'H', 'T', 'T', 'P', '/', 0x100, '.', 0x100, '\r', '\n'};
 
+__device__ __forceinline__ bool is_tchar(uint32_t c) {
+    // tchar = "!#$%&'*+-.^_`|~" / DIGIT / ALPHA  (bitmap over 0x20..0x7F)
+    const uint32_t m1 = 0x03FF6CFAu;  // 0x20-0x3F
+    const uint32_t m2 = 0xC7FFFFFEu;  // 0x40-0x5F
+    const uint32_t m3 = 0x57FFFFFFu;  // 0x60-0x7F
+    const uint32_t w = c < 0x40 ? m1 : (c < 0x60 ? m2 : m3);
+    return (c - 0x20u < 0x60u) && ((w >> (c & 31)) & 1);
+}
+
 // Per-dword SWAR: bit 7 of byte i set iff byte i < 0x20 or == 0x7F (exact).
 __device__ __forceinline__ uint32_t stop_bits(uint32_t x) {
     const uint32_t t = x & 0x7F7F7F7Fu;
@@ -61,6 +113,16 @@ __device__ __forceinline__ uint32_t stop_bits(uint32_t x) {
 }
 // bit 7 of each byte -> 4-bit nibble
 __device__ __forceinline__ uint32_t nib(uint32_t s) { return __builtin_amdgcn_ubfe((s >> 7) * 0x204081u, 21, 4); }
+// 16-bit mask of the stop bytes of a chunk
+__device__ __forceinline__ uint32_t stop_mask(uint4 w) {
+    return nib(stop_bits(w.x)) | nib(stop_bits(w.y)) << 4 | nib(stop_bits(w.z)) << 8 | nib(stop_bits(w.w)) << 12;
+}
+__device__ __forceinline__ uint32_t byte_of(uint4 w, uint32_t q) {
+    // two selects + v_perm_b32 (an indexed select would be lowered to scratch)
+    const bool upper = (q & 8) != 0;
+    const uint32_t lo = upper ? w.z : w.x, hi = upper ? w.w : w.y;
+    return __builtin_amdgcn_perm(hi, lo, (q & 7) | 0x0C0C0C00u);
+}
 
 // Rule-set image accessor: LDS (hot rule set) or global memory.
 template <bool kLds>
@@ -71,8 +133,6 @@ struct Img {
     __device__ __forceinline__ uint32_t u32(uint32_t o) const { return *(const uint32_t *)(p + o); }
     __device__ __forceinline__ uint64_t u64(uint32_t o) const { return *(const uint64_t *)(p + o); }
 };
-
-// Header fields: wave-uniform in the LDS path (kept in SGPRs there).
 template <bool kLds>
 __device__ __forceinline__ uint32_t uni(uint32_t v) {
     return kLds ? (uint32_t)__builtin_amdgcn_readfirstlane((int)v) : v;
@@ -83,14 +143,17 @@ __device__ __forceinline__ uint32_t uni(uint32_t v) {
 
 // ---------------------------------------------------------------- lane state
 struct Lane {
-    uint64_t wb;        // request start rounded down to 128 B (absolute)
-    uint32_t a0;        // position of request byte 0 relative to wb
+    uint64_t base;      // request start rounded down to 16 B (absolute address)
+    uint32_t a0;        // position of request byte 0 relative to base
     uint32_t lena;      // a0 + len
     uint32_t pa;        // next position to look at
+    uint32_t w;         // position of the window held in the lane's LDS slot
     uint32_t mode;
     uint32_t mark;      // token start (method/target/name) or version index
     uint32_t idx;       // request index
-    bool done;
+    bool done;          // verdict known
+    bool owed;          // verdict not yet written out
+    bool scan;          // an unconstrained value continues past the window
     uint8_t verdict;
     int32_t rule;
     uint32_t consumed;
@@ -102,55 +165,45 @@ struct Lane {
     bool have_cl, have_te, cl_bad, cl_ws, in_ows;
     uint32_t ndig;
     uint64_t clv, cl;
-    // DFAs of the current slot
-    uint32_t nd;
-    uint32_t dcls[kDfasPerPass], dtrans[kDfasPerPass], dmask[kDfasPerPass], dncls[kDfasPerPass];
-    uint32_t st[kDfasPerPass], saved[kDfasPerPass];
-    // rule accumulators for the current chunk group
+    // DFA of the current slot (kDfasPerPass == 1); dtrans == 0: none
+    uint32_t dcls, dtrans, dmask, dncls, st, saved;
     uint64_t acc[kChunksPerPass];
     uint32_t cg, dg;    // chunk group, DFA group of this pass
 };
+static_assert(kDfasPerPass == 1, "one DFA per slot per framing pass");
 
 template <bool kLds>
 __device__ __forceinline__ void slot_begin(const Img<kLds> &I, Lane &L, uint32_t slot) {
-    const uint32_t lo = I.u8(offsetof(ImgHeader, slot_dfa) + slot) + L.dg * kDfasPerPass;
+    const uint32_t lo = I.u8(offsetof(ImgHeader, slot_dfa) + slot) + L.dg;
     const uint32_t hi = I.u8(offsetof(ImgHeader, slot_dfa) + slot + 1);
-    L.nd = hi > lo ? min(hi - lo, (uint32_t)kDfasPerPass) : 0;
-#pragma unroll
-    for (int k = 0; k < kDfasPerPass; k++) {
-        L.st[k] = 0;
-        if ((uint32_t)k < L.nd) {
-            const uint32_t d = HDR_U32(I, dfa_off) + (lo + k) * sizeof(DevDfa);
-            L.dcls[k] = I.u32(d + 0);
-            L.dtrans[k] = I.u32(d + 4);
-            L.dmask[k] = I.u32(d + 8);
-            const uint32_t nc_st = I.u32(d + 12);
-            L.dncls[k] = nc_st & 0xFFFF;
-            L.st[k] = nc_st >> 16;
-        }
+    L.st = 0;
+    L.dcls = L.dtrans = L.dmask = L.dncls = 0;
+    if (lo < hi) {
+        const uint32_t d = HDR_U32(I, dfa_off) + lo * sizeof(DevDfa);
+        L.dcls = I.u32(d + 0);
+        L.dtrans = I.u32(d + 4);
+        L.dmask = I.u32(d + 8);
+        const uint32_t nc_st = I.u32(d + 12);
+        L.dncls = nc_st & 0xFFFF;
+        L.st = nc_st >> 16;
     }
 }
 
 template <bool kLds>
-__device__ __forceinline__ void slot_step(const Img<kLds> &I, Lane &L, uint32_t c) {
-#pragma unroll
-    for (int k = 0; k < kDfasPerPass; k++)
-        if (L.st[k] != 0) L.st[k] = I.u16(L.dtrans[k] + 2 * (L.st[k] * L.dncls[k] + I.u8(L.dcls[k] + c)));
+__device__ __forceinline__ void dfa_step(const Img<kLds> &I, Lane &L, uint32_t c) {
+    if (L.st) L.st = I.u16(L.dtrans + 2 * (L.st * L.dncls + I.u8(L.dcls + c)));
 }
 
-// AND the end states' masks of the pass's chunks into the accumulators.
+// AND the end state's masks of the pass's chunks into the accumulators.
 template <bool kLds>
 __device__ __forceinline__ void slot_end(const Img<kLds> &I, Lane &L) {
+    if (L.dtrans == 0) return;  // no DFA of this pass on the slot
     const uint32_t nchunks = HDR_U8(I, nchunks);
     const uint32_t nc = nchunks > L.cg ? min(nchunks - L.cg, (uint32_t)kChunksPerPass) : 0;
+    const uint32_t base = L.dmask + 8 * (L.st * nchunks + L.cg);
 #pragma unroll
-    for (int k = 0; k < kDfasPerPass; k++) {
-        if ((uint32_t)k >= L.nd) break;
-        const uint32_t base = L.dmask[k] + 8 * (L.st[k] * nchunks + L.cg);
-#pragma unroll
-        for (int c = 0; c < kChunksPerPass; c++)
-            if ((uint32_t)c < nc) L.acc[c] &= I.u64(base + 8 * c);
-    }
+    for (int c = 0; c < kChunksPerPass; c++)
+        if ((uint32_t)c < nc) L.acc[c] &= I.u64(base + 8 * c);
 }
 
 template <bool kLds>
@@ -174,6 +227,7 @@ __device__ __forceinline__ void frame_reset(const Img<kLds> &I, Lane &L) {
 
 __device__ __forceinline__ void finish(Lane &L, uint8_t v, int32_t rule = -1) {
     L.done = true;
+    L.scan = false;
     L.mode = M_DONE;
     L.verdict = v;
     L.rule = rule;
@@ -192,10 +246,9 @@ __device__ __forceinline__ void headers_done(const Img<kLds> &I, Lane &L) {
         finish(L, V_INCOMPLETE);
     } else {
         L.consumed = (uint32_t)total;
-        const uint32_t max_dfas = HDR_U8(I, max_slot_dfas);
-        const uint32_t ndg = max_dfas ? (max_dfas + kDfasPerPass - 1) / kDfasPerPass : 1;
+        const uint32_t ndg = max((uint32_t)HDR_U8(I, max_slot_dfas), 1u);
         const uint32_t nchunks = HDR_U8(I, nchunks);
-        if (L.dg + 1 < ndg) {  // more DFAs of this chunk group: frame again
+        if (L.dg + 1 < ndg) {  // more DFAs on some slot: frame again for this chunk group
             L.dg++;
             frame_reset(I, L);
         } else {
@@ -244,16 +297,27 @@ __device__ __forceinline__ bool line_done(const Img<kLds> &I, Lane &L) {
     return ok;
 }
 
+// ---------------------------------------------------------------- byte cursor
+// Bytes of the lane's window, read from LDS one at a time (branch-free; the
+// long-token loops below fetch them ahead of use).
+struct Cursor {
+    const uint8_t *slot;
+    uint32_t swz;       // chunk swizzle of this lane, << 4
+    uint32_t w;         // window start position
+    __device__ __forceinline__ uint4 chunk(uint32_t k) const {
+        return *(const uint4 *)(slot + (((k << 4) & (kWin - 16)) ^ swz));
+    }
+    // byte at position p (w <= p < w + kWin)
+    __device__ __forceinline__ uint32_t at(uint32_t p) const { return slot[((p - w) & (kWin - 1)) ^ swz]; }
+};
+
 // ---------------------------------------------------------------- parse one window
-// Consumes [L.pa, min(window end, request end)) from the lane's LDS slot.
-// Every loop has a single exit; errors set the mode to M_DONE, so later
-// blocks fall through (keeps the control flow shallow for the register
-// allocator).
+// Consumes [L.pa, min(window end, request end)).  Every loop has a single
+// exit; errors set the mode to M_DONE so later blocks fall through.
 template <bool kLds>
-__device__ __forceinline__ void parse_window(const Img<kLds> &I, Lane &L, const uint8_t *slot, uint32_t swz) {
-    const uint32_t lim = min((L.pa & ~(kWin - 1)) + kWin, L.lena);
-    // byte at p (p < lim): chunk (p >> 4) & 7 sits at position ((p >> 4) & 7) ^ sw
-    auto B = [&](uint32_t p) -> uint32_t { return slot[(p & (kWin - 1)) ^ swz]; };
+__device__ __forceinline__ void parse_window(const Img<kLds> &I, Lane &L, Cursor &C) {
+    const uint32_t lim = min(L.w + kWin, L.lena);
+    C.w = L.w;
     const uint32_t ncls_name = HDR_U16(I, name_ncls);
     const uint32_t name_cls = HDR_U32(I, name_cls_off), name_trans = HDR_U32(I, name_trans_off);
 
@@ -261,9 +325,9 @@ __device__ __forceinline__ void parse_window(const Img<kLds> &I, Lane &L, const 
     if (L.mode == M_METHOD) {  // 1*tchar SP
         uint32_t c = 0;
         for (; L.pa < lim; L.pa++) {
-            c = B(L.pa);
-            if (I.u8(name_cls + c) == 0) break;  // not a tchar (SP included)
-            slot_step(I, L, c);
+            c = C.at(L.pa);
+            if (!is_tchar(c)) break;
+            dfa_step(I, L, c);
         }
         if (L.pa < lim) {
             if (c != ' ' || L.pa == L.mark) {
@@ -280,10 +344,23 @@ __device__ __forceinline__ void parse_window(const Img<kLds> &I, Lane &L, const 
     }
     if (L.mode == M_TARGET) {  // 1*(VCHAR / obs-text) SP
         uint32_t c = 0;
-        for (; L.pa < lim; L.pa++) {
-            c = B(L.pa);
-            if (c <= 0x20 || c == 0x7F) break;
-            slot_step(I, L, c);
+        if (L.pa < lim) {
+            // software pipeline: byte p+2 and the class of byte p+1 are read
+            // while the transition on byte p is in flight
+            c = C.at(L.pa);
+            uint32_t k = L.dcls ? I.u8(L.dcls + c) : 0;
+            uint32_t c1 = L.pa + 1 < lim ? C.at(L.pa + 1) : 0;
+            while (c > 0x20 && c != 0x7F) {
+                const uint32_t p1 = L.pa + 1;
+                const uint32_t c2 = p1 + 1 < lim ? C.at(p1 + 1) : 0;
+                const uint32_t k1 = L.dcls ? I.u8(L.dcls + c1) : 0;
+                if (L.st) L.st = I.u16(L.dtrans + 2 * (L.st * L.dncls + k));
+                L.pa = p1;
+                if (p1 >= lim) break;
+                c = c1;
+                c1 = c2;
+                k = k1;
+            }
         }
         if (L.pa < lim) {
             if (c != ' ' || L.pa == L.mark) {
@@ -299,7 +376,7 @@ __device__ __forceinline__ void parse_window(const Img<kLds> &I, Lane &L, const 
     }
     if (L.mode == M_VERSION) {  // "HTTP/" DIGIT "." DIGIT CRLF
         for (; L.pa < lim && L.mark < 10; L.pa++, L.mark++) {
-            const uint32_t c = B(L.pa);
+            const uint32_t c = C.at(L.pa);
             const uint32_t want = kVer[L.mark];
             if (want == 0x100 ? c - '0' >= 10u : c != want) break;
         }
@@ -309,7 +386,7 @@ __device__ __forceinline__ void parse_window(const Img<kLds> &I, Lane &L, const 
     // ---- header lines
     while (L.mode >= M_LINE && L.mode < M_DONE && L.pa < lim) {
         if (L.mode == M_LINE) {
-            if (B(L.pa) == '\r') {
+            if (C.at(L.pa) == '\r') {
                 L.pa++;
                 L.mode = M_ENDLF;
             } else {
@@ -319,7 +396,7 @@ __device__ __forceinline__ void parse_window(const Img<kLds> &I, Lane &L, const 
             }
         }
         if (L.mode == M_ENDLF && L.pa < lim) {
-            if (B(L.pa) != '\n') {
+            if (C.at(L.pa) != '\n') {
                 finish(L, V_PARSE_ERROR);
             } else {
                 L.pa++;
@@ -328,11 +405,21 @@ __device__ __forceinline__ void parse_window(const Img<kLds> &I, Lane &L, const 
         }
         if (L.mode == M_NAME) {  // 1*tchar ":"  (obs-fold SP/HT is not a tchar)
             uint32_t c = 0;
-            for (; L.pa < lim; L.pa++) {
-                c = B(L.pa);
-                const uint32_t k = I.u8(name_cls + c);
-                if (k == 0) break;
-                L.nstate = I.u16(name_trans + 2 * (L.nstate * ncls_name + k));
+            if (L.pa < lim) {
+                c = C.at(L.pa);
+                uint32_t k = I.u8(name_cls + c);  // 0 = not a tchar
+                uint32_t c1 = L.pa + 1 < lim ? C.at(L.pa + 1) : 0;
+                while (k != 0) {
+                    const uint32_t p1 = L.pa + 1;
+                    const uint32_t c2 = p1 + 1 < lim ? C.at(p1 + 1) : 0;
+                    const uint32_t k1 = I.u8(name_cls + c1);
+                    L.nstate = I.u16(name_trans + 2 * (L.nstate * ncls_name + k));
+                    L.pa = p1;
+                    if (p1 >= lim) break;
+                    c = c1;
+                    c1 = c2;
+                    k = k1;
+                }
             }
             if (L.pa < lim) {
                 if (c != ':' || L.pa == L.mark) {
@@ -352,7 +439,7 @@ __device__ __forceinline__ void parse_window(const Img<kLds> &I, Lane &L, const 
         }
         if (L.mode == M_OWS) {
             for (; L.pa < lim; L.pa++) {
-                const uint32_t c = B(L.pa);
+                const uint32_t c = C.at(L.pa);
                 if (c != ' ' && c != '\t') break;
             }
             if (L.pa < lim) {
@@ -363,9 +450,8 @@ __device__ __forceinline__ void parse_window(const Img<kLds> &I, Lane &L, const 
                     if (L.slot != kNoSlot) {
                         slot_begin(I, L, L.slot);
                     } else {
-                        L.nd = 0;
-#pragma unroll
-                        for (int k = 0; k < kDfasPerPass; k++) L.st[k] = 0;
+                        L.st = 0;
+                        L.dcls = L.dtrans = 0;
                     }
                     L.in_ows = false;
                     L.clv = 0;
@@ -377,13 +463,10 @@ __device__ __forceinline__ void parse_window(const Img<kLds> &I, Lane &L, const 
         if (L.mode == M_VALUE) {  // a value some rule (or Content-Length framing) looks at
             uint32_t c = 0;
             for (; L.pa < lim; L.pa++) {
-                c = B(L.pa);
+                c = C.at(L.pa);
                 if ((c < 0x20 && c != '\t') || c == 0x7F) break;  // CR ends it; other CTLs are errors
                 const bool ws = c == ' ' || c == '\t';
-                if (ws && !L.in_ows) {
-#pragma unroll
-                    for (int k = 0; k < kDfasPerPass; k++) L.saved[k] = L.st[k];
-                }
+                if (ws && !L.in_ows) L.saved = L.st;
                 L.in_ows = ws;
                 L.cl_ws |= ws;
                 if (!ws) {
@@ -394,16 +477,13 @@ __device__ __forceinline__ void parse_window(const Img<kLds> &I, Lane &L, const 
                         L.cl_bad = true;
                     }
                 }
-                slot_step(I, L, c);
+                dfa_step(I, L, c);
             }
             if (L.pa < lim) {
                 if (c != '\r') {
                     finish(L, V_PARSE_ERROR);
                 } else {
-                    if (L.in_ows) {  // trailing OWS is not part of the value
-#pragma unroll
-                        for (int k = 0; k < kDfasPerPass; k++) L.st[k] = L.saved[k];
-                    }
+                    if (L.in_ows) L.st = L.saved;  // trailing OWS is not part of the value
                     L.pa++;
                     L.mode = M_LF;
                 }
@@ -412,17 +492,15 @@ __device__ __forceinline__ void parse_window(const Img<kLds> &I, Lane &L, const 
         if (L.mode == M_SKIP) {  // a value nobody looks at: find CR (or a CTL / DEL) 16 bytes a step
             uint32_t stop = 0;
             while (L.pa < lim) {
-                const uint32_t k = L.pa >> 4;
-                const uint4 w = *(const uint4 *)(slot + ((L.pa & (kWin - 16)) ^ swz));
-                uint32_t m = nib(stop_bits(w.x)) | nib(stop_bits(w.y)) << 4 | nib(stop_bits(w.z)) << 8 |
-                             nib(stop_bits(w.w)) << 12;
-                m &= 0xFFFFu << (L.pa & 15);
-                const uint32_t cend = (k + 1) * 16;
+                const uint4 w = C.chunk((L.pa - L.w) >> 4);
+                const uint32_t any = stop_bits(w.x) | stop_bits(w.y) | stop_bits(w.z) | stop_bits(w.w);
+                uint32_t m = any ? stop_mask(w) & (0xFFFFu << (L.pa & 15)) : 0;
+                const uint32_t cend = L.pa - (L.pa & 15) + 16;
                 if (cend > lim) m &= (1u << (lim & 15)) - 1u;  // lim inside this chunk
-                const uint32_t p = k * 16 + (uint32_t)__builtin_ctz(m | 0x10000u);
+                const uint32_t p = cend - 16 + (uint32_t)__builtin_ctz(m | 0x10000u);
                 L.pa = min(p, lim);
                 if (p < cend) {
-                    const uint32_t c = B(p);
+                    const uint32_t c = byte_of(w, p & 15);
                     if (c != '\t') {
                         stop = c | 0x100;
                         break;
@@ -437,10 +515,12 @@ __device__ __forceinline__ void parse_window(const Img<kLds> &I, Lane &L, const 
                     L.pa++;
                     L.mode = M_LF;
                 }
+            } else if (L.pa < L.lena) {
+                L.scan = true;  // the value continues past the window: the wave scans it
             }
         }
         if (L.mode == M_LF && L.pa < lim) {
-            if (B(L.pa) != '\n') {
+            if (C.at(L.pa) != '\n') {
                 finish(L, V_PARSE_ERROR);
             } else {
                 L.pa++;
@@ -451,26 +531,111 @@ __device__ __forceinline__ void parse_window(const Img<kLds> &I, Lane &L, const 
     }
 }
 
-// ---------------------------------------------------------------- DMA
-// Copies, for every working lane t, chunks [lo, hi] of the 128-byte window at
-// `win` into LDS slot t (chunk c stored at position c ^ s(t)).  packed =
-// window address | hi << 4 | lo << 1 | 1 (addresses are 128-byte aligned).
+// ---------------------------------------------------------------- window DMA
+// For every lane t with a window to load: chunks [0, hi] of the 256-byte
+// window at address `win` into LDS slot t (chunk c stored at position
+// c ^ (t & 15)).  packed = window address | hi (addresses are 16-byte aligned;
+// 0 = nothing to load).
 __device__ __forceinline__ void dma_windows(uint8_t *wave_lds, uint64_t packed, uint32_t lane) {
     const uint32_t plo = (uint32_t)packed, phi = (uint32_t)(packed >> 32);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's earlier LDS reads have landed
 #pragma unroll
-    for (int j = 0; j < 8; j++) {
-        const int t = 8 * j + (int)(lane >> 3);
+    for (int j = 0; j < (int)kWinChunks; j++) {
+        const int t = (int)(kWinPerInst * j + lane / kLanesPerWin);
         const uint32_t tlo = __shfl(plo, t), thi = __shfl(phi, t);
-        const uint32_t c = (lane & 7) ^ (((uint32_t)t >> 1) & 7);
-        const uint32_t clo = (tlo >> 1) & 7, chi = (tlo >> 4) & 7;
-        if ((tlo & 1) && c >= clo && c <= chi) {
-            const uint8_t *src = (const uint8_t *)((((uint64_t)thi) << 32) | (tlo & ~127u)) + 16 * c;
+        const uint32_t c = (lane % kLanesPerWin) ^ win_swizzle((uint32_t)t);
+        if ((tlo | thi) && c <= (tlo & 15)) {
+            const uint8_t *src = (const uint8_t *)((((uint64_t)thi) << 32) | (tlo & ~15u)) + 16 * c;
             __builtin_amdgcn_global_load_lds((const void *)src,
                                              (__attribute__((address_space(3))) void *)(wave_lds + j * 1024), 16, 0, 0);
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// ---------------------------------------------------------------- long-value scan
+// Lanes with L.scan set: find the first stop byte (< 0x20 other than HT, or
+// DEL) at or after L.pa in the lane's request, reading 1 KiB pieces of up to
+// kScanBatch lanes' requests together with coalesced loads.  The lane's pa
+// moves there (the next window starts at it); no stop before the request end
+// => INCOMPLETE.
+// The pieces land in the wave's window area (free between rounds) by LDS-DMA,
+// so all of a batch's loads are in flight together.
+__device__ __forceinline__ void scan_values(Lane &L, uint32_t lane, uint8_t *wave_lds) {
+    uint64_t pending = __ballot(L.scan);
+    while (pending) {
+        uint32_t who[kScanBatch], tpa[kScanBatch], tlen[kScanBatch];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // earlier LDS reads of the area have landed
+#pragma unroll
+        for (int i = 0; i < kScanBatch; i++) {
+            who[i] = 64;
+            tpa[i] = tlen[i] = 0;
+            if (pending) {
+                const uint32_t t = (uint32_t)__builtin_ctzll(pending);
+                pending &= pending - 1;
+                who[i] = t;
+                tpa[i] = (uint32_t)__builtin_amdgcn_readlane((int)L.pa, (int)t);
+                tlen[i] = (uint32_t)__builtin_amdgcn_readlane((int)L.lena, (int)t);
+                const uint32_t blo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)L.base, (int)t);
+                const uint32_t bhi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(L.base >> 32), (int)t);
+                const uint32_t q = (tpa[i] & ~15u) + 16 * lane;  // this lane's chunk of the piece
+                if (q < tlen[i])
+                    __builtin_amdgcn_global_load_lds((const void *)((const uint8_t *)((((uint64_t)bhi) << 32) | blo) + q),
+                                                     (__attribute__((address_space(3))) void *)(wave_lds + i * 1024),
+                                                     16, 0, 0);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int i = 0; i < kScanBatch; i++) {
+            const uint32_t t = who[i];
+            if (t >= 64) continue;
+            const uint32_t pa = tpa[i], lena = tlen[i];
+            const uint32_t q = (pa & ~15u) + 16 * lane;
+            const uint4 vi = *(const uint4 *)(wave_lds + i * 1024 + 16 * lane);
+            // vector part: does this lane's chunk hold any byte < 0x20 or DEL?
+            // (bytes before pa / past the request end and HT are sorted out
+            // below, in scalar code, for the candidate lanes only)
+            const uint32_t any = stop_bits(vi.x) | stop_bits(vi.y) | stop_bits(vi.z) | stop_bits(vi.w);
+            uint64_t cand = __ballot(q < lena && any != 0);
+            uint32_t res = 0;   // new position for lane t
+            bool hit = false, again = false;
+            while (cand) {  // wave-uniform; usually one iteration
+                const uint32_t fl = (uint32_t)__builtin_ctzll(cand);
+                cand &= cand - 1;
+                const uint32_t cb = (pa & ~15u) + 16 * fl;  // position of the candidate chunk
+                const uint32_t s0 = (uint32_t)__builtin_amdgcn_readlane((int)vi.x, (int)fl);
+                const uint32_t s1 = (uint32_t)__builtin_amdgcn_readlane((int)vi.y, (int)fl);
+                const uint32_t s2 = (uint32_t)__builtin_amdgcn_readlane((int)vi.z, (int)fl);
+                const uint32_t s3 = (uint32_t)__builtin_amdgcn_readlane((int)vi.w, (int)fl);
+                const uint32_t lo = cb < pa ? pa - cb : 0, hi = min(lena - cb, 16u);
+                uint32_t m = (nib(stop_bits(s0)) | nib(stop_bits(s1)) << 4 | nib(stop_bits(s2)) << 8 |
+                              nib(stop_bits(s3)) << 12) & (0xFFFFu << lo) & ((1u << hi) - 1u);
+                while (m) {  // HT is allowed inside values
+                    const uint32_t b = (uint32_t)__builtin_ctz(m);
+                    const uint32_t d = b < 4 ? s0 : b < 8 ? s1 : b < 12 ? s2 : s3;
+                    if (((d >> (8 * (b & 3))) & 0xFF) != '\t') break;
+                    m &= m - 1;
+                }
+                if (m) {
+                    res = cb + (uint32_t)__builtin_ctz(m);
+                    hit = true;
+                    break;
+                }
+            }
+            if (!hit) {
+                res = (pa & ~15u) + 1024;  // nothing in this piece
+                again = res < lena;
+                if (!again) res = lena;
+            }
+            if (lane == t) {
+                L.pa = max(res, L.pa);
+                if (hit) L.scan = false;
+                else if (!again) finish(L, V_INCOMPLETE);
+            }
+            if (again) pending |= 1ull << t;
+        }
+    }
 }
 
 struct Out {
@@ -499,33 +664,49 @@ __device__ __forceinline__ void emit(const Lane &L, const Out &O) {
 template <bool kLds>
 __device__ __forceinline__ void run_tile(Lane &L, const uint8_t *img, uint8_t *wave_lds, uint32_t lane, const Out &O) {
     const Img<kLds> I{img};
+    L.scan = false;
     if (!L.done) {
         L.cg = 0;
         L.dg = 0;
         acc_init(I, L);
         frame_reset(I, L);
-        if (L.lena == L.a0) {
-            finish(L, V_INCOMPLETE);
-            emit(L, O);
-        }
+        if (L.lena == L.a0) finish(L, V_INCOMPLETE);
     }
-    const uint8_t *slot = wave_lds + lane * kWin;
-    const uint32_t swz = ((lane >> 1) & 7) << 4;
+    Cursor C;
+    C.slot = wave_lds + lane * kWin;
+    C.swz = win_swizzle(lane) << 4;
+    PH_DECL
     while (__any(!L.done)) {
         uint64_t packed = 0;
         if (!L.done) {
-            const uint32_t w = L.pa & ~(kWin - 1);
-            const uint32_t lo = (L.pa - w) >> 4;
-            const uint32_t hi = min(L.lena - 1 - w, kWin - 1) >> 4;
-            packed = (L.wb + w) | (hi << 4) | (lo << 1) | 1u;
+            L.w = L.pa & ~15u;
+            const uint32_t hi = min(L.lena - 1 - L.w, kWin - 1) >> 4;
+            packed = (L.base + L.w) | hi;
         }
+        PH_MARK(3);
         dma_windows(wave_lds, packed, lane);
+        PH_MARK(0);
         if (!L.done) {
-            parse_window(I, L, slot, swz);
-            if (!L.done && L.pa >= L.lena) finish(L, V_INCOMPLETE);
-            if (L.done) emit(L, O);
+            parse_window(I, L, C);
+            if (!L.done && !L.scan && L.pa >= L.lena) finish(L, V_INCOMPLETE);
         }
+        PH_MARK(1);
+        PH_COUNT(5, __builtin_popcountll(__ballot(L.scan)));
+        scan_values(L, lane, wave_lds);
+        PH_MARK(2);
+        if (L.done && L.owed) {
+            emit(L, O);
+            L.owed = false;
+        }
+        PH_COUNT(4, 1);
     }
+    if (L.done && L.owed) {  // answered before any round
+        emit(L, O);
+        L.owed = false;
+    }
+    PH_MARK(3);
+    PH_COUNT(6, 1);
+    PH_FLUSH(lane);
 }
 
 }  // namespace
@@ -567,12 +748,13 @@ __global__ __launch_bounds__(kBlock) void http_classify_kernel(
         Lane L;
         L.idx = tile * 64 + lane;
         L.done = true;
+        L.owed = false;
         L.verdict = V_UNSUPPORTED;
         L.rule = -1;
         L.consumed = 0;
         L.mode = M_DONE;
-        L.wb = 0;
-        L.a0 = L.lena = L.pa = 0;
+        L.base = 0;
+        L.a0 = L.pa = L.w = L.lena = 0;
         const uint8_t *img = kHot ? s_img : nullptr;
         if (L.idx < n) {
             const uint32_t ci = conn_ids[L.idx];
@@ -582,17 +764,17 @@ __global__ __launch_bounds__(kBlock) void http_classify_kernel(
             const bool mine = !(conn.proto == PROTO_KAFKA || conn.proto == PROTO_MEMCACHE);
             const bool http = mine && conn.proto == PROTO_HTTP && conn.ruleset >= 0 && (uint32_t)conn.ruleset < T.nrulesets;
             const bool is_hot = http && hot_ok && conn.ruleset == hot;
-            if (mine && !http && (kHot || !hot_ok)) emit(L, O);  // unsupported connection: answered now
+            if (mine && !http && (kHot || !hot_ok)) L.owed = true;  // unsupported connection: answered as is
             if (http && is_hot == kHot) {
                 const uint64_t off = offs[L.idx];
                 const uint32_t len = lens[L.idx];
                 const uint64_t a = (uint64_t)(arena + off);
-                L.wb = a & ~(uint64_t)127;
-                L.a0 = (uint32_t)(a & 127);
-                L.lena = L.a0 + len;
-                if (L.lena < L.a0) L.lena = 0xFFFFFFFFu;  // len > 4 GiB - 128: framing stops there
+                L.base = a & ~(uint64_t)15;
+                L.a0 = (uint32_t)(a & 15);
+                L.lena = len > 0xFFFFFF00u ? 0xFFFFFF00u + L.a0 : L.a0 + len;  // > 4 GiB - 256: framing stops there
                 if (!kHot) img = T.images + T.rulesets[conn.ruleset].image_off;
                 L.done = false;
+                L.owed = true;
             }
         }
         run_tile<kHot>(L, img, wave_lds, lane, O);
@@ -610,7 +792,7 @@ __global__ __launch_bounds__(kBlock) void http_classify_kernel(
 }
 
 // Host-side launcher (called from the C-ABI): persistent grids of one
-// 1024-thread workgroup per CU; the hot-rule-set kernel, then (only if some
+// 512-thread workgroup per CU; the hot-rule-set kernel, then (only if some
 // HTTP connection uses another rule set) the general one.
 hipError_t LaunchHttpClassify(const uint8_t *arena, const uint64_t *offs, const uint32_t *lens, const uint32_t *conn_ids,
                               uint32_t n, const DevConn *conns, uint32_t nconns, const HttpTables &T, bool any_cold,
@@ -636,5 +818,18 @@ hipError_t LaunchHttpClassify(const uint8_t *arena, const uint64_t *offs, const 
                            conn_ids, n, conns, nconns, T, verdict, rule, consumed, counters, ncounters);
     return hipGetLastError();
 }
+
+#ifdef L7G_PHASE_TIMING
+hipError_t HttpPhaseTimes(uint64_t *out, bool reset) {
+    hipError_t rc = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), sizeof(unsigned long long) * 8);
+    if (rc == hipSuccess && reset) {
+        static const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        rc = hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof z);
+    }
+    return rc;
+}
+#else
+hipError_t HttpPhaseTimes(uint64_t *, bool) { return hipErrorNotSupported; }
+#endif
 
 }  // namespace l7

@@ -92,6 +92,13 @@ class Engine:
             raise RuntimeError(f"l7g_classify_host failed: HIP error {rc}")
         return v, r, c
 
+    def phase_times(self, reset=True):
+        """Per-phase cycle totals of the HTTP kernel (timing build only), or None."""
+        out = np.zeros(8, np.uint64)
+        if self._lib.l7g_debug_phase_times(self._h, out.ctypes.data, 1 if reset else 0) != 0:
+            return None
+        return out
+
     def stats(self):
         s = _lib.Stats()
         self._lib.l7g_stats(self._h, C.byref(s))

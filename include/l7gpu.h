@@ -98,6 +98,13 @@ int l7g_classify_host(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, c
 
 int l7g_stats(l7g_engine *e, l7g_stats_t *out);
 
+/* Profiling hook: per-phase cycle totals of the HTTP kernel (slots: 0 window
+ * DMA, 1 parse, 2 long-value scan, 3 other, 4 rounds, 5 scanned values,
+ * 6 tiles), summed over waves since the last reset.  Only the timing build
+ * (libl7gpu_timing.so, -DL7G_PHASE_TIMING) records them; the product build
+ * returns hipErrorNotSupported. */
+int l7g_debug_phase_times(l7g_engine *e, uint64_t *out8, int reset);
+
 /* Test hook: compile one Go regexp with the product's DFA compiler and run
  * the compiled tables on the host.  Returns 1 match, 0 no match, -1 compile
  * error (err set).  anchored: 1 = full match, 0 = Go regexp.Match. */

@@ -24,6 +24,7 @@ def timeit(eng, w, steps=10):
     d_k = torch.empty(n, dtype=torch.int32, device=dev)
     eng.update_policy(w.policy)
     eng.set_connections(w.conns)
+    eng.phase_times(reset=True)
     s = torch.cuda.current_stream()
     args = [t.data_ptr() for t in (d_a, d_o, d_l, d_c)] + [n] + [t.data_ptr() for t in (d_v, d_r, d_k)]
     for _ in range(3):
@@ -38,6 +39,15 @@ def timeit(eng, w, steps=10):
     ms = e0.elapsed_time(e1) / steps
     gbps = w.algorithmic_bytes() / (ms / 1e3) / 1e9
     hist = np.bincount(d_v.cpu().numpy(), minlength=5).tolist()
+    ph = eng.phase_times(reset=True)
+    if ph is not None:
+        eng.classify_device(*args, stream=s.cuda_stream)
+        torch.cuda.synchronize()
+        ph = eng.phase_times(reset=True).astype(np.float64)
+        cyc = ph[:4].sum()
+        hist = hist + [f"dma {ph[0]/cyc:.2f} parse {ph[1]/cyc:.2f} scan {ph[2]/cyc:.2f} other {ph[3]/cyc:.2f} "
+                       f"rounds/tile {ph[4]/max(ph[6],1):.2f} scans/tile {ph[5]/max(ph[6],1):.1f} "
+                       f"wave-cycles/tile {cyc/max(ph[6],1):.0f}"]
     return ms, gbps, hist
 
 
@@ -50,6 +60,7 @@ def variant(name, reqs, policy, nconns=1024):
 
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
+    only = sys.argv[2].split(",") if len(sys.argv) > 2 else None  # variant letters a..e
     eng = Engine(0)
     base = gen.http_requests(n, gen.SEED_BASE + 2)
     heads = [r[: r.index(b"X-Pad: ")] + b"\r\n" for r in base]
@@ -62,6 +73,8 @@ def main():
         ("no rules heads only", variant("e", heads, allow_all)),
     ]
     for name, w in rows:
+        if only and w.name not in only:
+            continue
         ms, gbps, hist = timeit(eng, w)
         print(f"{name:24s} n={w.n} bytes={w.lengths.astype(np.int64).sum()/w.n:7.1f}/req  {ms:8.4f} ms  "
               f"{gbps:8.1f} GB/s  {ms / w.n * 1e6:7.4f} ms/1M  hist={hist}", flush=True)
