@@ -155,6 +155,37 @@ static int load_kafka(ld *l, const jnode *j, ref_kafka_rule *k) {
     return 0;
 }
 
+/* memcache.L7RuleParser (proxylib/memcached/parser.go:114-148): keys command /
+ * keyExact / keyPrefix / keyRegex; anything else, or a key match without a
+ * known command, is a ParseError (policy NACK).  An unknown command without
+ * key matches leaves an "empty" rule that matches everything. */
+static int load_mc_rule(ld *l, const jnode *j, ref_mc_rule *m) {
+    const jnode *kv = jget(j, "rule");
+    if (!kv) kv = j;
+    if (kv->type != JN_OBJ) return 0;
+    int found = 0;
+    for (int i = 0; i < kv->n; i++) {
+        const char *k = kv->keys[i];
+        const jnode *v = kv->items[i];
+        if (v->type != JN_STR) return lerr(l, "NPDS: memcache rule value is not a string%s", NULL);
+        if (!strcmp(k, "command")) { m->group = ref_mc_group(v->str, v->slen); found = m->group != NULL; }
+        else if (!strcmp(k, "keyExact")) { free(m->key_exact); m->key_exact = dupn(v->str, v->slen); m->key_exact_len = v->slen; }
+        else if (!strcmp(k, "keyPrefix")) { free(m->key_prefix); m->key_prefix = dupn(v->str, v->slen); m->key_prefix_len = v->slen; }
+        else if (!strcmp(k, "keyRegex")) {
+            char e[256];
+            ref_re_free(m->key_re);
+            m->key_re = ref_re_compile(v->str, v->slen, e, sizeof e);
+            if (!m->key_re) return lerr(l, "%s", e);
+        } else return lerr(l, "NPDS: Unsupported key: %s", k);
+    }
+    if (!found) {
+        if (m->key_exact_len > 0 || m->key_prefix_len > 0 || m->key_re)
+            return lerr(l, "NPDS: command not specified but key was provided%s", NULL);
+        m->empty = 1;
+    }
+    return 0;
+}
+
 static int load_rule(ld *l, const jnode *j, ref_pnp_rule *r) {
     memset(r, 0, sizeof *r);
     const jnode *rp = jget(j, "remote_policies");
@@ -195,7 +226,11 @@ static int load_rule(ld *l, const jnode *j, ref_pnp_rule *r) {
     } else if (l7) {
         r->l7type = L7T_L7; r->nl7 = l7->n;
         r->l7 = calloc((size_t)l7->n + 1, sizeof(ref_mc_rule));
-        for (int i = 0; i < l7->n; i++) r->l7[i].id = l->next_id++;
+        int mc = r->l7proto && !strcmp(r->l7proto, "memcache");
+        for (int i = 0; i < l7->n; i++) {
+            r->l7[i].id = l->next_id++;
+            if (mc && load_mc_rule(l, l7->items[i], &r->l7[i]) < 0) return -1;
+        }
     }
     return 0;
 }
@@ -219,9 +254,19 @@ static int load_ports(ld *l, const jnode *arr, ref_port **out, int *nout) {
         if (rs && rs->type == JN_ARR) {
             ps[i].nrules = rs->n;
             ps[i].rules = calloc((size_t)rs->n + 1, sizeof(ref_pnp_rule));
+            const char *first = NULL;
             for (int k = 0; k < rs->n; k++) {
                 if (load_rule(l, rs->items[k], &ps[i].rules[k]) < 0) return -1;
                 if (ps[i].rules[k].l7type == L7T_HTTP) ps[i].has_http = 1;
+                /* proxylib: "Mismatching L7 types on the same port" (policymap.go:137-143) */
+                const ref_pnp_rule *pr = &ps[i].rules[k];
+                static const char *ONEOF[] = {"", "PortNetworkPolicyRule_HttpRules", "PortNetworkPolicyRule_KafkaRules",
+                                              "PortNetworkPolicyRule_L7Rules"};
+                const char *name = pr->l7proto && *pr->l7proto ? pr->l7proto : ONEOF[pr->l7type];
+                if (*name) {
+                    if (!first) first = name;
+                    else if (strcmp(first, name)) return lerr(l, "NPDS: Mismatching L7 types on the same port%s", NULL);
+                }
             }
         }
         if (ps[i].tcp)
@@ -240,6 +285,7 @@ static void free_ports(ref_port *ps, int n) {
                 free(r->http[q].m);
             }
             for (int q = 0; q < r->nkafka; q++) { free(r->kafka[q].topic); free(r->kafka[q].client); }
+            for (int q = 0; q < r->nl7; q++) { free(r->l7[q].key_exact); free(r->l7[q].key_prefix); ref_re_free(r->l7[q].key_re); }
             free(r->http); free(r->kafka); free(r->l7); free(r->remotes); free(r->l7proto);
         }
         free(ps[i].rules);
@@ -317,6 +363,7 @@ static void *run(void *arg) {
             const uint8_t *b = j->arena + j->off[i];
             if (c->proto == L7_PROTO_HTTP) ref_http_verdict(j->p, c, b, j->len[i], &o);
             else if (c->proto == L7_PROTO_KAFKA) ref_kafka_verdict(j->p, c, b, j->len[i], &o);
+            else if (c->proto == L7_PROTO_MEMCACHE) ref_memcache_verdict(j->p, c, b, j->len[i], &o);
             else o.verdict = L7_UNSUPPORTED;
         }
         j->verdict[i] = o.verdict; j->rule[i] = o.rule; j->consumed[i] = o.consumed;

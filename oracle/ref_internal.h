@@ -40,8 +40,11 @@ typedef struct {
     int id;
 } ref_kafka_rule;
 
-typedef struct {
-    char *command; char *key_exact; char *key_prefix; ref_re *key_re;
+typedef struct {  /* memcache.Rule (proxylib/memcached/parser.go:35-44) */
+    const void *group;                 /* MemcacheOpCodeMap entry, NULL = command not found */
+    char *key_exact; size_t key_exact_len;
+    char *key_prefix; size_t key_prefix_len;
+    ref_re *key_re;
     int empty; int id;
 } ref_mc_rule;
 
@@ -63,6 +66,8 @@ struct ref_policy { ref_netpolicy *p; int np; int nrules_total; };
 typedef struct { uint8_t verdict; int32_t rule; uint32_t consumed; } ref_out_t;
 void ref_http_verdict(const ref_policy *pol, const ref_conn_t *c, const uint8_t *buf, uint32_t len, ref_out_t *o);
 void ref_kafka_verdict(const ref_policy *pol, const ref_conn_t *c, const uint8_t *buf, uint32_t len, ref_out_t *o);
+void ref_memcache_verdict(const ref_policy *pol, const ref_conn_t *c, const uint8_t *buf, uint32_t len, ref_out_t *o);
+const void *ref_mc_group(const char *name, size_t n);
 
 int ref_port_lookup(const ref_netpolicy *np, int ingress, uint32_t port, const ref_port **exact, const ref_port **wild);
 int ref_remote_ok(const ref_pnp_rule *r, uint64_t id);

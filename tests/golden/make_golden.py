@@ -12,6 +12,9 @@ Sources (file:line in the reference):
   http_xlate pkg/envoy/server_test.go:38-96 (getHTTPRule expected HeaderMatchers)
   kafka      pkg/kafka/policy_test.go:52-127 (MatchesRule assertions)
              pkg/proxy/kafka_test.go:167-258 (produce allowedTopic ok / disallowedTopic denied)
+  memcache   proxylib/proxylib_memcached_test.go:30-118 (request bytes), :120-161 (policy
+             "bm1", port 80, remotes 1/3/4, connection src 1), :169-732 (request-side
+             CheckOnData expectations: PASS/DROP n => ALLOW/DENY consumed n, MORE => INCOMPLETE)
 Kafka requests are encoded to wire bytes with cilium_amd.gen's restatement of
 the optiopay encoders (valid CRCs), exactly what the reference decoder reads.
 """
@@ -160,6 +163,81 @@ def kafka_section():
     return {"requests": reqs, "cases": cases}
 
 
+MC_TEXT = {
+    "setHelloText": b"set key 0 0 5\r\nhello\r\n",
+    "getKeysText": b"get key1 key2 key3\r\n",
+    "gatKeysText": b"gat 5 key1 key2 key3\r\n",
+    "getResponse": b"VALUE key3 0 4\r\nxDDD\r\nVALUE key4 0 3\r\nxDD\r\nEND\r\n",
+    "deleteText": b"delete key\r\n",
+    "incrText": b"incr key 5\r\n",
+    "touchText": b"touch key 55\r\n",
+    "slabsText": b"slabs automove 1\r\n",
+    "lruCrawlerText": b"lru_crawler metadump all\r\n",
+    "statsText": b"stats\r\n",
+    "flushAllText": b"flush_all 15\r\n",
+    "watchText": b"watch mutations\r\n",
+}
+MC_TEXT["getResponse[:5]"] = MC_TEXT["getResponse"][:5]
+MC_TEXT["getKeysText[:-1]"] = MC_TEXT["getKeysText"][:-1]
+MC_BIN = {
+    "getHello": bytes([128, 0, 0, 5, 0, 0, 0, 0, 0, 0, 0, 5, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0]) + b"Hello",
+    "setHello": bytes([128, 1, 0, 5, 8, 0, 0, 0, 0, 0, 0, 18, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
+                       0, 0, 0, 0, 0, 0, 0, 0]) + b"HelloWorld",
+}
+MC_BIN["getHello[:10]"] = MC_BIN["getHello"][:10]
+MC_BIN["getHello[:26]"] = MC_BIN["getHello"][:26]
+
+
+def memcache_section():
+    E = lambda cmd, **k: dict({"command": cmd}, **k)  # noqa: E731
+    ex = lambda cmd, key="": E(cmd, keyExact=key)  # noqa: E731
+    T = [  # (test name, l7 rule list (None = no l7 rule block), [(request, expect)])
+        ("text set pass", [ex("set")], [("setHelloText", "ALLOW")]),
+        ("text set drop", [ex("set", "trolo")], [("setHelloText", "DENY")]),
+        ("text get pass", [ex("get")], [("getKeysText", "ALLOW"), ("getKeysText", "ALLOW")]),
+        ("text get more", [ex("get")], [("getResponse[:5]", "INCOMPLETE")]),
+        ("text get drop", [ex("set")], [("getKeysText", "DENY")]),
+        ("text gat pass", [ex("gat")], [("gatKeysText", "ALLOW"), ("gatKeysText", "ALLOW")]),
+        ("text gat more", [ex("gat")], [("getResponse[:5]", "INCOMPLETE")]),
+        ("text gat drop", [ex("set")], [("gatKeysText", "DENY")]),
+        ("text delete pass", [ex("delete")], [("deleteText", "ALLOW")]),
+        ("text delete drop", [ex("set")], [("deleteText", "DENY")]),
+        ("text incr pass", [ex("incr")], [("incrText", "ALLOW")]),
+        ("text incr drop", [ex("incr", "otherKey")], [("incrText", "DENY")]),
+        ("text touch pass", [ex("touch", "key")], [("touchText", "ALLOW")]),
+        ("text touch drop", [ex("touch", "otherKey")], [("touchText", "DENY")]),
+        ("text slabs pass", [E("slabs")], [("slabsText", "ALLOW")]),
+        ("text slabs drop", [ex("touch", "otherKey")], [("slabsText", "DENY")]),
+        ("text lru_crawler response req more and pass", [E("lru_crawler")], [("lruCrawlerText", "ALLOW")]),
+        ("text stats response req more and pass", [E("stats")], [("statsText", "ALLOW")]),
+        ("text flush_all pass", [E("flush_all")], [("flushAllText", "ALLOW")]),
+        ("text flush_all denied", [E("get")], [("flushAllText", "DENY")]),
+        ("text watch passed", [E("watch")], [("watchText", "ALLOW")]),
+        ("text partial linefeed", [ex("set")], [("getKeysText[:-1]", "INCOMPLETE")]),
+        ("text set pass on empty rule", [], [("setHelloText", "ALLOW")]),
+        ("bin get pass exact key", [ex("get", "Hello")], [("getHello", "ALLOW")]),
+        ("bin get pass prefix key", [E("get", keyPrefix="Hell")], [("getHello", "ALLOW")]),
+        ("bin get pass regex key", [E("get", keyRegex="^.el.o$")], [("getHello", "ALLOW")]),
+        ("bin get drop", [ex("set")], [("getHello", "DENY")]),
+        ("bin get more", [ex("get")], [("getHello[:10]", "INCOMPLETE")]),
+        ("bin get split", [ex("get")], [("getHello", "ALLOW")]),
+        ("bin get remaining key", [ex("get")], [("getHello[:26]", "INCOMPLETE")]),
+        ("bin set drop and allow", [ex("set")], [("setHello", "ALLOW"), ("getHello", "DENY")]),
+    ]
+    reqs = {k: v.hex() for k, v in {**MC_TEXT, **MC_BIN}.items()}
+    cases = []
+    for name, rules, checks in T:
+        # the reference writes an empty `l7_rules: < l7_rules: < > >` for the "empty rule" case:
+        # one L7 rule with an empty map (=> empty rule, matches everything)
+        cases.append({"name": name, "l7_rules": rules if rules else [{}], "checks": [
+            {"request": r, "expect": e,
+             "consumed": len(bytes.fromhex(reqs[r])) if e != "INCOMPLETE" else 0} for r, e in checks]})
+    return {"ref": "proxylib/proxylib_memcached_test.go:30-732", "requests": reqs, "cases": cases,
+            "policy_template": {"name": "bm1", "policy": 2, "port": 80, "remote_policies": [1, 3, 4],
+                                "l7_proto": "memcache"},
+            "conn": {"policy_name": "bm1", "port": 80, "ingress": True, "src_id": 1, "dst_id": 2}}
+
+
 def main():
     data = {
         "note": "Known-answer tests transcribed from the reference's own tests; 'expect' is the reference's asserted outcome.",
@@ -167,6 +245,7 @@ def main():
         "http": http_section(),
         "http_translation": xlate_section(),
         "kafka": kafka_section(),
+        "memcache": memcache_section(),
     }
     with open(OUT, "w") as f:
         json.dump(data, f, indent=1, sort_keys=True)

@@ -4,9 +4,10 @@ import numpy as np
 import pytest
 
 from cilium_amd import api, gen
-from cilium_amd._lib import ALLOW, DENY, PROTO_HTTP, PROTO_KAFKA
+from cilium_amd._lib import ALLOW, DENY, INCOMPLETE, PARSE_ERROR, PROTO_HTTP, PROTO_KAFKA, PROTO_MEMCACHE
 
 VERDICT = {"ALLOW": ALLOW, "DENY": DENY}
+VERDICT_ALL = {"ALLOW": ALLOW, "DENY": DENY, "INCOMPLETE": INCOMPLETE, "PARSE_ERROR": PARSE_ERROR}
 
 
 def test_regex_kats(oracle, kats):
@@ -79,3 +80,49 @@ def test_kafka_empty_rule_list_is_wildcard_free(oracle):
     c["src_id"] = 5
     v, r, _ = pol.classify([c], np.frombuffer(req, np.uint8), [0], [len(req)], [0])
     assert v[0] == ALLOW and r[0] == 0
+
+
+def memcache_policy(M, l7_rules):
+    t = M["policy_template"]
+    return api.policy_set(api.network_policy(t["name"], t["policy"], ingress=[
+        (t["port"], [api.port_rule(remote_policies=t["remote_policies"], l7proto=t["l7_proto"], l7=l7_rules)])]))
+
+
+def _mc_conn(pol, M):
+    c = M["conn"]
+    return {"policy": pol.names[c["policy_name"]], "port": c["port"], "ingress": int(c["ingress"]),
+            "proto": PROTO_MEMCACHE, "src_id": c["src_id"], "dst_id": c["dst_id"]}
+
+
+def test_memcache_kats(oracle, kats):
+    M = kats["memcache"]
+    assert len(M["cases"]) == 31
+    for case in M["cases"]:
+        pol = oracle.Policy(memcache_policy(M, case["l7_rules"]))
+        for chk in case["checks"]:
+            b = bytes.fromhex(M["requests"][chk["request"]])
+            v, r, cons = pol.classify([_mc_conn(pol, M)], np.frombuffer(b, np.uint8), [0], [len(b)], [0])
+            assert VERDICT_ALL[chk["expect"]] == int(v[0]), (case["name"], chk)
+            assert int(cons[0]) == chk["consumed"], (case["name"], chk)
+
+
+def test_memcache_wrong_remote_denied(oracle, kats):
+    M = kats["memcache"]
+    pol = oracle.Policy(memcache_policy(M, [{"command": "set"}]))
+    b = bytes.fromhex(M["requests"]["setHelloText"])
+    c = _mc_conn(pol, M)
+    c["src_id"] = 2  # not in remote_policies 1/3/4
+    v, _, _ = pol.classify([c], np.frombuffer(b, np.uint8), [0], [len(b)], [0])
+    assert v[0] == DENY
+
+
+@pytest.mark.parametrize("rule,msg", [
+    ({"command": "set", "bogus": "x"}, "Unsupported key: bogus"),
+    ({"keyExact": "k"}, "command not specified but key was provided"),
+    ({"command": "nosuch", "keyPrefix": "k"}, "command not specified but key was provided"),
+    ({"command": "get", "keyRegex": "a**"}, "invalid nested repetition operator"),
+])
+def test_memcache_rule_parse_errors(oracle, kats, rule, msg):
+    # memcache.L7RuleParser (proxylib/memcached/parser.go:114-148): ParseError => policy NACK
+    with pytest.raises(ValueError, match=msg):
+        oracle.Policy(memcache_policy(kats["memcache"], [rule]))
