@@ -29,7 +29,8 @@ class Stats(C.Structure):
         "policies", "rules", "http_rulesets", "http_chunks", "http_dfas", "http_dfa_states",
         "kafka_rulesets", "kafka_rules", "kafka_topics")] + [
         ("table_bytes", C.c_uint64), ("http_image_bytes", C.c_uint64), ("hot_ruleset", C.c_int32),
-        ("hot_image_bytes", C.c_uint32)]
+        ("hot_image_bytes", C.c_uint32)] + [
+        (n, C.c_uint32) for n in ("mc_rulesets", "mc_rules", "mc_dfas", "mc_dfa_states")]
 
 
 EXPORTS = (

@@ -12,6 +12,7 @@
 #include "device_tables.h"
 #include "engine/http_compile.h"
 #include "engine/kafka_compile.h"
+#include "engine/mc_compile.h"
 #include "policy/policy.h"
 #include "regex/re_dfa.h"
 
@@ -24,6 +25,10 @@ hipError_t LaunchKafkaClassify(const uint8_t *arena, const uint64_t *offs, const
                                uint32_t n, const DevConn *conns, uint32_t nconns, const KafkaTables &T,
                                uint8_t *verdict, int32_t *rule, uint32_t *consumed, uint64_t *counters,
                                uint32_t ncounters, hipStream_t stream);
+hipError_t LaunchMemcacheClassify(const uint8_t *arena, const uint64_t *offs, const uint32_t *lens,
+                                  const uint32_t *conn_ids, uint32_t n, const DevConn *conns, uint32_t nconns,
+                                  const McTables &T, uint8_t *verdict, int32_t *rule, uint32_t *consumed,
+                                  uint64_t *counters, uint32_t ncounters, hipStream_t stream);
 hipError_t HttpPhaseTimes(uint64_t *out, bool reset);
 }  // namespace l7
 
@@ -35,6 +40,7 @@ struct l7g_engine {
     std::unique_ptr<PolicySet> ps;
     std::unique_ptr<HttpCompiler> hc;
     std::unique_ptr<KafkaCompiler> kc;
+    std::unique_ptr<McCompiler> mc;
     std::vector<l7g_conn_t> attrs;
     std::vector<DevConn> conns;
     uint8_t *d_blob = nullptr;
@@ -43,8 +49,9 @@ struct l7g_engine {
     size_t conns_cap = 0;
     HttpTables ht{};
     KafkaTables kt{};
+    McTables mt{};
     bool tables_dirty = true, conns_dirty = true;
-    bool has_http = false, has_kafka = false;
+    bool has_http = false, has_kafka = false, has_mc = false;
     int32_t hot_ruleset = -1;  // HTTP rule set staged in LDS (most connections)
     bool any_cold = false;     // some HTTP connection uses another rule set
 };
@@ -69,7 +76,7 @@ size_t Put(std::vector<uint8_t> &blob, const std::vector<T> &v) {
 // Resolve every connection to its rule set (once per connection / policy version).
 bool ResolveConns(l7g_engine *e, std::string *err) {
     e->conns.assign(e->attrs.size(), DevConn{-1, PROTO_NONE, {0, 0, 0}});
-    e->has_http = e->has_kafka = false;
+    e->has_http = e->has_kafka = e->has_mc = false;
     for (size_t i = 0; i < e->attrs.size(); i++) {
         const l7g_conn_t &a = e->attrs[i];
         DevConn &c = e->conns[i];
@@ -86,6 +93,12 @@ bool ResolveConns(l7g_engine *e, std::string *err) {
             c.ruleset = e->kc->RulesetFor(a.policy, a.ingress != 0, a.port, a.src_id, err);
             if (c.ruleset < 0) return false;
             e->has_kafka = true;
+        } else if (a.proto == PROTO_MEMCACHE) {
+            // proxylib matches on the connection's SrcId in both directions
+            // (proxylib/proxylib/connection.go:176-179)
+            c.ruleset = e->mc->RulesetFor(a.policy, a.ingress != 0, a.port, a.src_id, err);
+            if (c.ruleset < 0) return false;
+            e->has_mc = true;
         }
     }
     // The rule set serving the most connections has its image staged in LDS
@@ -113,6 +126,8 @@ hipError_t Upload(l7g_engine *e) {
         const KafkaImage &K = e->kc->image();
         size_t k_rs = Put(blob, K.rulesets), k_r = Put(blob, K.rules), k_idx = Put(blob, K.index),
                k_th = Put(blob, K.topic_hash), k_ch = Put(blob, K.client_hash), k_s = Put(blob, K.strings);
+        const McImage &M = e->mc->image();
+        size_t m_rs = Put(blob, M.rulesets), m_img = Put(blob, M.images);
         uint8_t *d = nullptr;
         if ((rc = hipMalloc(&d, blob.size())) != hipSuccess) return rc;
         if ((rc = hipMemcpy(d, blob.data(), blob.size(), hipMemcpyHostToDevice)) != hipSuccess) { hipFree(d); return rc; }
@@ -134,6 +149,10 @@ hipError_t Upload(l7g_engine *e) {
         KT.nrulesets = (uint32_t)K.rulesets.size();
         KT.topic_mask = K.topic_mask;
         KT.client_mask = K.client_mask;
+        McTables &MT = e->mt;
+        MT.rulesets = (const DevRuleset *)(d + m_rs);
+        MT.images = d + m_img;
+        MT.nrulesets = (uint32_t)M.rulesets.size();
         e->tables_dirty = false;
     }
     if (e->conns_dirty) {
@@ -162,6 +181,7 @@ l7g_engine *l7g_engine_create(int device, char *err, size_t errlen) {
         e->ps = std::make_unique<PolicySet>();
         e->hc = std::make_unique<HttpCompiler>(e->ps.get());
         e->kc = std::make_unique<KafkaCompiler>(e->ps.get());
+        e->mc = std::make_unique<McCompiler>(e->ps.get());
         return e;
     }
     int ndev = 0;
@@ -176,6 +196,7 @@ l7g_engine *l7g_engine_create(int device, char *err, size_t errlen) {
     e->ps = std::make_unique<PolicySet>();
     e->hc = std::make_unique<HttpCompiler>(e->ps.get());
     e->kc = std::make_unique<KafkaCompiler>(e->ps.get());
+    e->mc = std::make_unique<McCompiler>(e->ps.get());
     return e;
 }
 
@@ -196,13 +217,16 @@ int l7g_policy_update(l7g_engine *e, const char *json, size_t len, char *err, si
     if (!LoadPolicySet(json, len, ps.get(), &m)) { set_err(err, errlen, m); return -1; }
     auto hc = std::make_unique<HttpCompiler>(ps.get());
     auto kc = std::make_unique<KafkaCompiler>(ps.get());
+    auto mc = std::make_unique<McCompiler>(ps.get());
     std::swap(e->ps, ps);
     std::swap(e->hc, hc);
     std::swap(e->kc, kc);
+    std::swap(e->mc, mc);
     if (!ResolveConns(e, &m)) {  // roll back: previous version stays in force
         std::swap(e->ps, ps);
         std::swap(e->hc, hc);
         std::swap(e->kc, kc);
+        std::swap(e->mc, mc);
         std::string m2;
         ResolveConns(e, &m2);
         set_err(err, errlen, m);
@@ -241,13 +265,16 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, const uint64_t *off, const
     const uint32_t ncounters = counters ? (uint32_t)e->ps->nrules + 8 : 0;
     // The kernels each classify only their own protocol's requests and skip
     // the rest, so a mixed batch needs one launch per protocol present.
-    if (e->has_http || !e->has_kafka)
+    if (e->has_http || (!e->has_kafka && !e->has_mc))
         rc = LaunchHttpClassify(arena, off, len, conn, n, e->d_conns, (uint32_t)e->conns.size(), e->ht, e->any_cold,
                                 verdict, rule,
                                 consumed, counters, ncounters, s);
     if (rc == hipSuccess && e->has_kafka)
         rc = LaunchKafkaClassify(arena, off, len, conn, n, e->d_conns, (uint32_t)e->conns.size(), e->kt, verdict, rule,
                                  consumed, counters, ncounters, s);
+    if (rc == hipSuccess && e->has_mc)
+        rc = LaunchMemcacheClassify(arena, off, len, conn, n, e->d_conns, (uint32_t)e->conns.size(), e->mt, verdict,
+                                    rule, consumed, counters, ncounters, s);
     return (int)rc;
 }
 
@@ -299,6 +326,11 @@ int l7g_stats(l7g_engine *e, l7g_stats_t *out) {
     out->http_image_bytes = H.images.size();
     out->hot_ruleset = e->hot_ruleset;
     out->hot_image_bytes = e->hot_ruleset >= 0 ? H.rulesets[e->hot_ruleset].image_len : 0;
+    const McImage &M = e->mc->image();
+    out->mc_rulesets = (uint32_t)M.rulesets.size();
+    out->mc_rules = (uint32_t)M.rules;
+    out->mc_dfas = (uint32_t)M.dfas;
+    out->mc_dfa_states = (uint32_t)M.dfa_states;
     return 0;
 }
 

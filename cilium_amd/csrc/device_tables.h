@@ -137,6 +137,45 @@ struct KafkaTables {
     uint32_t pad;
 };
 
+// ---------------- memcached ----------------
+// One image per rule set (same DevRuleset directory as HTTP).  A rule set is
+// the ordered memcache.Rule list the connection's port entries evaluate
+// (proxylib/proxylib/policymap.go:91-236) up to the first unconditional allow,
+// plus the terminal verdict.  Rules are in chunks of <= 64 (u64 masks).
+// Rule r holds for a request iff
+//   empty_r  ||  (cmd_r(command or opcode)  &&  for every key: pred_r(key))
+// (memcache.Rule.Matches, proxylib/memcached/parser.go:47-100).  pred_r is the
+// rule's one effective key predicate (keyExact > keyPrefix > keyRegex, none =
+// true); they are compiled into byte DFAs whose states carry the mask of
+// rules whose predicate holds if the key ends there (exact / prefix as raw-
+// byte anchored patterns, keyRegex unanchored as Go regexp.Match).  The kernel
+// walks kMcMaxDfas DFAs per pass over the request, as many passes as needed.
+constexpr int kMcTextRows = 32;     // McText ids (engine/mc_groups.h), padded
+constexpr int kMcMaxChunks = 4;     // <= 256 rules per rule set
+constexpr int kMcMaxDfas = 4;       // key DFAs walked per key byte in one pass over the line
+struct McImgHeader {       // 64 B, at offset 0 of every memcache image
+    uint8_t nchunks;
+    uint8_t terminal;      // verdict when no rule matches (V_ALLOW or V_DENY), rule -1
+    uint8_t ndfa;
+    uint8_t pad0;
+    uint32_t text_off;     // u64[kMcTextRows][nchunks]: rules whose command group admits text id
+    uint32_t op_off;       // u64[256][nchunks]: rules whose group admits the binary opcode
+    uint32_t empty_off;    // u64[nchunks]: empty rules (match everything)
+    uint32_t nopred_off;   // u64[nchunks]: rules without a key predicate (informational)
+    uint32_t rule_off;     // i32[nchunks * 64]: global rule ids
+    uint32_t dfa_off;      // DevDfa[ndfa] (mask rows: u64[nstates][nchunks])
+    uint32_t owned_off;    // u64[ndfa][nchunks]: rules whose key predicate DFA d evaluates
+    uint32_t pad1[8];
+};
+static_assert(sizeof(McImgHeader) == 64, "McImgHeader layout");
+
+struct McTables {
+    const DevRuleset *rulesets;
+    const uint8_t *images;
+    uint32_t nrulesets;
+    uint32_t pad;
+};
+
 // FNV-1a over lower-cased ASCII (header names are tchar, i.e. ASCII)
 static inline uint32_t l7_fnv_step(uint32_t h, uint8_t c) {
     if (c >= 'A' && c <= 'Z') c = (uint8_t)(c + 32);

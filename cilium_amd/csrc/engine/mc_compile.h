@@ -1,0 +1,44 @@
+// memcached rule-set compiler (product code): proxylib's memcache policy
+// semantics lowered to device tables (device_tables.h McImgHeader).
+//
+// For a connection (policy, direction, port, source identity) proxylib
+// evaluates PortNetworkPolicies.Matches (proxylib/proxylib/policymap.go:210-236):
+// the exact-port entry, then the port-0 entry, each only if installed (every
+// rule's parser registered, :113-148).  An entry without L7 rules allows; a
+// rule group admitting the identity with no L7 rules allows; otherwise the
+// group's memcache.Rule list is tried in order.  That order is fixed per
+// connection, so it is resolved here once into a rule set: the ordered rule
+// list up to the first unconditional allow + the terminal verdict.
+#pragma once
+#include <cstdint>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../device_tables.h"
+#include "../policy/policy.h"
+
+namespace l7 {
+
+struct McImage {
+    std::vector<DevRuleset> rulesets;
+    std::vector<uint8_t> images;
+    size_t rules = 0, dfas = 0, dfa_states = 0;
+};
+
+class McCompiler {
+public:
+    explicit McCompiler(const PolicySet *ps) : ps_(ps) {}
+    // remote = the connection's source identity (proxylib/proxylib/connection.go:176-179)
+    int RulesetFor(int policy, bool ingress, uint32_t port, uint64_t remote, std::string *err);
+    const McImage &image() const { return img_; }
+    int max_dfa_states = 4096;
+
+private:
+    const PolicySet *ps_;
+    McImage img_;
+    std::map<std::pair<std::vector<int>, int>, int> cache_;
+    int Compile(const std::vector<const McRule *> &rules, uint8_t terminal, std::string *err);
+};
+
+}  // namespace l7

@@ -1,0 +1,334 @@
+// memcached request classification on gfx950 (product code).
+//
+// One lane per request.  The first byte picks the framing, as the parser
+// selection of proxylib/memcached/parser.go:186-202 does:
+//   binary (>= 0x80): the 24-byte header (binary/parser.go:58-139) gives the
+//     opcode, key and frame length = body + 24;
+//   text: the first "\r\n" ends the command line (text/parser.go:84-93); the
+//     line is split like bytes.Fields (Unicode White_Space) and classified by
+//     its first token (:101-156); storage commands add tokens[4] + 2 bytes.
+// Each lane walks its line once, byte by byte, from 16-byte aligned vector
+// loads held in registers.  Key tokens are fed to the rule set's key DFAs as
+// they stream past, so no token offsets are stored; at the end of each key
+// the DFA masks fold into an AND over keys (memcache.Rule.Matches, "every
+// key", proxylib/memcached/parser.go:67-97).  The verdict is the first rule
+// (in evaluation order) with  empty || (command && all keys), else the rule
+// set's terminal verdict.
+//
+// Batch conventions: MORE => INCOMPLETE; a Go panic or ERROR
+// => PARSE_ERROR; PASS/DROP => ALLOW/DENY with consumed = proxylib's frame
+// length (it may exceed the buffer); a frame length outside 1..2^32-1 =>
+// PARSE_ERROR.
+#include <hip/hip_runtime.h>
+
+#include "../device_tables.h"
+#include "../engine/mc_groups.h"
+
+namespace l7 {
+
+namespace {
+
+constexpr int kBlock = 256;
+
+// 16-byte aligned register window over one request (the arena is readable up
+// to the 16-byte boundary after its last byte; see include/l7gpu.h).
+struct Reader {
+    const uint8_t *b;
+    uint64_t base;
+    uint32_t w0, w1, w2, w3;
+};
+
+__device__ __forceinline__ uint32_t rd(Reader &r, uint32_t i) {
+    const uint64_t a = (uint64_t)(r.b + i);
+    const uint64_t base = a & ~(uint64_t)15;
+    if (base != r.base) {
+        const uint4 v = *(const uint4 *)base;
+        r.w0 = v.x; r.w1 = v.y; r.w2 = v.z; r.w3 = v.w;
+        r.base = base;
+    }
+    const uint32_t k = (uint32_t)(a >> 2) & 3;
+    const uint32_t w = k == 0 ? r.w0 : k == 1 ? r.w1 : k == 2 ? r.w2 : r.w3;
+    return (w >> ((a & 3) * 8)) & 0xFF;
+}
+
+// Length of the Unicode White_Space rune starting at b[i] (unicode.IsSpace),
+// 0 if none.  Multi-byte spaces begin with a UTF-8 lead byte, and a lead byte
+// is always a rune start when a buffer is decoded from its beginning, so the
+// test needs no decoding context (see oracle/memcache_ref.c mc_space_len).
+__device__ __forceinline__ uint32_t space_len(const uint8_t *b, uint32_t i, uint32_t len, uint32_t c) {
+    if (c == ' ' || (c >= 0x09 && c <= 0x0D)) return 1;
+    if (c < 0xC2 || c > 0xE3 || i + 1 >= len) return 0;
+    const uint32_t c1 = b[i + 1];
+    if (c == 0xC2) return (c1 == 0x85 || c1 == 0xA0) ? 2 : 0;
+    if (i + 2 >= len) return 0;
+    const uint32_t c2 = b[i + 2];
+    if (c == 0xE1) return (c1 == 0x9A && c2 == 0x80) ? 3 : 0;
+    if (c == 0xE2) {
+        if (c1 == 0x80) return ((c2 >= 0x80 && c2 <= 0x8A) || c2 == 0xA8 || c2 == 0xA9 || c2 == 0xAF) ? 3 : 0;
+        return (c1 == 0x81 && c2 == 0x9F) ? 3 : 0;
+    }
+    if (c == 0xE3) return (c1 == 0x80 && c2 == 0x80) ? 3 : 0;
+    return 0;
+}
+
+// text command name bytes packed little-endian into 4 words (compile-time)
+__host__ __device__ constexpr uint32_t pk(const char *s, uint32_t n, uint32_t w) {
+    return (4 * w + 0 < n ? (uint32_t)(uint8_t)s[4 * w + 0] : 0u) |
+           (4 * w + 1 < n ? (uint32_t)(uint8_t)s[4 * w + 1] << 8 : 0u) |
+           (4 * w + 2 < n ? (uint32_t)(uint8_t)s[4 * w + 2] << 16 : 0u) |
+           (4 * w + 3 < n ? (uint32_t)(uint8_t)s[4 * w + 3] << 24 : 0u);
+}
+#define MC_CMD(id, lit)                                                                                   \
+    if (clen == sizeof(lit) - 1 && cw[0] == pk(lit, sizeof(lit) - 1, 0) && cw[1] == pk(lit, sizeof(lit) - 1, 1) && \
+        cw[2] == pk(lit, sizeof(lit) - 1, 2) && cw[3] == pk(lit, sizeof(lit) - 1, 3))                    \
+        return id;
+
+// McText id of a command token (engine/mc_groups.h); kMcOther if none.
+__device__ __forceinline__ uint32_t text_id(const uint32_t cw[4], uint32_t clen) {
+    MC_CMD(kMcGet, "get") MC_CMD(kMcGets, "gets") MC_CMD(kMcGat, "gat") MC_CMD(kMcGats, "gats")
+    MC_CMD(kMcSet, "set") MC_CMD(kMcAdd, "add") MC_CMD(kMcReplace, "replace") MC_CMD(kMcAppend, "append")
+    MC_CMD(kMcPrepend, "prepend") MC_CMD(kMcCas, "cas") MC_CMD(kMcDelete, "delete") MC_CMD(kMcIncr, "incr")
+    MC_CMD(kMcDecr, "decr") MC_CMD(kMcTouch, "touch") MC_CMD(kMcSlabs, "slabs") MC_CMD(kMcLru, "lru")
+    MC_CMD(kMcLruCrawler, "lru_crawler") MC_CMD(kMcStats, "stats") MC_CMD(kMcVersion, "version")
+    MC_CMD(kMcMisbehave, "misbehave") MC_CMD(kMcFlushAll, "flush_all") MC_CMD(kMcCacheMemlimit, "cache_memlimit")
+    MC_CMD(kMcQuit, "quit") MC_CMD(kMcWatch, "watch")
+    return kMcOther;
+}
+#undef MC_CMD
+
+enum : int { F_NONE = 0, F_GET, F_GAT, F_STORAGE, F_KEY1, F_NOKEY, F_BAD };
+
+struct Image {
+    const uint8_t *p;
+    uint32_t nch, ndfa, terminal;
+    uint32_t d0, dn;  // DFAs [d0, d0+dn) are walked in the current pass over the request
+};
+
+__device__ __forceinline__ const uint64_t *u64at(const Image &I, uint32_t off) { return (const uint64_t *)(I.p + off); }
+__device__ __forceinline__ uint32_t hdr32(const Image &I, int byte_off) { return *(const uint32_t *)(I.p + byte_off); }
+
+#define MC_OFF(field) ((int)offsetof(McImgHeader, field))
+
+struct Keys {
+    uint32_t st[kMcMaxDfas];   // DFA states of the key being read
+    uint64_t all[kMcMaxChunks];  // AND over finished keys of their pass masks
+};
+
+__device__ __forceinline__ void keys_reset(const Image &I, Keys &K) {
+#pragma unroll
+    for (int d = 0; d < kMcMaxDfas; d++)
+        if ((uint32_t)d < I.dn) {
+            const DevDfa *dd = (const DevDfa *)(I.p + hdr32(I, MC_OFF(dfa_off))) + I.d0 + d;
+            K.st[d] = dd->start;
+        }
+}
+
+__device__ __forceinline__ void keys_step(const Image &I, Keys &K, uint32_t c) {
+#pragma unroll
+    for (int d = 0; d < kMcMaxDfas; d++)
+        if ((uint32_t)d < I.dn && K.st[d] != 0) {
+            const DevDfa *dd = (const DevDfa *)(I.p + hdr32(I, MC_OFF(dfa_off))) + I.d0 + d;
+            const uint32_t cls = I.p[dd->cls_off + c];
+            K.st[d] = ((const uint16_t *)(I.p + dd->trans_off))[K.st[d] * dd->ncls + cls];
+        }
+}
+
+// A key ended: AND its pass mask into K.all.  In this pass a rule passes if
+// its predicate is not evaluated by the pass's DFAs (no predicate, or another
+// pass owns it) or one of the pass's DFAs accepts the key.
+__device__ __forceinline__ void keys_end(const Image &I, Keys &K) {
+    const uint64_t *owned = u64at(I, hdr32(I, MC_OFF(owned_off)));
+#pragma unroll
+    for (int c = 0; c < kMcMaxChunks; c++) {
+        if ((uint32_t)c >= I.nch) break;
+        uint64_t own = 0, acc = 0;
+#pragma unroll
+        for (int d = 0; d < kMcMaxDfas; d++)
+            if ((uint32_t)d < I.dn) {
+                const DevDfa *dd = (const DevDfa *)(I.p + hdr32(I, MC_OFF(dfa_off))) + I.d0 + d;
+                own |= owned[(I.d0 + d) * I.nch + c];
+                acc |= ((const uint64_t *)(I.p + dd->mask_off))[K.st[d] * I.nch + c];
+            }
+        K.all[c] &= ~own | acc;
+    }
+    keys_reset(I, K);
+}
+
+// First-token classification (text/parser.go:101-156)
+__device__ __forceinline__ void classify_cmd(const uint32_t cw[4], uint32_t clen, int &fr, uint32_t &id) {
+    id = text_id(cw, clen);
+    const uint32_t p3 = cw[0] & 0xFFFFFF;
+    if (clen >= 3 && p3 == ('g' | 'e' << 8 | 't' << 16)) fr = F_GET;
+    else if (clen >= 3 && p3 == ('g' | 'a' << 8 | 't' << 16)) fr = F_GAT;
+    else if (id >= kMcSet && id <= kMcCas) fr = F_STORAGE;
+    else if (id >= kMcDelete && id <= kMcTouch) fr = F_KEY1;
+    else if (id >= kMcSlabs && id <= kMcWatch) fr = F_NOKEY;
+    else fr = F_BAD;
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(kBlock) void memcache_classify_kernel(
+    const uint8_t *__restrict__ arena, const uint64_t *__restrict__ offs, const uint32_t *__restrict__ lens,
+    const uint32_t *__restrict__ conn_ids, uint32_t n, const DevConn *__restrict__ conns, uint32_t nconns,
+    McTables T, uint8_t *__restrict__ out_verdict, int32_t *__restrict__ out_rule, uint32_t *__restrict__ out_consumed,
+    uint64_t *__restrict__ counters, uint32_t ncounters) {
+    for (uint32_t idx = blockIdx.x * kBlock + threadIdx.x; idx < n; idx += gridDim.x * kBlock) {
+        const uint32_t ci = conn_ids[idx];
+        if (ci >= nconns) continue;
+        const DevConn conn = conns[ci];
+        if (conn.proto != PROTO_MEMCACHE || conn.ruleset < 0 || (uint32_t)conn.ruleset >= T.nrulesets) continue;
+        const DevRuleset rs = T.rulesets[conn.ruleset];
+        Image I;
+        I.p = T.images + rs.image_off;
+        {
+            const uint32_t h0 = *(const uint32_t *)I.p;
+            I.nch = h0 & 0xFF;
+            I.terminal = (h0 >> 8) & 0xFF;
+            I.ndfa = (h0 >> 16) & 0xFF;
+        }
+        const uint8_t *b = arena + offs[idx];
+        const uint32_t len = lens[idx];
+        uint8_t verdict = V_PARSE_ERROR;
+        int32_t rule = -1;
+        uint32_t consumed = 0;
+        Keys K;
+#pragma unroll
+        for (int c = 0; c < kMcMaxChunks; c++) K.all[c] = ~0ull;
+        const uint64_t *cmdmask = nullptr;
+        uint64_t frame = 0;
+        bool staged = false;  // framing succeeded: match against the rules
+        // More key DFAs than one pass walks: re-read the request once per
+        // group of kMcMaxDfas (framing is identical in every pass).
+        for (uint32_t d0 = 0;; d0 += kMcMaxDfas) {
+        I.d0 = d0;
+        I.dn = I.ndfa - d0 < (uint32_t)kMcMaxDfas ? I.ndfa - d0 : (uint32_t)kMcMaxDfas;
+        keys_reset(I, K);
+        do {
+            if (len == 0) { verdict = V_INCOMPLETE; break; }  // NOP, 0
+            const uint32_t b0 = b[0];
+            if (b0 >= 0x80) {
+                // ---- binary header (binary/parser.go:72-139)
+                if (len < 24) { verdict = V_INCOMPLETE; break; }
+                const uint32_t keylen = (uint32_t)b[2] << 8 | b[3];
+                const uint32_t extras = b[4];
+                const uint32_t body = (uint32_t)b[8] << 24 | (uint32_t)b[9] << 16 | (uint32_t)b[10] << 8 | b[11];
+                if (keylen > 0 && 24 + keylen + extras > len) { verdict = V_INCOMPLETE; break; }
+                // (b0 & 0x80) == RequestMagic always holds here (getOpcodeAndKey)
+                cmdmask = u64at(I, hdr32(I, MC_OFF(op_off))) + (size_t)b[1] * I.nch;
+                Reader R{b, ~0ull, 0, 0, 0, 0};
+                for (uint32_t i = 24 + extras, e = 24 + extras + keylen; i < e; i++) keys_step(I, K, rd(R, i));
+                keys_end(I, K);
+                frame = (uint32_t)(body + 24u);  // uint32 arithmetic, then int()
+            } else {
+                // ---- text command line
+                Reader R{b, ~0ull, 0, 0, 0, 0};
+                uint32_t i = 0, lf = 0;
+                bool found = false, in_tok = false;
+                uint32_t nt = 0;              // tokens started
+                uint32_t cw[4] = {0, 0, 0, 0}, clen = 0;
+                int fr = F_NONE;
+                uint32_t cmd_id = kMcOther;
+                bool key_tok = false;         // current token is a key
+                bool a_ok = false, a_bad = false, a_neg = false;  // strconv.Atoi(tokens[4])
+                uint32_t a_n = 0;
+                uint64_t a_v = 0;
+                while (i < len) {
+                    const uint32_t c = rd(R, i);
+                    if (c == '\r' && i + 1 < len && b[i + 1] == '\n') { lf = i; found = true; break; }
+                    const uint32_t sp = space_len(b, i, len, c);
+                    if (sp) {
+                        if (in_tok) {  // token nt-1 ended
+                            if (nt == 1) classify_cmd(cw, clen, fr, cmd_id);
+                            if (key_tok) keys_end(I, K);
+                            in_tok = false;
+                        }
+                        i += sp;
+                        continue;
+                    }
+                    if (!in_tok) {
+                        in_tok = true;
+                        nt++;
+                        key_tok = (fr == F_GET && nt >= 2) || (fr == F_GAT && nt >= 3) ||
+                                  ((fr == F_STORAGE || fr == F_KEY1) && nt == 2);
+                    }
+                    if (nt == 1) {
+                        if (clen < 16) cw[clen >> 2] |= c << ((clen & 3) * 8);
+                        clen++;
+                    } else if (key_tok) {
+                        keys_step(I, K, c);
+                    }
+                    if (fr == F_STORAGE && nt == 5) {
+                        if (a_n == 0 && (c == '+' || c == '-')) { a_neg = c == '-'; a_ok = false; /* until a digit */ }
+                        else if (c < '0' || c > '9') { a_ok = false; a_bad = true; }
+                        else {
+                            const uint64_t d = c - '0';
+                            if (a_v > (~0ull - d) / 10) a_bad = true;
+                            else a_v = a_v * 10 + d;
+                            if (a_v > 0x7FFFFFFFFFFFFFFFull + (a_neg ? 1u : 0u)) a_bad = true;
+                            a_ok = !a_bad;
+                        }
+                        a_n++;
+                    }
+                    i++;
+                }
+                if (!found) { verdict = V_INCOMPLETE; break; }  // MORE
+                if (in_tok) {
+                    if (nt == 1) classify_cmd(cw, clen, fr, cmd_id);
+                    if (key_tok) keys_end(I, K);
+                }
+                if (nt == 0) break;  // tokens[0] panics
+                if (fr == F_BAD) break;  // ERROR, 0
+                if (fr == F_GAT && nt < 2) break;  // tokens[2:] panics
+                if ((fr == F_STORAGE || fr == F_KEY1) && nt < 2) break;  // tokens[1:2] panics
+                frame = (uint64_t)lf + 2;
+                if (fr == F_STORAGE) {
+                    if (nt < 5) break;  // tokens[4] panics
+                    if (!a_ok) break;
+                    const int64_t nb = a_neg ? (int64_t)(0 - a_v) : (int64_t)a_v;
+                    frame = frame + (uint64_t)nb + 2u;  // Go int arithmetic
+                }
+                cmdmask = u64at(I, hdr32(I, MC_OFF(text_off))) + (size_t)cmd_id * I.nch;
+            }
+            staged = true;
+        } while (false);
+        if (!staged || d0 + kMcMaxDfas >= I.ndfa) break;
+        }
+        do {
+            if (!staged) break;
+            if ((int64_t)frame <= 0 || frame > 0xFFFFFFFFull) { verdict = V_PARSE_ERROR; break; }
+            consumed = (uint32_t)frame;
+            // ---- first matching rule (PortNetworkPolicyRule(s).Matches order)
+            const uint64_t *empty = u64at(I, hdr32(I, MC_OFF(empty_off)));
+            const int32_t *ids = (const int32_t *)(I.p + hdr32(I, MC_OFF(rule_off)));
+            verdict = (uint8_t)I.terminal;
+#pragma unroll
+            for (int c = 0; c < kMcMaxChunks; c++) {
+                if ((uint32_t)c >= I.nch) break;
+                const uint64_t ok = empty[c] | (cmdmask[c] & K.all[c]);
+                if (ok) { verdict = V_ALLOW; rule = ids[c * 64 + __builtin_ctzll(ok)]; break; }
+            }
+        } while (false);
+        out_verdict[idx] = verdict;
+        out_rule[idx] = rule;
+        out_consumed[idx] = consumed;
+        if (counters) {
+            atomicAdd((unsigned long long *)&counters[ncounters - 8 + verdict], 1ull);
+            if (rule >= 0 && (uint32_t)rule < ncounters - 8) atomicAdd((unsigned long long *)&counters[rule], 1ull);
+        }
+    }
+}
+
+hipError_t LaunchMemcacheClassify(const uint8_t *arena, const uint64_t *offs, const uint32_t *lens,
+                                  const uint32_t *conn_ids, uint32_t n, const DevConn *conns, uint32_t nconns,
+                                  const McTables &T, uint8_t *verdict, int32_t *rule, uint32_t *consumed,
+                                  uint64_t *counters, uint32_t ncounters, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    uint32_t blocks = (n + kBlock - 1) / kBlock;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(memcache_classify_kernel, dim3(blocks), dim3(kBlock), 0, stream, arena, offs, lens, conn_ids, n,
+                       conns, nconns, T, verdict, rule, consumed, counters, ncounters);
+    return hipGetLastError();
+}
+
+}  // namespace l7

@@ -7,6 +7,8 @@
 //   * unique remote_policies            npds.proto:77 (validate.rules)
 #include "policy.h"
 
+#include "../engine/mc_groups.h"
+
 #include <algorithm>
 #include <cctype>
 #include <cstring>
@@ -18,6 +20,16 @@ namespace l7 {
 bool PortRule::RemoteOk(uint64_t id) const {
     if (remotes.empty()) return true;
     return std::binary_search(remotes.begin(), remotes.end(), id);
+}
+
+std::string PortRule::ParserName() const {
+    if (!l7proto.empty()) return l7proto;
+    switch (type) {
+        case Http: return "PortNetworkPolicyRule_HttpRules";
+        case Kafka: return "PortNetworkPolicyRule_KafkaRules";
+        case L7: return "PortNetworkPolicyRule_L7Rules";
+        default: return "";
+    }
 }
 
 void NetworkPolicy::Lookup(bool in, uint32_t port, const PortPolicy **exact, const PortPolicy **wild) const {
@@ -37,6 +49,7 @@ using json::Value;
 struct Loader {
     std::string err;
     int next_id = 0;
+    bool mc_stop = false;  // an earlier rule of this port has an unregistered parser
     bool fail(const std::string &m) { if (err.empty()) err = m; return false; }
 
     static const Value *list(const Value *v, const char *inner) {
@@ -191,9 +204,44 @@ struct Loader {
                 x.id = next_id++;
                 const Value *m = lr.get("rule");
                 if (!m) m = &lr;
-                if (m->isObj()) for (auto &kv : m->obj) if (kv.second.isStr()) x.kv.emplace_back(kv.first, kv.second.str);
+                if (m->isObj())
+                    for (auto &kv : m->obj) {
+                        if (kv.second.isStr()) x.kv.emplace_back(kv.first, kv.second.str);
+                        else if (r->l7proto == "memcache" && !mc_stop) return fail("NPDS: memcache rule value is not a string");
+                    }
                 r->l7.push_back(std::move(x));
             }
+            if (r->l7proto == "memcache" && !mc_stop)
+                for (auto &x : r->l7) {
+                    r->mc.emplace_back();
+                    if (!memcache(x, &r->mc.back())) return false;
+                }
+        }
+        return true;
+    }
+
+    // memcache.L7RuleParser (proxylib/memcached/parser.go:114-148)
+    bool memcache(const L7Rule &x, McRule *m) {
+        m->id = x.id;
+        bool found = false;
+        for (auto &kv : x.kv) {
+            const std::string &k = kv.first, &v = kv.second;
+            if (k == "command") { m->group = McGroupIndex(v); found = m->group >= 0; }
+            else if (k == "keyExact") m->key_exact = v;
+            else if (k == "keyPrefix") m->key_prefix = v;
+            else if (k == "keyRegex") {
+                std::string e;
+                auto ast = re::Parse(v, &e);
+                if (!ast) return fail(e);
+                m->key_re = std::shared_ptr<re::Node>(std::move(ast));
+                m->key_re_src = v;
+            } else return fail("NPDS: Unsupported key: " + k);
+        }
+        if (!found) {
+            if (!m->key_exact.empty() || !m->key_prefix.empty() || m->key_re)
+                return fail("NPDS: command not specified but key was provided");
+            m->group = -1;
+            m->empty = true;
         }
         return true;
     }
@@ -210,11 +258,16 @@ struct Loader {
                 if (pr->isStr() && pr->str == "UDP") p.tcp = false;
                 if (pr->type == Value::Num && pr->inum != 0) p.tcp = false;
             }
+            mc_stop = false;
             if (auto *rs = pj.get("rules"); rs && rs->isArr())
                 for (auto &rj : rs->arr) {
                     p.rules.emplace_back();
-                    if (!rule(rj, &p.rules.back())) return false;
-                    if (p.rules.back().type == PortRule::Http) p.has_http = true;
+                    PortRule &r = p.rules.back();
+                    if (!rule(rj, &r)) return false;
+                    if (r.type == PortRule::Http) p.has_http = true;
+                    std::string pn = r.ParserName();
+                    if (!pn.empty() && pn != "memcache") { mc_stop = true; p.mc_installed = false; }
+                    if (!mc_stop && !r.mc.empty()) p.mc_have_l7 = true;
                 }
             if (p.tcp)
                 for (auto &q : *out) if (q.tcp && q.port == p.port) return fail("PortNetworkPolicy: Duplicate port number");

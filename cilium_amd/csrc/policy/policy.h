@@ -40,6 +40,17 @@ struct KafkaRule {
 
 struct L7Rule { std::vector<std::pair<std::string, std::string>> kv; int id = -1; };
 
+// memcache.Rule (proxylib/memcached/parser.go:35-44), parsed by the loader
+// from an l7_proto "memcache" rule's key/value map (parser.go:114-148).
+struct McRule {
+    int group = -1;          // MemcacheOpCodeMap entry (engine/mc_groups.h), -1 = none
+    std::string key_exact, key_prefix;
+    std::shared_ptr<re::Node> key_re;
+    std::string key_re_src;
+    bool empty = false;      // no command and no key: matches every request
+    int id = -1;
+};
+
 struct PortRule {
     std::vector<uint64_t> remotes;  // empty = any remote
     enum Type { None, Http, Kafka, L7 } type = None;
@@ -47,10 +58,24 @@ struct PortRule {
     std::vector<KafkaRule> kafka;
     std::string l7proto;
     std::vector<L7Rule> l7;
+    std::vector<McRule> mc;  // l7proto == "memcache": its parsed L7 rules
+    // proxylib parser name: l7_proto, else the oneof type name, "" = no L7
+    // (proxylib/proxylib/policymap.go:68-75)
+    std::string ParserName() const;
     bool RemoteOk(uint64_t id) const;
 };
 
-struct PortPolicy { uint32_t port = 0; bool tcp = true; std::vector<PortRule> rules; bool has_http = false; };
+struct PortPolicy {
+    uint32_t port = 0;
+    bool tcp = true;
+    std::vector<PortRule> rules;
+    bool has_http = false;
+    // proxylib view (policymap.go:113-148): the entry is installed only if every
+    // rule's parser is registered ("memcache" or none); HaveL7Rules = some
+    // rule has parsed L7 rules.
+    bool mc_installed = true;
+    bool mc_have_l7 = false;
+};
 
 struct NetworkPolicy {
     std::string name;

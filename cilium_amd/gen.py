@@ -8,6 +8,8 @@ cfg1  1 rule  {Method:"GET", Path:"/public/.*"}                  (HTTP)
 cfg2  64 HTTP rules over Method/Path/Host + literal X-Token header  (HTTP, bench)
 cfg3  Kafka produce/fetch/metadata stream, ~1k PortRuleKafka rules  (Kafka)
 cfg4  10k HTTP rules across 512 identities                          (HTTP)
+cfg5  mixed stream 50 % HTTP / 30 % Kafka / 20 % memcached (text + binary)
+      memcached part: text and binary commands against the mc rules below
 """
 import struct
 import zlib
@@ -16,7 +18,7 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from . import api
-from ._lib import PROTO_HTTP, PROTO_KAFKA
+from ._lib import PROTO_HTTP, PROTO_KAFKA, PROTO_MEMCACHE
 from .engine import CONN_DTYPE
 
 SEED_BASE = 0x1C1D0000
@@ -397,3 +399,165 @@ def kafka_workload(n, nconns=256, seed=None, adversarial=False):
     conn_ids = rng.integers(0, nconns, size=n).astype(np.uint32)
     conns = make_conns(nconns, 0, 9092, True, PROTO_KAFKA, 2000 + np.arange(nconns))
     return Workload("cfg3", arena, offs, lens, conn_ids, conns, cfg3_policy())
+
+
+# ------------------------------------------------------------------ memcached
+# proxylib memcached: text protocol lines
+# (text/parser.go:72-198) and 24-byte-header binary packets (binary/parser.go).
+MC_PORT = 11211
+
+
+def mc_rules():
+    """memcache.Rule maps (proxylib/memcached/parser.go:114-148) for cfg5."""
+    return [
+        {"command": "get", "keyPrefix": "user:"},
+        {"command": "set", "keyRegex": "^session:[0-9a-f]{8}$"},
+        {"command": "delete", "keyExact": "tmp"},
+        {"command": "storage", "keyPrefix": "cache:"},
+        {"command": "gat", "keyRegex": "^user:[0-9]+$"},
+        {"command": "stats"},
+        {"command": "touch", "keyRegex": "é|ü"},
+        {"command": "writeGroup", "keyExact": "counter"},
+    ]
+
+
+def mc_policy():
+    """Two groups on the memcached port (mc rules for remotes 3000-3127,
+    version-only for any remote), plus a port-0 entry allowing 'noop'."""
+    groups = [api.port_rule(remote_policies=list(range(3000, 3128)), l7proto="memcache", l7=mc_rules()),
+              api.port_rule(l7proto="memcache", l7=[{"command": "version"}])]
+    wild = [api.port_rule(l7proto="memcache", l7=[{"command": "noop"}, {"command": "flush_all"}])]
+    return api.policy_set(api.network_policy("10.0.0.5", 5, ingress=[(MC_PORT, groups), (0, wild)]))
+
+
+def _mc_key(rng, i):
+    k = int(rng.integers(0, 10))
+    if k < 4:
+        return b"user:%d" % int(rng.integers(0, 100000))
+    if k < 6:
+        return b"session:%08x" % int(rng.integers(0, 1 << 32)) if rng.random() < 0.8 else b"session:zz%d" % i
+    if k == 6:
+        return b"cache:" + bytes(rng.choice(_ALNUM, size=int(rng.integers(1, 40))))
+    if k == 7:
+        return [b"tmp", b"counter", b"k\xc3\xa9y", b"\xfc\xfc"][int(rng.integers(0, 4))]
+    return b"obj%d" % int(rng.integers(0, 1 << 20))
+
+
+def mc_bin(opcode, key=b"", extras=b"", value=b"", magic=0x80, body=None):
+    bl = len(extras) + len(key) + len(value) if body is None else body
+    return struct.pack(">BBHBBHIIQ", magic, opcode, len(key), len(extras), 0, 0, bl, 0, 0) + extras + key + value
+
+
+def memcache_requests(n, seed):
+    rng = np.random.default_rng(seed)
+    out = []
+    text_cmds = [b"get", b"gets", b"gat", b"gats", b"set", b"add", b"replace", b"append", b"prepend", b"cas",
+                 b"delete", b"incr", b"decr", b"touch", b"stats", b"version", b"flush_all", b"quit"]
+    for i in range(n):
+        if rng.random() < 0.3:  # binary
+            op = int(rng.choice([0, 1, 2, 4, 9, 10, 12, 13, 17, 20, 28, 16, 11, 5]))
+            key = _mc_key(rng, i)
+            extras = b"" if op in (0, 4, 9, 12, 13, 20, 10, 16, 11) else bytes(8)
+            value = bytes(rng.integers(0, 256, size=int(rng.integers(0, 200)), dtype=np.uint8)) if op in (1, 2, 17) else b""
+            out.append(mc_bin(op, b"" if op in (10, 16, 11) else key, extras, value))
+            continue
+        c = text_cmds[int(rng.integers(0, len(text_cmds)))]
+        if c in (b"get", b"gets"):
+            line = c + b" " + b" ".join(_mc_key(rng, i) for _ in range(int(rng.integers(1, 5))))
+        elif c in (b"gat", b"gats"):
+            line = c + b" %d " % int(rng.integers(0, 1000)) + b" ".join(_mc_key(rng, i) for _ in range(int(rng.integers(1, 4))))
+        elif c in (b"set", b"add", b"replace", b"append", b"prepend", b"cas"):
+            vlen = int(rng.integers(0, 600))
+            line = c + b" %s %d %d %d" % (_mc_key(rng, i), int(rng.integers(0, 65536)), int(rng.integers(0, 3600)), vlen)
+            if c == b"cas":
+                line += b" %d" % int(rng.integers(0, 1 << 40))
+            if rng.random() < 0.2:
+                line += b" noreply"
+            out.append(line + b"\r\n" + bytes(rng.choice(_ALNUM, size=vlen)) + b"\r\n")
+            continue
+        elif c in (b"delete",):
+            line = c + b" " + _mc_key(rng, i) + (b" noreply" if rng.random() < 0.2 else b"")
+        elif c in (b"incr", b"decr"):
+            line = c + b" " + _mc_key(rng, i) + b" %d" % int(rng.integers(0, 100))
+        elif c == b"touch":
+            line = c + b" " + _mc_key(rng, i) + b" %d" % int(rng.integers(0, 100))
+        elif c == b"flush_all":
+            line = c + (b" %d" % int(rng.integers(0, 100)) if rng.random() < 0.5 else b"")
+        else:
+            line = c
+        out.append(line + b"\r\n")
+    return out
+
+
+_MC_SPACES = [b" ", b"\t", b"\x0b", b"\x0c", b"\r", b"\n", b"\xc2\x85", b"\xc2\xa0", b"\xe1\x9a\x80", b"\xe2\x80\x80",
+              b"\xe2\x80\x8a", b"\xe2\x80\xa8", b"\xe2\x80\xa9", b"\xe2\x80\xaf", b"\xe2\x81\x9f", b"\xe3\x80\x80"]
+_MC_NOT_SPACES = [b"\xc2\x84", b"\xe2\x80\x8b", b"\xe2\x80", b"\xc2", b"\xe3\x80", b"\xff", b"\x00", b"\xe2\x82\xac",
+                  b"\xed\xa0\x80", b"\xf0\x9f\x98\x80"]
+
+
+def memcache_adversarial(n, seed):
+    """Mutated memcached requests: Unicode / control separators, truncation,
+    lone CR, empty lines, unknown and get*/gat*-prefixed commands, bad or
+    huge storage lengths, short / wrapped binary headers."""
+    rng = np.random.default_rng(seed)
+    base = memcache_requests(n, seed + 3)
+    out = []
+    for r in base:
+        op = int(rng.integers(0, 14))
+        if r[0] >= 0x80:
+            r = bytearray(r)
+            if op < 3:
+                r = r[: int(rng.integers(0, len(r) + 1))]
+            elif op < 5 and len(r) >= 12:
+                r[8:12] = struct.pack(">I", int(rng.choice([0, 0xFFFFFFE8, 0xFFFFFFF0, 0x7FFFFFFF, 5, 1 << 31])))
+            elif op < 7 and len(r) >= 5:
+                r[4] = int(rng.integers(0, 256))
+            elif op < 8 and len(r) >= 4:
+                r[2:4] = struct.pack(">H", int(rng.integers(0, 70)))
+            elif op < 9:
+                r[0] = int(rng.choice([0x80, 0x81, 0xFF, 0x90]))
+            out.append(bytes(r))
+            continue
+        lf = r.find(b"\r\n")
+        line, rest = r[:lf], r[lf:]
+        toks = line.split(b" ")
+        if op == 0:  # Unicode / control separators
+            line = b"".join(t + _MC_SPACES[int(rng.integers(0, len(_MC_SPACES)))] for t in toks)
+        elif op == 1:  # non-space multibyte junk glued to tokens
+            line = b"".join(t + _MC_NOT_SPACES[int(rng.integers(0, len(_MC_NOT_SPACES)))] + b" " for t in toks)
+        elif op == 2:  # truncation
+            out.append(r[: int(rng.integers(0, len(r)))])
+            continue
+        elif op == 3:  # ends with a lone CR / LF
+            out.append(line + rng.choice([b"\r", b"\n", b"\n\r", b""]))
+            continue
+        elif op == 4:  # empty / blank line
+            line = [b"", b"   ", b"\t", b"\xe3\x80\x80"][int(rng.integers(0, 4))]
+        elif op == 5:  # unknown or prefixed commands
+            toks[0] = [b"getx", b"gatt", b"ge", b"GET", b"sets", b"foo", b"gatherall", b"lru", b"watch", b"misbehave",
+                       b"cache_memlimit", b"slabs", b"lru_crawler", b"decr"][int(rng.integers(0, 14))]
+            line = b" ".join(toks)
+        elif op == 6 and toks[0] in (b"set", b"add", b"replace", b"append", b"prepend", b"cas"):  # bad lengths
+            if len(toks) >= 5:
+                toks[4] = [b"-1", b"+7", b"abc", b"", b"99999999999999999999", b"9223372036854775807", b"-9223372036854775808",
+                           b"4294967290", b"-", b"+", b"007", b"-0"][int(rng.integers(0, 12))]
+            line = b" ".join(toks)
+        elif op == 7:  # drop trailing tokens
+            line = b" ".join(toks[: int(rng.integers(1, len(toks) + 1))])
+        elif op == 8:  # leading whitespace
+            line = b"  " + line
+        out.append(line + rest)
+    return out
+
+
+def memcache_workload(n, nconns=256, seed=None, adversarial=False):
+    seed = SEED_BASE + 5 if seed is None else seed
+    reqs = memcache_adversarial(n, seed) if adversarial else memcache_requests(n, seed)
+    arena, offs, lens = pack(reqs)
+    rng = np.random.default_rng(seed + 1)
+    conn_ids = rng.integers(0, nconns, size=n).astype(np.uint32)
+    # remotes: 3/4 inside the mc-rule group, 1/4 outside; a few on another port (port-0 entry)
+    src = np.where(np.arange(nconns) % 4 != 3, 3000 + np.arange(nconns) % 128, 9000 + np.arange(nconns))
+    conns = make_conns(nconns, 0, MC_PORT, True, PROTO_MEMCACHE, src)
+    conns["port"][::16] = 11212
+    return Workload("cfg5-mc", arena, offs, lens, conn_ids, conns, mc_policy())

@@ -19,6 +19,10 @@
  *                       kafka.ReadRequest + canAccess/MatchesRule  pkg/kafka/request.go:186-229,
  *                                                                  pkg/proxy/kafka.go:117-153,
  *                                                                  pkg/kafka/policy.go:200-225
+ *                       proxylib OnData (memcache parser) -> Connection.Matches
+ *                                                                  proxylib/proxylib.go:97-110,
+ *                                                                  proxylib/memcached/parser.go:186-202,
+ *                                                                  proxylib/proxylib/policymap.go:210-236
  *   l7g_counters        Endpoint.UpdateProxyStatistics counters    pkg/endpoint/endpoint.go:2207-2233
  *
  * Verdict codes match the oracle (oracle/l7ref.h) and DESIGN.md.
@@ -61,6 +65,7 @@ typedef struct {
     uint64_t http_image_bytes;  /* all HTTP rule-set images */
     int32_t hot_ruleset;        /* HTTP rule set staged in LDS, -1 none */
     uint32_t hot_image_bytes;
+    uint32_t mc_rulesets, mc_rules, mc_dfas, mc_dfa_states;
 } l7g_stats_t;
 
 /* Engine bound to one HIP device.  err receives a message on failure.
@@ -81,7 +86,9 @@ int32_t l7g_policy_nrules(l7g_engine *e);
 int l7g_conns_set(l7g_engine *e, const l7g_conn_t *conns, uint32_t n, char *err, size_t errlen);
 
 /* Classifies n requests resident in device memory: request i is
- * arena[off[i] .. off[i]+len[i]) on connection conn[i].  Writes verdict[i],
+ * arena[off[i] .. off[i]+len[i]) on connection conn[i].  The arena must stay
+ * readable up to the next 16-byte boundary past its last byte (true of every
+ * hipMalloc / torch allocation); the kernels read aligned 16-byte words.  Writes verdict[i],
  * rule[i] (global rule id, -1 = none) and consumed[i] (bytes of the first
  * complete request; 0 unless ALLOW/DENY).  Asynchronous on `stream`
  * (a hipStream_t, NULL = default stream).  counters may be NULL, else a

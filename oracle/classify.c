@@ -20,7 +20,7 @@
 #include <string.h>
 #include "ref_internal.h"
 
-typedef struct { char *err; size_t errlen; int failed; int next_id; } ld;
+typedef struct { char *err; size_t errlen; int failed; int next_id; int mc_stop; } ld;
 
 static int lerr(ld *l, const char *fmt, const char *a) {
     if (!l->failed) { snprintf(l->err, l->errlen, fmt, a ? a : ""); l->failed = 1; }
@@ -226,7 +226,7 @@ static int load_rule(ld *l, const jnode *j, ref_pnp_rule *r) {
     } else if (l7) {
         r->l7type = L7T_L7; r->nl7 = l7->n;
         r->l7 = calloc((size_t)l7->n + 1, sizeof(ref_mc_rule));
-        int mc = r->l7proto && !strcmp(r->l7proto, "memcache");
+        int mc = !l->mc_stop && r->l7proto && !strcmp(r->l7proto, "memcache");
         for (int i = 0; i < l7->n; i++) {
             r->l7[i].id = l->next_id++;
             if (mc && load_mc_rule(l, l7->items[i], &r->l7[i]) < 0) return -1;
@@ -254,19 +254,19 @@ static int load_ports(ld *l, const jnode *arr, ref_port **out, int *nout) {
         if (rs && rs->type == JN_ARR) {
             ps[i].nrules = rs->n;
             ps[i].rules = calloc((size_t)rs->n + 1, sizeof(ref_pnp_rule));
-            const char *first = NULL;
+            /* proxylib parses a port's rules in order and stops at the first rule
+             * whose L7 parser is not registered (policymap.go:118-131): later
+             * memcache rules are never parsed, so they raise no ParseError.  With
+             * "memcache" the only registered parser, the "Mismatching L7 types"
+             * panic (:135-140) cannot fire. */
+            l->mc_stop = 0;
             for (int k = 0; k < rs->n; k++) {
                 if (load_rule(l, rs->items[k], &ps[i].rules[k]) < 0) return -1;
                 if (ps[i].rules[k].l7type == L7T_HTTP) ps[i].has_http = 1;
-                /* proxylib: "Mismatching L7 types on the same port" (policymap.go:137-143) */
                 const ref_pnp_rule *pr = &ps[i].rules[k];
-                static const char *ONEOF[] = {"", "PortNetworkPolicyRule_HttpRules", "PortNetworkPolicyRule_KafkaRules",
-                                              "PortNetworkPolicyRule_L7Rules"};
-                const char *name = pr->l7proto && *pr->l7proto ? pr->l7proto : ONEOF[pr->l7type];
-                if (*name) {
-                    if (!first) first = name;
-                    else if (strcmp(first, name)) return lerr(l, "NPDS: Mismatching L7 types on the same port%s", NULL);
-                }
+                if ((pr->l7proto && *pr->l7proto && strcmp(pr->l7proto, "memcache")) ||
+                    ((!pr->l7proto || !*pr->l7proto) && pr->l7type != L7T_NONE))
+                    l->mc_stop = 1;
             }
         }
         if (ps[i].tcp)
