@@ -53,6 +53,7 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     from cilium_amd import Engine, gen
+    from cilium_amd import dist as l7dist
 
     t0 = time.time()
     w = gen.http_workload(2, args.requests, seed=gen.SEED_BASE + 2 + 7919 * rank)
@@ -60,7 +61,9 @@ def main():
     log(f"[rank {rank}] generated {n} requests ({w.arena.nbytes / 1e9:.2f} GB) in {time.time() - t0:.1f}s")
 
     eng = Engine(local)
-    eng.update_policy(w.policy)
+    # the policy arrives at rank 0 (NPDS) and is broadcast to every rank over RCCL
+    policy = l7dist.broadcast_policy(w.policy, dist, device=dev) if dist is not None else w.policy
+    eng.update_policy(policy)
     eng.set_connections(w.conns)
     nrules = eng.nrules
 
@@ -87,7 +90,7 @@ def main():
         if i is not None:
             ev[i][1].record(stream)
         if dist is not None:
-            dist.all_reduce(step_counters)  # RCCL over xGMI: per-rule hit counters
+            l7dist.allreduce_counters(step_counters, dist)  # RCCL over xGMI: per-rule hit counters
         totals.add_(step_counters)
 
     for _ in range(args.warmup):

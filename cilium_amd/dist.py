@@ -1,0 +1,58 @@
+"""Multi-GPU plumbing for the verdict path.
+
+One process per GPU.  Requests are independent given their connection, so
+the data path shards by connection with no collective; the two exchange
+steps are
+  * policy distribution: the policy set (cilium.NetworkPolicy list, JSON)
+    arrives at rank 0 (the NPDS client, proxylib/proxylib/instance.go:168-219)
+    and is broadcast as bytes; every rank compiles the same immutable tables;
+  * per-rule hit counters: one all-reduce(sum) of the (rules + 8) uint64
+    counters per batch (the UpdateProxyStatistics feed,
+    pkg/endpoint/endpoint.go:2207-2233).
+`torch.distributed` with backend "nccl" is RCCL over xGMI on the MI355X box;
+the same functions run over "gloo" on CPU tensors in the tests.
+"""
+import json
+
+import numpy as np
+
+
+def broadcast_policy(policy, dist, src=0, device=None):
+    """Return the policy JSON bytes held by `src` on every rank.
+    `policy` (dict / str / bytes) is only read on `src`."""
+    import torch
+    rank = dist.get_rank()
+    if rank == src:
+        b = policy if isinstance(policy, bytes) else (policy if isinstance(policy, str) else json.dumps(policy)).encode()
+        n = torch.tensor([len(b)], dtype=torch.int64, device=device)
+    else:
+        b = None
+        n = torch.zeros(1, dtype=torch.int64, device=device)
+    dist.broadcast(n, src)
+    buf = torch.empty(int(n.item()), dtype=torch.uint8, device=device)
+    if rank == src:
+        buf.copy_(torch.frombuffer(bytearray(b), dtype=torch.uint8))
+    dist.broadcast(buf, src)
+    return bytes(buf.cpu().numpy().tobytes())
+
+
+def allreduce_counters(counters, dist):
+    """Sum per-rule hit counters (int64 tensor, rules + 8) over all ranks, in place."""
+    dist.all_reduce(counters)
+    return counters
+
+
+def shard_by_connection(conn_ids, lengths, nconns, world):
+    """Assign whole connections to ranks as contiguous connection ranges with
+    balanced payload bytes (a connection's stream stays on one GPU: framing
+    state, reply queues).  Returns (owner[nconns], request index list per rank)."""
+    conn_ids = np.asarray(conn_ids, np.int64)
+    per_conn = np.bincount(conn_ids, weights=np.asarray(lengths, np.float64), minlength=nconns)
+    cum = np.cumsum(per_conn)
+    total = cum[-1] if nconns else 0.0
+    # connection c goes to the rank whose byte range holds its midpoint
+    mid = cum - per_conn / 2
+    owner = np.minimum((mid * world // max(total, 1.0)).astype(np.int64), world - 1) if nconns else np.zeros(0, np.int64)
+    owner = np.maximum.accumulate(owner)  # contiguous, non-decreasing ranges
+    req_owner = owner[conn_ids]
+    return owner, [np.nonzero(req_owner == r)[0] for r in range(world)]
