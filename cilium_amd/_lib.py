@@ -20,7 +20,7 @@ VERDICT_NAMES = {DENY: "DENY", ALLOW: "ALLOW", PARSE_ERROR: "PARSE_ERROR",
 class Conn(C.Structure):
     """l7g_conn_t (20 bytes; same layout as the oracle's ref_conn_t)."""
     _fields_ = [("policy", C.c_int32), ("port", C.c_uint32), ("ingress", C.c_uint8),
-                ("proto", C.c_uint8), ("_pad", C.c_uint16), ("src_id", C.c_uint32),
+                ("proto", C.c_uint8), ("flags", C.c_uint16), ("src_id", C.c_uint32),
                 ("dst_id", C.c_uint32)]
 
 
@@ -35,7 +35,7 @@ class Stats(C.Structure):
 
 EXPORTS = (
     "l7g_engine_create", "l7g_engine_destroy", "l7g_policy_update", "l7g_policy_index",
-    "l7g_policy_nrules", "l7g_conns_set", "l7g_classify", "l7g_classify_host", "l7g_stats",
+    "l7g_policy_nrules", "l7g_conns_set", "l7g_conn_update", "l7g_classify", "l7g_classify_host", "l7g_stats",
     "l7g_debug_regex", "l7g_debug_phase_times",
 )
 
@@ -59,6 +59,7 @@ def load():
     lib.l7g_policy_nrules.restype = C.c_int32
     lib.l7g_policy_nrules.argtypes = [vp]
     lib.l7g_conns_set.argtypes = [vp, vp, C.c_uint32, cp, sz]
+    lib.l7g_conn_update.argtypes = [vp, C.c_uint32, vp, cp, sz]
     lib.l7g_classify.argtypes = [vp, vp, vp, vp, vp, C.c_uint32, vp, vp, vp, vp, vp]
     lib.l7g_classify_host.argtypes = [vp, vp, C.c_uint64, vp, vp, vp, C.c_uint32, vp, vp, vp]
     lib.l7g_stats.argtypes = [vp, C.POINTER(Stats)]

@@ -88,6 +88,14 @@ def build(verbose=False, jobs=8, timing=False, variant=None, defines=()):
         if r.returncode != 0:
             raise RuntimeError(f"link failed: {' '.join(link)}\n{r.stdout}\n{r.stderr}")
         os.replace(LIB_OUT + ".tmp", LIB_OUT)
+    if not variant:
+        # proxylib drop-in name: Envoy's Go filter dlopen()s "libcilium.so"
+        # (pkg/envoy/server.go:227); it binds the five proxylib symbols.
+        alias = os.path.join(HERE, "libcilium.so")
+        if not os.path.islink(alias) or os.readlink(alias) != os.path.basename(LIB_OUT):
+            if os.path.lexists(alias):
+                os.remove(alias)
+            os.symlink(os.path.basename(LIB_OUT), alias)
     return LIB_OUT
 
 

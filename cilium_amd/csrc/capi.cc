@@ -53,6 +53,11 @@ struct l7g_engine {
     bool tables_dirty = true, conns_dirty = true;
     bool has_http = false, has_kafka = false, has_mc = false;
     int32_t hot_ruleset = -1;  // HTTP rule set staged in LDS (most connections)
+    // l7g_classify_host scratch (grow-only), guarded by smu
+    std::mutex smu;
+    hipStream_t sstream = nullptr;
+    uint8_t *s_arena = nullptr, *s_req = nullptr;
+    size_t s_arena_cap = 0, s_n_cap = 0;
     bool any_cold = false;     // some HTTP connection uses another rule set
 };
 
@@ -73,36 +78,38 @@ size_t Put(std::vector<uint8_t> &blob, const std::vector<T> &v) {
     return off;
 }
 
-// Resolve every connection to its rule set (once per connection / policy version).
-bool ResolveConns(l7g_engine *e, std::string *err) {
-    e->conns.assign(e->attrs.size(), DevConn{-1, PROTO_NONE, {0, 0, 0}});
-    e->has_http = e->has_kafka = e->has_mc = false;
-    for (size_t i = 0; i < e->attrs.size(); i++) {
-        const l7g_conn_t &a = e->attrs[i];
-        DevConn &c = e->conns[i];
-        c.proto = a.proto;
-        if (a.proto == PROTO_HTTP) {
-            // remote identity: ingress = source, egress = destination (cilium_l7policy.cc:144-150)
-            uint64_t remote = a.ingress ? a.src_id : a.dst_id;
-            c.ruleset = e->hc->RulesetFor(a.policy, a.ingress != 0, a.port, remote, err);
-            if (c.ruleset < 0) return false;
-            e->has_http = true;
-        } else if (a.proto == PROTO_KAFKA) {
-            // Kafka rules are selected by the source identity in both directions
-            // (pkg/proxy/kafka.go:327,357)
-            c.ruleset = e->kc->RulesetFor(a.policy, a.ingress != 0, a.port, a.src_id, err);
-            if (c.ruleset < 0) return false;
-            e->has_kafka = true;
-        } else if (a.proto == PROTO_MEMCACHE) {
-            // proxylib matches on the connection's SrcId in both directions
-            // (proxylib/proxylib/connection.go:176-179)
-            c.ruleset = e->mc->RulesetFor(a.policy, a.ingress != 0, a.port, a.src_id, err);
-            if (c.ruleset < 0) return false;
-            e->has_mc = true;
-        }
+// Resolve connection i to its rule set (once per connection / policy version).
+bool ResolveOne(l7g_engine *e, size_t i, std::string *err) {
+    const l7g_conn_t &a = e->attrs[i];
+    DevConn &c = e->conns[i];
+    c = DevConn{-1, PROTO_NONE, 0, {0, 0}};
+    c.proto = a.proto;
+    c.flags = (uint8_t)(a.flags & 3);
+    if (a.proto == PROTO_HTTP) {
+        // remote identity: ingress = source, egress = destination (cilium_l7policy.cc:144-150)
+        uint64_t remote = a.ingress ? a.src_id : a.dst_id;
+        c.ruleset = e->hc->RulesetFor(a.policy, a.ingress != 0, a.port, remote, err);
+        if (c.ruleset < 0) return false;
+        e->has_http = true;
+    } else if (a.proto == PROTO_KAFKA) {
+        // Kafka rules are selected by the source identity in both directions
+        // (pkg/proxy/kafka.go:327,357)
+        c.ruleset = e->kc->RulesetFor(a.policy, a.ingress != 0, a.port, a.src_id, err);
+        if (c.ruleset < 0) return false;
+        e->has_kafka = true;
+    } else if (a.proto == PROTO_MEMCACHE) {
+        // proxylib matches on the connection's SrcId in both directions
+        // (proxylib/proxylib/connection.go:176-179)
+        c.ruleset = e->mc->RulesetFor(a.policy, a.ingress != 0, a.port, a.src_id, err);
+        if (c.ruleset < 0) return false;
+        e->has_mc = true;
     }
-    // The rule set serving the most connections has its image staged in LDS
-    // by every workgroup (if it fits); the others are read from HBM/L2.
+    return true;
+}
+
+// The HTTP rule set serving the most connections has its image staged in LDS
+// by every workgroup (if it fits); the others are read from HBM/L2.
+void PickHot(l7g_engine *e) {
     std::vector<uint32_t> uses(e->hc->image().rulesets.size(), 0);
     for (size_t i = 0; i < e->attrs.size(); i++)
         if (e->attrs[i].proto == PROTO_HTTP && e->conns[i].ruleset >= 0) uses[e->conns[i].ruleset]++;
@@ -113,6 +120,19 @@ bool ResolveConns(l7g_engine *e, std::string *err) {
     e->any_cold = false;
     for (size_t i = 0; i < e->attrs.size(); i++)
         if (e->attrs[i].proto == PROTO_HTTP && e->conns[i].ruleset != e->hot_ruleset) e->any_cold = true;
+}
+
+size_t TableRulesets(const l7g_engine *e) {
+    return e->hc->image().rulesets.size() + e->kc->image().rulesets.size() + e->mc->image().rulesets.size();
+}
+
+// Resolve every connection (policy update / connection table replaced).
+bool ResolveConns(l7g_engine *e, std::string *err) {
+    e->conns.assign(e->attrs.size(), DevConn{-1, PROTO_NONE, 0, {0, 0}});
+    e->has_http = e->has_kafka = e->has_mc = false;
+    for (size_t i = 0; i < e->attrs.size(); i++)
+        if (!ResolveOne(e, i, err)) return false;
+    PickHot(e);
     e->tables_dirty = e->conns_dirty = true;
     return true;
 }
@@ -207,6 +227,9 @@ void l7g_engine_destroy(l7g_engine *e) {
     hipDeviceSynchronize();
     if (e->d_blob) hipFree(e->d_blob);
     if (e->d_conns) hipFree(e->d_conns);
+    if (e->s_arena) hipFree(e->s_arena);
+    if (e->s_req) hipFree(e->s_req);
+    if (e->sstream) hipStreamDestroy(e->sstream);
     delete e;
 }
 
@@ -254,6 +277,34 @@ int l7g_conns_set(l7g_engine *e, const l7g_conn_t *conns, uint32_t n, char *err,
     return 0;
 }
 
+int l7g_conn_update(l7g_engine *e, uint32_t index, const l7g_conn_t *conn, char *err, size_t errlen) {
+    std::lock_guard<std::mutex> g(e->mu);
+    if (index >= e->attrs.size()) {
+        l7g_conn_t none{};
+        none.policy = -1;
+        e->attrs.resize((size_t)index + 1, none);
+        e->conns.resize((size_t)index + 1, DevConn{-1, PROTO_NONE, 0, {0, 0}});
+    }
+    const l7g_conn_t prev = e->attrs[index];
+    const size_t nrs = TableRulesets(e);
+    e->attrs[index] = *conn;
+    std::string m;
+    if (!ResolveOne(e, index, &m)) {
+        e->attrs[index] = prev;
+        ResolveOne(e, index, &m);
+        set_err(err, errlen, m);
+        return -1;
+    }
+    if (TableRulesets(e) != nrs) e->tables_dirty = true;
+    if (conn->proto == PROTO_HTTP || prev.proto == PROTO_HTTP) {
+        const int32_t hot = e->hot_ruleset;
+        PickHot(e);
+        if (hot != e->hot_ruleset) e->tables_dirty = true;
+    }
+    e->conns_dirty = true;
+    return 0;
+}
+
 int l7g_classify(l7g_engine *e, const uint8_t *arena, const uint64_t *off, const uint32_t *len, const uint32_t *conn,
                  uint32_t n, uint8_t *verdict, int32_t *rule, uint32_t *consumed, uint64_t *counters, void *stream) {
     std::lock_guard<std::mutex> g(e->mu);
@@ -281,30 +332,44 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, const uint64_t *off, const
 int l7g_classify_host(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const uint64_t *off, const uint32_t *len,
                       const uint32_t *conn, uint32_t n, uint8_t *verdict, int32_t *rule, uint32_t *consumed) {
     if (e->device < 0) return (int)hipErrorNoDevice;
+    std::lock_guard<std::mutex> g(e->smu);
     hipError_t rc = hipSetDevice(e->device);
     if (rc != hipSuccess) return (int)rc;
-    uint8_t *d_a = nullptr, *d_v = nullptr;
-    uint64_t *d_o = nullptr;
-    uint32_t *d_l = nullptr, *d_c = nullptr, *d_cons = nullptr;
-    int32_t *d_r = nullptr;
-    size_t nn = std::max<uint32_t>(n, 1);
-    rc = hipMalloc(&d_a, arena_len + 64);
-    if (rc == hipSuccess) rc = hipMalloc(&d_o, nn * 8);
-    if (rc == hipSuccess) rc = hipMalloc(&d_l, nn * 4);
-    if (rc == hipSuccess) rc = hipMalloc(&d_c, nn * 4);
-    if (rc == hipSuccess) rc = hipMalloc(&d_v, nn);
-    if (rc == hipSuccess) rc = hipMalloc(&d_r, nn * 4);
-    if (rc == hipSuccess) rc = hipMalloc(&d_cons, nn * 4);
-    if (rc == hipSuccess && arena_len) rc = hipMemcpy(d_a, arena, arena_len, hipMemcpyHostToDevice);
-    if (rc == hipSuccess && n) rc = hipMemcpy(d_o, off, n * 8, hipMemcpyHostToDevice);
-    if (rc == hipSuccess && n) rc = hipMemcpy(d_l, len, n * 4, hipMemcpyHostToDevice);
-    if (rc == hipSuccess && n) rc = hipMemcpy(d_c, conn, n * 4, hipMemcpyHostToDevice);
-    if (rc == hipSuccess) rc = (hipError_t)l7g_classify(e, d_a, d_o, d_l, d_c, n, d_v, d_r, d_cons, nullptr, nullptr);
-    if (rc == hipSuccess) rc = hipDeviceSynchronize();
-    if (rc == hipSuccess && n) rc = hipMemcpy(verdict, d_v, n, hipMemcpyDeviceToHost);
-    if (rc == hipSuccess && n) rc = hipMemcpy(rule, d_r, n * 4, hipMemcpyDeviceToHost);
-    if (rc == hipSuccess && n) rc = hipMemcpy(consumed, d_cons, n * 4, hipMemcpyDeviceToHost);
-    hipFree(d_a); hipFree(d_o); hipFree(d_l); hipFree(d_c); hipFree(d_v); hipFree(d_r); hipFree(d_cons);
+    if (!e->sstream && (rc = hipStreamCreateWithFlags(&e->sstream, hipStreamNonBlocking)) != hipSuccess) return (int)rc;
+    // grow-only device scratch: arena (+64 B so aligned 16-byte reads stay inside) and per-request arrays
+    const size_t need_a = arena_len + 64, need_n = std::max<uint32_t>(n, 1);
+    if (need_a > e->s_arena_cap) {
+        if (e->s_arena) hipFree(e->s_arena);
+        e->s_arena = nullptr;
+        e->s_arena_cap = 0;
+        size_t cap = std::max<size_t>(need_a, 1 << 16);
+        if ((rc = hipMalloc(&e->s_arena, cap)) != hipSuccess) return (int)rc;
+        e->s_arena_cap = cap;
+    }
+    if (need_n > e->s_n_cap) {
+        if (e->s_req) hipFree(e->s_req);
+        e->s_req = nullptr;
+        e->s_n_cap = 0;
+        size_t cap = std::max<size_t>(need_n, 1024);
+        if ((rc = hipMalloc(&e->s_req, cap * 25)) != hipSuccess) return (int)rc;
+        e->s_n_cap = cap;
+    }
+    uint8_t *base = e->s_req;
+    const size_t cap = e->s_n_cap;
+    uint64_t *d_o = (uint64_t *)base;
+    uint32_t *d_l = (uint32_t *)(base + cap * 8), *d_c = (uint32_t *)(base + cap * 12), *d_cons = (uint32_t *)(base + cap * 16);
+    int32_t *d_r = (int32_t *)(base + cap * 20);
+    uint8_t *d_v = base + cap * 24;
+    hipStream_t s = e->sstream;
+    if (arena_len) rc = hipMemcpyAsync(e->s_arena, arena, arena_len, hipMemcpyHostToDevice, s);
+    if (rc == hipSuccess && n) rc = hipMemcpyAsync(d_o, off, n * 8, hipMemcpyHostToDevice, s);
+    if (rc == hipSuccess && n) rc = hipMemcpyAsync(d_l, len, n * 4, hipMemcpyHostToDevice, s);
+    if (rc == hipSuccess && n) rc = hipMemcpyAsync(d_c, conn, n * 4, hipMemcpyHostToDevice, s);
+    if (rc == hipSuccess) rc = (hipError_t)l7g_classify(e, e->s_arena, d_o, d_l, d_c, n, d_v, d_r, d_cons, nullptr, s);
+    if (rc == hipSuccess && n) rc = hipMemcpyAsync(verdict, d_v, n, hipMemcpyDeviceToHost, s);
+    if (rc == hipSuccess && n) rc = hipMemcpyAsync(rule, d_r, n * 4, hipMemcpyDeviceToHost, s);
+    if (rc == hipSuccess && n) rc = hipMemcpyAsync(consumed, d_cons, n * 4, hipMemcpyDeviceToHost, s);
+    if (rc == hipSuccess) rc = hipStreamSynchronize(s);
     return (int)rc;
 }
 

@@ -22,7 +22,8 @@ constexpr int kNumSlots = SLOT_CUSTOM0 + kMaxCustomHeaders;
 struct DevConn {
     int32_t ruleset;   // index into HttpTables::rulesets / KafkaTables::rulesets
     uint8_t proto;     // PROTO_*
-    uint8_t pad[3];
+    uint8_t flags;     // memcached: L7G_CONN_MC_TEXT / _BINARY (0 = by first byte)
+    uint8_t pad[2];
 };
 
 // ---------------- HTTP ----------------

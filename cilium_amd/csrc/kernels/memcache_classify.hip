@@ -15,10 +15,12 @@
 // (in evaluation order) with  empty || (command && all keys), else the rule
 // set's terminal verdict.
 //
-// Batch conventions: MORE => INCOMPLETE; a Go panic or ERROR
-// => PARSE_ERROR; PASS/DROP => ALLOW/DENY with consumed = proxylib's frame
-// length (it may exceed the buffer); a frame length outside 1..2^32-1 =>
-// PARSE_ERROR.
+// Batch conventions (include/l7gpu.h): PASS/DROP => ALLOW/DENY
+// with consumed = proxylib's frame length (it may exceed the buffer); MORE n
+// => INCOMPLETE, consumed n (NOP => 0); panic / ERROR 0 => PARSE_ERROR,
+// consumed 0; binary ERROR_INVALID_FRAME_TYPE => PARSE_ERROR, consumed 2; a
+// frame length outside 1..2^32-1 => PARSE_ERROR.  The connection flags hold
+// the parser its first byte chose (0: this buffer's first byte decides).
 #include <hip/hip_runtime.h>
 
 #include "../device_tables.h"
@@ -205,16 +207,21 @@ __global__ __launch_bounds__(kBlock) void memcache_classify_kernel(
         I.dn = I.ndfa - d0 < (uint32_t)kMcMaxDfas ? I.ndfa - d0 : (uint32_t)kMcMaxDfas;
         keys_reset(I, K);
         do {
-            if (len == 0) { verdict = V_INCOMPLETE; break; }  // NOP, 0
-            const uint32_t b0 = b[0];
-            if (b0 >= 0x80) {
+            uint32_t mode = conn.flags & 3;
+            if (len == 0 && mode == 0) { verdict = V_INCOMPLETE; break; }  // NOP, 0
+            if (mode == 0) mode = b[0] >= 0x80 ? 2 : 1;
+            if (mode == 2) {
                 // ---- binary header (binary/parser.go:72-139)
-                if (len < 24) { verdict = V_INCOMPLETE; break; }
+                if (len < 24) { verdict = V_INCOMPLETE; consumed = 24 - len; break; }  // MORE headerMissing
                 const uint32_t keylen = (uint32_t)b[2] << 8 | b[3];
                 const uint32_t extras = b[4];
                 const uint32_t body = (uint32_t)b[8] << 24 | (uint32_t)b[9] << 16 | (uint32_t)b[10] << 8 | b[11];
-                if (keylen > 0 && 24 + keylen + extras > len) { verdict = V_INCOMPLETE; break; }
-                // (b0 & 0x80) == RequestMagic always holds here (getOpcodeAndKey)
+                if (keylen > 0 && 24 + keylen + extras > len) {  // MORE keyMissing
+                    verdict = V_INCOMPLETE;
+                    consumed = 24 + keylen + extras - len;
+                    break;
+                }
+                if ((b[0] & 0x80) == 0) { consumed = 2; break; }  // ERROR, ERROR_INVALID_FRAME_TYPE
                 cmdmask = u64at(I, hdr32(I, MC_OFF(op_off))) + (size_t)b[1] * I.nch;
                 Reader R{b, ~0ull, 0, 0, 0, 0};
                 for (uint32_t i = 24 + extras, e = 24 + extras + keylen; i < e; i++) keys_step(I, K, rd(R, i));
@@ -272,7 +279,11 @@ __global__ __launch_bounds__(kBlock) void memcache_classify_kernel(
                     }
                     i++;
                 }
-                if (!found) { verdict = V_INCOMPLETE; break; }  // MORE
+                if (!found) {  // MORE 1 if the data ends in '\r', else MORE 2
+                    verdict = V_INCOMPLETE;
+                    consumed = (len > 0 && b[len - 1] == '\r') ? 1 : 2;
+                    break;
+                }
                 if (in_tok) {
                     if (nt == 1) classify_cmd(cw, clen, fr, cmd_id);
                     if (key_tok) keys_end(I, K);

@@ -1,0 +1,511 @@
+// proxylib C-ABI over the GPU verdict path (product code, include/proxylib_abi.h).
+//
+//   OpenModule / CloseModule   proxylib/proxylib.go:124-155, instance.go:85-143
+//   OnNewConnection            proxylib/proxylib.go:57-74, connection.go:65-101
+//   OnData                     proxylib/proxylib.go:98-108, connection.go:104-174
+//   Close                      proxylib/proxylib.go:112-116
+// and the "memcache" parser (proxylib/memcached/parser.go:186-202 with
+// text/parser.go:72-330 and binary/parser.go:58-205).  Every request-direction
+// parser step asks the device for the frame's verdict (l7g_classify_host on
+// the connection's slot of the engine's connection table): the kernel frames
+// the request, tokenises it and evaluates the policy; the host keeps what
+// proxylib keeps per connection — the parser chosen by the first byte, the
+// text reply-intent queue, the binary inject queue and request/reply counts —
+// and drives the op loop and inject buffers exactly as connection.go does.
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <shared_mutex>
+#include <string>
+#include <vector>
+
+#include "../../../include/l7gpu.h"
+#include "../../../include/proxylib_abi.h"
+
+namespace {
+
+constexpr int64_t NOP = 256;  // proxylib-internal op (types.go:34)
+
+struct Instance {
+    uint64_t id = 0, open = 0;
+    std::string node, xds, alog;
+    l7g_engine *eng = nullptr;
+    std::mutex mu;                 // slot allocation / policy swaps
+    std::vector<uint32_t> free_slots;
+    uint32_t next_slot = 0;
+};
+
+std::mutex g_inst_mu;
+std::map<uint64_t, std::shared_ptr<Instance>> g_instances;
+uint64_t g_last_instance = 0;
+
+// ---------------------------------------------------------------- bytes.Fields
+// Unicode White_Space rune length at s[i] (unicode.IsSpace), 0 if none; a
+// multi-byte space starts with a UTF-8 lead byte, which is always a rune
+// start, so no decoding context is needed.
+size_t SpaceLen(const uint8_t *s, size_t i, size_t n) {
+    uint8_t c = s[i];
+    if (c == ' ' || (c >= 0x09 && c <= 0x0D)) return 1;
+    if (c < 0xC2 || c > 0xE3 || i + 1 >= n) return 0;
+    uint8_t c1 = s[i + 1];
+    if (c == 0xC2) return (c1 == 0x85 || c1 == 0xA0) ? 2 : 0;
+    if (i + 2 >= n) return 0;
+    uint8_t c2 = s[i + 2];
+    if (c == 0xE1) return (c1 == 0x9A && c2 == 0x80) ? 3 : 0;
+    if (c == 0xE2 && c1 == 0x80) return ((c2 >= 0x80 && c2 <= 0x8A) || c2 == 0xA8 || c2 == 0xA9 || c2 == 0xAF) ? 3 : 0;
+    if (c == 0xE2 && c1 == 0x81) return c2 == 0x9F ? 3 : 0;
+    if (c == 0xE3) return (c1 == 0x80 && c2 == 0x80) ? 3 : 0;
+    return 0;
+}
+
+std::vector<std::string> Fields(const uint8_t *s, size_t n) {
+    std::vector<std::string> out;
+    size_t i = 0, start = 0;
+    bool in = false;
+    while (i < n) {
+        size_t sp = SpaceLen(s, i, n);
+        if (sp) {
+            if (in) out.emplace_back((const char *)s + start, i - start);
+            in = false;
+            i += sp;
+        } else {
+            if (!in) { start = i; in = true; }
+            i++;
+        }
+    }
+    if (in) out.emplace_back((const char *)s + start, n - start);
+    return out;
+}
+
+struct Panic {};  // a Go runtime panic inside the parser (recovered => PARSER_ERROR)
+
+long FindCRLF(const std::string &d, size_t from = 0) {
+    size_t p = d.find("\r\n", from);
+    return p == std::string::npos ? -1 : (long)p;
+}
+
+const char kDeniedText[] = "CLIENT_ERROR access denied\r\n";  // text/parser.go:327
+const uint8_t kDeniedBinary[37] = {0x81, 0, 0, 0, 0, 0, 0, 8, 0, 0, 0, 0x0d, 0, 0, 0, 0, 0, 0, 0,
+                                   0,    0, 0, 0, 0, 'a', 'c', 'c', 'e', 's', 's', ' ', 'd', 'e', 'n', 'i', 'e', 'd'};
+
+// ---------------------------------------------------------------- connection
+struct Connection {
+    std::shared_ptr<Instance> ins;
+    uint64_t id = 0;
+    bool ingress = false;
+    uint32_t src = 0, dst = 0, port = 0;
+    std::string policy, proto;
+    GoSlice *orig = nullptr, *reply = nullptr;
+    uint32_t slot = 0;
+    // memcache parser state
+    int mode = 0;  // 0 none yet, L7G_CONN_MC_TEXT, L7G_CONN_MC_BINARY
+    struct Intent { std::string command; bool denied; };
+    std::deque<Intent> reply_queue;
+    bool watching = false;
+    struct Queued { uint8_t magic; uint32_t request; };
+    std::deque<Queued> inject_queue;
+    uint32_t requests = 0, replies = 0;
+
+    GoSlice *InjectBuf(bool r) const { return r ? reply : orig; }
+    int64_t Inject(bool r, const void *data, size_t n) {  // connection.go:190-203
+        GoSlice *b = InjectBuf(r);
+        size_t room = (size_t)(b->cap - b->len), k = n < room ? n : room;
+        memcpy((uint8_t *)b->data + b->len, data, k);
+        b->len += (GoInt)k;
+        return (int64_t)k;
+    }
+    bool InjectFull(bool r) const { const GoSlice *b = InjectBuf(r); return b->len == b->cap; }
+
+    l7g_conn_t Attrs() const {
+        l7g_conn_t a{};
+        a.policy = l7g_policy_index(ins->eng, policy.data(), policy.size());
+        a.port = port;
+        a.ingress = ingress ? 1 : 0;
+        a.proto = L7G_PROTO_MEMCACHE;
+        a.flags = (uint16_t)mode;
+        a.src_id = src;
+        a.dst_id = dst;
+        return a;
+    }
+    // Device verdict for the request at the start of `data` (one kernel lane).
+    bool Verdict(const std::string &data, uint8_t *v, int32_t *rule, uint32_t *consumed) {
+        uint64_t off = 0;
+        uint32_t len = (uint32_t)data.size(), cid = slot;
+        return l7g_classify_host(ins->eng, (const uint8_t *)data.data(), data.size(), &off, &len, &cid, 1, v, rule,
+                                 consumed) == 0;
+    }
+
+    // ---- text parser (text/parser.go:72-262)
+    int64_t TextInjectFromQueue() {
+        int injected = 0;
+        for (auto &r : reply_queue) {
+            if (!r.denied) break;
+            injected++;
+            Inject(true, kDeniedText, sizeof kDeniedText - 1);
+        }
+        for (int i = 0; i < injected; i++) reply_queue.pop_front();
+        return (int64_t)injected * (int64_t)(sizeof kDeniedText - 1);
+    }
+    static bool IsStorage(const std::string &c) {
+        return c == "set" || c == "add" || c == "replace" || c == "append" || c == "prepend" || c == "cas";
+    }
+    static bool IsRetrieval(const std::string &c) { return c.compare(0, 3, "get") == 0 || c.compare(0, 3, "gat") == 0; }
+    int64_t UntilEnd(const std::string &d, int64_t *n) {  // text/parser.go:266-273
+        size_t e = d.find("\r\nEND\r\n");
+        if (e != std::string::npos && e > 0) { *n = (int64_t)e + 7; return FILTEROP_PASS; }
+        *n = 1;
+        return FILTEROP_MORE;
+    }
+    int64_t TextOnData(bool r, const std::vector<std::string> &in, int64_t *n, bool *err) {
+        if (r) {
+            int64_t inj = TextInjectFromQueue();
+            if (inj > 0) { *n = inj; return FILTEROP_INJECT; }
+            if (in.empty()) { *n = 0; return NOP; }
+        }
+        std::string d;
+        for (auto &b : in) d += b;
+        long lf = FindCRLF(d);
+        if (lf < 0) { *n = (!d.empty() && d.back() == '\r') ? 1 : 2; return FILTEROP_MORE; }
+        auto tok = Fields((const uint8_t *)d.data(), (size_t)lf);
+        if (!r) {
+            uint8_t v;
+            int32_t rule;
+            uint32_t cons;
+            if (!Verdict(d, &v, &rule, &cons)) { *err = true; *n = 0; return FILTEROP_ERROR; }
+            if (v == L7G_INCOMPLETE) { *n = cons; return FILTEROP_MORE; }  // (not reached: CRLF found)
+            if (v != L7G_ALLOW && v != L7G_DENY) { *n = 0; return FILTEROP_ERROR; }  // panic / ERROR, 0
+            const std::string &cmd = tok[0];
+            const size_t nt = tok.size();
+            bool noreply = false;
+            if (IsRetrieval(cmd)) noreply = false;
+            else if (IsStorage(cmd)) noreply = nt == (cmd[0] == 'c' ? 7u : 6u);
+            else if (cmd == "delete") noreply = nt == 3;
+            else if (cmd == "incr" || cmd == "decr" || cmd == "touch") noreply = nt == 4;
+            else if (cmd == "flush_all" || cmd == "cache_memlimit") noreply = tok.back() == "noreply";
+            else if (cmd == "quit") noreply = true;
+            else if (cmd == "watch") watching = true;
+            *n = cons;
+            if (v == L7G_ALLOW) {
+                if (!noreply) reply_queue.push_back({cmd, false});
+                return FILTEROP_PASS;
+            }
+            if (!noreply) {
+                if (reply_queue.empty()) Inject(true, kDeniedText, sizeof kDeniedText - 1);
+                else reply_queue.push_back({cmd, true});
+            }
+            return FILTEROP_DROP;
+        }
+        if (reply_queue.empty()) throw Panic();  // p.replyQueue[0]
+        const Intent intent = reply_queue.front();
+        if (watching) { *n = lf + 2; return FILTEROP_PASS; }
+        if (tok.empty()) throw Panic();  // tokens[0]
+        const std::string &c = intent.command, &t0 = tok[0];
+        if (t0 == "ERROR" || t0 == "CLIENT_ERROR" || t0 == "SERVER_ERROR" || IsStorage(c) || c == "delete" || c == "incr" ||
+            c == "decr" || c == "touch" || c == "slabs" || c == "lru" || c == "flush_all" || c == "cache_memlimit" ||
+            c == "version" || c == "misbehave") {
+            reply_queue.pop_front();
+            *n = lf + 2;
+            return FILTEROP_PASS;
+        }
+        if (IsRetrieval(c) || c == "stats") {
+            int64_t op = UntilEnd(d, n);
+            if (op == FILTEROP_PASS) reply_queue.pop_front();
+            return op;
+        }
+        if (c == "lru_crawler") {
+            if (t0 == "OK" || t0 == "BUSY" || t0 == "BADCLASS") { reply_queue.pop_front(); *n = lf + 2; return FILTEROP_PASS; }
+            int64_t op = UntilEnd(d, n);
+            if (op == FILTEROP_PASS) reply_queue.pop_front();
+            return op;
+        }
+        *n = 0;
+        return FILTEROP_ERROR;
+    }
+
+    // ---- binary parser (binary/parser.go:58-205)
+    void BinaryInjectDenied(uint8_t magic) {
+        uint8_t m[sizeof kDeniedBinary];
+        memcpy(m, kDeniedBinary, sizeof m);
+        m[0] = magic;
+        Inject(true, m, sizeof m);
+        replies++;
+    }
+    int64_t BinaryOnData(bool r, const std::vector<std::string> &in, int64_t *n, bool *err) {
+        if (r) {
+            if (!inject_queue.empty() && inject_queue.front().request == replies + 1) {
+                BinaryInjectDenied(inject_queue.front().magic);
+                inject_queue.pop_front();
+                *n = sizeof kDeniedBinary;
+                return FILTEROP_INJECT;
+            }
+            if (in.empty()) { *n = 0; return NOP; }
+        }
+        std::string d;
+        for (auto &b : in) d += b;
+        if (!r) {
+            uint8_t v;
+            int32_t rule;
+            uint32_t cons;
+            if (!Verdict(d, &v, &rule, &cons)) { *err = true; *n = 0; return FILTEROP_ERROR; }
+            if (v == L7G_INCOMPLETE) { *n = cons; return FILTEROP_MORE; }
+            if (v != L7G_ALLOW && v != L7G_DENY) { *n = cons; return FILTEROP_ERROR; }  // ERROR, INVALID_FRAME_TYPE / 0
+            requests++;
+            *n = cons;
+            if (v == L7G_ALLOW) return FILTEROP_PASS;
+            const uint8_t magic = (uint8_t)(0x81 | (uint8_t)d[0]);
+            if (requests == replies + 1) BinaryInjectDenied(magic);
+            else inject_queue.push_back({magic, requests});
+            inject_queue.push_back({magic, requests});  // enqueued again (binary/parser.go:129-135)
+            return FILTEROP_DROP;
+        }
+        const uint8_t *b = (const uint8_t *)d.data();
+        if (d.size() < 24) { *n = 24 - (int64_t)d.size(); return FILTEROP_MORE; }
+        const uint32_t body = (uint32_t)b[8] << 24 | (uint32_t)b[9] << 16 | (uint32_t)b[10] << 8 | b[11];
+        const uint32_t keylen = (uint32_t)b[2] << 8 | b[3], extras = b[4];
+        if (keylen > 0 && 24 + keylen + extras > d.size()) { *n = 24 + keylen + extras - (int64_t)d.size(); return FILTEROP_MORE; }
+        if ((b[0] & 0x80) != 0x80) { *n = FILTEROP_ERROR_INVALID_FRAME_TYPE; return FILTEROP_ERROR; }
+        replies++;
+        *n = (int64_t)(uint32_t)(body + 24u);
+        return FILTEROP_PASS;
+    }
+
+    // memcache.Parser.OnData (memcached/parser.go:186-202)
+    int64_t ParserOnData(bool r, const std::vector<std::string> &in, bool first_nonempty, int64_t *n, bool *err) {
+        if (mode == 0) {
+            if (!first_nonempty) { *n = 0; return NOP; }
+            mode = (uint8_t)in[0][0] >= 128 ? L7G_CONN_MC_BINARY : L7G_CONN_MC_TEXT;
+            std::lock_guard<std::mutex> g(ins->mu);
+            l7g_conn_t a = Attrs();
+            if (l7g_conn_update(ins->eng, slot, &a, nullptr, 0) != 0) { *err = true; *n = 0; return FILTEROP_ERROR; }
+        }
+        return mode == L7G_CONN_MC_TEXT ? TextOnData(r, in, n, err) : BinaryOnData(r, in, n, err);
+    }
+};
+
+std::shared_mutex g_conn_mu;
+std::map<uint64_t, std::shared_ptr<Connection>> g_conns;
+
+std::string Str(GoString s) { return s.p && s.n > 0 ? std::string(s.p, (size_t)s.n) : std::string(); }
+
+// net.SplitHostPort + strconv.ParseUint(port, 10, 32), port != 0 (connection.go:71-78)
+bool DstPort(const std::string &addr, uint32_t *port) {
+    std::string p;
+    if (!addr.empty() && addr[0] == '[') {
+        size_t e = addr.find(']');
+        if (e == std::string::npos || e + 1 >= addr.size() || addr[e + 1] != ':') return false;
+        if (addr.find_first_of("[]", e + 1) != std::string::npos) return false;
+        p = addr.substr(e + 2);
+    } else {
+        size_t c = addr.rfind(':');
+        if (c == std::string::npos) return false;
+        if (addr.find(':') != c) return false;  // too many colons
+        if (addr.find_first_of("[]") != std::string::npos) return false;
+        p = addr.substr(c + 1);
+    }
+    if (p.empty() || p.size() > 20) return false;
+    uint64_t v = 0;
+    for (char ch : p) {
+        if (ch < '0' || ch > '9') return false;
+        v = v * 10 + (uint64_t)(ch - '0');
+        if (v > 0xFFFFFFFFull) return false;
+    }
+    if (v == 0) return false;
+    *port = (uint32_t)v;
+    return true;
+}
+
+std::shared_ptr<Instance> FindInstance(uint64_t id) {
+    std::lock_guard<std::mutex> g(g_inst_mu);
+    auto it = g_instances.find(id);
+    return it == g_instances.end() ? nullptr : it->second;
+}
+
+}  // namespace
+
+extern "C" {
+
+uint64_t OpenModule(GoSlice params, uint8_t debug) {
+    (void)debug;
+    std::string node, xds, alog;
+    const GoString *kv = (const GoString *)params.data;
+    for (GoInt i = 0; i < params.len; i++) {
+        std::string k = Str(kv[2 * i]), v = Str(kv[2 * i + 1]);
+        if (k == "access-log-path") alog = v;
+        else if (k == "xds-path") xds = v;
+        else if (k == "node-id") node = v;
+        else return 0;
+    }
+    std::lock_guard<std::mutex> g(g_inst_mu);
+    for (auto &it : g_instances) {  // instance.go:91-105
+        Instance &o = *it.second;
+        if ((node.empty() || o.node == node) && xds == o.xds && alog == o.alog) {
+            o.open++;
+            return o.id;
+        }
+    }
+    const char *dev = getenv("L7G_DEVICE");
+    int device = dev && *dev ? atoi(dev) : 0;
+    char err[256];
+    l7g_engine *e = l7g_engine_create(device, err, sizeof err);
+    if (!e) return 0;  // no GPU: fail loudly, there is no CPU verdict path
+    auto ins = std::make_shared<Instance>();
+    ins->id = ++g_last_instance;
+    ins->open = 1;
+    ins->node = node.empty() ? "host~127.0.0.1~libcilium-" + std::to_string(ins->id) + "~localdomain" : node;
+    ins->xds = xds;
+    ins->alog = alog;
+    ins->eng = e;
+    g_instances[ins->id] = ins;
+    return ins->id;
+}
+
+void CloseModule(uint64_t id) {
+    std::shared_ptr<Instance> dead;
+    {
+        std::lock_guard<std::mutex> g(g_inst_mu);
+        auto it = g_instances.find(id);
+        if (it == g_instances.end()) return;
+        if (--it->second->open > 0) return;
+        dead = it->second;
+        g_instances.erase(it);
+    }
+    // connections still referencing the instance keep it alive until closed
+    std::unique_lock<std::shared_mutex> g(g_conn_mu);
+    bool used = false;
+    for (auto &c : g_conns) used |= c.second->ins == dead;
+    if (!used) { l7g_engine_destroy(dead->eng); dead->eng = nullptr; }
+}
+
+FilterResult OnNewConnection(uint64_t instance_id, GoString proto, uint64_t connection_id, uint8_t ingress,
+                             uint32_t src_id, uint32_t dst_id, GoString src_addr, GoString dst_addr,
+                             GoString policy_name, GoSlice *orig_buf, GoSlice *reply_buf) {
+    (void)src_addr;
+    auto ins = FindInstance(instance_id);
+    if (!ins) return FILTER_INVALID_INSTANCE;
+    std::string p = Str(proto);
+    if (p != "memcache") return FILTER_UNKNOWN_PARSER;
+    uint32_t port;
+    if (!DstPort(Str(dst_addr), &port)) return FILTER_INVALID_ADDRESS;
+    auto c = std::make_shared<Connection>();
+    c->ins = ins;
+    c->id = connection_id;
+    c->ingress = ingress != 0;
+    c->src = src_id;
+    c->dst = dst_id;
+    c->port = port;
+    c->policy = Str(policy_name);
+    c->proto = p;
+    c->orig = orig_buf;
+    c->reply = reply_buf;
+    {
+        std::lock_guard<std::mutex> g(ins->mu);
+        if (!ins->free_slots.empty()) { c->slot = ins->free_slots.back(); ins->free_slots.pop_back(); }
+        else c->slot = ins->next_slot++;
+        l7g_conn_t a = c->Attrs();
+        if (l7g_conn_update(ins->eng, c->slot, &a, nullptr, 0) != 0) {
+            ins->free_slots.push_back(c->slot);
+            return FILTER_UNKNOWN_ERROR;
+        }
+    }
+    std::shared_ptr<Connection> old;
+    {
+        std::unique_lock<std::shared_mutex> g(g_conn_mu);
+        auto &slot = g_conns[connection_id];
+        old = slot;
+        slot = c;
+    }
+    if (old) {
+        std::lock_guard<std::mutex> g(old->ins->mu);
+        old->ins->free_slots.push_back(old->slot);
+    }
+    return FILTER_OK;
+}
+
+FilterResult OnData(uint64_t connection_id, uint8_t reply, uint8_t end_stream, GoSlice *data, GoSlice *ops) {
+    (void)end_stream;
+    std::shared_ptr<Connection> c;
+    {
+        std::shared_lock<std::shared_mutex> g(g_conn_mu);
+        auto it = g_conns.find(connection_id);
+        if (it == g_conns.end()) return FILTER_UNKNOWN_CONNECTION;
+        c = it->second;
+    }
+    // input: copies of the caller's [][]byte (not retained past the call)
+    std::vector<std::string> in;
+    const GoSlice *bufs = (const GoSlice *)data->data;
+    for (GoInt i = 0; i < data->len; i++) in.emplace_back((const char *)bufs[i].data, (size_t)bufs[i].len);
+    int64_t *op = (int64_t *)ops->data;
+    try {
+        while (ops->len < ops->cap) {  // connection.go:138-172
+            int64_t n = 0;
+            bool err = false;
+            const bool first_nonempty = !in.empty() && !in[0].empty();
+            int64_t o = c->ParserOnData(reply != 0, in, first_nonempty, &n, &err);
+            if (err) return FILTER_UNKNOWN_ERROR;  // device failure
+            if (o == NOP) break;
+            if (n == 0) return FILTER_PARSER_ERROR;
+            op[2 * ops->len] = o;
+            op[2 * ops->len + 1] = n;
+            ops->len++;
+            if (o == FILTEROP_MORE) break;
+            if (o == FILTEROP_PASS || o == FILTEROP_DROP) {  // advanceInput (connection.go:104-116)
+                int64_t k = n;
+                while (k > 0 && !in.empty()) {
+                    if ((size_t)k < in[0].size()) { in[0].erase(0, (size_t)k); k = 0; }
+                    else { k -= (int64_t)in[0].size(); in.erase(in.begin()); }
+                }
+            }
+            if (o == FILTEROP_INJECT && c->InjectFull(reply != 0)) break;
+        }
+    } catch (const Panic &) {
+        return FILTER_PARSER_ERROR;
+    }
+    return FILTER_OK;
+}
+
+void Close(uint64_t connection_id) {
+    std::shared_ptr<Connection> c;
+    {
+        std::unique_lock<std::shared_mutex> g(g_conn_mu);
+        auto it = g_conns.find(connection_id);
+        if (it == g_conns.end()) return;
+        c = it->second;
+        g_conns.erase(it);
+    }
+    std::lock_guard<std::mutex> g(c->ins->mu);
+    l7g_conn_t none{};
+    none.policy = -1;
+    if (c->ins->eng) l7g_conn_update(c->ins->eng, c->slot, &none, nullptr, 0);
+    c->ins->free_slots.push_back(c->slot);
+}
+
+int l7g_proxylib_policy_update(uint64_t instance_id, const char *json, size_t len, char *err, size_t errlen) {
+    auto ins = FindInstance(instance_id);
+    if (!ins) {
+        if (err && errlen) snprintf(err, errlen, "unknown instance %llu", (unsigned long long)instance_id);
+        return -1;
+    }
+    std::lock_guard<std::mutex> g(ins->mu);
+    if (l7g_policy_update(ins->eng, json, len, err, errlen) != 0) return -1;
+    // policy names may map to new indices: re-resolve this instance's connections
+    std::shared_lock<std::shared_mutex> gc(g_conn_mu);
+    for (auto &kv : g_conns) {
+        Connection &c = *kv.second;
+        if (c.ins != ins) continue;
+        l7g_conn_t a = c.Attrs();
+        if (l7g_conn_update(ins->eng, c.slot, &a, err, errlen) != 0) return -1;
+    }
+    return 0;
+}
+
+uint64_t l7g_proxylib_connections(void) {
+    std::shared_lock<std::shared_mutex> g(g_conn_mu);
+    return g_conns.size();
+}
+
+}  // extern "C"

@@ -106,7 +106,7 @@ class Engine:
 
 
 CONN_DTYPE = np.dtype([("policy", "<i4"), ("port", "<u4"), ("ingress", "u1"), ("proto", "u1"),
-                       ("_pad", "<u2"), ("src_id", "<u4"), ("dst_id", "<u4")])
+                       ("flags", "<u2"), ("src_id", "<u4"), ("dst_id", "<u4")])
 assert CONN_DTYPE.itemsize == C.sizeof(Conn)
 
 
@@ -116,7 +116,7 @@ def conns_array(conns):
     arr = np.zeros(len(conns), CONN_DTYPE)
     for i, c in enumerate(conns):
         if isinstance(c, dict):
-            for k in ("policy", "port", "ingress", "proto", "src_id", "dst_id"):
+            for k in ("policy", "port", "ingress", "proto", "flags", "src_id", "dst_id"):
                 arr[i][k] = c.get(k, 0)
         else:
             arr[i] = (c[0], c[1], c[2], c[3], 0, c[4], c[5])

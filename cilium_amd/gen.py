@@ -560,4 +560,6 @@ def memcache_workload(n, nconns=256, seed=None, adversarial=False):
     src = np.where(np.arange(nconns) % 4 != 3, 3000 + np.arange(nconns) % 128, 9000 + np.arange(nconns))
     conns = make_conns(nconns, 0, MC_PORT, True, PROTO_MEMCACHE, src)
     conns["port"][::16] = 11212
+    if adversarial:  # connections whose parser (text / binary) was already chosen by earlier traffic
+        conns["flags"] = rng.integers(0, 3, size=nconns)
     return Workload("cfg5-mc", arena, offs, lens, conn_ids, conns, mc_policy())

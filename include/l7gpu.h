@@ -11,7 +11,8 @@
  *                       (policies in the cilium.NetworkPolicy shape, envoy/cilium/npds.proto:31-182,
  *                        as JSON; see DESIGN.md §Policy JSON)
  *   l7g_policy_index    NetworkPolicyMap::GetPolicyInstance        envoy/cilium_network_policy.h:213-221
- *   l7g_conns_set       proxylib OnNewConnection / Close           proxylib/proxylib.go:57-74,112-116
+ *   l7g_conns_set,      proxylib OnNewConnection / Close           proxylib/proxylib.go:57-74,112-116
+ *   l7g_conn_update
  *                       Cilium::SocketOption (identity, port, dir) envoy/cilium_l7policy.cc:133-150
  *   l7g_classify        per request: AccessFilter::decodeHeaders -> NetworkPolicyMap::Allowed
  *                                                                  envoy/cilium_l7policy.cc:127-182,
@@ -47,13 +48,17 @@ enum {
     L7G_UNSUPPORTED = 4, /* framing not handled on the device (chunked body, compressed Kafka set) */
 };
 
+/* memcached: proxylib picks the text or binary parser from the first byte a
+ * connection carries and keeps it (proxylib/memcached/parser.go:186-202). */
+enum { L7G_CONN_MC_TEXT = 1, L7G_CONN_MC_BINARY = 2 };
+
 /* Connection attributes (20 bytes; identical layout to the oracle's ref_conn_t). */
 typedef struct {
     int32_t policy;   /* l7g_policy_index(name), -1 = no policy for this endpoint (deny) */
     uint32_t port;    /* destination port */
     uint8_t ingress;  /* 1 = ingress */
     uint8_t proto;    /* L7G_PROTO_* */
-    uint16_t _pad;
+    uint16_t flags;   /* L7G_CONN_MC_*: memcached parser chosen for the connection (0 = by first byte) */
     uint32_t src_id;  /* source security identity */
     uint32_t dst_id;  /* destination security identity */
 } l7g_conn_t;
@@ -85,12 +90,20 @@ int32_t l7g_policy_nrules(l7g_engine *e);
  * sets the connections need.  0 = ok. */
 int l7g_conns_set(l7g_engine *e, const l7g_conn_t *conns, uint32_t n, char *err, size_t errlen);
 
+/* Sets (or adds, growing the table) connection `index` alone; rule sets are
+ * compiled on first use.  The proxylib shim calls it from OnNewConnection /
+ * Close and when a memcached connection's parser is chosen.  0 = ok. */
+int l7g_conn_update(l7g_engine *e, uint32_t index, const l7g_conn_t *conn, char *err, size_t errlen);
+
 /* Classifies n requests resident in device memory: request i is
  * arena[off[i] .. off[i]+len[i]) on connection conn[i].  The arena must stay
  * readable up to the next 16-byte boundary past its last byte (true of every
  * hipMalloc / torch allocation); the kernels read aligned 16-byte words.  Writes verdict[i],
- * rule[i] (global rule id, -1 = none) and consumed[i] (bytes of the first
- * complete request; 0 unless ALLOW/DENY).  Asynchronous on `stream`
+ * rule[i] (global rule id, -1 = none) and consumed[i]: for ALLOW/DENY the
+ * bytes of the first request (proxylib's PASS/DROP length, which may exceed
+ * len[i] for memcached data blocks); for memcached INCOMPLETE the proxylib
+ * MORE byte count (0 = NOP) and for memcached PARSE_ERROR the OpError code
+ * (2 = INVALID_FRAME_TYPE; 0 = parser error); 0 otherwise.  Asynchronous on `stream`
  * (a hipStream_t, NULL = default stream).  counters may be NULL, else a
  * device array of (rules + 8) uint64 that accumulates per-rule allow hits
  * followed by per-verdict totals.  Returns 0 or a HIP error code. */
@@ -98,7 +111,8 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, const uint64_t *off, const
                  const uint32_t *conn, uint32_t n, uint8_t *verdict, int32_t *rule, uint32_t *consumed,
                  uint64_t *counters, void *stream);
 
-/* Same with host buffers: copies in, classifies, copies out, synchronises. */
+/* Same with host buffers: copies in, classifies, copies out, synchronises
+ * (engine-owned device scratch and stream; safe to call from any thread). */
 int l7g_classify_host(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const uint64_t *off,
                       const uint32_t *len, const uint32_t *conn, uint32_t n, uint8_t *verdict, int32_t *rule,
                       uint32_t *consumed);

@@ -301,7 +301,7 @@ void ref_policy_free(ref_policy *p) {
 
 ref_policy *ref_policy_load(const char *json, size_t len, char *err, size_t errlen) {
     char dummy[8];
-    ld l = {err ? err : dummy, err ? errlen : sizeof dummy, 0, 0};
+    ld l = {err ? err : dummy, err ? errlen : sizeof dummy, 0, 0, 0};
     if (l.errlen) l.err[0] = 0;
     jnode *root = jparse(json, len, l.err, l.errlen);
     if (!root) return NULL;

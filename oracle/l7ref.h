@@ -40,12 +40,17 @@ void ref_policy_free(ref_policy *p);
 
 /* Connection attributes, as passed to proxylib OnNewConnection
  * (proxylib/proxylib.go:57-74) / Envoy SocketOption (envoy/cilium_l7policy.cc:133-150). */
+/* memcached parser selection (proxylib/memcached/parser.go:186-202): the
+ * first byte a connection carries picks text or binary for its lifetime.
+ * 0 = not chosen yet (this buffer's first byte decides). */
+enum { L7_CONN_MC_TEXT = 1, L7_CONN_MC_BINARY = 2 };
+
 typedef struct {
     int32_t policy;     /* index of the NetworkPolicy in the loaded set, -1 = unknown */
     uint32_t port;      /* destination port */
     uint8_t ingress;    /* 1 = ingress */
     uint8_t proto;      /* L7_PROTO_* */
-    uint16_t _pad;
+    uint16_t flags;     /* L7_CONN_MC_*: memcached framing chosen for the connection */
     uint32_t src_id;    /* source identity */
     uint32_t dst_id;    /* destination identity */
 } ref_conn_t;

@@ -13,10 +13,13 @@
  *                                          PortNetworkPolicies.Matches (exact port,
  *                                          then port 0, none => deny); remote = SrcId
  *                                          (proxylib/proxylib/connection.go:176-179)
- * Batch conventions (shared with the product): a Go panic or an
- * ERROR op => PARSE_ERROR; MORE => INCOMPLETE; PASS/DROP => ALLOW/DENY with
- * consumed = the frame length proxylib returns (it may exceed the buffer);
- * frame lengths outside 1..2^32-1 => PARSE_ERROR.
+ * Batch conventions (shared with the product): PASS/DROP =>
+ * ALLOW/DENY with consumed = the frame length proxylib returns (it may exceed
+ * the buffer); MORE n => INCOMPLETE with consumed = n (NOP => 0); a Go panic
+ * or ERROR, 0 => PARSE_ERROR with consumed 0; the binary parser's ERROR,
+ * INVALID_FRAME_TYPE => PARSE_ERROR with consumed 2; frame lengths outside
+ * 1..2^32-1 => PARSE_ERROR.  The connection's flags carry the parser chosen
+ * by its first byte (0 = not yet: this buffer's first byte decides).
  */
 #include <stdlib.h>
 #include <string.h>
@@ -226,19 +229,23 @@ static int mc_port_installed(const ref_port *pp) {
 void ref_memcache_verdict(const ref_policy *pol, const ref_conn_t *c, const uint8_t *b, uint32_t len, ref_out_t *o) {
     o->rule = -1;
     o->consumed = 0;
-    if (len == 0) { o->verdict = L7_INCOMPLETE; return; }  /* NOP */
     mc_meta m;
     memset(&m, 0, sizeof m);
     uint64_t frame = 0;
     mc_tok onekey, toks[256];
     mc_tok *big = NULL;
-    if (b[0] >= 128) {  /* binary (binary/parser.go:58-139) */
-        if (len < 24) { o->verdict = L7_INCOMPLETE; return; }
+    int mode = c->flags & 3;
+    if (len == 0 && mode == 0) { o->verdict = L7_INCOMPLETE; return; }  /* NOP, 0 (no parser yet) */
+    if (mode == 0) mode = b[0] >= 128 ? L7_CONN_MC_BINARY : L7_CONN_MC_TEXT;
+    if (mode == L7_CONN_MC_BINARY) {  /* binary (binary/parser.go:58-139) */
+        if (len < 24) { o->verdict = L7_INCOMPLETE; o->consumed = 24 - len; return; }  /* MORE headerMissing */
         uint32_t body = (uint32_t)b[8] << 24 | (uint32_t)b[9] << 16 | (uint32_t)b[10] << 8 | b[11];
         uint32_t keylen = (uint32_t)b[2] << 8 | b[3];
         uint32_t extras = b[4];
-        if (keylen > 0 && 24 + keylen + extras > len) { o->verdict = L7_INCOMPLETE; return; }
-        if ((b[0] & 0x80) != 0x80) { o->verdict = L7_PARSE_ERROR; return; }
+        if (keylen > 0 && 24 + keylen + extras > len) {  /* MORE keyMissing */
+            o->verdict = L7_INCOMPLETE; o->consumed = 24 + keylen + extras - len; return;
+        }
+        if ((b[0] & 0x80) != 0x80) { o->verdict = L7_PARSE_ERROR; o->consumed = 2; return; }  /* ERROR, INVALID_FRAME_TYPE */
         m.binary = 1;
         m.opcode = b[1];
         onekey = (mc_tok){keylen ? 24 + extras : 0, keylen};
@@ -248,7 +255,9 @@ void ref_memcache_verdict(const ref_policy *pol, const ref_conn_t *c, const uint
         uint32_t lf = 0;
         int found = 0;
         for (uint32_t i = 0; i + 1 < len; i++) if (b[i] == '\r' && b[i + 1] == '\n') { lf = i; found = 1; break; }
-        if (!found) { o->verdict = L7_INCOMPLETE; return; }
+        if (!found) {  /* MORE 1 if the data ends in '\r', else MORE 2 (text/parser.go:87-93) */
+            o->verdict = L7_INCOMPLETE; o->consumed = (len > 0 && b[len - 1] == '\r') ? 1 : 2; return;
+        }
         int nt = mc_fields(b, lf, toks, 256);
         mc_tok *t = toks;
         if (nt > 256) { big = malloc(sizeof(mc_tok) * (size_t)nt); mc_fields(b, lf, big, nt); t = big; }

@@ -188,6 +188,11 @@ MC_BIN["getHello[:10]"] = MC_BIN["getHello"][:10]
 MC_BIN["getHello[:26]"] = MC_BIN["getHello"][:26]
 
 
+# MORE n the reference asserts for the incomplete requests (:240-242, :294-296,
+# :570-572, :671-672, :705-708)
+MC_MORE = {"getResponse[:5]": 2, "getKeysText[:-1]": 1, "getHello[:10]": 14, "getHello[:26]": 3}
+
+
 def memcache_section():
     E = lambda cmd, **k: dict({"command": cmd}, **k)  # noqa: E731
     ex = lambda cmd, key="": E(cmd, keyExact=key)  # noqa: E731
@@ -231,11 +236,101 @@ def memcache_section():
         # one L7 rule with an empty map (=> empty rule, matches everything)
         cases.append({"name": name, "l7_rules": rules if rules else [{}], "checks": [
             {"request": r, "expect": e,
-             "consumed": len(bytes.fromhex(reqs[r])) if e != "INCOMPLETE" else 0} for r, e in checks]})
+             "consumed": len(bytes.fromhex(reqs[r])) if e != "INCOMPLETE" else MC_MORE[r]} for r, e in checks]})
     return {"ref": "proxylib/proxylib_memcached_test.go:30-732", "requests": reqs, "cases": cases,
             "policy_template": {"name": "bm1", "policy": 2, "port": 80, "remote_policies": [1, 3, 4],
                                 "l7_proto": "memcache"},
             "conn": {"policy_name": "bm1", "port": 80, "ingress": True, "src_id": 1, "dst_id": 2}}
+
+
+MC_REPLY = {  # reply-direction payloads (proxylib/proxylib_memcached_test.go:35-118)
+    "stored": b"STORED\r\n",
+    "notFound": b"NOT_FOUND\r\n",
+    "okText": b"OK\r\n",
+    "getResponse": MC_TEXT["getResponse"],
+    "lruCrawlerResponse": b"key=key3 exp=1538047402 la=1538046902 cas=1 fetch=no cls=1 size=67\r\n"
+                          b"key=key4 exp=1538047402 la=1538046902 cas=2 fetch=no cls=1 size=66\r\nEND\r\n",
+    "statsResponse": b"STAT evictions 0\r\nSTAT reclaimed 2\r\nSTAT crawler_reclaimed\r\nSTAT crawler_items_checked 18\r\n"
+                     b"STAT lrutail_reflocked 0\r\nSTAT moves_to_cold 6\r\nSTAT moves_to_warm 0\r\n"
+                     b"STAT moves_within_lru 0\r\nSTAT direct_reclaims 0\r\nSTAT lru_bumps_dropped 0\r\nEND\r\n",
+    "watchReply": b"OK\r\n" + b"".join(
+        b"ts=15381359%s gid=%d type=item_store key=key%d status=stored cmd=set ttl=500 clsid=1\r\n" % (t, g, k)
+        for t, g, k in ((b"70.404892", 5, 3), (b"70.404898", 6, 4), (b"74.340708", 7, 3), (b"74.340714", 8, 4),
+                        (b"76.436863", 9, 3))),
+    "getHelloResp": bytes([129, 0, 0, 0, 4, 0, 0, 0, 0, 0, 0, 9, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0])
+                    + b"World",
+}
+MC_DENIED_TEXT = "CLIENT_ERROR access denied\r\n"
+MC_DENIED_BIN = bytes([0x81, 0, 0, 0, 0, 0, 0, 8, 0, 0, 0, 0x0d] + [0] * 12) + b"access denied"
+
+
+def memcache_ops_section():
+    """Full proxylib op sequences of the 31 memcached cases (CheckOnData calls,
+    proxylib_memcached_test.go:169-732): direction, buffers, expected ops
+    [(op, n)] with op MORE 0 / PASS 1 / DROP 2 / INJECT 3, result, and the
+    reply inject buffer contents (checked up to the buffer's length, as
+    helpers_test.go:100-109 does; inject buffers hold 30 bytes, :153)."""
+    MORE, PASS, DROP, INJECT = 0, 1, 2, 3
+    T, B, R = MC_TEXT, MC_BIN, MC_REPLY
+    dt, db = MC_DENIED_TEXT.encode(), MC_DENIED_BIN
+    L = len
+
+    def call(reply, bufs, ops, inject=b""):
+        return {"reply": reply, "data": [b.hex() for b in bufs], "ops": ops, "result": "OK", "inject": inject.hex()}
+
+    pass_text = lambda req, resp: [call(False, [T[req]], [[PASS, L(T[req])], [MORE, 2]]),  # noqa: E731
+                                   call(True, [R[resp]], [[PASS, L(R[resp])]])]
+    drop_text = lambda req: [call(False, [T[req]], [[DROP, L(T[req])], [MORE, 2]], dt)]  # noqa: E731
+    gr = R["getResponse"]
+    calls = {
+        "text set pass": pass_text("setHelloText", "stored"),
+        "text set drop": drop_text("setHelloText"),
+        "text get pass": [call(False, [T["getKeysText"]] * 2, [[PASS, 20], [PASS, 20], [MORE, 2]]),
+                          call(True, [gr, gr], [[PASS, L(gr)], [PASS, L(gr)]])],
+        "text get more": [call(False, [T["getResponse[:5]"]], [[MORE, 2]])],
+        "text get drop": drop_text("getKeysText"),
+        "text gat pass": [call(False, [T["gatKeysText"]] * 2, [[PASS, 22], [PASS, 22], [MORE, 2]]),
+                          call(True, [gr, gr], [[PASS, L(gr)], [PASS, L(gr)]])],
+        "text gat more": [call(False, [T["getResponse[:5]"]], [[MORE, 2]])],
+        "text gat drop": drop_text("gatKeysText"),
+        "text delete pass": pass_text("deleteText", "notFound"),
+        "text delete drop": drop_text("deleteText"),
+        "text incr pass": pass_text("incrText", "notFound"),
+        "text incr drop": drop_text("incrText"),
+        "text touch pass": pass_text("touchText", "notFound"),
+        "text touch drop": drop_text("touchText"),
+        "text slabs pass": pass_text("slabsText", "okText"),
+        "text slabs drop": drop_text("slabsText"),
+        "text lru_crawler response req more and pass": [
+            call(False, [T["lruCrawlerText"]], [[PASS, L(T["lruCrawlerText"])], [MORE, 2]]),
+            call(True, [R["lruCrawlerResponse"][:5]], [[MORE, 2]]),
+            call(True, [R["lruCrawlerResponse"]], [[PASS, L(R["lruCrawlerResponse"])]])],
+        "text stats response req more and pass": [
+            call(False, [T["statsText"]], [[PASS, L(T["statsText"])], [MORE, 2]]),
+            call(True, [R["statsResponse"][:5]], [[MORE, 2]]),
+            call(True, [R["statsResponse"]], [[PASS, L(R["statsResponse"])]])],
+        "text flush_all pass": [call(False, [T["flushAllText"]], [[PASS, L(T["flushAllText"])], [MORE, 2]])],
+        "text flush_all denied": drop_text("flushAllText"),
+        "text watch passed": [call(False, [T["watchText"]], [[PASS, L(T["watchText"])], [MORE, 2]]),
+                              call(True, [R["watchReply"]], [[PASS, 4]] + [[PASS, 91]] * 5)],
+        "text partial linefeed": [call(False, [T["getKeysText[:-1]"]], [[MORE, 1]])],
+        "text set pass on empty rule": pass_text("setHelloText", "stored"),
+        "bin get pass exact key": [call(False, [B["getHello"]], [[PASS, 29], [MORE, 24]])],
+        "bin get pass prefix key": [call(False, [B["getHello"]], [[PASS, 29], [MORE, 24]])],
+        "bin get pass regex key": [call(False, [B["getHello"]], [[PASS, 29], [MORE, 24]])],
+        "bin get drop": [call(False, [B["getHello"]], [[DROP, 29], [MORE, 24]], db)],
+        "bin get more": [call(False, [B["getHello[:10]"]], [[MORE, 14]])],
+        "bin get split": [call(False, [B["getHello"][:10], B["getHello"][10:]], [[PASS, 29], [MORE, 24]])],
+        "bin get remaining key": [call(False, [B["getHello[:26]"]], [[MORE, 3]])],
+        "bin set drop and allow": [call(False, [B["setHello"], B["getHello"]], [[PASS, 42], [DROP, 29], [MORE, 24]], db),
+                                   call(True, [R["getHelloResp"]], [[PASS, 33], [INJECT, 37]], db)],
+    }
+    assert len(calls) == 31
+    return {"ref": "proxylib/proxylib_memcached_test.go:120-732, helpers_test.go:52-144",
+            "connection": {"proto": "memcache", "conn_id": 1, "ingress": True, "src_id": 1, "dst_id": 2,
+                           "src_addr": "1.1.1.1:34567", "dst_addr": "2.2.2.2:80", "policy_name": "bm1",
+                           "inject_buf": 30},
+            "calls": calls}
 
 
 def main():
@@ -246,6 +341,7 @@ def main():
         "http_translation": xlate_section(),
         "kafka": kafka_section(),
         "memcache": memcache_section(),
+        "memcache_ops": memcache_ops_section(),
     }
     with open(OUT, "w") as f:
         json.dump(data, f, indent=1, sort_keys=True)
