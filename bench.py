@@ -77,7 +77,7 @@ def main():
     step_counters = torch.zeros(nrules + 8, dtype=torch.int64, device=dev)
     totals = torch.zeros(nrules + 8, dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream()
-    ptrs = [t.data_ptr() for t in (d_arena, d_off, d_len, d_cid)]
+    ptrs = [d_arena.data_ptr(), d_arena.numel()] + [t.data_ptr() for t in (d_off, d_len, d_cid)]
     outs = [t.data_ptr() for t in (d_v, d_r, d_c)]
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]

@@ -60,7 +60,7 @@ def load():
     lib.l7g_policy_nrules.argtypes = [vp]
     lib.l7g_conns_set.argtypes = [vp, vp, C.c_uint32, cp, sz]
     lib.l7g_conn_update.argtypes = [vp, C.c_uint32, vp, cp, sz]
-    lib.l7g_classify.argtypes = [vp, vp, vp, vp, vp, C.c_uint32, vp, vp, vp, vp, vp]
+    lib.l7g_classify.argtypes = [vp, vp, C.c_uint64, vp, vp, vp, C.c_uint32, vp, vp, vp, vp, vp]
     lib.l7g_classify_host.argtypes = [vp, vp, C.c_uint64, vp, vp, vp, C.c_uint32, vp, vp, vp]
     lib.l7g_stats.argtypes = [vp, C.POINTER(Stats)]
     lib.l7g_debug_regex.argtypes = [cp, sz, C.c_int, cp, sz, cp, sz]

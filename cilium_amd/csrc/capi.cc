@@ -17,7 +17,7 @@
 #include "regex/re_dfa.h"
 
 namespace l7 {
-hipError_t LaunchHttpClassify(const uint8_t *arena, const uint64_t *offs, const uint32_t *lens, const uint32_t *conn_ids,
+hipError_t LaunchHttpClassify(const uint8_t *arena, uint64_t arena_len, const uint64_t *offs, const uint32_t *lens, const uint32_t *conn_ids,
                               uint32_t n, const DevConn *conns, uint32_t nconns, const HttpTables &T, bool any_cold,
                               uint8_t *verdict, int32_t *rule, uint32_t *consumed, uint64_t *counters,
                               uint32_t ncounters, hipStream_t stream);
@@ -305,7 +305,8 @@ int l7g_conn_update(l7g_engine *e, uint32_t index, const l7g_conn_t *conn, char 
     return 0;
 }
 
-int l7g_classify(l7g_engine *e, const uint8_t *arena, const uint64_t *off, const uint32_t *len, const uint32_t *conn,
+int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const uint64_t *off, const uint32_t *len,
+                 const uint32_t *conn,
                  uint32_t n, uint8_t *verdict, int32_t *rule, uint32_t *consumed, uint64_t *counters, void *stream) {
     std::lock_guard<std::mutex> g(e->mu);
     if (e->device < 0) return (int)hipErrorNoDevice;
@@ -317,7 +318,7 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, const uint64_t *off, const
     // The kernels each classify only their own protocol's requests and skip
     // the rest, so a mixed batch needs one launch per protocol present.
     if (e->has_http || (!e->has_kafka && !e->has_mc))
-        rc = LaunchHttpClassify(arena, off, len, conn, n, e->d_conns, (uint32_t)e->conns.size(), e->ht, e->any_cold,
+        rc = LaunchHttpClassify(arena, arena_len, off, len, conn, n, e->d_conns, (uint32_t)e->conns.size(), e->ht, e->any_cold,
                                 verdict, rule,
                                 consumed, counters, ncounters, s);
     if (rc == hipSuccess && e->has_kafka)
@@ -365,7 +366,7 @@ int l7g_classify_host(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, c
     if (rc == hipSuccess && n) rc = hipMemcpyAsync(d_o, off, n * 8, hipMemcpyHostToDevice, s);
     if (rc == hipSuccess && n) rc = hipMemcpyAsync(d_l, len, n * 4, hipMemcpyHostToDevice, s);
     if (rc == hipSuccess && n) rc = hipMemcpyAsync(d_c, conn, n * 4, hipMemcpyHostToDevice, s);
-    if (rc == hipSuccess) rc = (hipError_t)l7g_classify(e, e->s_arena, d_o, d_l, d_c, n, d_v, d_r, d_cons, nullptr, s);
+    if (rc == hipSuccess) rc = (hipError_t)l7g_classify(e, e->s_arena, arena_len, d_o, d_l, d_c, n, d_v, d_r, d_cons, nullptr, s);
     if (rc == hipSuccess && n) rc = hipMemcpyAsync(verdict, d_v, n, hipMemcpyDeviceToHost, s);
     if (rc == hipSuccess && n) rc = hipMemcpyAsync(rule, d_r, n * 4, hipMemcpyDeviceToHost, s);
     if (rc == hipSuccess && n) rc = hipMemcpyAsync(consumed, d_cons, n * 4, hipMemcpyDeviceToHost, s);

@@ -19,16 +19,16 @@
 //      fetched while the current transition is in flight, so a byte costs one
 //      dependent LDS round trip.  Values nobody constrains are skipped 16
 //      bytes a step (SWAR CTL/DEL test).
-//   3. scan: a lane whose unconstrained value runs past its window hands the
-//      rest to the wave: for up to 16 such lanes at a time the wave reads 1 KiB
-//      pieces of each lane's request with coalesced 16-byte-per-lane loads
-//      (all pieces in flight together) and finds the value's end (first byte
-//      < 0x20 other than HT, or DEL) by ballot.  The lane's next window starts
-//      there.
+//   3. skip: a lane whose unconstrained value runs past its window looks up
+//      where it ends in the arena's value-stop map (first byte < 0x20 other
+//      than HT, or DEL), built beforehand by http_stopmap_kernel in one
+//      coalesced pass over the arena: 128 bytes of map cover 1 KiB of
+//      request, so the value's bytes are never loaded by this kernel.  The
+//      lane's next window starts at the stop byte.
 //
-// For the benchmark stream a tile takes two windows per request (head, then
-// the end of the header block) and one scan (the long pad header), so the pad
-// bytes are read once, by coalesced loads.
+// For the benchmark stream a tile takes two windows per request (the head,
+// then the end of the header block) and one map lookup (the long pad header);
+// the pad bytes are read once, by the stop-map stream.
 //
 // One 512-thread workgroup per CU: 8 waves x 16 KiB windows + the hot rule
 // set's image (<= 28 KiB) + rule counters = 160 KiB of LDS.
@@ -40,6 +40,7 @@
 // kDfasPerPass DFAs per slot are evaluated in several framing passes.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstddef>
 
 #include "../device_tables.h"
@@ -64,7 +65,6 @@ constexpr uint32_t kOffImg = kWaves * kWaveLds;
 constexpr uint32_t kOffCnt = kOffImg + kLdsImageBytes;
 constexpr uint32_t kLdsBytes = kOffCnt + (8 + kLdsRuleCounters) * 4;
 static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
-constexpr int kScanBatch = kWaveLds / 1024;    // lanes whose long values are scanned together
 constexpr uint32_t kLanesPerWin = kWinChunks;  // DMA: one lane per 16-byte chunk of a window
 constexpr uint32_t kWinPerInst = 64 / kLanesPerWin;
 static_assert(kWinChunks == 8 || kWinChunks == 16, "window size");
@@ -553,87 +553,58 @@ __device__ __forceinline__ void dma_windows(uint8_t *wave_lds, uint64_t packed, 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// ---------------------------------------------------------------- long-value scan
-// Lanes with L.scan set: find the first stop byte (< 0x20 other than HT, or
-// DEL) at or after L.pa in the lane's request, reading 1 KiB pieces of up to
-// kScanBatch lanes' requests together with coalesced loads.  The lane's pa
-// moves there (the next window starts at it); no stop before the request end
-// => INCOMPLETE.
-// The pieces land in the wave's window area (free between rounds) by LDS-DMA,
-// so all of a batch's loads are in flight together.
-__device__ __forceinline__ void scan_values(Lane &L, uint32_t lane, uint8_t *wave_lds) {
-    uint64_t pending = __ballot(L.scan);
-    while (pending) {
-        uint32_t who[kScanBatch], tpa[kScanBatch], tlen[kScanBatch];
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // earlier LDS reads of the area have landed
+// ---------------------------------------------------------------- long-value skip
+// A value nobody constrains ends at its first "value stop" byte (< 0x20 other
+// than HT, or DEL: CR normally, anything else is an error).  Bytes past the
+// lane's window are not loaded at all: http_stopmap_kernel has already marked
+// every value-stop byte of the arena in a bitmap (one u16 per 16-byte chunk),
+// so the lane reads 128 bytes of map (1 KiB of arena) and takes the first mark
+// at or after L.pa.  The next window starts at that byte.
+constexpr uint32_t kMapSpan = 1024;  // arena bytes covered by one map read
+
+// bit 7 of each byte set iff the byte is a value stop
+__device__ __forceinline__ uint32_t vstop_bits(uint32_t x) {
+    const uint32_t t = x ^ 0x09090909u;  // HT -> 0
+    const uint32_t ht = ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;
+    return stop_bits(x) & ~ht;
+}
+
+struct StopMap {
+    const uint16_t *map;  // u16 per 16-byte chunk from base (+ 72 chunks of slack)
+    uint64_t base;        // arena address rounded down to 16 bytes
+};
+
+__device__ __forceinline__ void map_skip(Lane &L, const StopMap &M) {
+    while (__any(L.scan)) {
+        if (L.scan) {
+            const uint64_t a = L.base + L.pa - M.base;  // arena-relative position of pa
+            const uint64_t c0 = (a >> 4) & ~7ull;        // first chunk of a 16-byte map group
+            const uint32_t from = (uint32_t)(a - (c0 << 4));  // bit of pa in the 1024-bit span
+            const uint4 *mp = (const uint4 *)(M.map + c0);
+            uint4 m[8];
 #pragma unroll
-        for (int i = 0; i < kScanBatch; i++) {
-            who[i] = 64;
-            tpa[i] = tlen[i] = 0;
-            if (pending) {
-                const uint32_t t = (uint32_t)__builtin_ctzll(pending);
-                pending &= pending - 1;
-                who[i] = t;
-                tpa[i] = (uint32_t)__builtin_amdgcn_readlane((int)L.pa, (int)t);
-                tlen[i] = (uint32_t)__builtin_amdgcn_readlane((int)L.lena, (int)t);
-                const uint32_t blo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)L.base, (int)t);
-                const uint32_t bhi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(L.base >> 32), (int)t);
-                const uint32_t q = (tpa[i] & ~15u) + 16 * lane;  // this lane's chunk of the piece
-                if (q < tlen[i])
-                    __builtin_amdgcn_global_load_lds((const void *)((const uint8_t *)((((uint64_t)bhi) << 32) | blo) + q),
-                                                     (__attribute__((address_space(3))) void *)(wave_lds + i * 1024),
-                                                     16, 0, 0);
-            }
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            for (int k = 0; k < 8; k++) m[k] = mp[k];
+            uint32_t hit = 0xFFFFFFFFu;
 #pragma unroll
-        for (int i = 0; i < kScanBatch; i++) {
-            const uint32_t t = who[i];
-            if (t >= 64) continue;
-            const uint32_t pa = tpa[i], lena = tlen[i];
-            const uint32_t q = (pa & ~15u) + 16 * lane;
-            const uint4 vi = *(const uint4 *)(wave_lds + i * 1024 + 16 * lane);
-            // vector part: does this lane's chunk hold any byte < 0x20 or DEL?
-            // (bytes before pa / past the request end and HT are sorted out
-            // below, in scalar code, for the candidate lanes only)
-            const uint32_t any = stop_bits(vi.x) | stop_bits(vi.y) | stop_bits(vi.z) | stop_bits(vi.w);
-            uint64_t cand = __ballot(q < lena && any != 0);
-            uint32_t res = 0;   // new position for lane t
-            bool hit = false, again = false;
-            while (cand) {  // wave-uniform; usually one iteration
-                const uint32_t fl = (uint32_t)__builtin_ctzll(cand);
-                cand &= cand - 1;
-                const uint32_t cb = (pa & ~15u) + 16 * fl;  // position of the candidate chunk
-                const uint32_t s0 = (uint32_t)__builtin_amdgcn_readlane((int)vi.x, (int)fl);
-                const uint32_t s1 = (uint32_t)__builtin_amdgcn_readlane((int)vi.y, (int)fl);
-                const uint32_t s2 = (uint32_t)__builtin_amdgcn_readlane((int)vi.z, (int)fl);
-                const uint32_t s3 = (uint32_t)__builtin_amdgcn_readlane((int)vi.w, (int)fl);
-                const uint32_t lo = cb < pa ? pa - cb : 0, hi = min(lena - cb, 16u);
-                uint32_t m = (nib(stop_bits(s0)) | nib(stop_bits(s1)) << 4 | nib(stop_bits(s2)) << 8 |
-                              nib(stop_bits(s3)) << 12) & (0xFFFFu << lo) & ((1u << hi) - 1u);
-                while (m) {  // HT is allowed inside values
-                    const uint32_t b = (uint32_t)__builtin_ctz(m);
-                    const uint32_t d = b < 4 ? s0 : b < 8 ? s1 : b < 12 ? s2 : s3;
-                    if (((d >> (8 * (b & 3))) & 0xFF) != '\t') break;
-                    m &= m - 1;
-                }
-                if (m) {
-                    res = cb + (uint32_t)__builtin_ctz(m);
-                    hit = true;
-                    break;
+            for (int k = 7; k >= 0; k--) {  // the last assignment is the first hit
+#pragma unroll
+                for (int j = 3; j >= 0; j--) {
+                    const uint32_t i = 4 * k + j;  // dword i covers span bits 32i .. 32i+31
+                    uint32_t d = j == 0 ? m[k].x : j == 1 ? m[k].y : j == 2 ? m[k].z : m[k].w;
+                    d = (from >> 5) > i ? 0u : (from >> 5) == i ? d & (0xFFFFFFFFu << (from & 31)) : d;
+                    if (d) hit = 32 * i + (uint32_t)__builtin_ctz(d);
                 }
             }
-            if (!hit) {
-                res = (pa & ~15u) + 1024;  // nothing in this piece
-                again = res < lena;
-                if (!again) res = lena;
+            const uint64_t span0 = M.base + (c0 << 4) - L.base;  // span start, request-relative
+            if (hit != 0xFFFFFFFFu && span0 + hit < L.lena) {
+                L.pa = (uint32_t)(span0 + hit);
+                L.scan = false;
+            } else if (span0 + kMapSpan >= L.lena) {
+                L.pa = L.lena;
+                finish(L, V_INCOMPLETE);
+            } else {
+                L.pa = (uint32_t)(span0 + kMapSpan);
             }
-            if (lane == t) {
-                L.pa = max(res, L.pa);
-                if (hit) L.scan = false;
-                else if (!again) finish(L, V_INCOMPLETE);
-            }
-            if (again) pending |= 1ull << t;
         }
     }
 }
@@ -662,7 +633,8 @@ __device__ __forceinline__ void emit(const Lane &L, const Out &O) {
 
 // All rounds of one tile.
 template <bool kLds>
-__device__ __forceinline__ void run_tile(Lane &L, const uint8_t *img, uint8_t *wave_lds, uint32_t lane, const Out &O) {
+__device__ __forceinline__ void run_tile(Lane &L, const uint8_t *img, uint8_t *wave_lds, uint32_t lane, const Out &O,
+                                         const StopMap &M) {
     const Img<kLds> I{img};
     L.scan = false;
     if (!L.done) {
@@ -692,7 +664,7 @@ __device__ __forceinline__ void run_tile(Lane &L, const uint8_t *img, uint8_t *w
         }
         PH_MARK(1);
         PH_COUNT(5, __builtin_popcountll(__ballot(L.scan)));
-        scan_values(L, lane, wave_lds);
+        map_skip(L, M);
         PH_MARK(2);
         if (L.done && L.owed) {
             emit(L, O);
@@ -720,8 +692,9 @@ __global__ __launch_bounds__(kBlock) void http_classify_kernel(
     const uint8_t *__restrict__ arena, const uint64_t *__restrict__ offs, const uint32_t *__restrict__ lens,
     const uint32_t *__restrict__ conn_ids, uint32_t n, const DevConn *__restrict__ conns, uint32_t nconns,
     HttpTables T, uint8_t *__restrict__ out_verdict, int32_t *__restrict__ out_rule, uint32_t *__restrict__ out_consumed,
-    uint64_t *__restrict__ counters, uint32_t ncounters) {
+    uint64_t *__restrict__ counters, uint32_t ncounters, const uint16_t *__restrict__ smap, uint64_t arena_len) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
+    const StopMap M{smap, (uint64_t)arena & ~(uint64_t)15};
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63, wave = tid >> 6;
     uint8_t *s_img = lds + kOffImg;
@@ -768,6 +741,9 @@ __global__ __launch_bounds__(kBlock) void http_classify_kernel(
             if (http && is_hot == kHot) {
                 const uint64_t off = offs[L.idx];
                 const uint32_t len = lens[L.idx];
+                if (off > arena_len || len > arena_len - off) {  // outside the arena: out of contract
+                    L.owed = true;
+                } else {
                 const uint64_t a = (uint64_t)(arena + off);
                 L.base = a & ~(uint64_t)15;
                 L.a0 = (uint32_t)(a & 15);
@@ -775,9 +751,10 @@ __global__ __launch_bounds__(kBlock) void http_classify_kernel(
                 if (!kHot) img = T.images + T.rulesets[conn.ruleset].image_off;
                 L.done = false;
                 L.owed = true;
+                }
             }
         }
-        run_tile<kHot>(L, img, wave_lds, lane, O);
+        run_tile<kHot>(L, img, wave_lds, lane, O, M);
     }
     if (counters) {
         __syncthreads();
@@ -791,13 +768,38 @@ __global__ __launch_bounds__(kBlock) void http_classify_kernel(
     }
 }
 
+// Value-stop map of the whole arena: bit b of map[c] <=> byte 16c+b (from
+// the arena address rounded down to 16) is < 0x20 other than HT, or DEL.
+// Coalesced 16-byte loads, 2-byte stores: a pure HBM stream.
+constexpr int kMapBlock = 256;
+__global__ __launch_bounds__(kMapBlock) void http_stopmap_kernel(const uint8_t *__restrict__ base, uint64_t nchunks,
+                                                                 uint16_t *__restrict__ map) {
+    const uint4 *src = (const uint4 *)base;
+    const uint64_t stride = (uint64_t)gridDim.x * kMapBlock * 4;
+    for (uint64_t c0 = (uint64_t)blockIdx.x * kMapBlock * 4 + threadIdx.x; c0 < nchunks; c0 += stride) {
+        uint4 w[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint64_t c = c0 + (uint64_t)k * kMapBlock;
+            w[k] = c < nchunks ? src[c] : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint64_t c = c0 + (uint64_t)k * kMapBlock;
+            if (c < nchunks)
+                map[c] = (uint16_t)(nib(vstop_bits(w[k].x)) | nib(vstop_bits(w[k].y)) << 4 | nib(vstop_bits(w[k].z)) << 8 |
+                                    nib(vstop_bits(w[k].w)) << 12);
+        }
+    }
+}
+
 // Host-side launcher (called from the C-ABI): persistent grids of one
 // 512-thread workgroup per CU; the hot-rule-set kernel, then (only if some
 // HTTP connection uses another rule set) the general one.
-hipError_t LaunchHttpClassify(const uint8_t *arena, const uint64_t *offs, const uint32_t *lens, const uint32_t *conn_ids,
-                              uint32_t n, const DevConn *conns, uint32_t nconns, const HttpTables &T, bool any_cold,
-                              uint8_t *verdict, int32_t *rule, uint32_t *consumed, uint64_t *counters,
-                              uint32_t ncounters, hipStream_t stream) {
+hipError_t LaunchHttpClassify(const uint8_t *arena, uint64_t arena_len, const uint64_t *offs, const uint32_t *lens,
+                              const uint32_t *conn_ids, uint32_t n, const DevConn *conns, uint32_t nconns,
+                              const HttpTables &T, bool any_cold, uint8_t *verdict, int32_t *rule, uint32_t *consumed,
+                              uint64_t *counters, uint32_t ncounters, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     static int num_cus = 0;
     if (num_cus == 0) {
@@ -806,17 +808,30 @@ hipError_t LaunchHttpClassify(const uint8_t *arena, const uint64_t *offs, const 
             hipDeviceGetAttribute(&num_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || num_cus <= 0)
             num_cus = 256;
     }
+    // value-stop map of the arena (stream-ordered scratch, freed after the batch)
+    const uint64_t nchunks = (((uint64_t)arena & 15) + arena_len + 15) / 16;
+    uint16_t *smap = nullptr;
+    hipError_t rc = hipMallocAsync((void **)&smap, (nchunks + 72) * sizeof(uint16_t), stream);
+    if (rc != hipSuccess) return rc;
+    if (nchunks) {
+        const uint64_t per_block = (uint64_t)kMapBlock * 4;
+        const uint32_t mblocks = (uint32_t)std::min<uint64_t>((nchunks + per_block - 1) / per_block, (uint64_t)num_cus * 16);
+        hipLaunchKernelGGL(http_stopmap_kernel, dim3(mblocks), dim3(kMapBlock), 0, stream,
+                           (const uint8_t *)((uint64_t)arena & ~(uint64_t)15), nchunks, smap);
+    }
     const uint32_t ntiles = (n + 63) / 64;
     uint32_t blocks = (ntiles + kWaves - 1) / kWaves;
     blocks = min(blocks, (uint32_t)num_cus);
     const bool hot = T.hot_ruleset >= 0;
     if (hot)
         hipLaunchKernelGGL(http_classify_kernel<true>, dim3(blocks), dim3(kBlock), 0, stream, arena, offs, lens, conn_ids,
-                           n, conns, nconns, T, verdict, rule, consumed, counters, ncounters);
+                           n, conns, nconns, T, verdict, rule, consumed, counters, ncounters, smap, arena_len);
     if (!hot || any_cold)
         hipLaunchKernelGGL(http_classify_kernel<false>, dim3(blocks), dim3(kBlock), 0, stream, arena, offs, lens,
-                           conn_ids, n, conns, nconns, T, verdict, rule, consumed, counters, ncounters);
-    return hipGetLastError();
+                           conn_ids, n, conns, nconns, T, verdict, rule, consumed, counters, ncounters, smap, arena_len);
+    rc = hipGetLastError();
+    hipError_t rf = hipFreeAsync(smap, stream);
+    return rc != hipSuccess ? rc : rf;
 }
 
 #ifdef L7G_PHASE_TIMING

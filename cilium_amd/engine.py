@@ -67,10 +67,11 @@ class Engine:
         self._conns = arr
 
     # --------------------------------------------------------- classification
-    def classify_device(self, arena_ptr, off_ptr, len_ptr, conn_ptr, n, verdict_ptr, rule_ptr,
+    def classify_device(self, arena_ptr, arena_len, off_ptr, len_ptr, conn_ptr, n, verdict_ptr, rule_ptr,
                         consumed_ptr, counters_ptr=0, stream=0):
-        """All pointers are device addresses (e.g. torch tensor .data_ptr())."""
-        rc = self._lib.l7g_classify(self._h, arena_ptr, off_ptr, len_ptr, conn_ptr, n, verdict_ptr,
+        """All pointers are device addresses (e.g. torch tensor .data_ptr());
+        every request lies inside [arena_ptr, arena_ptr + arena_len)."""
+        rc = self._lib.l7g_classify(self._h, arena_ptr, arena_len, off_ptr, len_ptr, conn_ptr, n, verdict_ptr,
                                     rule_ptr, consumed_ptr, counters_ptr or None, stream or None)
         if rc != 0:
             raise RuntimeError(f"l7g_classify failed: HIP error {rc}")

@@ -96,9 +96,11 @@ int l7g_conns_set(l7g_engine *e, const l7g_conn_t *conns, uint32_t n, char *err,
 int l7g_conn_update(l7g_engine *e, uint32_t index, const l7g_conn_t *conn, char *err, size_t errlen);
 
 /* Classifies n requests resident in device memory: request i is
- * arena[off[i] .. off[i]+len[i]) on connection conn[i].  The arena must stay
- * readable up to the next 16-byte boundary past its last byte (true of every
- * hipMalloc / torch allocation); the kernels read aligned 16-byte words.  Writes verdict[i],
+ * arena[off[i] .. off[i]+len[i]) on connection conn[i], inside
+ * [arena, arena + arena_len) (an HTTP request reaching past it is answered
+ * UNSUPPORTED).  The arena must stay readable up to the next 16-byte boundary
+ * past its last byte (true of every hipMalloc / torch allocation); the kernels
+ * read aligned 16-byte words.  Writes verdict[i],
  * rule[i] (global rule id, -1 = none) and consumed[i]: for ALLOW/DENY the
  * bytes of the first request (proxylib's PASS/DROP length, which may exceed
  * len[i] for memcached data blocks); for memcached INCOMPLETE the proxylib
@@ -107,7 +109,7 @@ int l7g_conn_update(l7g_engine *e, uint32_t index, const l7g_conn_t *conn, char 
  * (a hipStream_t, NULL = default stream).  counters may be NULL, else a
  * device array of (rules + 8) uint64 that accumulates per-rule allow hits
  * followed by per-verdict totals.  Returns 0 or a HIP error code. */
-int l7g_classify(l7g_engine *e, const uint8_t *arena, const uint64_t *off, const uint32_t *len,
+int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const uint64_t *off, const uint32_t *len,
                  const uint32_t *conn, uint32_t n, uint8_t *verdict, int32_t *rule, uint32_t *consumed,
                  uint64_t *counters, void *stream);
 

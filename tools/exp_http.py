@@ -26,7 +26,8 @@ def timeit(eng, w, steps=10):
     eng.set_connections(w.conns)
     eng.phase_times(reset=True)
     s = torch.cuda.current_stream()
-    args = [t.data_ptr() for t in (d_a, d_o, d_l, d_c)] + [n] + [t.data_ptr() for t in (d_v, d_r, d_k)]
+    args = [d_a.data_ptr(), d_a.numel()] + [t.data_ptr() for t in (d_o, d_l, d_c)] + [n] + \
+        [t.data_ptr() for t in (d_v, d_r, d_k)]
     for _ in range(3):
         eng.classify_device(*args, stream=s.cuda_stream)
     torch.cuda.synchronize()
