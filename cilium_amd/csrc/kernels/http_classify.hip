@@ -154,6 +154,7 @@ struct Lane {
     bool done;          // verdict known
     bool owed;          // verdict not yet written out
     bool scan;          // an unconstrained value continues past the window
+    bool tail;          // the skipped value ends in "\r\n\r\n" (end of the header block)
     uint8_t verdict;
     int32_t rule;
     uint32_t consumed;
@@ -460,7 +461,40 @@ __device__ __forceinline__ void parse_window(const Img<kLds> &I, Lane &L, Cursor
                 }
             }
         }
-        if (L.mode == M_VALUE) {  // a value some rule (or Content-Length framing) looks at
+        if (L.mode == M_VALUE && !(L.ninfo & NI_CL)) {  // a value some rule looks at: DFA walk only
+            // software pipeline as for the target: byte p+1 and its class are
+            // read while the transition on byte p is in flight
+            uint32_t c = 0;
+            if (L.pa < lim) {
+                c = C.at(L.pa);
+                uint32_t k = L.dcls ? I.u8(L.dcls + c) : 0;
+                uint32_t c1 = L.pa + 1 < lim ? C.at(L.pa + 1) : 0;
+                while (!((c < 0x20 && c != '\t') || c == 0x7F)) {  // CR ends it; other CTLs are errors
+                    const uint32_t p1 = L.pa + 1;
+                    const uint32_t c2 = p1 + 1 < lim ? C.at(p1 + 1) : 0;
+                    const uint32_t k1 = L.dcls ? I.u8(L.dcls + c1) : 0;
+                    const bool ws = c == ' ' || c == '\t';
+                    if (ws && !L.in_ows) L.saved = L.st;
+                    L.in_ows = ws;
+                    if (L.st) L.st = I.u16(L.dtrans + 2 * (L.st * L.dncls + k));
+                    L.pa = p1;
+                    if (p1 >= lim) break;
+                    c = c1;
+                    c1 = c2;
+                    k = k1;
+                }
+            }
+            if (L.pa < lim) {
+                if (c != '\r') {
+                    finish(L, V_PARSE_ERROR);
+                } else {
+                    if (L.in_ows) L.st = L.saved;  // trailing OWS is not part of the value
+                    L.pa++;
+                    L.mode = M_LF;
+                }
+            }
+        }
+        if (L.mode == M_VALUE) {  // Content-Length (and possibly a rule's DFA on it)
             uint32_t c = 0;
             for (; L.pa < lim; L.pa++) {
                 c = C.at(L.pa);
@@ -599,6 +633,13 @@ __device__ __forceinline__ void map_skip(Lane &L, const StopMap &M) {
             if (hit != 0xFFFFFFFFu && span0 + hit < L.lena) {
                 L.pa = (uint32_t)(span0 + hit);
                 L.scan = false;
+                // the value was the last header when "\r\n\r\n" follows: check
+                // those four bytes now instead of loading a window for them
+                if (L.pa + 4 <= L.lena) {
+                    const uint8_t *q = (const uint8_t *)(L.base + L.pa);
+                    const uint32_t w = (uint32_t)q[0] | (uint32_t)q[1] << 8 | (uint32_t)q[2] << 16 | (uint32_t)q[3] << 24;
+                    L.tail = w == 0x0A0D0A0Du;
+                }
             } else if (span0 + kMapSpan >= L.lena) {
                 L.pa = L.lena;
                 finish(L, V_INCOMPLETE);
@@ -606,6 +647,21 @@ __device__ __forceinline__ void map_skip(Lane &L, const StopMap &M) {
                 L.pa = (uint32_t)(span0 + kMapSpan);
             }
         }
+    }
+}
+
+// The skipped value ended at the CR of "\r\n\r\n": what parse_window does for
+// those four bytes (M_SKIP -> M_LF -> line_done -> M_LINE -> M_ENDLF ->
+// headers_done), without another window.
+template <bool kLds>
+__device__ __forceinline__ void finish_tail(const Img<kLds> &I, Lane &L) {
+    L.tail = false;
+    L.pa += 4;
+    if (line_done(I, L)) {
+        L.mode = M_LINE;
+        headers_done(I, L);
+    } else {
+        finish(L, V_PARSE_ERROR);
     }
 }
 
@@ -637,6 +693,7 @@ __device__ __forceinline__ void run_tile(Lane &L, const uint8_t *img, uint8_t *w
                                          const StopMap &M) {
     const Img<kLds> I{img};
     L.scan = false;
+    L.tail = false;
     if (!L.done) {
         L.cg = 0;
         L.dg = 0;
@@ -665,6 +722,7 @@ __device__ __forceinline__ void run_tile(Lane &L, const uint8_t *img, uint8_t *w
         PH_MARK(1);
         PH_COUNT(5, __builtin_popcountll(__ballot(L.scan)));
         map_skip(L, M);
+        if (L.tail) finish_tail(I, L);
         PH_MARK(2);
         if (L.done && L.owed) {
             emit(L, O);
