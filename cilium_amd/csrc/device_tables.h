@@ -50,12 +50,14 @@ constexpr uint32_t kLdsImageBytes = 28 * 1024;  // LDS budget for the hot rule-s
 enum : uint8_t { NI_CUSTOM = 0x0F /* custom index + 1 */, NI_HOST = 0x10, NI_CL = 0x20, NI_TE = 0x40 };
 constexpr uint16_t kNameBad = 0, kNameOther = 1, kNameStart = 2;
 
-struct DevDfa {            // 16 B
+struct DevDfa {            // 24 B
     uint32_t cls_off;      // u8[256]: byte -> class
     uint32_t trans_off;    // u16[nstates][ncls]; state 0 = dead
     uint32_t mask_off;     // u64[nstates][nchunks]
     uint16_t ncls;
     uint16_t start;
+    uint32_t absorb;       // states >= absorb (and 0) loop back on every HT/SP/VCHAR/obs-text byte
+    uint32_t pad;
 };
 struct DevHdrName {        // 12 B: a custom header name the rule set looks at
     uint32_t hash;         // FNV-1a of the lower-cased name

@@ -181,6 +181,42 @@ NameDfa BuildNameDfa(const std::vector<std::string> &custom) {
     return d;
 }
 
+// Renumber d's states so that those absorbing on header-token bytes (HT, SP,
+// VCHAR, obs-text: each such byte leads back to the state) come last,
+// [absorb, nstates); the dead state keeps number 0.  The kernel stops walking
+// a token once its state is absorbing: the rest of the token cannot change it.
+uint32_t SortAbsorbing(re::DFA &d) {
+    const int n = d.nstates;
+    std::vector<char> ab(n, 0);
+    for (int s = 1; s < n; s++) {
+        bool a = true;
+        for (int b = 0; b < 256 && a; b++) {
+            const bool token_byte = b == '\t' || (b >= 0x20 && b != 0x7F);
+            if (token_byte && d.next[(size_t)s * d.ncls + d.cls[b]] != s) a = false;
+        }
+        ab[s] = a;
+    }
+    std::vector<int> order{0};
+    for (int s = 1; s < n; s++)
+        if (!ab[s]) order.push_back(s);
+    const uint32_t absorb = (uint32_t)order.size();
+    for (int s = 1; s < n; s++)
+        if (ab[s]) order.push_back(s);
+    std::vector<int> id(n);
+    for (int i = 0; i < n; i++) id[order[i]] = i;
+    std::vector<uint16_t> next((size_t)n * d.ncls);
+    std::vector<std::vector<uint64_t>> acc(n);
+    for (int i = 0; i < n; i++) {
+        for (int c = 0; c < d.ncls; c++)
+            next[(size_t)i * d.ncls + c] = (uint16_t)id[d.next[(size_t)order[i] * d.ncls + c]];
+        acc[i] = d.accept[order[i]];
+    }
+    d.next.swap(next);
+    d.accept.swap(acc);
+    d.start = id[d.start];
+    return absorb;
+}
+
 template <class T>
 uint32_t Append(std::vector<uint8_t> &img, const T *p, size_t n) {
     size_t off = (img.size() + 15) & ~(size_t)15;
@@ -233,7 +269,7 @@ int HttpCompiler::Compile(const std::vector<const HttpRule *> &rules, uint8_t te
     H.nchunks = (uint8_t)nchunks;
     H.nhdr = (uint8_t)custom.size();
     H.terminal = terminal;
-    struct Built { int slot; re::DFA d; std::vector<uint64_t> masks; };
+    struct Built { int slot; re::DFA d; std::vector<uint64_t> masks; uint32_t absorb; };
     std::vector<Built> built;
     for (auto &kv : by_slot) {
         const int slot = kv.first;
@@ -276,7 +312,8 @@ int HttpCompiler::Compile(const std::vector<const HttpRule *> &rules, uint8_t te
         if (!build(allp)) return -1;
         H.max_slot_dfas = (uint8_t)std::max<size_t>(H.max_slot_dfas, dfas.size());
         for (size_t g = 0; g < dfas.size(); g++) {
-            Built b{slot, std::move(dfas[g]), {}};
+            Built b{slot, std::move(dfas[g]), {}, 0};
+            b.absorb = SortAbsorbing(b.d);  // before the masks, which follow the new numbering
             const std::vector<int> &sub = groups[g];
             std::vector<int> local(pats.size(), -1);
             for (size_t q = 0; q < sub.size(); q++) local[sub[q]] = (int)q;
@@ -342,6 +379,7 @@ int HttpCompiler::Compile(const std::vector<const HttpRule *> &rules, uint8_t te
         dd[k].cls_off = Append(img, d.cls, 256);
         dd[k].trans_off = Append(img, d.next.data(), d.next.size());
         dd[k].mask_off = Append(img, built[k].masks.data(), built[k].masks.size());
+        dd[k].absorb = built[k].absorb;
         H.total_states += (uint32_t)d.nstates;
     }
     memcpy(img.data() + H.dfa_off, dd.data(), dd.size() * sizeof(DevDfa));

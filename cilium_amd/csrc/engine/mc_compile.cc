@@ -159,6 +159,7 @@ int McCompiler::Compile(const std::vector<const McRule *> &rules, uint8_t termin
         dd[k].cls_off = Append(img, d.cls, 256);
         dd[k].trans_off = Append(img, d.next.data(), d.next.size());
         dd[k].mask_off = Append(img, masks.data(), masks.size());
+        dd[k].absorb = (uint32_t)d.nstates;  // (unused by the memcached kernel)
         states += (size_t)d.nstates;
     }
     if (!dd.empty()) memcpy(img.data() + H.dfa_off, dd.data(), dd.size() * sizeof(DevDfa));

@@ -117,6 +117,23 @@ __device__ __forceinline__ uint32_t nib(uint32_t s) { return __builtin_amdgcn_ub
 __device__ __forceinline__ uint32_t stop_mask(uint4 w) {
     return nib(stop_bits(w.x)) | nib(stop_bits(w.y)) << 4 | nib(stop_bits(w.z)) << 8 | nib(stop_bits(w.w)) << 12;
 }
+// bit 7 of byte i set iff byte i <= 0x20 or == 0x7F (ends a request target)
+__device__ __forceinline__ uint32_t tstop_bits(uint32_t x) {
+    const uint32_t t = x & 0x7F7F7F7Fu;
+    return (~(t + 0x5F5F5F5Fu) | (t + 0x01010101u)) & ~x & 0x80808080u;
+}
+// bit 7 of byte i set iff byte i ends a header value: < 0x20 other than HT, or DEL
+__device__ __forceinline__ uint32_t vstop_bits(uint32_t x) {
+    const uint32_t t = x ^ 0x09090909u;  // HT -> 0
+    const uint32_t ht = ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;
+    return stop_bits(x) & ~ht;
+}
+__device__ __forceinline__ uint32_t tstop_mask(uint4 w) {
+    return nib(tstop_bits(w.x)) | nib(tstop_bits(w.y)) << 4 | nib(tstop_bits(w.z)) << 8 | nib(tstop_bits(w.w)) << 12;
+}
+__device__ __forceinline__ uint32_t vstop_mask(uint4 w) {
+    return nib(vstop_bits(w.x)) | nib(vstop_bits(w.y)) << 4 | nib(vstop_bits(w.z)) << 8 | nib(vstop_bits(w.w)) << 12;
+}
 __device__ __forceinline__ uint32_t byte_of(uint4 w, uint32_t q) {
     // two selects + v_perm_b32 (an indexed select would be lowered to scratch)
     const bool upper = (q & 8) != 0;
@@ -168,6 +185,7 @@ struct Lane {
     uint64_t clv, cl;
     // DFA of the current slot (kDfasPerPass == 1); dtrans == 0: none
     uint32_t dcls, dtrans, dmask, dncls, st, saved;
+    uint32_t dabs;      // states >= dabs (and 0) are absorbing
     uint64_t acc[kChunksPerPass];
     uint32_t cg, dg;    // chunk group, DFA group of this pass
 };
@@ -178,7 +196,7 @@ __device__ __forceinline__ void slot_begin(const Img<kLds> &I, Lane &L, uint32_t
     const uint32_t lo = I.u8(offsetof(ImgHeader, slot_dfa) + slot) + L.dg;
     const uint32_t hi = I.u8(offsetof(ImgHeader, slot_dfa) + slot + 1);
     L.st = 0;
-    L.dcls = L.dtrans = L.dmask = L.dncls = 0;
+    L.dcls = L.dtrans = L.dmask = L.dncls = L.dabs = 0;
     if (lo < hi) {
         const uint32_t d = HDR_U32(I, dfa_off) + lo * sizeof(DevDfa);
         L.dcls = I.u32(d + 0);
@@ -187,6 +205,7 @@ __device__ __forceinline__ void slot_begin(const Img<kLds> &I, Lane &L, uint32_t
         const uint32_t nc_st = I.u32(d + 12);
         L.dncls = nc_st & 0xFFFF;
         L.st = nc_st >> 16;
+        L.dabs = I.u32(d + 16);
     }
 }
 
@@ -312,6 +331,22 @@ struct Cursor {
     __device__ __forceinline__ uint32_t at(uint32_t p) const { return slot[((p - w) & (kWin - 1)) ^ swz]; }
 };
 
+// First byte at or after pa (and before lim, inside the window) that ends a
+// token, 16 bytes a step: kKind 0 = request target (<= 0x20 or DEL), 1 =
+// header value (CTL other than HT, or DEL).  lim if none.
+template <int kKind>
+__device__ __forceinline__ uint32_t find_stop(const Cursor &C, uint32_t pa, uint32_t lim) {
+    while (pa < lim) {
+        const uint4 w = C.chunk((pa - C.w) >> 4);
+        uint32_t m = (kKind == 0 ? tstop_mask(w) : vstop_mask(w)) & (0xFFFFu << (pa & 15));
+        const uint32_t cend = (pa & ~15u) + 16;
+        if (cend > lim) m &= (1u << (lim & 15)) - 1u;
+        if (m) return (pa & ~15u) + (uint32_t)__builtin_ctz(m);
+        pa = cend;
+    }
+    return lim;
+}
+
 // ---------------------------------------------------------------- parse one window
 // Consumes [L.pa, min(window end, request end)).  Every loop has a single
 // exit; errors set the mode to M_DONE so later blocks fall through.
@@ -351,7 +386,7 @@ __device__ __forceinline__ void parse_window(const Img<kLds> &I, Lane &L, Cursor
             c = C.at(L.pa);
             uint32_t k = L.dcls ? I.u8(L.dcls + c) : 0;
             uint32_t c1 = L.pa + 1 < lim ? C.at(L.pa + 1) : 0;
-            while (c > 0x20 && c != 0x7F) {
+            while (c > 0x20 && c != 0x7F && L.st != 0 && L.st < L.dabs) {
                 const uint32_t p1 = L.pa + 1;
                 const uint32_t c2 = p1 + 1 < lim ? C.at(p1 + 1) : 0;
                 const uint32_t k1 = L.dcls ? I.u8(L.dcls + c1) : 0;
@@ -362,6 +397,10 @@ __device__ __forceinline__ void parse_window(const Img<kLds> &I, Lane &L, Cursor
                 c1 = c2;
                 k = k1;
             }
+        }
+        if (L.pa < lim && c > 0x20 && c != 0x7F) {  // absorbing state: the rest of the target cannot change it
+            L.pa = find_stop<0>(C, L.pa, lim);
+            c = L.pa < lim ? C.at(L.pa) : 0;
         }
         if (L.pa < lim) {
             if (c != ' ' || L.pa == L.mark) {
@@ -469,7 +508,9 @@ __device__ __forceinline__ void parse_window(const Img<kLds> &I, Lane &L, Cursor
                 c = C.at(L.pa);
                 uint32_t k = L.dcls ? I.u8(L.dcls + c) : 0;
                 uint32_t c1 = L.pa + 1 < lim ? C.at(L.pa + 1) : 0;
-                while (!((c < 0x20 && c != '\t') || c == 0x7F)) {  // CR ends it; other CTLs are errors
+                // CR ends it, other CTLs are errors; an absorbing state outside an
+                // OWS run ends the walk (trailing OWS needs the state before it)
+                while (!((c < 0x20 && c != '\t') || c == 0x7F) && (L.in_ows || (L.st != 0 && L.st < L.dabs))) {
                     const uint32_t p1 = L.pa + 1;
                     const uint32_t c2 = p1 + 1 < lim ? C.at(p1 + 1) : 0;
                     const uint32_t k1 = L.dcls ? I.u8(L.dcls + c1) : 0;
@@ -483,6 +524,10 @@ __device__ __forceinline__ void parse_window(const Img<kLds> &I, Lane &L, Cursor
                     c1 = c2;
                     k = k1;
                 }
+            }
+            if (L.pa < lim && !((c < 0x20 && c != '\t') || c == 0x7F)) {  // absorbing: skip to the value's end
+                L.pa = find_stop<1>(C, L.pa, lim);
+                c = L.pa < lim ? C.at(L.pa) : 0;
             }
             if (L.pa < lim) {
                 if (c != '\r') {
@@ -595,13 +640,6 @@ __device__ __forceinline__ void dma_windows(uint8_t *wave_lds, uint64_t packed, 
 // so the lane reads 128 bytes of map (1 KiB of arena) and takes the first mark
 // at or after L.pa.  The next window starts at that byte.
 constexpr uint32_t kMapSpan = 1024;  // arena bytes covered by one map read
-
-// bit 7 of each byte set iff the byte is a value stop
-__device__ __forceinline__ uint32_t vstop_bits(uint32_t x) {
-    const uint32_t t = x ^ 0x09090909u;  // HT -> 0
-    const uint32_t ht = ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;
-    return stop_bits(x) & ~ht;
-}
 
 struct StopMap {
     const uint16_t *map;  // u16 per 16-byte chunk from base (+ 72 chunks of slack)

@@ -3,7 +3,7 @@ bit-exact on verdict, matched rule id and consumed bytes."""
 import numpy as np
 import pytest
 
-from cilium_amd import gen
+from cilium_amd import api, gen
 from cilium_amd._lib import ALLOW, DENY, INCOMPLETE, PARSE_ERROR, PROTO_HTTP, UNSUPPORTED
 
 pytestmark = pytest.mark.gpu
@@ -152,3 +152,26 @@ def test_unaligned_offsets_and_tail(engine, oracle):
                      gen.make_conns(1, 0, 80, True, PROTO_HTTP, [5]), gen.cfg2_policy())
     got, ref = both(engine, oracle, w, 1)
     assert_same(got, ref, w)
+
+
+def test_absorbing_states_and_trailing_ows(engine, oracle):
+    """Walks that stop once a DFA state is absorbing (every further byte loops
+    back): `.*` tails, dead states, UTF-8 after the point of no return, and
+    trailing OWS after a state that would die on the next byte."""
+    rules = api.http_rules_from_api([
+        api.PortRuleHTTP(path="/p/.*", host="h\\..*"),
+        api.PortRuleHTTP(path="/exact", host="abc"),
+        api.PortRuleHTTP(method="GET", path="/u/é.*", headers=["X-A: abc"]),
+    ])
+    pol = api.policy_set(api.network_policy("ep", 1, ingress=[(80, [api.port_rule(http=rules)])]))
+    reqs = []
+    for host in [b"h.x", b"h.", b"h.\xc3\xa9\xff\x80 tail", b"abc", b"abc ", b"abc \t ", b"abc x", b"abcd", b"ab c",
+                 b"h." + b"a" * 240 + b"   ", b"abc" + b" " * 300, b"h." + b"b" * 230 + b" \t\x01"]:
+        for path in [b"/p/", b"/p/" + b"z" * 300, b"/exact", b"/exactly", b"/u/\xc3\xa9\xc3", b"/q\x80\xff/x"]:
+            for xa in [b"", b"X-A: abc\r\n", b"X-A: abc  \r\n", b"X-A: abcd\r\n", b"X-A: ab\tc\r\n"]:
+                reqs.append(b"GET " + path + b" HTTP/1.1\r\nHost: " + host + b"\r\n" + xa + b"X-Pad: " + b"p" * 40 + b"\r\n\r\n")
+    conns = gen.make_conns(1, 0, 80, True, PROTO_HTTP, [9])
+    w = wl_from_reqs(reqs, pol, conns)
+    got, ref = both(engine, oracle, w, 4)
+    assert_same(got, ref, w)
+    assert (got[0] == ALLOW).sum() > 20 and (got[0] == DENY).sum() > 20
