@@ -19,16 +19,17 @@
 //      fetched while the current transition is in flight, so a byte costs one
 //      dependent LDS round trip.  Values nobody constrains are skipped 16
 //      bytes a step (SWAR CTL/DEL test).
-//   3. skip: a lane whose unconstrained value runs past its window looks up
-//      where it ends in the arena's value-stop map (first byte < 0x20 other
-//      than HT, or DEL), built beforehand by http_stopmap_kernel in one
-//      coalesced pass over the arena: 128 bytes of map cover 1 KiB of
-//      request, so the value's bytes are never loaded by this kernel.  The
-//      lane's next window starts at the stop byte.
+//   3. skip: before its first window the wave streams its tile's byte span
+//      once (coalesced LDS-DMA, 16 pieces of 1 KiB in flight) and keeps a
+//      bit per 16-byte chunk holding a value-stop byte (< 0x20 other than HT,
+//      or DEL) in registers.  A lane whose unconstrained value runs past its
+//      window finds the first marked chunk after it by ds_bpermute and reads
+//      just that chunk; when the stop is the CR of "\r\n\r\n" the request
+//      finishes there, otherwise the next window starts at the stop.
 //
-// For the benchmark stream a tile takes two windows per request (the head,
-// then the end of the header block) and one map lookup (the long pad header);
-// the pad bytes are read once, by the stop-map stream.
+// For the benchmark stream a tile takes the span stream, one window per
+// request (the head) and one map lookup (the long pad header); constrained
+// values stop being walked once their DFA state is absorbing.
 //
 // One 512-thread workgroup per CU: 8 waves x 16 KiB windows + the hot rule
 // set's image (<= 28 KiB) + rule counters = 160 KiB of LDS.
@@ -632,57 +633,162 @@ __device__ __forceinline__ void dma_windows(uint8_t *wave_lds, uint64_t packed, 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// ---------------------------------------------------------------- long-value skip
+// ---------------------------------------------------------------- value-stop map of a tile
 // A value nobody constrains ends at its first "value stop" byte (< 0x20 other
-// than HT, or DEL: CR normally, anything else is an error).  Bytes past the
-// lane's window are not loaded at all: http_stopmap_kernel has already marked
-// every value-stop byte of the arena in a bitmap (one u16 per 16-byte chunk),
-// so the lane reads 128 bytes of map (1 KiB of arena) and takes the first mark
-// at or after L.pa.  The next window starts at that byte.
-constexpr uint32_t kMapSpan = 1024;  // arena bytes covered by one map read
+// than HT, or DEL: CR normally, anything else is an error).  Before its first
+// window the wave streams the byte span of its tile (packed batches keep the
+// 64 requests side by side) through its window area, 1 KiB pieces with kRing
+// of them in flight, and keeps one bit per 16-byte chunk -- "holds a value
+// stop" -- in registers: lane l holds pieces 4l..4l+3.  A long value is then
+// skipped by finding the first marked chunk at or after L.pa (the owning
+// lane's bits, by ds_bpermute) and reading only that chunk and the next.
+// A tile whose span exceeds kSpanMax has no map; its long values continue
+// window by window.
+constexpr int kRing = (int)(kWaveLds / 1024);
+constexpr uint64_t kSpanMax = 256 * 1024;
 
-struct StopMap {
-    const uint16_t *map;  // u16 per 16-byte chunk from base (+ 72 chunks of slack)
-    uint64_t base;        // arena address rounded down to 16 bytes
+struct TileMap {
+    uint64_t lo, hi;  // span [lo, hi), 16-byte aligned; lo == hi: no map
+    uint32_t m[8];    // pieces 4*lane .. 4*lane+3, 64 chunk bits each
 };
 
-__device__ __forceinline__ void map_skip(Lane &L, const StopMap &M) {
-    while (__any(L.scan)) {
-        if (L.scan) {
-            const uint64_t a = L.base + L.pa - M.base;  // arena-relative position of pa
-            const uint64_t c0 = (a >> 4) & ~7ull;        // first chunk of a 16-byte map group
-            const uint32_t from = (uint32_t)(a - (c0 << 4));  // bit of pa in the 1024-bit span
-            const uint4 *mp = (const uint4 *)(M.map + c0);
-            uint4 m[8];
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint32_t byte_at32(uint4 a, uint4 b, uint32_t i) {
+    // byte i (0..31) of the 32 bytes a, b (little endian)
+    const uint32_t d = i < 16 ? (i < 8 ? (i < 4 ? a.x : a.y) : (i < 12 ? a.z : a.w))
+                              : (i < 24 ? (i < 20 ? b.x : b.y) : (i < 28 ? b.z : b.w));
+    return (d >> (8 * (i & 3))) & 0xFF;
+}
+
+__device__ __forceinline__ void build_tile_map(TileMap &T, const Lane &L, uint32_t lane, uint8_t *wave_lds) {
 #pragma unroll
-            for (int k = 0; k < 8; k++) m[k] = mp[k];
-            uint32_t hit = 0xFFFFFFFFu;
+    for (int q = 0; q < 8; q++) T.m[q] = 0;
+    uint64_t lo = L.done ? ~0ull : L.base;
+    uint64_t hi = L.done ? 0ull : L.base + ((L.lena + 15u) & ~15u);
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t l2 = (uint64_t)__shfl_xor((unsigned long long)lo, o);
+        const uint64_t h2 = (uint64_t)__shfl_xor((unsigned long long)hi, o);
+        lo = l2 < lo ? l2 : lo;
+        hi = h2 > hi ? h2 : hi;
+    }
+    lo = uniform64(lo);
+    hi = uniform64(hi);
+    T.lo = T.hi = lo;
+    if (lo >= hi || hi - lo > kSpanMax) return;
+    T.hi = hi;
+    const uint32_t npieces = (uint32_t)((hi - lo + 1023) >> 10);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // earlier LDS reads of the window area have landed
+    // piece j -> slot s; an idle slot still issues its load (at the span
+    // start), so a slot is examined with exactly kRing-1 loads behind it
+#define MAP_ISSUE(s, j)                                                                                   \
+    do {                                                                                                  \
+        const uint64_t a_ = lo + ((uint64_t)(j) << 10) + 16 * lane;                                       \
+        __builtin_amdgcn_global_load_lds((const void *)((j) < npieces && a_ < hi ? a_ : lo),               \
+                                         (__attribute__((address_space(3))) void *)(wave_lds + (s) * 1024), \
+                                         16, 0, 0);                                                       \
+    } while (0)
 #pragma unroll
-            for (int k = 7; k >= 0; k--) {  // the last assignment is the first hit
+    for (int s = 0; s < kRing; s++) MAP_ISSUE(s, (uint32_t)s);
+    for (uint32_t j0 = 0; j0 < npieces; j0 += kRing) {
 #pragma unroll
-                for (int j = 3; j >= 0; j--) {
-                    const uint32_t i = 4 * k + j;  // dword i covers span bits 32i .. 32i+31
-                    uint32_t d = j == 0 ? m[k].x : j == 1 ? m[k].y : j == 2 ? m[k].z : m[k].w;
-                    d = (from >> 5) > i ? 0u : (from >> 5) == i ? d & (0xFFFFFFFFu << (from & 31)) : d;
-                    if (d) hit = 32 * i + (uint32_t)__builtin_ctz(d);
+        for (int s = 0; s < kRing; s++) {
+            const uint32_t j = j0 + s;
+            wait_vmcnt<kRing - 1>();
+            if (j < npieces) {
+                // inline asm: a plain LDS read here would make hipcc drain every
+                // in-flight LDS-DMA first (vmcnt(0)), serialising the ring
+                uint4 v;
+                asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)"
+                             : "=v"(v)
+                             : "v"((uint32_t)(uintptr_t)(wave_lds + s * 1024 + 16 * lane))
+                             : "memory");
+                const bool ok = lo + ((uint64_t)j << 10) + 16 * lane < hi;
+                const uint32_t any = vstop_bits(v.x) | vstop_bits(v.y) | vstop_bits(v.z) | vstop_bits(v.w);
+                const uint64_t M = __ballot(ok && any != 0);
+                if (lane == (j >> 2)) {  // j & 3 == s & 3: a constant register index
+                    T.m[2 * (s & 3)] = (uint32_t)M;
+                    T.m[2 * (s & 3) + 1] = (uint32_t)(M >> 32);
                 }
             }
-            const uint64_t span0 = M.base + (c0 << 4) - L.base;  // span start, request-relative
-            if (hit != 0xFFFFFFFFu && span0 + hit < L.lena) {
-                L.pa = (uint32_t)(span0 + hit);
-                L.scan = false;
-                // the value was the last header when "\r\n\r\n" follows: check
-                // those four bytes now instead of loading a window for them
-                if (L.pa + 4 <= L.lena) {
-                    const uint8_t *q = (const uint8_t *)(L.base + L.pa);
-                    const uint32_t w = (uint32_t)q[0] | (uint32_t)q[1] << 8 | (uint32_t)q[2] << 16 | (uint32_t)q[3] << 24;
-                    L.tail = w == 0x0A0D0A0Du;
+            MAP_ISSUE(s, j + kRing);
+        }
+    }
+    wait_vmcnt<0>();
+#undef MAP_ISSUE
+}
+
+// Lanes with L.scan set: skip the rest of the value with the tile map.
+__device__ __forceinline__ void map_skip(Lane &L, const TileMap &T) {
+    if (T.lo == T.hi) {  // no map: the value continues window by window
+        L.scan = false;
+        return;
+    }
+    while (__any(L.scan)) {
+        const bool act = L.scan;
+        // span-relative chunk to search from; the request's chunks end at kend
+        uint32_t k = act ? (uint32_t)((L.base + L.pa - T.lo) >> 4) : 0;
+        const uint32_t kend = act ? (uint32_t)((L.base + L.lena - T.lo + 15) >> 4) : 0;
+        uint32_t found = 0xFFFFFFFFu;
+        bool look = act && k < kend;
+        while (__any(look)) {  // every lane takes part in the shuffles
+            const uint32_t j = k >> 6;
+            const int owner = (int)((j >> 2) & 63);
+            uint32_t d[8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) d[q] = (uint32_t)__shfl((int)T.m[q], owner);
+            const uint32_t w = j & 3;
+            const uint32_t mlo = w == 0 ? d[0] : w == 1 ? d[2] : w == 2 ? d[4] : d[6];
+            const uint32_t mhi = w == 0 ? d[1] : w == 1 ? d[3] : w == 2 ? d[5] : d[7];
+            const uint64_t M = (((uint64_t)mhi << 32) | mlo) & (~0ull << (k & 63));
+            if (look) {
+                if (M) {
+                    found = (j << 6) + (uint32_t)__builtin_ctzll(M);
+                    look = false;
+                } else {
+                    k = (j + 1) << 6;
+                    look = k < kend;
                 }
-            } else if (span0 + kMapSpan >= L.lena) {
+            }
+        }
+        if (act) {
+            if (found >= kend) {  // no value stop before the request's end
                 L.pa = L.lena;
                 finish(L, V_INCOMPLETE);
             } else {
-                L.pa = (uint32_t)(span0 + kMapSpan);
+                const uint64_t ca = T.lo + ((uint64_t)found << 4);  // the marked chunk
+                const uint4 w0 = *(const uint4 *)ca;
+                const uint4 w1 = ca + 16 < T.hi ? *(const uint4 *)(ca + 16) : make_uint4(0, 0, 0, 0);
+                const uint32_t cpos = (uint32_t)(ca - L.base);  // request-relative
+                const uint32_t lo_b = L.pa > cpos ? L.pa - cpos : 0;
+                const uint32_t hi_b = min(L.lena - cpos, 16u);
+                const uint32_t m = vstop_mask(w0) & (0xFFFFu << lo_b) & ((1u << hi_b) - 1u);
+                if (m) {
+                    const uint32_t b = (uint32_t)__builtin_ctz(m);
+                    L.pa = cpos + b;
+                    L.scan = false;
+                    // "\r\n\r\n" here ends the header block: no window needed for it
+                    if (L.pa + 4 <= L.lena) {
+                        const uint32_t t4 = byte_at32(w0, w1, b) | byte_at32(w0, w1, b + 1) << 8 |
+                                            byte_at32(w0, w1, b + 2) << 16 | byte_at32(w0, w1, b + 3) << 24;
+                        L.tail = t4 == 0x0A0D0A0Du;
+                    }
+                } else {  // the chunk's stops lie before pa: search on
+                    L.pa = cpos + 16;
+                    if (L.pa >= L.lena) {
+                        L.pa = L.lena;
+                        finish(L, V_INCOMPLETE);
+                    }
+                }
             }
         }
     }
@@ -727,8 +833,7 @@ __device__ __forceinline__ void emit(const Lane &L, const Out &O) {
 
 // All rounds of one tile.
 template <bool kLds>
-__device__ __forceinline__ void run_tile(Lane &L, const uint8_t *img, uint8_t *wave_lds, uint32_t lane, const Out &O,
-                                         const StopMap &M) {
+__device__ __forceinline__ void run_tile(Lane &L, const uint8_t *img, uint8_t *wave_lds, uint32_t lane, const Out &O) {
     const Img<kLds> I{img};
     L.scan = false;
     L.tail = false;
@@ -739,6 +844,8 @@ __device__ __forceinline__ void run_tile(Lane &L, const uint8_t *img, uint8_t *w
         frame_reset(I, L);
         if (L.lena == L.a0) finish(L, V_INCOMPLETE);
     }
+    TileMap TM;
+    build_tile_map(TM, L, lane, wave_lds);
     Cursor C;
     C.slot = wave_lds + lane * kWin;
     C.swz = win_swizzle(lane) << 4;
@@ -759,7 +866,7 @@ __device__ __forceinline__ void run_tile(Lane &L, const uint8_t *img, uint8_t *w
         }
         PH_MARK(1);
         PH_COUNT(5, __builtin_popcountll(__ballot(L.scan)));
-        map_skip(L, M);
+        map_skip(L, TM);
         if (L.tail) finish_tail(I, L);
         PH_MARK(2);
         if (L.done && L.owed) {
@@ -788,9 +895,8 @@ __global__ __launch_bounds__(kBlock) void http_classify_kernel(
     const uint8_t *__restrict__ arena, const uint64_t *__restrict__ offs, const uint32_t *__restrict__ lens,
     const uint32_t *__restrict__ conn_ids, uint32_t n, const DevConn *__restrict__ conns, uint32_t nconns,
     HttpTables T, uint8_t *__restrict__ out_verdict, int32_t *__restrict__ out_rule, uint32_t *__restrict__ out_consumed,
-    uint64_t *__restrict__ counters, uint32_t ncounters, const uint16_t *__restrict__ smap, uint64_t arena_len) {
+    uint64_t *__restrict__ counters, uint32_t ncounters, uint64_t arena_len) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
-    const StopMap M{smap, (uint64_t)arena & ~(uint64_t)15};
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63, wave = tid >> 6;
     uint8_t *s_img = lds + kOffImg;
@@ -850,7 +956,7 @@ __global__ __launch_bounds__(kBlock) void http_classify_kernel(
                 }
             }
         }
-        run_tile<kHot>(L, img, wave_lds, lane, O, M);
+        run_tile<kHot>(L, img, wave_lds, lane, O);
     }
     if (counters) {
         __syncthreads();
@@ -860,31 +966,6 @@ __global__ __launch_bounds__(kBlock) void http_classify_kernel(
             if (!v) continue;
             if (i < 8) atomicAdd((unsigned long long *)&counters[nrules + i], (unsigned long long)v);
             else if (i - 8 < nrules) atomicAdd((unsigned long long *)&counters[i - 8], (unsigned long long)v);
-        }
-    }
-}
-
-// Value-stop map of the whole arena: bit b of map[c] <=> byte 16c+b (from
-// the arena address rounded down to 16) is < 0x20 other than HT, or DEL.
-// Coalesced 16-byte loads, 2-byte stores: a pure HBM stream.
-constexpr int kMapBlock = 256;
-__global__ __launch_bounds__(kMapBlock) void http_stopmap_kernel(const uint8_t *__restrict__ base, uint64_t nchunks,
-                                                                 uint16_t *__restrict__ map) {
-    const uint4 *src = (const uint4 *)base;
-    const uint64_t stride = (uint64_t)gridDim.x * kMapBlock * 4;
-    for (uint64_t c0 = (uint64_t)blockIdx.x * kMapBlock * 4 + threadIdx.x; c0 < nchunks; c0 += stride) {
-        uint4 w[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const uint64_t c = c0 + (uint64_t)k * kMapBlock;
-            w[k] = c < nchunks ? src[c] : make_uint4(0, 0, 0, 0);
-        }
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const uint64_t c = c0 + (uint64_t)k * kMapBlock;
-            if (c < nchunks)
-                map[c] = (uint16_t)(nib(vstop_bits(w[k].x)) | nib(vstop_bits(w[k].y)) << 4 | nib(vstop_bits(w[k].z)) << 8 |
-                                    nib(vstop_bits(w[k].w)) << 12);
         }
     }
 }
@@ -904,30 +985,17 @@ hipError_t LaunchHttpClassify(const uint8_t *arena, uint64_t arena_len, const ui
             hipDeviceGetAttribute(&num_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || num_cus <= 0)
             num_cus = 256;
     }
-    // value-stop map of the arena (stream-ordered scratch, freed after the batch)
-    const uint64_t nchunks = (((uint64_t)arena & 15) + arena_len + 15) / 16;
-    uint16_t *smap = nullptr;
-    hipError_t rc = hipMallocAsync((void **)&smap, (nchunks + 72) * sizeof(uint16_t), stream);
-    if (rc != hipSuccess) return rc;
-    if (nchunks) {
-        const uint64_t per_block = (uint64_t)kMapBlock * 4;
-        const uint32_t mblocks = (uint32_t)std::min<uint64_t>((nchunks + per_block - 1) / per_block, (uint64_t)num_cus * 16);
-        hipLaunchKernelGGL(http_stopmap_kernel, dim3(mblocks), dim3(kMapBlock), 0, stream,
-                           (const uint8_t *)((uint64_t)arena & ~(uint64_t)15), nchunks, smap);
-    }
     const uint32_t ntiles = (n + 63) / 64;
     uint32_t blocks = (ntiles + kWaves - 1) / kWaves;
     blocks = min(blocks, (uint32_t)num_cus);
     const bool hot = T.hot_ruleset >= 0;
     if (hot)
         hipLaunchKernelGGL(http_classify_kernel<true>, dim3(blocks), dim3(kBlock), 0, stream, arena, offs, lens, conn_ids,
-                           n, conns, nconns, T, verdict, rule, consumed, counters, ncounters, smap, arena_len);
+                           n, conns, nconns, T, verdict, rule, consumed, counters, ncounters, arena_len);
     if (!hot || any_cold)
         hipLaunchKernelGGL(http_classify_kernel<false>, dim3(blocks), dim3(kBlock), 0, stream, arena, offs, lens,
-                           conn_ids, n, conns, nconns, T, verdict, rule, consumed, counters, ncounters, smap, arena_len);
-    rc = hipGetLastError();
-    hipError_t rf = hipFreeAsync(smap, stream);
-    return rc != hipSuccess ? rc : rf;
+                           conn_ids, n, conns, nconns, T, verdict, rule, consumed, counters, ncounters, arena_len);
+    return hipGetLastError();
 }
 
 #ifdef L7G_PHASE_TIMING
