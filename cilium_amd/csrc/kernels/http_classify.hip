@@ -129,6 +129,29 @@ __device__ __forceinline__ uint32_t vstop_bits(uint32_t x) {
     const uint32_t ht = ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;
     return stop_bits(x) & ~ht;
 }
+// nonzero iff some byte of the chunk is < 0x20 or DEL (HT included: a superset
+// of the value stops, for the tile map)
+__device__ __forceinline__ uint32_t stop_any(uint4 w) {
+    const uint32_t a = w.x & 0x7F7F7F7Fu, b = w.y & 0x7F7F7F7Fu, c = w.z & 0x7F7F7F7Fu, d = w.w & 0x7F7F7F7Fu;
+    const uint32_t s = ((~(a + 0x60606060u) | (a + 0x01010101u)) & ~w.x) | ((~(b + 0x60606060u) | (b + 0x01010101u)) & ~w.y) |
+                       ((~(c + 0x60606060u) | (c + 0x01010101u)) & ~w.z) | ((~(d + 0x60606060u) | (d + 0x01010101u)) & ~w.w);
+    return s & 0x80808080u;
+}
+// bit 7 of byte i set iff byte i is one of [0-9A-Za-z-] (a subset of tchar)
+__device__ __forceinline__ uint32_t alnum_bits(uint32_t x) {
+    const uint32_t h = x | 0x80808080u;
+    const uint32_t l = x | 0xA0A0A0A0u;  // letters folded to lower case, bit 7 set
+    const uint32_t dig = (h - 0x30303030u) & ~(h - 0x3A3A3A3Au);
+    const uint32_t let = (l - 0x61616161u) & ~(l - 0x7B7B7B7Bu);
+    const uint32_t t = x ^ 0x2D2D2D2Du;  // '-' -> 0
+    const uint32_t dash = ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t);
+    return (dig | let | dash) & ~x & 0x80808080u;
+}
+// 16-bit mask of the bytes of a chunk that are not [0-9A-Za-z-]
+__device__ __forceinline__ uint32_t nonalnum_mask(uint4 w) {
+    return (nib(~alnum_bits(w.x) & 0x80808080u) | nib(~alnum_bits(w.y) & 0x80808080u) << 4 |
+            nib(~alnum_bits(w.z) & 0x80808080u) << 8 | nib(~alnum_bits(w.w) & 0x80808080u) << 12);
+}
 __device__ __forceinline__ uint32_t tstop_mask(uint4 w) {
     return nib(tstop_bits(w.x)) | nib(tstop_bits(w.y)) << 4 | nib(tstop_bits(w.z)) << 8 | nib(tstop_bits(w.w)) << 12;
 }
@@ -334,12 +357,13 @@ struct Cursor {
 
 // First byte at or after pa (and before lim, inside the window) that ends a
 // token, 16 bytes a step: kKind 0 = request target (<= 0x20 or DEL), 1 =
-// header value (CTL other than HT, or DEL).  lim if none.
+// header value (CTL other than HT, or DEL), 2 = simple header name (not
+// [0-9A-Za-z-]).  lim if none.
 template <int kKind>
 __device__ __forceinline__ uint32_t find_stop(const Cursor &C, uint32_t pa, uint32_t lim) {
     while (pa < lim) {
         const uint4 w = C.chunk((pa - C.w) >> 4);
-        uint32_t m = (kKind == 0 ? tstop_mask(w) : vstop_mask(w)) & (0xFFFFu << (pa & 15));
+        uint32_t m = (kKind == 0 ? tstop_mask(w) : kKind == 1 ? vstop_mask(w) : nonalnum_mask(w)) & (0xFFFFu << (pa & 15));
         const uint32_t cend = (pa & ~15u) + 16;
         if (cend > lim) m &= (1u << (lim & 15)) - 1u;
         if (m) return (pa & ~15u) + (uint32_t)__builtin_ctz(m);
@@ -416,6 +440,22 @@ __device__ __forceinline__ void parse_window(const Img<kLds> &I, Lane &L, Cursor
         }
     }
     if (L.mode == M_VERSION) {  // "HTTP/" DIGIT "." DIGIT CRLF
+        if (L.mark == 0 && L.pa + 10 <= lim) {  // all ten bytes in the window: compare them at once
+            const uint32_t k0 = (L.pa - L.w) >> 4, o = L.pa & 15, i = o >> 2, sh = o & 3;
+            const uint4 a = C.chunk(k0), b = C.chunk(k0 + 1);  // (b unused when the bytes end in a)
+            const uint32_t e0 = i == 0 ? a.x : i == 1 ? a.y : i == 2 ? a.z : a.w;
+            const uint32_t e1 = i == 0 ? a.y : i == 1 ? a.z : i == 2 ? a.w : b.x;
+            const uint32_t e2 = i == 0 ? a.z : i == 1 ? a.w : i == 2 ? b.x : b.y;
+            const uint32_t e3 = i == 0 ? a.w : i == 1 ? b.x : i == 2 ? b.y : b.z;
+            const uint32_t r0 = __builtin_amdgcn_alignbyte(e1, e0, sh);
+            const uint32_t r1 = __builtin_amdgcn_alignbyte(e2, e1, sh);
+            const uint32_t r2 = __builtin_amdgcn_alignbyte(e3, e2, sh);
+            if (r0 == 0x50545448u && (r1 & 0x00FF00FFu) == 0x002E002Fu && ((r1 >> 8) & 0xFF) - '0' < 10u &&
+                (r1 >> 24) - '0' < 10u && (r2 & 0xFFFFu) == 0x0A0Du) {
+                L.pa += 10;
+                L.mark = 10;
+            }
+        }
         for (; L.pa < lim && L.mark < 10; L.pa++, L.mark++) {
             const uint32_t c = C.at(L.pa);
             const uint32_t want = kVer[L.mark];
@@ -450,7 +490,7 @@ __device__ __forceinline__ void parse_window(const Img<kLds> &I, Lane &L, Cursor
                 c = C.at(L.pa);
                 uint32_t k = I.u8(name_cls + c);  // 0 = not a tchar
                 uint32_t c1 = L.pa + 1 < lim ? C.at(L.pa + 1) : 0;
-                while (k != 0) {
+                while (k != 0 && L.nstate != kNameOther) {
                     const uint32_t p1 = L.pa + 1;
                     const uint32_t c2 = p1 + 1 < lim ? C.at(p1 + 1) : 0;
                     const uint32_t k1 = I.u8(name_cls + c1);
@@ -460,6 +500,17 @@ __device__ __forceinline__ void parse_window(const Img<kLds> &I, Lane &L, Cursor
                     c = c1;
                     c1 = c2;
                     k = k1;
+                }
+                if (L.pa < lim && k != 0) {
+                    // a name the rule set does not know (the DFA state loops on
+                    // every tchar): only where it ends matters.  [0-9A-Za-z-]
+                    // runs are skipped 16 bytes a step, other tchars one by one.
+                    L.pa = find_stop<2>(C, L.pa, lim);
+                    c = L.pa < lim ? C.at(L.pa) : 0;
+                    while (L.pa < lim && c != ':' && is_tchar(c)) {
+                        L.pa++;
+                        c = L.pa < lim ? C.at(L.pa) : 0;
+                    }
                 }
             }
             if (L.pa < lim) {
@@ -713,8 +764,7 @@ __device__ __forceinline__ void build_tile_map(TileMap &T, const Lane &L, uint32
                              : "v"((uint32_t)(uintptr_t)(wave_lds + s * 1024 + 16 * lane))
                              : "memory");
                 const bool ok = lo + ((uint64_t)j << 10) + 16 * lane < hi;
-                const uint32_t any = vstop_bits(v.x) | vstop_bits(v.y) | vstop_bits(v.z) | vstop_bits(v.w);
-                const uint64_t M = __ballot(ok && any != 0);
+                const uint64_t M = __ballot(ok && stop_any(v) != 0);  // HT marks too: map_skip sorts it out
                 if (lane == (j >> 2)) {  // j & 3 == s & 3: a constant register index
                     T.m[2 * (s & 3)] = (uint32_t)M;
                     T.m[2 * (s & 3) + 1] = (uint32_t)(M >> 32);

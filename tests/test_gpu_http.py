@@ -175,3 +175,26 @@ def test_absorbing_states_and_trailing_ows(engine, oracle):
     got, ref = both(engine, oracle, w, 4)
     assert_same(got, ref, w)
     assert (got[0] == ALLOW).sum() > 20 and (got[0] == DENY).sum() > 20
+
+
+def test_header_name_and_version_fast_paths(engine, oracle):
+    """SWAR version compare and the skip over names no rule knows: every
+    alignment, window-boundary crossings, tchars outside [0-9A-Za-z-], and
+    malformed names / versions."""
+    pol = gen.cfg2_policy()
+    names = [b"X_Custom_Name", b"x.y", b"Some-Very-Long-Header-Name-Exceeding-Sixteen-Bytes", b"Bad Name",
+             b"Bad\x01Name", b"X-Tokenx", b"X-Tok", b"X-Token", b"host", b"Ho_st", b"A" * 70, b"a~b!c#d", b"\xc3\xa9t\xc3\xa9"]
+    versions = [b"HTTP/1.1", b"HTTP/2.0", b"HTTP/1.x", b"HTTQ/1.1", b"HTTP/1,1", b"HTTP/11.1", b"HTTP/1.1 "]
+    reqs = []
+    for i in range(260):
+        path = b"/public/abc/7/" + b"p" * (i % 240)
+        v = versions[i % len(versions)] if i % 3 == 0 else b"HTTP/1.1"
+        eol = b"\n" if i % 37 == 5 else b"\r\n"
+        nm = names[i % len(names)]
+        hdrs = b"Host: svc-7.q\r\n" + nm + b": v" + b"\r\n" + b"X-Token: 123\r\n"
+        reqs.append(b"GET " + path + b" " + v + eol + hdrs + b"\r\n")
+    conns = gen.make_conns(1, 0, 80, True, PROTO_HTTP, [3])
+    w = wl_from_reqs(reqs, pol, conns)
+    got, ref = both(engine, oracle, w, 4)
+    assert_same(got, ref, w)
+    assert len(set(got[0].tolist())) >= 2
