@@ -77,7 +77,7 @@ __device__ __forceinline__ uint32_t win_swizzle(uint32_t t) {
 
 // Optional per-phase cycle accounting (debug builds with -DL7G_PHASE_TIMING:
 // libl7gpu_timing.so, used by tools/exp_http.py).  Slots: 0 dma, 1 parse,
-// 2 scan, 3 emit/other, 4 rounds, 5 scan batches, 6 tiles.
+// 2 tile map + skips, 3 emit/other, 4 rounds, 5 skips, 6 tiles.
 #ifdef L7G_PHASE_TIMING
 __device__ unsigned long long g_phase[8];
 #define PH_DECL uint64_t ph_t = __builtin_amdgcn_s_memtime(); uint64_t ph_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -894,12 +894,13 @@ __device__ __forceinline__ void run_tile(Lane &L, const uint8_t *img, uint8_t *w
         frame_reset(I, L);
         if (L.lena == L.a0) finish(L, V_INCOMPLETE);
     }
+    PH_DECL
     TileMap TM;
     build_tile_map(TM, L, lane, wave_lds);
+    PH_MARK(2);
     Cursor C;
     C.slot = wave_lds + lane * kWin;
     C.swz = win_swizzle(lane) << 4;
-    PH_DECL
     while (__any(!L.done)) {
         uint64_t packed = 0;
         if (!L.done) {
