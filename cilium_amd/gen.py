@@ -45,8 +45,17 @@ class Workload:
                         self.conn_ids[idx], self.conns, self.policy, self.meta)
 
     def algorithmic_bytes(self):
-        """B_i = len_i + 16 (offset u64 + len u32 + meta u32) + 9 (verdict u8 + rule i32 + consumed u32)."""
-        return int(self.lengths.astype(np.int64).sum()) + 25 * self.n
+        """B_i = len_i + 16 (offset u64 + len u32 + meta u32) + 9 (verdict u8 + rule i32 + consumed u32).
+
+        memcached requests count only the bytes the parser must inspect (the
+        command line, or the 24-byte header + extras + key): the data block of a
+        storage command is framed by its length and never read
+        (text/parser.go:186-198, binary/parser.go:86-105).  Generators that
+        know this set meta["payload_bytes"]."""
+        payload = self.meta.get("payload_bytes")
+        if payload is None:
+            payload = int(self.lengths.astype(np.int64).sum())
+        return int(payload) + 25 * self.n
 
 
 def pack(reqs):
@@ -562,4 +571,59 @@ def memcache_workload(n, nconns=256, seed=None, adversarial=False):
     conns["port"][::16] = 11212
     if adversarial:  # connections whose parser (text / binary) was already chosen by earlier traffic
         conns["flags"] = rng.integers(0, 3, size=nconns)
-    return Workload("cfg5-mc", arena, offs, lens, conn_ids, conns, mc_policy())
+    meta = {} if adversarial else {"payload_bytes": mc_inspected_bytes(reqs)}
+    return Workload("cfg5-mc", arena, offs, lens, conn_ids, conns, mc_policy(), meta)
+
+
+def mc_inspected_bytes(reqs):
+    """Bytes a memcached parser reads per request: text = the command line up to
+    and including its CRLF; binary = 24-byte header + extras + key."""
+    tot = 0
+    for r in reqs:
+        if r and r[0] >= 0x80:
+            tot += min(len(r), 24 + (r[4] if len(r) > 4 else 0) + (int.from_bytes(r[2:4], "big") if len(r) > 3 else 0))
+        else:
+            lf = r.find(b"\r\n")
+            tot += len(r) if lf < 0 else lf + 2
+    return tot
+
+
+# ------------------------------------------------------------------ cfg5 mixed stream, tiling
+def mixed_workload(n, seed=None):
+    """cfg5: 50 % HTTP (cfg2 rules), 30 % Kafka (cfg3 rules), 20 % memcached,
+    interleaved in one batch; three endpoint policies (HTTP, Kafka, memcached)."""
+    seed = SEED_BASE + 5 if seed is None else seed
+    nh, nk = n // 2, (n * 3) // 10
+    nm = n - nh - nk
+    h = http_workload(2, nh, seed=seed + 11)
+    k = kafka_workload(nk, seed=seed + 13)
+    m = memcache_workload(nm, seed=seed + 17)
+    pol = {"policies": [h.policy["policies"][0], dict(k.policy["policies"][0], name="10.0.0.2"),
+                        m.policy["policies"][0]]}
+    conns = np.concatenate([h.conns, k.conns, m.conns])
+    ch, ck = len(h.conns), len(k.conns)
+    conns["policy"][ch:ch + ck] = 1
+    conns["policy"][ch + ck:] = 2
+    arena = np.concatenate([h.arena, k.arena, m.arena])
+    offs = np.concatenate([h.offsets, k.offsets + np.uint64(len(h.arena)),
+                           m.offsets + np.uint64(len(h.arena) + len(k.arena))])
+    lens = np.concatenate([h.lengths, k.lengths, m.lengths])
+    cids = np.concatenate([h.conn_ids, k.conn_ids + np.uint32(ch), m.conn_ids + np.uint32(ch + ck)])
+    perm = np.random.default_rng(seed).permutation(len(offs))
+    # repack in arrival order, the way a batch packer appends requests
+    buf = arena.tobytes()
+    arena2, offs2, lens2 = pack([buf[int(o):int(o) + int(l)] for o, l in zip(offs[perm], lens[perm])])
+    payload = int(h.lengths.astype(np.int64).sum() + k.lengths.astype(np.int64).sum()) + m.meta["payload_bytes"]
+    return Workload("cfg5", arena2, offs2, lens2, cids[perm], conns, pol, {"payload_bytes": payload})
+
+
+def tile_offsets(w, k):
+    """Request metadata for k back-to-back copies of w's arena (copy j at byte
+    offset j * len(arena)).  The arena itself is replicated on the device, so a
+    100M-request stream needs only the unique part on the host; every copy's
+    verdicts must equal the oracle's verdicts of the unique part."""
+    if k == 1:
+        return w.offsets, w.lengths, w.conn_ids
+    shift = (np.arange(k, dtype=np.uint64) * np.uint64(len(w.arena)))[:, None]
+    offs = (w.offsets[None, :] + shift).reshape(-1)
+    return offs, np.tile(w.lengths, k), np.tile(w.conn_ids, k)

@@ -129,3 +129,16 @@ def test_memcache_port_entries(engine, oracle):
     got, ref = both(engine, oracle, w, 1)
     assert_same(got, ref, w)
     assert set(got[0].tolist()) == {ALLOW, DENY}
+
+
+def test_cfg5_mixed_tiled_parity(engine, oracle):
+    """bench.py's cfg5 stream (gen.mixed_workload, repacked in arrival order) and
+    its tiling: every copy of the arena gets the oracle's verdicts of the unique part."""
+    w = gen.mixed_workload(12000)
+    got1, ref = both(engine, oracle, w)
+    assert_same(got1, ref, w)
+    offs, lens, cids = gen.tile_offsets(w, 3)
+    got = engine.classify(np.tile(w.arena, 3), offs, lens, cids)
+    for g, r in zip(got, ref):
+        assert np.array_equal(np.asarray(g).reshape(3, -1), np.broadcast_to(np.asarray(r).reshape(1, -1), (3, w.n)))
+    assert w.algorithmic_bytes() < int(w.lengths.astype(np.int64).sum()) + 25 * w.n

@@ -35,6 +35,10 @@ for step in "$@"; do
             i=$((i+1))
             run pmc$i 180 rocprofv3 --pmc $ctrs -d "$OUT/pmc$i" -o pmc --output-format csv -- python3 -u bench.py --steps 3 --warmup 1 --no-cpu-baseline
         done ;;
+    bench_cfg*) run $step 900 python -u bench.py --workload ${step#bench_} --steps 10 --warmup 3 ;;
+    prof_cfg*) run $step 900 rocprofv3 --kernel-trace --stats -d "$OUT/$step" -o prof --output-format csv -- python3 -u bench.py --workload ${step#prof_} --steps 10 --warmup 2 --no-cpu-baseline ;;
+    fetch_cfg*) run $step 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/$step" -o pmc --output-format csv -- python3 -u bench.py --workload ${step#fetch_} --steps 3 --warmup 1 --no-cpu-baseline ;;
+    write_cfg*) run $step 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/$step" -o pmc --output-format csv -- python3 -u bench.py --workload ${step#write_} --steps 3 --warmup 1 --no-cpu-baseline ;;
     *) echo "unknown step $step" ;;
     esac
 done
