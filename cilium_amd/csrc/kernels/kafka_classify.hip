@@ -21,11 +21,39 @@ constexpr int kBlock = 256;
 constexpr uint32_t kMaxParseBuf = 6553500;
 constexpr uint32_t kInf = 0xFFFFFFFFu;
 
+// Per-lane byte cursor: the decoders walk their request forward, so each lane
+// keeps the 16-byte aligned chunk it last touched in registers and serves
+// field bytes from it; one dwordx4 load replaces up to 16 byte loads.  A chunk
+// that holds a request byte never leaves that byte's page, so the aligned
+// over-read is safe for any arena alignment.
+struct Cur {
+    uintptr_t line;  // address of the cached chunk (~0 = none)
+    uint32_t w[4];
+};
+__device__ __forceinline__ void cur_fill(Cur &c, uintptr_t a) {
+    const uintptr_t ln = a & ~(uintptr_t)15;
+    if (ln != c.line) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(ln);
+        c.w[0] = v.x; c.w[1] = v.y; c.w[2] = v.z; c.w[3] = v.w;
+        c.line = ln;
+    }
+}
+__device__ __forceinline__ uint32_t cur_word(const Cur &c, uint32_t k) {
+    return k < 8 ? (k < 4 ? c.w[0] : c.w[1]) : (k < 12 ? c.w[2] : c.w[3]);
+}
+__device__ __forceinline__ uint32_t cur_byte(Cur &c, const uint8_t *p) {
+    const uintptr_t a = (uintptr_t)p;
+    cur_fill(c, a);
+    const uint32_t k = (uint32_t)(a & 15);
+    return (cur_word(c, k) >> ((k & 3) * 8)) & 0xFFu;
+}
+
 struct KDec {
     const uint8_t *b;
     uint32_t pos, end;
     int64_t limit;  // LimitReader remaining, -1 = none
     int err;        // 0 ok, 1 EOF, 2 ErrUnexpectedEOF, 3 other
+    Cur *c;
 };
 
 __device__ __forceinline__ uint32_t kavail(const KDec &d) {
@@ -45,16 +73,16 @@ __device__ __forceinline__ uint32_t kread(KDec &d, uint32_t n) {
     if (take < n) d.err = 2;
     return at;
 }
-__device__ __forceinline__ uint64_t be_load(const uint8_t *p, int n) {
+__device__ __forceinline__ uint64_t be_load(Cur &c, const uint8_t *p, int n) {
     uint64_t v = 0;
-    for (int i = 0; i < n; i++) v = (v << 8) | p[i];
+    for (int i = 0; i < n; i++) v = (v << 8) | cur_byte(c, p + i);
     return v;
 }
 __device__ __forceinline__ int64_t dec_int(KDec &d, int n) {
     if (d.err) return 0;
     uint32_t at = kread(d, (uint32_t)n);
     if (d.err) return 0;
-    uint64_t v = be_load(d.b + at, n);
+    uint64_t v = be_load(*d.c, d.b + at, n);
     return n == 1 ? (int64_t)(int8_t)v : n == 2 ? (int64_t)(int16_t)v : n == 4 ? (int64_t)(int32_t)v : (int64_t)v;
 }
 // DecodeString -> (off, len); len < 1 => ""
@@ -83,18 +111,32 @@ __device__ __forceinline__ void dec_bytes(KDec &d) {
     kread(d, (uint32_t)sl);
 }
 
-__device__ uint32_t crc32_ieee(const uint32_t *tab, const uint8_t *p, uint32_t n) {
+// CRC32-IEEE (hash/crc32.ChecksumIEEE), slicing-by-8: tab holds 8 LDS tables
+// of 256 entries; the body advances 8 aligned bytes per step with eight
+// independent table reads, so the serial chain is one step per 8 bytes.
+__device__ __forceinline__ uint32_t crc32_ieee(const uint32_t *tab, Cur &cur, const uint8_t *p, uint32_t n) {
     uint32_t c = 0xFFFFFFFFu;
-    for (uint32_t i = 0; i < n; i++) c = tab[(c ^ p[i]) & 0xFF] ^ (c >> 8);
+    uint32_t i = 0;
+    for (; i < n && (((uintptr_t)(p + i)) & 7); i++) c = tab[(c ^ cur_byte(cur, p + i)) & 0xFF] ^ (c >> 8);
+    for (; i + 8 <= n; i += 8) {
+        const uintptr_t a = (uintptr_t)(p + i);
+        cur_fill(cur, a);
+        const uint32_t k = (uint32_t)(a & 15);
+        const uint32_t lo = (k ? cur.w[2] : cur.w[0]) ^ c, hi = k ? cur.w[3] : cur.w[1];
+        c = tab[7 * 256 + (lo & 0xFF)] ^ tab[6 * 256 + ((lo >> 8) & 0xFF)] ^ tab[5 * 256 + ((lo >> 16) & 0xFF)] ^
+            tab[4 * 256 + (lo >> 24)] ^ tab[3 * 256 + (hi & 0xFF)] ^ tab[2 * 256 + ((hi >> 8) & 0xFF)] ^
+            tab[1 * 256 + ((hi >> 16) & 0xFF)] ^ tab[hi >> 24];
+    }
+    for (; i < n; i++) c = tab[(c ^ cur_byte(cur, p + i)) & 0xFF] ^ (c >> 8);
     return ~c;
 }
 
 // readMessageSet on the shared position; 0 ok, -1 error, -2 compressed
-__device__ int read_message_set(const uint8_t *b, uint32_t &pos, uint32_t end, int32_t size, int16_t version,
-                                const uint32_t *crctab) {
+__device__ __forceinline__ int read_message_set(Cur &cur, const uint8_t *b, uint32_t &pos, uint32_t end, int32_t size,
+                                int16_t version, const uint32_t *crctab) {
     if (size < 0) return 0;
     if ((uint32_t)size > kMaxParseBuf) return -1;
-    KDec dec{b, pos, end, size, 0};
+    KDec dec{b, pos, end, size, 0, &cur};
     int rc = 0;
     for (;;) {
         (void)dec_int(dec, 8);
@@ -104,10 +146,10 @@ __device__ int read_message_set(const uint8_t *b, uint32_t &pos, uint32_t end, i
         if ((uint32_t)msize > kMaxParseBuf) { rc = -1; break; }
         uint32_t at = kread(dec, (uint32_t)msize);
         if (dec.err) break;
-        KDec md{b, at, at + (uint32_t)msize, -1, 0};
+        KDec md{b, at, at + (uint32_t)msize, -1, 0, &cur};
         uint32_t crc = (uint32_t)dec_int(md, 4);
         if (msize <= 4) break;
-        if (crc != crc32_ieee(crctab, b + at + 4, (uint32_t)msize - 4)) break;  // stop, no drain
+        if (crc != crc32_ieee(crctab, cur, b + at + 4, (uint32_t)msize - 4)) break;  // stop, no drain
         (void)dec_int(md, 1);
         int8_t attr = (int8_t)dec_int(md, 1);
         if (version >= 1) (void)dec_int(md, 8);
@@ -122,16 +164,16 @@ __device__ int read_message_set(const uint8_t *b, uint32_t &pos, uint32_t end, i
     return rc;
 }
 
-__device__ int32_t str_lookup(const DevStrSlot *tab, uint32_t mask, const uint8_t *strings, const uint8_t *s,
-                              uint32_t n) {
+__device__ __forceinline__ int32_t str_lookup(const DevStrSlot *tab, uint32_t mask, const uint8_t *strings, Cur &cur,
+                              const uint8_t *s, uint32_t n) {
     uint32_t h = kFnvBasis;
-    for (uint32_t i = 0; i < n; i++) h = (h ^ s[i]) * 16777619u;
+    for (uint32_t i = 0; i < n; i++) h = (h ^ cur_byte(cur, s + i)) * 16777619u;
     for (uint32_t slot = h & mask;; slot = (slot + 1) & mask) {
         const DevStrSlot e = tab[slot];
         if (!e.used) return -1;
         if (e.hash == h && e.len == n) {
             bool eq = true;
-            for (uint32_t i = 0; i < n && eq; i++) eq = strings[e.str_off + i] == s[i];
+            for (uint32_t i = 0; i < n && eq; i++) eq = strings[e.str_off + i] == cur_byte(cur, s + i);
             if (eq) return e.id;
         }
     }
@@ -163,7 +205,7 @@ __device__ __forceinline__ bool rule_matches(const DevKafkaRule &r, const ReqInf
 }
 
 // first position of topic `tid`'s rule list that matches, kInf if none
-__device__ uint32_t topic_first(const KafkaTables &T, const DevKafkaRuleset &rs, const ReqInfo &q, int32_t tid) {
+__device__ __forceinline__ uint32_t topic_first(const KafkaTables &T, const DevKafkaRuleset &rs, const ReqInfo &q, int32_t tid) {
     if (tid < 0 || rs.ntopics == 0) return kInf;
     const uint32_t *dir = T.index + rs.topics_off;
     uint32_t lo = 0, hi = rs.ntopics;
@@ -187,13 +229,22 @@ __global__ __launch_bounds__(kBlock) void kafka_classify_kernel(
     const uint32_t *__restrict__ conn_ids, uint32_t n, const DevConn *__restrict__ conns, uint32_t nconns,
     KafkaTables T, uint8_t *__restrict__ out_verdict, int32_t *__restrict__ out_rule, uint32_t *__restrict__ out_consumed,
     uint64_t *__restrict__ counters, uint32_t ncounters) {
-    __shared__ uint32_t crctab[256];
-    for (uint32_t i = threadIdx.x; i < 256; i += kBlock) {
-        uint32_t c = i;
+    static_assert(kBlock == 256, "one CRC table entry per thread");
+    __shared__ uint32_t crctab[8 * 256];
+    __shared__ uint32_t s_verdicts[8];
+    {
+        const uint32_t t = threadIdx.x;
+        uint32_t c = t;
         for (int k = 0; k < 8; k++) c = (c & 1) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
-        crctab[i] = c;
+        crctab[t] = c;
+        if (t < 8) s_verdicts[t] = 0;
+        __syncthreads();
+        for (int k = 1; k < 8; k++) {
+            const uint32_t prev = crctab[(k - 1) * 256 + t];
+            crctab[k * 256 + t] = (prev >> 8) ^ crctab[prev & 0xFF];
+            __syncthreads();
+        }
     }
-    __syncthreads();
     for (uint32_t idx = blockIdx.x * kBlock + threadIdx.x; idx < n; idx += gridDim.x * kBlock) {
         const uint32_t ci = conn_ids[idx];
         if (ci >= nconns) continue;
@@ -201,13 +252,15 @@ __global__ __launch_bounds__(kBlock) void kafka_classify_kernel(
         if (conn.proto != PROTO_KAFKA) continue;
         const uint8_t *b = arena + offs[idx];
         const uint32_t len = lens[idx];
+        Cur cur;
+        cur.line = ~(uintptr_t)0;
         uint8_t verdict = V_PARSE_ERROR;
         int32_t rule = -1;
         uint32_t consumed = 0;
         // ---- proto.ReadReq
         do {
             if (len < 4) { verdict = V_INCOMPLETE; break; }
-            const int32_t size = (int32_t)be_load(b, 4);
+            const int32_t size = (int32_t)be_load(cur, b, 4);
             if (size <= 0) { verdict = V_PARSE_ERROR; break; }
             if (len < 6) { verdict = V_INCOMPLETE; break; }
             if ((uint64_t)(uint32_t)size + 4 > kMaxParseBuf) { verdict = V_PARSE_ERROR; break; }
@@ -215,8 +268,8 @@ __global__ __launch_bounds__(kBlock) void kafka_classify_kernel(
             if (rawlen > len) { verdict = V_INCOMPLETE; break; }
             if (rawlen < 12) { verdict = V_PARSE_ERROR; break; }
             ReqInfo q;
-            q.kind = (int16_t)be_load(b + 4, 2);
-            q.version = (int16_t)be_load(b + 6, 2);
+            q.kind = (int16_t)be_load(cur, b + 4, 2);
+            q.version = (int16_t)be_load(cur, b + 6, 2);
             q.typed = (q.kind == 0 || q.kind == 1 || q.kind == 2 || q.kind == 3 || q.kind == 8 || q.kind == 9) ? 1
                     : (q.kind == 10 ? 2 : 0);
             q.client = -2;
@@ -224,20 +277,20 @@ __global__ __launch_bounds__(kBlock) void kafka_classify_kernel(
             uint32_t ntopics = 0, cmax = 0;  // raw topic count; max over topics of first matching rule
             int rc = 0;
             if (q.typed) {
-                KDec d{b, 0, rawlen, -1, 0};
+                KDec d{b, 0, rawlen, -1, 0, &cur};
                 bool bad = false;
                 (void)dec_int(d, 4); (void)dec_int(d, 2);
                 const int16_t ver = (int16_t)dec_int(d, 2);
                 (void)dec_int(d, 4);
                 uint32_t co, cl;
                 dec_string(d, co, cl);
-                if (!d.err && cl > 0) q.client = str_lookup(T.client_hash, T.client_mask, T.strings, b + co, cl);
+                if (!d.err && cl > 0) q.client = str_lookup(T.client_hash, T.client_mask, T.strings, cur, b + co, cl);
                 if (q.client < 0) q.client = -2;
                 const bool topics_on = q.typed == 1;
                 auto on_topic = [&](uint32_t to, uint32_t tl) {
                     if (!topics_on) return;
                     ntopics++;
-                    int32_t tid = tl > 0 ? str_lookup(T.topic_hash, T.topic_mask, T.strings, b + to, tl) : -1;
+                    int32_t tid = tl > 0 ? str_lookup(T.topic_hash, T.topic_mask, T.strings, cur, b + to, tl) : -1;
                     uint32_t e = topic_first(T, rs, q, tid);
                     cmax = cmax > e ? cmax : e;
                 };
@@ -260,7 +313,7 @@ __global__ __launch_bounds__(kBlock) void kafka_classify_kernel(
                             if (d.err) { rc = -1; break; }
                             const int32_t ss = (int32_t)dec_int(d, 4);
                             if (d.err) { rc = -1; break; }
-                            rc = read_message_set(b, d.pos, d.end, ss, ver, crctab);
+                            rc = read_message_set(cur, b, d.pos, d.end, ss, ver, crctab);
                             if (rc) break;
                         }
                     }
@@ -371,9 +424,14 @@ __global__ __launch_bounds__(kBlock) void kafka_classify_kernel(
         out_rule[idx] = rule;
         out_consumed[idx] = consumed;
         if (counters) {
-            atomicAdd((unsigned long long *)&counters[ncounters - 8 + verdict], 1ull);
+            atomicAdd(&s_verdicts[verdict], 1u);  // per-verdict totals: one global atomic per block
             if (rule >= 0 && (uint32_t)rule < ncounters - 8) atomicAdd((unsigned long long *)&counters[rule], 1ull);
         }
+    }
+    if (counters) {
+        __syncthreads();
+        if (threadIdx.x < 8 && s_verdicts[threadIdx.x])
+            atomicAdd((unsigned long long *)&counters[ncounters - 8 + threadIdx.x], (unsigned long long)s_verdicts[threadIdx.x]);
     }
 }
 

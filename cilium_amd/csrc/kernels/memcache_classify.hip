@@ -175,6 +175,9 @@ __global__ __launch_bounds__(kBlock) void memcache_classify_kernel(
     const uint32_t *__restrict__ conn_ids, uint32_t n, const DevConn *__restrict__ conns, uint32_t nconns,
     McTables T, uint8_t *__restrict__ out_verdict, int32_t *__restrict__ out_rule, uint32_t *__restrict__ out_consumed,
     uint64_t *__restrict__ counters, uint32_t ncounters) {
+    __shared__ uint32_t s_verdicts[8];
+    if (threadIdx.x < 8) s_verdicts[threadIdx.x] = 0;
+    __syncthreads();
     for (uint32_t idx = blockIdx.x * kBlock + threadIdx.x; idx < n; idx += gridDim.x * kBlock) {
         const uint32_t ci = conn_ids[idx];
         if (ci >= nconns) continue;
@@ -324,9 +327,14 @@ __global__ __launch_bounds__(kBlock) void memcache_classify_kernel(
         out_rule[idx] = rule;
         out_consumed[idx] = consumed;
         if (counters) {
-            atomicAdd((unsigned long long *)&counters[ncounters - 8 + verdict], 1ull);
+            atomicAdd(&s_verdicts[verdict], 1u);  // per-verdict totals: one global atomic per block
             if (rule >= 0 && (uint32_t)rule < ncounters - 8) atomicAdd((unsigned long long *)&counters[rule], 1ull);
         }
+    }
+    if (counters) {
+        __syncthreads();
+        if (threadIdx.x < 8 && s_verdicts[threadIdx.x])
+            atomicAdd((unsigned long long *)&counters[ncounters - 8 + threadIdx.x], (unsigned long long)s_verdicts[threadIdx.x]);
     }
 }
 

@@ -21,6 +21,7 @@ run() {  # run <name> <seconds> <cmd...>
 for step in "$@"; do
     case $step in
     smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
+    ktests) run ktests 400 python -u -m pytest tests/test_gpu_kafka.py tests/test_gpu_memcache.py tests/test_gpu_proxylib.py -m gpu -v --timeout 120 --timeout-method thread ;;
     mctests) run mctests 400 python -u -m pytest tests/test_gpu_memcache.py -m gpu -v --timeout 120 --timeout-method thread ;;
     tests) run tests 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
     testsall) run testsall 900 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread ;;
