@@ -24,11 +24,14 @@ hipError_t LaunchHttpClassify(const uint8_t *arena, uint64_t arena_len, const ui
 hipError_t LaunchKafkaClassify(const uint8_t *arena, const uint64_t *offs, const uint32_t *lens, const uint32_t *conn_ids,
                                uint32_t n, const DevConn *conns, uint32_t nconns, const KafkaTables &T,
                                uint8_t *verdict, int32_t *rule, uint32_t *consumed, uint64_t *counters,
-                               uint32_t ncounters, hipStream_t stream);
+                               uint32_t ncounters, const uint32_t *sel, const uint32_t *sel_count, hipStream_t stream);
 hipError_t LaunchMemcacheClassify(const uint8_t *arena, const uint64_t *offs, const uint32_t *lens,
                                   const uint32_t *conn_ids, uint32_t n, const DevConn *conns, uint32_t nconns,
                                   const McTables &T, uint8_t *verdict, int32_t *rule, uint32_t *consumed,
-                                  uint64_t *counters, uint32_t ncounters, hipStream_t stream);
+                                  uint64_t *counters, uint32_t ncounters, const uint32_t *sel, const uint32_t *sel_count,
+                                  hipStream_t stream);
+hipError_t LaunchPartition(const uint32_t *conn_ids, uint32_t n, const DevConn *conns, uint32_t nconns,
+                           uint32_t *sel_kafka, uint32_t *sel_mc, uint32_t *counts, hipStream_t stream);
 hipError_t HttpPhaseTimes(uint64_t *out, bool reset);
 }  // namespace l7
 
@@ -59,6 +62,11 @@ struct l7g_engine {
     uint8_t *s_arena = nullptr, *s_req = nullptr;
     size_t s_arena_cap = 0, s_n_cap = 0;
     bool any_cold = false;     // some HTTP connection uses another rule set
+    // mixed-batch protocol split (grow-only, stream-ordered): [counts(2) | kafka idx | memcached idx]
+    uint32_t *d_sel = nullptr;
+    size_t sel_cap = 0;
+    hipStream_t sel_stream = nullptr;
+    bool sel_used = false;
 };
 
 static void set_err(char *err, size_t errlen, const std::string &m) {
@@ -227,6 +235,7 @@ void l7g_engine_destroy(l7g_engine *e) {
     hipDeviceSynchronize();
     if (e->d_blob) hipFree(e->d_blob);
     if (e->d_conns) hipFree(e->d_conns);
+    if (e->d_sel) hipFree(e->d_sel);
     if (e->s_arena) hipFree(e->s_arena);
     if (e->s_req) hipFree(e->s_req);
     if (e->sstream) hipStreamDestroy(e->sstream);
@@ -316,17 +325,39 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
     hipStream_t s = (hipStream_t)stream;
     const uint32_t ncounters = counters ? (uint32_t)e->ps->nrules + 8 : 0;
     // The kernels each classify only their own protocol's requests and skip
-    // the rest, so a mixed batch needs one launch per protocol present.
-    if (e->has_http || (!e->has_kafka && !e->has_mc))
-        rc = LaunchHttpClassify(arena, arena_len, off, len, conn, n, e->d_conns, (uint32_t)e->conns.size(), e->ht, e->any_cold,
+    // the rest, so a mixed batch needs one launch per protocol present.  With
+    // more than one protocol the Kafka and memcached kernels walk index lists
+    // written by partition_kernel instead of the whole batch.
+    const uint32_t nconns = (uint32_t)e->conns.size();
+    const bool mixed = (int)e->has_http + (int)e->has_kafka + (int)e->has_mc > 1;
+    uint32_t *sel_k = nullptr, *sel_m = nullptr, *cnt = nullptr;
+    if (mixed && n > 0) {
+        const size_t need = 2 + 2 * (size_t)n;
+        if (e->sel_used && e->sel_stream != s) rc = hipStreamSynchronize(e->sel_stream);  // scratch reuse across streams
+        if (rc == hipSuccess && need > e->sel_cap) {
+            if (e->d_sel) { hipDeviceSynchronize(); hipFree(e->d_sel); e->d_sel = nullptr; e->sel_cap = 0; }
+            rc = hipMalloc(&e->d_sel, need * sizeof(uint32_t));
+            if (rc == hipSuccess) e->sel_cap = need;
+        }
+        if (rc != hipSuccess) return (int)rc;
+        cnt = e->d_sel;
+        sel_k = e->d_sel + 2;
+        sel_m = sel_k + n;
+        e->sel_stream = s;
+        e->sel_used = true;
+        rc = hipMemsetAsync(cnt, 0, 2 * sizeof(uint32_t), s);
+        if (rc == hipSuccess) rc = LaunchPartition(conn, n, e->d_conns, nconns, sel_k, sel_m, cnt, s);
+    }
+    if (rc == hipSuccess && (e->has_http || (!e->has_kafka && !e->has_mc)))
+        rc = LaunchHttpClassify(arena, arena_len, off, len, conn, n, e->d_conns, nconns, e->ht, e->any_cold,
                                 verdict, rule,
                                 consumed, counters, ncounters, s);
     if (rc == hipSuccess && e->has_kafka)
-        rc = LaunchKafkaClassify(arena, off, len, conn, n, e->d_conns, (uint32_t)e->conns.size(), e->kt, verdict, rule,
-                                 consumed, counters, ncounters, s);
+        rc = LaunchKafkaClassify(arena, off, len, conn, n, e->d_conns, nconns, e->kt, verdict, rule,
+                                 consumed, counters, ncounters, sel_k, cnt, s);
     if (rc == hipSuccess && e->has_mc)
-        rc = LaunchMemcacheClassify(arena, off, len, conn, n, e->d_conns, (uint32_t)e->conns.size(), e->mt, verdict,
-                                    rule, consumed, counters, ncounters, s);
+        rc = LaunchMemcacheClassify(arena, off, len, conn, n, e->d_conns, nconns, e->mt, verdict,
+                                    rule, consumed, counters, ncounters, sel_m, cnt ? cnt + 1 : nullptr, s);
     return (int)rc;
 }
 

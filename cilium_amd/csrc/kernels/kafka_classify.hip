@@ -228,7 +228,8 @@ __global__ __launch_bounds__(kBlock) void kafka_classify_kernel(
     const uint8_t *__restrict__ arena, const uint64_t *__restrict__ offs, const uint32_t *__restrict__ lens,
     const uint32_t *__restrict__ conn_ids, uint32_t n, const DevConn *__restrict__ conns, uint32_t nconns,
     KafkaTables T, uint8_t *__restrict__ out_verdict, int32_t *__restrict__ out_rule, uint32_t *__restrict__ out_consumed,
-    uint64_t *__restrict__ counters, uint32_t ncounters) {
+    uint64_t *__restrict__ counters, uint32_t ncounters, const uint32_t *__restrict__ sel,
+    const uint32_t *__restrict__ sel_count) {
     static_assert(kBlock == 256, "one CRC table entry per thread");
     __shared__ uint32_t crctab[8 * 256];
     __shared__ uint32_t s_verdicts[8];
@@ -245,7 +246,10 @@ __global__ __launch_bounds__(kBlock) void kafka_classify_kernel(
             __syncthreads();
         }
     }
-    for (uint32_t idx = blockIdx.x * kBlock + threadIdx.x; idx < n; idx += gridDim.x * kBlock) {
+    // sel: this protocol's request indices from partition_kernel (mixed batches), else all n
+    const uint32_t m = sel ? *sel_count : n;
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < m; i += gridDim.x * kBlock) {
+        const uint32_t idx = sel ? sel[i] : i;
         const uint32_t ci = conn_ids[idx];
         if (ci >= nconns) continue;
         const DevConn conn = conns[ci];
@@ -438,12 +442,12 @@ __global__ __launch_bounds__(kBlock) void kafka_classify_kernel(
 hipError_t LaunchKafkaClassify(const uint8_t *arena, const uint64_t *offs, const uint32_t *lens, const uint32_t *conn_ids,
                                uint32_t n, const DevConn *conns, uint32_t nconns, const KafkaTables &T,
                                uint8_t *verdict, int32_t *rule, uint32_t *consumed, uint64_t *counters,
-                               uint32_t ncounters, hipStream_t stream) {
+                               uint32_t ncounters, const uint32_t *sel, const uint32_t *sel_count, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     uint32_t blocks = (n + kBlock - 1) / kBlock;
     if (blocks > 8192) blocks = 8192;
     hipLaunchKernelGGL(kafka_classify_kernel, dim3(blocks), dim3(kBlock), 0, stream, arena, offs, lens, conn_ids, n,
-                       conns, nconns, T, verdict, rule, consumed, counters, ncounters);
+                       conns, nconns, T, verdict, rule, consumed, counters, ncounters, sel, sel_count);
     return hipGetLastError();
 }
 
