@@ -113,11 +113,13 @@ struct DevKafkaRule {      // 24 B
     uint8_t has_topic;
     uint8_t pad[3];
 };
-struct DevKafkaRuleset {   // 32 B
+struct DevKafkaRuleset {   // 36 B
     uint32_t rule_first, nrules;     // rules in evaluation order
     uint32_t topicless_off, ntopicless;  // u32 rule positions (Topic == "") in index[]
     uint32_t topics_off, ntopics;    // sorted (topic_id, list_off, list_cnt) triples in index[]
     uint32_t bykey_off;              // 65 (off, cnt) pairs in index[]: key 0..63, 64 = other kinds
+    uint32_t tdense_off;             // (list_off, list_cnt) per interned topic id in index[]; ~0u = use the
+                                     // sorted directory (rule set x topic count over the dense budget)
     uint8_t any;                     // rules.Kafka != nil (pkg/proxy/kafka.go:139-142)
     uint8_t pad[3];
 };

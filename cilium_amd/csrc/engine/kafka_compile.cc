@@ -77,6 +77,8 @@ int KafkaCompiler::RulesetFor(int policy, bool ingress, uint32_t port, uint64_t 
     return id;
 }
 
+static constexpr size_t kDenseTopicBudget = size_t(64) << 20;  // u32 entries in index[] (256 MiB)
+
 int KafkaCompiler::Compile(const std::vector<const KafkaRule *> &rules, bool any) {
     KafkaImage &I = img_;
     DevKafkaRuleset rs{};
@@ -117,6 +119,18 @@ int KafkaCompiler::Compile(const std::vector<const KafkaRule *> &rules, bool any
     rs.topics_off = (uint32_t)I.index.size();
     rs.ntopics = (uint32_t)by_topic.size();
     I.index.insert(I.index.end(), dir.begin(), dir.end());
+    // Dense (off, cnt) per interned topic id: one lookup instead of a binary
+    // search per request topic.  Bounded so many rule sets over many topics
+    // keep to the sorted directory.
+    rs.tdense_off = ~0u;
+    if (!by_topic.empty() && I.index.size() + 2 * I.ntopics <= kDenseTopicBudget) {
+        rs.tdense_off = (uint32_t)I.index.size();
+        I.index.resize(I.index.size() + 2 * I.ntopics, 0);
+        for (size_t t = 0; t < dir.size(); t += 3) {
+            I.index[rs.tdense_off + 2 * dir[t]] = dir[t + 1];
+            I.index[rs.tdense_off + 2 * dir[t] + 1] = dir[t + 2];
+        }
+    }
     std::vector<uint32_t> keydir;
     for (auto &l : bykey) {
         keydir.push_back((uint32_t)I.index.size() + 0);  // patched below

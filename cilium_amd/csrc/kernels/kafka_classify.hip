@@ -117,7 +117,24 @@ __device__ __forceinline__ void dec_bytes(KDec &d) {
 __device__ __forceinline__ uint32_t crc32_ieee(const uint32_t *tab, Cur &cur, const uint8_t *p, uint32_t n) {
     uint32_t c = 0xFFFFFFFFu;
     uint32_t i = 0;
-    for (; i < n && (((uintptr_t)(p + i)) & 7); i++) c = tab[(c ^ cur_byte(cur, p + i)) & 0xFF] ^ (c >> 8);
+    for (; i < n && (((uintptr_t)(p + i)) & 15); i++) c = tab[(c ^ cur_byte(cur, p + i)) & 0xFF] ^ (c >> 8);
+    // Bulk: 128 aligned bytes per batch, eight dwordx4 loads issued together so
+    // one memory latency covers 16 slicing steps (a lane walks its message
+    // alone; back-to-back dependent loads were the kernel's critical path).
+    for (; i + 128 <= n; i += 128) {
+        const uint4 *q = reinterpret_cast<const uint4 *>(p + i);
+        uint4 v[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) v[j] = q[j];
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            const uint4 &x = v[j >> 1];
+            const uint32_t lo = ((j & 1) ? x.z : x.x) ^ c, hi = (j & 1) ? x.w : x.y;
+            c = tab[7 * 256 + (lo & 0xFF)] ^ tab[6 * 256 + ((lo >> 8) & 0xFF)] ^ tab[5 * 256 + ((lo >> 16) & 0xFF)] ^
+                tab[4 * 256 + (lo >> 24)] ^ tab[3 * 256 + (hi & 0xFF)] ^ tab[2 * 256 + ((hi >> 8) & 0xFF)] ^
+                tab[1 * 256 + ((hi >> 16) & 0xFF)] ^ tab[hi >> 24];
+        }
+    }
     for (; i + 8 <= n; i += 8) {
         const uintptr_t a = (uintptr_t)(p + i);
         cur_fill(cur, a);
@@ -173,7 +190,9 @@ __device__ __forceinline__ int32_t str_lookup(const DevStrSlot *tab, uint32_t ma
         if (!e.used) return -1;
         if (e.hash == h && e.len == n) {
             bool eq = true;
-            for (uint32_t i = 0; i < n && eq; i++) eq = strings[e.str_off + i] == cur_byte(cur, s + i);
+            Cur tc;
+            tc.line = ~(uintptr_t)0;
+            for (uint32_t i = 0; i < n && eq; i++) eq = cur_byte(tc, strings + e.str_off + i) == cur_byte(cur, s + i);
             if (eq) return e.id;
         }
     }
@@ -207,14 +226,22 @@ __device__ __forceinline__ bool rule_matches(const DevKafkaRule &r, const ReqInf
 // first position of topic `tid`'s rule list that matches, kInf if none
 __device__ __forceinline__ uint32_t topic_first(const KafkaTables &T, const DevKafkaRuleset &rs, const ReqInfo &q, int32_t tid) {
     if (tid < 0 || rs.ntopics == 0) return kInf;
-    const uint32_t *dir = T.index + rs.topics_off;
-    uint32_t lo = 0, hi = rs.ntopics;
-    while (lo < hi) {
-        uint32_t m = (lo + hi) >> 1;
-        if (dir[3 * m] < (uint32_t)tid) lo = m + 1; else hi = m;
+    uint32_t off, cnt;
+    if (rs.tdense_off != ~0u) {
+        const uint2 e = *reinterpret_cast<const uint2 *>(T.index + rs.tdense_off + 2 * (uint32_t)tid);
+        off = e.x;
+        cnt = e.y;
+    } else {
+        const uint32_t *dir = T.index + rs.topics_off;
+        uint32_t lo = 0, hi = rs.ntopics;
+        while (lo < hi) {
+            uint32_t m = (lo + hi) >> 1;
+            if (dir[3 * m] < (uint32_t)tid) lo = m + 1; else hi = m;
+        }
+        if (lo >= rs.ntopics || dir[3 * lo] != (uint32_t)tid) return kInf;
+        off = dir[3 * lo + 1];
+        cnt = dir[3 * lo + 2];
     }
-    if (lo >= rs.ntopics || dir[3 * lo] != (uint32_t)tid) return kInf;
-    const uint32_t off = dir[3 * lo + 1], cnt = dir[3 * lo + 2];
     for (uint32_t i = 0; i < cnt; i++) {
         uint32_t p = T.index[off + i];
         if (rule_matches(T.rules[rs.rule_first + p], q)) return p;

@@ -38,6 +38,14 @@ for step in "$@"; do
         done ;;
     bench_cfg*) run $step 900 python -u bench.py --workload ${step#bench_} --steps 10 --warmup 3 ;;
     prof_cfg*) run $step 900 rocprofv3 --kernel-trace --stats -d "$OUT/$step" -o prof --output-format csv -- python3 -u bench.py --workload ${step#prof_} --steps 10 --warmup 2 --no-cpu-baseline ;;
+    pmc_cfg*)
+        wl=${step#pmc_}; i=0
+        for ctrs in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY" \
+                    "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE SQ_WAIT_INST_LDS SQ_INST_CYCLES_VMEM" \
+                    "FETCH_SIZE" "WRITE_SIZE"; do
+            i=$((i+1))
+            run ${step}_$i 180 rocprofv3 --pmc $ctrs -d "$OUT/${step}_$i" -o pmc --output-format csv -- python3 -u bench.py --workload $wl --steps 3 --warmup 1 --no-cpu-baseline
+        done ;;
     fetch_cfg*) run $step 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/$step" -o pmc --output-format csv -- python3 -u bench.py --workload ${step#fetch_} --steps 3 --warmup 1 --no-cpu-baseline ;;
     write_cfg*) run $step 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/$step" -o pmc --output-format csv -- python3 -u bench.py --workload ${step#write_} --steps 3 --warmup 1 --no-cpu-baseline ;;
     *) echo "unknown step $step" ;;
