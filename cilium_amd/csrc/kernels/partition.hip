@@ -5,7 +5,10 @@
 // stream (cfg5) most of their lanes would only discover "not my protocol" and
 // idle while the others decode.  This kernel writes, for each of those two
 // protocols, the list of request indices that belong to it; the classifiers
-// then walk only their own list.  One block owns 4096 consecutive requests
+// then walk only their own list.  Kafka requests are further grouped by length
+// class, so a wave of the one-lane-per-request Kafka kernel holds requests of
+// similar size and no longer waits on one long produce request among short
+// fetches (a wave runs as long as its longest lane).  One block owns 4096 consecutive requests
 // (16 per lane, protocol kept in registers between the count and the write
 // pass) and takes its slot range with one atomic per protocol.
 #include <hip/hip_runtime.h>
@@ -18,63 +21,84 @@ namespace {
 constexpr int kBlock = 256;
 constexpr int kPer = 16;
 constexpr int kWaves = kBlock / 64;
+// list classes: 0..3 Kafka by request length (< 256 B, < 1 KiB, < 4 KiB, larger), 4 memcached
+constexpr int kClasses = 5;
+
+__device__ __forceinline__ uint8_t kafka_class(uint32_t len) {
+    return len < 256 ? 0 : len < 1024 ? 1 : len < 4096 ? 2 : 3;
+}
 }  // namespace
 
-__global__ __launch_bounds__(kBlock) void partition_kernel(const uint32_t *__restrict__ conn_ids, uint32_t n,
+// Lists: class c < 4 at sel_kafka + c * n, class 4 at sel_mc; counts[c] entries each.
+__global__ __launch_bounds__(kBlock) void partition_kernel(const uint32_t *__restrict__ conn_ids,
+                                                           const uint32_t *__restrict__ lens, uint32_t n,
                                                            const DevConn *__restrict__ conns, uint32_t nconns,
                                                            uint32_t *__restrict__ sel_kafka,
                                                            uint32_t *__restrict__ sel_mc,
                                                            uint32_t *__restrict__ counts) {
-    __shared__ uint32_t s_off[kWaves][2];
+    __shared__ uint32_t s_off[kWaves][kClasses];
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint64_t start = (uint64_t)blockIdx.x * (kBlock * kPer);
     const uint64_t below = (1ull << lane) - 1;
-    uint8_t p[kPer];
-    uint32_t ck = 0, cm = 0;
+    uint8_t p[kPer];  // class + 1, 0 = none
+    uint32_t cnt[kClasses] = {};
 #pragma unroll
     for (int r = 0; r < kPer; r++) {
         const uint64_t idx = start + (uint64_t)r * kBlock + threadIdx.x;
-        uint8_t proto = 0;
+        uint8_t cls = 0;
         if (idx < n) {
             const uint32_t ci = conn_ids[idx];
-            if (ci < nconns) proto = conns[ci].proto;
+            if (ci < nconns) {
+                const uint8_t proto = conns[ci].proto;
+                if (proto == PROTO_KAFKA) cls = 1 + kafka_class(lens[idx]);
+                else if (proto == PROTO_MEMCACHE) cls = 1 + 4;
+            }
         }
-        p[r] = proto;
-        ck += __popcll(__ballot(proto == PROTO_KAFKA));
-        cm += __popcll(__ballot(proto == PROTO_MEMCACHE));
+        p[r] = cls;
+#pragma unroll
+        for (int c = 0; c < kClasses; c++) cnt[c] += __popcll(__ballot(cls == c + 1));
     }
-    if (lane == 0) { s_off[wave][0] = ck; s_off[wave][1] = cm; }
+    if (lane == 0)
+        for (int c = 0; c < kClasses; c++) s_off[wave][c] = cnt[c];
     __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t tk = 0, tm = 0;
-        for (int w = 0; w < kWaves; w++) { tk += s_off[w][0]; tm += s_off[w][1]; }
-        uint32_t bk = tk ? atomicAdd(&counts[0], tk) : 0, bm = tm ? atomicAdd(&counts[1], tm) : 0;
+    if (threadIdx.x < kClasses) {
+        const int c = threadIdx.x;
+        uint32_t t = 0;
+        for (int w = 0; w < kWaves; w++) t += s_off[w][c];
+        uint32_t b = t ? atomicAdd(&counts[c], t) : 0;
         for (int w = 0; w < kWaves; w++) {
-            const uint32_t a = s_off[w][0], b = s_off[w][1];
-            s_off[w][0] = bk; s_off[w][1] = bm;
-            bk += a; bm += b;
+            const uint32_t a = s_off[w][c];
+            s_off[w][c] = b;
+            b += a;
         }
     }
     __syncthreads();
-    uint32_t ok = s_off[wave][0], om = s_off[wave][1];
+    uint32_t off[kClasses];
+#pragma unroll
+    for (int c = 0; c < kClasses; c++) off[c] = s_off[wave][c];
 #pragma unroll
     for (int r = 0; r < kPer; r++) {
         const uint32_t idx = (uint32_t)(start + (uint64_t)r * kBlock + threadIdx.x);
-        const uint64_t mk = __ballot(p[r] == PROTO_KAFKA), mm = __ballot(p[r] == PROTO_MEMCACHE);
-        if (p[r] == PROTO_KAFKA) sel_kafka[ok + __popcll(mk & below)] = idx;
-        if (p[r] == PROTO_MEMCACHE) sel_mc[om + __popcll(mm & below)] = idx;
-        ok += __popcll(mk);
-        om += __popcll(mm);
+#pragma unroll
+        for (int c = 0; c < kClasses; c++) {
+            const uint64_t mk = __ballot(p[r] == c + 1);
+            if (p[r] == c + 1) {
+                uint32_t *dst = c < 4 ? sel_kafka + (size_t)c * n : sel_mc;
+                dst[off[c] + __popcll(mk & below)] = idx;
+            }
+            off[c] += __popcll(mk);
+        }
     }
 }
 
-// counts[0..1] must be zero on entry (the caller clears them on `stream`).
-hipError_t LaunchPartition(const uint32_t *conn_ids, uint32_t n, const DevConn *conns, uint32_t nconns,
-                           uint32_t *sel_kafka, uint32_t *sel_mc, uint32_t *counts, hipStream_t stream) {
+// counts[0..4] must be zero on entry (the caller clears them on `stream`).
+hipError_t LaunchPartition(const uint32_t *conn_ids, const uint32_t *lens, uint32_t n, const DevConn *conns,
+                           uint32_t nconns, uint32_t *sel_kafka, uint32_t *sel_mc, uint32_t *counts,
+                           hipStream_t stream) {
     if (n == 0) return hipSuccess;
     const uint32_t blocks = (uint32_t)(((uint64_t)n + kBlock * kPer - 1) / (kBlock * kPer));
-    hipLaunchKernelGGL(partition_kernel, dim3(blocks), dim3(kBlock), 0, stream, conn_ids, n, conns, nconns, sel_kafka,
-                       sel_mc, counts);
+    hipLaunchKernelGGL(partition_kernel, dim3(blocks), dim3(kBlock), 0, stream, conn_ids, lens, n, conns, nconns,
+                       sel_kafka, sel_mc, counts);
     return hipGetLastError();
 }
 
