@@ -63,7 +63,7 @@ struct l7g_engine {
     uint8_t *s_arena = nullptr, *s_req = nullptr;
     size_t s_arena_cap = 0, s_n_cap = 0;
     bool any_cold = false;     // some HTTP connection uses another rule set
-    // protocol split (grow-only, stream-ordered): [counts(8) | 4 x n Kafka idx | n memcached idx]
+    // protocol split (grow-only, stream-ordered): [counts(16) | L7_KAFKA_CLASSES x n Kafka idx | n memcached idx]
     uint32_t *d_sel = nullptr;
     size_t sel_cap = 0;
     hipStream_t sel_stream = nullptr;
@@ -331,11 +331,11 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
     // written by partition_kernel instead of the whole batch.
     const uint32_t nconns = (uint32_t)e->conns.size();
     // Kafka batches always go through the split: it also groups Kafka requests
-    // into four length classes (one list of up to n entries each).
+    // into L7_KAFKA_CLASSES length classes (one list of up to n entries each).
     const bool mixed = (int)e->has_http + (int)e->has_kafka + (int)e->has_mc > 1;
     uint32_t *sel_k = nullptr, *sel_m = nullptr, *cnt = nullptr;
     if ((mixed || e->has_kafka) && n > 0) {
-        const size_t need = 8 + 5 * (size_t)n;
+        const size_t need = 16 + (L7_KAFKA_CLASSES + 1) * (size_t)n;
         if (e->sel_used && e->sel_stream != s) rc = hipStreamSynchronize(e->sel_stream);  // scratch reuse across streams
         if (rc == hipSuccess && need > e->sel_cap) {
             if (e->d_sel) { hipDeviceSynchronize(); hipFree(e->d_sel); e->d_sel = nullptr; e->sel_cap = 0; }
@@ -343,12 +343,12 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
             if (rc == hipSuccess) e->sel_cap = need;
         }
         if (rc != hipSuccess) return (int)rc;
-        cnt = e->d_sel;  // [0..3] Kafka length classes, [4] memcached
-        sel_k = e->d_sel + 8;
-        sel_m = sel_k + 4 * (size_t)n;
+        cnt = e->d_sel;  // [0, L7_KAFKA_CLASSES) Kafka length classes, then memcached
+        sel_k = e->d_sel + 16;
+        sel_m = sel_k + L7_KAFKA_CLASSES * (size_t)n;
         e->sel_stream = s;
         e->sel_used = true;
-        rc = hipMemsetAsync(cnt, 0, 8 * sizeof(uint32_t), s);
+        rc = hipMemsetAsync(cnt, 0, 16 * sizeof(uint32_t), s);
         if (rc == hipSuccess) rc = LaunchPartition(conn, len, n, e->d_conns, nconns, sel_k, sel_m, cnt, s);
     }
     if (rc == hipSuccess && (e->has_http || (!e->has_kafka && !e->has_mc)))
@@ -360,7 +360,7 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
                                  consumed, counters, ncounters, sel_k, cnt, s);
     if (rc == hipSuccess && e->has_mc)
         rc = LaunchMemcacheClassify(arena, off, len, conn, n, e->d_conns, nconns, e->mt, verdict,
-                                    rule, consumed, counters, ncounters, mixed ? sel_m : nullptr, mixed ? cnt + 4 : nullptr, s);
+                                    rule, consumed, counters, ncounters, mixed ? sel_m : nullptr, mixed ? cnt + L7_KAFKA_CLASSES : nullptr, s);
     return (int)rc;
 }
 

@@ -274,16 +274,19 @@ __global__ __launch_bounds__(kBlock) void kafka_classify_kernel(
         }
     }
     // sel: this protocol's request indices from partition_kernel (mixed batches), else all n
-    // (four length classes, class c at sel + c * n, sel_count[c] entries each)
-    uint32_t kc[4] = {n, 0, 0, 0};
-    if (sel)
-        for (int c = 0; c < 4; c++) kc[c] = sel_count[c];
-    const uint32_t m = kc[0] + kc[1] + kc[2] + kc[3];
+    // (L7_KAFKA_CLASSES length classes, class c at sel + c * n, sel_count[c] entries each)
+    constexpr int kCls = L7_KAFKA_CLASSES;
+    uint32_t kc[kCls] = {n};
+    uint32_t m = n;
+    if (sel) {
+        m = 0;
+        for (int c = 0; c < kCls; c++) { kc[c] = sel_count[c]; m += kc[c]; }
+    }
     for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < m; i += gridDim.x * kBlock) {
         uint32_t idx = i;
         if (sel) {
             uint32_t c = 0, j = i;
-            while (c < 3 && j >= kc[c]) { j -= kc[c]; c++; }
+            while (c < kCls - 1 && j >= kc[c]) { j -= kc[c]; c++; }
             idx = sel[(size_t)c * n + j];
         }
         const uint32_t ci = conn_ids[idx];

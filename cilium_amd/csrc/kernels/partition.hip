@@ -21,15 +21,17 @@ namespace {
 constexpr int kBlock = 256;
 constexpr int kPer = 16;
 constexpr int kWaves = kBlock / 64;
-// list classes: 0..3 Kafka by request length (< 256 B, < 1 KiB, < 4 KiB, larger), 4 memcached
-constexpr int kClasses = 5;
+// list classes: 0..kKafkaClasses-1 Kafka by request length, then memcached
+constexpr int kKafkaClasses = L7_KAFKA_CLASSES;
+constexpr int kClasses = kKafkaClasses + 1;
 
 __device__ __forceinline__ uint8_t kafka_class(uint32_t len) {
-    return len < 256 ? 0 : len < 1024 ? 1 : len < 4096 ? 2 : 3;
+    return len < 192 ? 0 : len < 384 ? 1 : len < 640 ? 2 : len < 896 ? 3 : len < 1280 ? 4 : len < 2048 ? 5
+         : len < 4096 ? 6 : 7;
 }
 }  // namespace
 
-// Lists: class c < 4 at sel_kafka + c * n, class 4 at sel_mc; counts[c] entries each.
+// Lists: Kafka class c at sel_kafka + c * n, memcached at sel_mc; counts[c] entries each.
 __global__ __launch_bounds__(kBlock) void partition_kernel(const uint32_t *__restrict__ conn_ids,
                                                            const uint32_t *__restrict__ lens, uint32_t n,
                                                            const DevConn *__restrict__ conns, uint32_t nconns,
@@ -51,7 +53,7 @@ __global__ __launch_bounds__(kBlock) void partition_kernel(const uint32_t *__res
             if (ci < nconns) {
                 const uint8_t proto = conns[ci].proto;
                 if (proto == PROTO_KAFKA) cls = 1 + kafka_class(lens[idx]);
-                else if (proto == PROTO_MEMCACHE) cls = 1 + 4;
+                else if (proto == PROTO_MEMCACHE) cls = 1 + kKafkaClasses;
             }
         }
         p[r] = cls;
@@ -83,7 +85,7 @@ __global__ __launch_bounds__(kBlock) void partition_kernel(const uint32_t *__res
         for (int c = 0; c < kClasses; c++) {
             const uint64_t mk = __ballot(p[r] == c + 1);
             if (p[r] == c + 1) {
-                uint32_t *dst = c < 4 ? sel_kafka + (size_t)c * n : sel_mc;
+                uint32_t *dst = c < kKafkaClasses ? sel_kafka + (size_t)c * n : sel_mc;
                 dst[off[c] + __popcll(mk & below)] = idx;
             }
             off[c] += __popcll(mk);
@@ -91,7 +93,7 @@ __global__ __launch_bounds__(kBlock) void partition_kernel(const uint32_t *__res
     }
 }
 
-// counts[0..4] must be zero on entry (the caller clears them on `stream`).
+// counts[0..kClasses) must be zero on entry (the caller clears them on `stream`).
 hipError_t LaunchPartition(const uint32_t *conn_ids, const uint32_t *lens, uint32_t n, const DevConn *conns,
                            uint32_t nconns, uint32_t *sel_kafka, uint32_t *sel_mc, uint32_t *counts,
                            hipStream_t stream) {
