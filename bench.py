@@ -41,11 +41,11 @@ WORKLOADS = {
     "cfg2": (1_000_000, 1_000_000, "cfg2: 64 HTTP rules (Method/Path/Host regex + literal X-Token), "
                                    "256B-2KB HTTP/1.1 requests", "http_classify_kernel"),
     "cfg3": (1_000_000, 1_000_000, "cfg3: Kafka produce/fetch/metadata stream, 1002 PortRuleKafka rules over 1k topics",
-             "kafka_classify_kernel"),
+             "partition_kernel (length classes) + kafka_classify_kernel"),
     "cfg4": (10_000_000, 1_000_000, "cfg4: 10k HTTP rules across 512 remote identities (~20-rule groups), "
                                     "256B-2KB HTTP/1.1 requests", "http_classify_kernel"),
     "cfg5": (100_000_000, 2_000_000, "cfg5: mixed 50% HTTP (cfg2 rules) / 30% Kafka (cfg3 rules) / 20% memcached "
-                                     "text+binary", "http+kafka+memcache kernels (3 launches)"),
+                                     "text+binary", "partition + http + kafka + memcache kernels (4 launches)"),
 }
 
 
