@@ -251,7 +251,7 @@ __device__ __forceinline__ uint32_t topic_first(const KafkaTables &T, const DevK
 
 }  // namespace
 
-__global__ __launch_bounds__(kBlock) void kafka_classify_kernel(
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5, 8))) void kafka_classify_kernel(
     const uint8_t *__restrict__ arena, const uint64_t *__restrict__ offs, const uint32_t *__restrict__ lens,
     const uint32_t *__restrict__ conn_ids, uint32_t n, const DevConn *__restrict__ conns, uint32_t nconns,
     KafkaTables T, uint8_t *__restrict__ out_verdict, int32_t *__restrict__ out_rule, uint32_t *__restrict__ out_consumed,
