@@ -118,16 +118,16 @@ __device__ __forceinline__ uint32_t crc32_ieee(const uint32_t *tab, Cur &cur, co
     uint32_t c = 0xFFFFFFFFu;
     uint32_t i = 0;
     for (; i < n && (((uintptr_t)(p + i)) & 15); i++) c = tab[(c ^ cur_byte(cur, p + i)) & 0xFF] ^ (c >> 8);
-    // Bulk: 128 aligned bytes per batch, eight dwordx4 loads issued together so
-    // one memory latency covers 16 slicing steps (a lane walks its message
+    // Bulk: 64 aligned bytes per batch, four dwordx4 loads issued together so
+    // one memory latency covers 8 slicing steps (a lane walks its message
     // alone; back-to-back dependent loads were the kernel's critical path).
-    for (; i + 128 <= n; i += 128) {
+    for (; i + 64 <= n; i += 64) {
         const uint4 *q = reinterpret_cast<const uint4 *>(p + i);
-        uint4 v[8];
+        uint4 v[4];
 #pragma unroll
-        for (int j = 0; j < 8; j++) v[j] = q[j];
+        for (int j = 0; j < 4; j++) v[j] = q[j];
 #pragma unroll
-        for (int j = 0; j < 16; j++) {
+        for (int j = 0; j < 8; j++) {
             const uint4 &x = v[j >> 1];
             const uint32_t lo = ((j & 1) ? x.z : x.x) ^ c, hi = (j & 1) ? x.w : x.y;
             c = tab[7 * 256 + (lo & 0xFF)] ^ tab[6 * 256 + ((lo >> 8) & 0xFF)] ^ tab[5 * 256 + ((lo >> 16) & 0xFF)] ^
@@ -251,7 +251,7 @@ __device__ __forceinline__ uint32_t topic_first(const KafkaTables &T, const DevK
 
 }  // namespace
 
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5, 8))) void kafka_classify_kernel(
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) void kafka_classify_kernel(
     const uint8_t *__restrict__ arena, const uint64_t *__restrict__ offs, const uint32_t *__restrict__ lens,
     const uint32_t *__restrict__ conn_ids, uint32_t n, const DevConn *__restrict__ conns, uint32_t nconns,
     KafkaTables T, uint8_t *__restrict__ out_verdict, int32_t *__restrict__ out_rule, uint32_t *__restrict__ out_consumed,
