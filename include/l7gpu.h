@@ -108,7 +108,10 @@ int l7g_conn_update(l7g_engine *e, uint32_t index, const l7g_conn_t *conn, char 
  * (2 = INVALID_FRAME_TYPE; 0 = parser error); 0 otherwise.  Asynchronous on `stream`
  * (a hipStream_t, NULL = default stream).  counters may be NULL, else a
  * device array of (rules + 8) uint64 that accumulates per-rule allow hits
- * followed by per-verdict totals.  Returns 0 or a HIP error code. */
+ * followed by per-verdict totals.  Batches with Kafka requests or with more
+ * than one protocol use an engine-owned scratch of (9 n + 16) uint32 (the
+ * partition lists); it grows on demand, and a call on a different stream than
+ * the previous one first waits for that stream.  Returns 0 or a HIP error code. */
 int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const uint64_t *off, const uint32_t *len,
                  const uint32_t *conn, uint32_t n, uint8_t *verdict, int32_t *rule, uint32_t *consumed,
                  uint64_t *counters, void *stream);
