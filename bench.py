@@ -1,20 +1,38 @@
 """Benchmark: L7 verdicts/s + scanned GB/s (HBM roofline fraction) on MI355X.
 
-One step = one classification pass over one batch of synthetic requests that
-are already resident in HBM (default: BASELINE.json configs[1] = cfg2: 64 HTTP
-rules over Method/Path/Host regexes + literal X-Token header, 256 B-2 KB
-HTTP/1.1 requests, 1M requests per GPU), plus the per-step RCCL all-reduce of
-the per-rule hit counters when N > 1.  Weak scaling: every rank classifies its
-own shard (request batches are independent; no payload crosses GPUs).
+One step = one l7g_classify pass over one batch of synthetic requests that are
+already resident in HBM, plus the per-step RCCL all-reduce of the per-rule hit
+counters when N > 1.
+
+Default workload: cfg5 (BASELINE.json configs[4], the largest single-GPU
+config and the one the "1/2/4/8 GPUs" metric names): 100M mixed requests per
+GPU -- 50 % HTTP (cfg2's 64 rules), 30 % Kafka (cfg3's ~1k rules), 20 %
+memcached text + binary -- built from a 2M-request unique stream.
+
+Multi-GPU (N > 1, one process per GPU): every rank generates the SAME unique
+stream (same seed, same policy), rank 0's policy bytes are broadcast over
+RCCL, and the stream is sharded by connection (whole connections per rank,
+each protocol's bytes balanced over ranks: cilium_amd/dist.py).  Each rank
+tiles its shard up to the per-GPU request count (weak scaling), classifies it
+every step and all-reduces the counters.  Every rank checks every verdict of
+its last step against the oracle's verdicts for its shard; the mismatch count
+is summed over ranks.
 
 --workload picks another BASELINE.json config:
   cfg1  1 rule GET /public/.*            1M HTTP requests
-  cfg2  64 HTTP rules (default)          1M HTTP requests
+  cfg2  64 HTTP rules                    1M HTTP requests
   cfg3  ~1k PortRuleKafka rules          1M Kafka requests
   cfg4  10k HTTP rules, 512 identities   10M HTTP requests (1M unique, tiled)
-  cfg5  mixed HTTP/Kafka/memcached       100M requests (2M unique, tiled)
-Tiled workloads replicate the unique arena on the device; every copy is
-checked against the oracle's verdicts of the unique part.
+  cfg5  mixed HTTP/Kafka/memcached       100M requests (2M unique, tiled; default)
+
+Besides the device-resident rate (`value`) the line reports:
+  * roofline   -- the dominant kernel's algorithmic bytes / its device time
+                  (HIP events around each launch, on the launch stream);
+  * kernels    -- the same per kernel of the step;
+  * e2e        -- pinned host arena -> H2D -> classify -> D2H, the unique
+                  shard in 8 chunks on 2 streams (PCIe-inclusive; never `value`);
+  * cpu_baseline -- the oracle (C restatement) on the host: all cores the
+                  process may use, and one core, with nproc and the CPU model.
 
 Usage:  python bench.py [--gpus N --steps K --warmup W --workload cfgX]
         (N > 1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
@@ -34,34 +52,117 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E peak (/opt/skills/guides/MI355X_MICROARCH.md)
 METRIC = "L7 verdicts/sec + scanned GB/s (HBM roofline frac), 1/2/4/8 MI355X"
 
-# workload -> (default requests per GPU, default unique requests, description, kernel(s) timed)
+# workload -> (default requests per GPU, default unique requests, description)
 WORKLOADS = {
-    "cfg1": (1_000_000, 1_000_000, "cfg1: 1 HTTP rule {Method: GET, Path: /public/.*}, 256B-2KB HTTP/1.1 requests",
-             "http_classify_kernel"),
+    "cfg1": (1_000_000, 1_000_000, "cfg1: 1 HTTP rule {Method: GET, Path: /public/.*}, 256B-2KB HTTP/1.1 requests"),
     "cfg2": (1_000_000, 1_000_000, "cfg2: 64 HTTP rules (Method/Path/Host regex + literal X-Token), "
-                                   "256B-2KB HTTP/1.1 requests", "http_classify_kernel"),
-    "cfg3": (1_000_000, 1_000_000, "cfg3: Kafka produce/fetch/metadata stream, 1002 PortRuleKafka rules over 1k topics",
-             "partition_kernel (length classes) + kafka_classify_kernel"),
+                                   "256B-2KB HTTP/1.1 requests"),
+    "cfg3": (1_000_000, 1_000_000, "cfg3: Kafka produce/fetch/metadata stream, 1002 PortRuleKafka rules over 1k topics"),
     "cfg4": (10_000_000, 1_000_000, "cfg4: 10k HTTP rules across 512 remote identities (~20-rule groups), "
-                                    "256B-2KB HTTP/1.1 requests", "http_classify_kernel"),
+                                    "256B-2KB HTTP/1.1 requests"),
     "cfg5": (100_000_000, 2_000_000, "cfg5: mixed 50% HTTP (cfg2 rules) / 30% Kafka (cfg3 rules) / 20% memcached "
-                                     "text+binary", "partition + http + kafka + memcache kernels (4 launches)"),
+                                     "text+binary"),
 }
+KERNEL_NAMES = {"partition": "partition_kernel", "http": "http_classify_kernel",
+                "kafka": "kafka_classify_kernel", "memcache": "memcache_classify_kernel"}
 
 
-def make_workload(gen, name, n, seed):
+def make_workload(gen, name, n):
     cfg = int(name[3:])
     if cfg in (1, 2):
-        return gen.http_workload(cfg, n, seed=seed)
+        return gen.http_workload(cfg, n)
     if cfg == 3:
-        return gen.kafka_workload(n, seed=seed)
+        return gen.kafka_workload(n)
     if cfg == 4:
-        return gen.cfg4_workload(n, seed=seed)
-    return gen.mixed_workload(n, seed=seed)
+        return gen.cfg4_workload(n)
+    return gen.mixed_workload(n)
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_info():
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count() or 1
+    return {"nproc": os.cpu_count(), "usable_cores": usable, "model": model}
+
+
+def e2e_pipeline(torch, eng, w, dev, nchunks=8, reps=3):
+    """Pinned host arena -> H2D -> classify -> D2H for the unique shard, cut
+    into nchunks request ranges alternating over two streams (the copies of
+    one chunk overlap the kernels of the other).  Returns (seconds per pass,
+    bytes moved per pass)."""
+    n = w.n
+    bounds = np.linspace(0, n, nchunks + 1).astype(np.int64)
+    h_arena = torch.from_numpy(np.ascontiguousarray(w.arena)).pin_memory()
+    offs = w.offsets.astype(np.int64)
+    ends = offs + w.lengths.astype(np.int64)
+    rel = np.empty(n, np.int64)
+    spans = []
+    for c in range(nchunks):
+        a, b = bounds[c], bounds[c + 1]
+        lo = int(offs[a:b].min()) if b > a else 0
+        hi = int(ends[a:b].max()) if b > a else 0
+        rel[a:b] = offs[a:b] - lo
+        spans.append((a, b, lo, hi))
+    h_off = torch.from_numpy(rel).pin_memory()
+    h_len = torch.from_numpy(w.lengths.view(np.int32)).pin_memory()
+    h_cid = torch.from_numpy(w.conn_ids.view(np.int32)).pin_memory()
+    h_v = torch.empty(n, dtype=torch.uint8).pin_memory()
+    h_r = torch.empty(n, dtype=torch.int32).pin_memory()
+    h_c = torch.empty(n, dtype=torch.int32).pin_memory()
+    max_bytes = max(hi - lo for _, _, lo, hi in spans) + 64
+    max_req = int(max(b - a for a, b, _, _ in spans))
+    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    bufs = [dict(arena=torch.empty(max_bytes, dtype=torch.uint8, device=dev),
+                 off=torch.empty(max_req, dtype=torch.int64, device=dev),
+                 len=torch.empty(max_req, dtype=torch.int32, device=dev),
+                 cid=torch.empty(max_req, dtype=torch.int32, device=dev),
+                 v=torch.empty(max_req, dtype=torch.uint8, device=dev),
+                 r=torch.empty(max_req, dtype=torch.int32, device=dev),
+                 c=torch.empty(max_req, dtype=torch.int32, device=dev)) for _ in range(2)]
+    done = [torch.cuda.Event(), torch.cuda.Event()]
+
+    def one_pass():
+        for c, (a, b, lo, hi) in enumerate(spans):
+            k = c & 1
+            s, B = streams[k], bufs[k]
+            m = int(b - a)
+            with torch.cuda.stream(s):
+                s.wait_event(done[k])  # buffer set k: previous chunk's D2H finished
+                B["arena"][:hi - lo].copy_(h_arena[lo:hi], non_blocking=True)
+                B["off"][:m].copy_(h_off[a:b], non_blocking=True)
+                B["len"][:m].copy_(h_len[a:b], non_blocking=True)
+                B["cid"][:m].copy_(h_cid[a:b], non_blocking=True)
+                eng.classify_device(B["arena"].data_ptr(), hi - lo, B["off"].data_ptr(), B["len"].data_ptr(),
+                                    B["cid"].data_ptr(), m, B["v"].data_ptr(), B["r"].data_ptr(), B["c"].data_ptr(),
+                                    stream=s.cuda_stream)
+                h_v[a:b].copy_(B["v"][:m], non_blocking=True)
+                h_r[a:b].copy_(B["r"][:m], non_blocking=True)
+                h_c[a:b].copy_(B["c"][:m], non_blocking=True)
+                done[k].record(s)
+        torch.cuda.synchronize(dev)
+
+    one_pass()  # warm-up (allocations, first-touch)
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        one_pass()
+        ts.append(time.perf_counter() - t0)
+    moved = sum(hi - lo for _, _, lo, hi in spans) + n * (16 + 9)
+    return float(np.median(ts)), moved, (h_v.numpy().copy(), h_r.numpy().copy(), h_c.numpy().view(np.uint32).copy())
 
 
 def main():
@@ -69,11 +170,13 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default="cfg5", choices=sorted(WORKLOADS))
     ap.add_argument("--requests", type=int, default=0, help="requests per GPU (weak scaling); 0 = workload default")
     ap.add_argument("--unique", type=int, default=0, help="unique requests generated (tiled up to --requests)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="oracle threads (0 = every usable core)")
+    ap.add_argument("--profile-steps", type=int, default=3, help="extra steps with per-kernel HIP events")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -91,28 +194,36 @@ def main():
     from cilium_amd import Engine, gen
     from cilium_amd import dist as l7dist
 
-    dflt_n, dflt_u, wdesc, kname = WORKLOADS[args.workload]
+    dflt_n, dflt_u, wdesc = WORKLOADS[args.workload]
     want = args.requests or dflt_n
-    uniq = min(args.unique or dflt_u, want)
-    tiles = max(1, want // uniq)
+    uniq = args.unique or dflt_u
     t0 = time.time()
-    w = make_workload(gen, args.workload, uniq, gen.SEED_BASE + int(args.workload[3:]) + 7919 * rank)
+    # the same stream (and policy) on every rank: fixed per-config seed
+    full = make_workload(gen, args.workload, uniq)
+    if world > 1:
+        _, shards = l7dist.shard_by_connection(full.conn_ids, full.lengths, len(full.conns), world,
+                                               full.conns["proto"])
+        w = gen.select(full, shards[rank], name=f"{full.name}[rank {rank}/{world}]")
+    else:
+        w = full
     nu = w.n
+    tiles = max(1, want // max(nu, 1))
     offs, lens, cids = gen.tile_offsets(w, tiles)
     n = len(offs)
-    log(f"[rank {rank}] {args.workload}: generated {nu} unique requests ({w.arena.nbytes / 1e9:.2f} GB) x {tiles} "
-        f"= {n} requests in {time.time() - t0:.1f}s")
+    pbytes = gen.protocol_bytes(w)
+    log(f"[rank {rank}] {args.workload}: {full.n} unique requests generated, shard {nu} "
+        f"({w.arena.nbytes / 1e9:.2f} GB) x {tiles} = {n} requests in {time.time() - t0:.1f}s")
 
     eng = Engine(local)
-    # the policy arrives at rank 0 (NPDS) and is broadcast to every rank over RCCL
-    policy = l7dist.broadcast_policy(w.policy, dist, device=dev) if dist is not None else w.policy
+    # the policy arrives at rank 0 (the NPDS client) and is broadcast to every rank over RCCL
+    policy = l7dist.broadcast_policy(full.policy, dist, device=dev) if dist is not None else full.policy
     eng.update_policy(policy)
     eng.set_connections(w.conns)
     nrules = eng.nrules
 
-    d_arena = torch.from_numpy(w.arena).to(dev)
+    d_arena = torch.from_numpy(np.ascontiguousarray(w.arena)).to(dev)
     if tiles > 1:
-        d_arena = d_arena.repeat(tiles)  # device-side replication of the unique arena
+        d_arena = d_arena.repeat(tiles)  # device-side replication of the unique shard
     d_off = torch.from_numpy(offs.view(np.int64)).to(dev)
     d_len = torch.from_numpy(lens.view(np.int32)).to(dev)
     d_cid = torch.from_numpy(cids.view(np.int32)).to(dev)
@@ -153,66 +264,121 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    if dist is not None:
-        t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kernel_ms = float(t[0]), float(t[1])
 
-    total_requests = n * world * args.steps
-    verdicts_per_s = total_requests / elapsed
-    alg_bytes = w.algorithmic_bytes() * tiles  # per launch, per GPU
-    scanned_gbps = alg_bytes * world * args.steps / elapsed / 1e9
-    achieved = alg_bytes / (kernel_ms / 1e3) / 1e9
+    # per-kernel device time: extra steps with HIP events around every launch
+    stage_ms = {k: 0.0 for k in Engine.STAGES}
+    if args.profile_steps > 0:
+        eng.profile(True)
+        acc = []
+        for _ in range(args.profile_steps):
+            eng.classify_device(*ptrs, n, *outs, stream=stream.cuda_stream)
+            acc.append(eng.profile_last())
+        eng.profile(False)
+        stage_ms = {k: float(np.mean([a[k] for a in acc])) for k in Engine.STAGES}
+    torch.cuda.synchronize()
+
+    # parity of the last step on this rank's shard: every verdict, rule id and
+    # consumed length against the oracle (test infrastructure, run after timing)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import refpy  # parity oracle: the checker and the CPU baseline, never the product path
+    cinfo = cpu_info()
+    threads = args.cpu_threads or min(cinfo["usable_cores"], 128)
+    verdict = d_v.cpu().numpy()
+    rule = d_r.cpu().numpy()
+    consumed = d_c.cpu().numpy().view(np.uint32)
+    pol = refpy.Policy(policy)
+    t1 = time.perf_counter()
+    rv, rr, rc = pol.classify(w.conns, w.arena, w.offsets, w.lengths, w.conn_ids, threads)
+    cpu_all_s = time.perf_counter() - t1
+    mism = 0
+    for j in range(tiles):
+        sl = slice(j * nu, (j + 1) * nu)
+        mism += int(((verdict[sl] != rv) | (rule[sl] != rr) | (consumed[sl] != rc)).sum())
+    if mism:
+        log(f"[rank {rank}] PARITY FAILURE: {mism} of {n} requests differ from the oracle")
+
+    # e2e: host arena in pinned memory, PCIe both ways, chunked on two streams
+    e2e = None
+    if not args.no_e2e:
+        t_e2e, moved, eout = e2e_pipeline(torch, eng, w, dev)
+        e2e_mism = int(((eout[0] != rv) | (eout[1] != rr) | (eout[2] != rc)).sum())
+        e2e = {"s": t_e2e, "requests": nu, "bytes": moved, "mismatches": e2e_mism}
+
+    # ---- aggregate over ranks
+    if dist is not None:
+        t = torch.tensor([elapsed, kernel_ms] + [stage_ms[k] for k in Engine.STAGES] +
+                         [e2e["s"] if e2e else 0.0], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        vals = t.tolist()
+        elapsed, kernel_ms = vals[0], vals[1]
+        stage_ms = dict(zip(Engine.STAGES, vals[2:6]))
+        if e2e:
+            e2e["s"] = vals[6]
+        cnt = torch.tensor([mism, n, nu, e2e["mismatches"] if e2e else 0, e2e["bytes"] if e2e else 0],
+                           dtype=torch.int64, device=dev)
+        dist.all_reduce(cnt)
+        mism, checked, e2e_reqs, e2e_mism, e2e_bytes = [int(x) for x in cnt.tolist()]
+        if e2e:
+            e2e.update(requests=e2e_reqs, mismatches=e2e_mism, bytes=e2e_bytes)
+    else:
+        checked = n
+
+    # CPU baseline (rank 0 at N = 1): the parity run above on every usable
+    # core, plus one core on a bounded sample
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        m1 = min(nu, 300_000)
+        sub = w.subset(np.arange(m1))
+        t2 = time.perf_counter()
+        refpy.Policy(w.policy).classify(sub.conns, sub.arena, sub.offsets, sub.lengths, sub.conn_ids, 1)
+        cpu_1_s = time.perf_counter() - t2
+        cpu = {"value": round(nu / cpu_all_s, 1), "unit": "verdicts/s", "cores": threads, "kind": "port",
+               "sample": f"the {nu} unique requests of the {args.workload} arena ({w.arena.nbytes / 1e9:.2f} GB), one "
+                         f"pass of the oracle/ C restatement on {threads} threads ({cpu_all_s:.2f} s wall); single "
+                         f"core: the first {m1} requests ({cpu_1_s:.2f} s)",
+               "scanned_gbps": round(float(w.lengths.astype(np.int64).sum()) / cpu_all_s / 1e9, 3),
+               "single_core_verdicts_per_s": round(m1 / cpu_1_s, 1),
+               "nproc": cinfo["nproc"], "usable_cores": cinfo["usable_cores"], "cpu_model": cinfo["model"]}
 
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
         return
 
-    # ---- parity of the last step on this rank's shard + CPU baseline (oracle, N = 1 only)
-    verdict = d_v.cpu().numpy()
-    rule = d_r.cpu().numpy()
-    consumed = d_c.cpu().numpy().view(np.uint32)
-    parity = None
-    cpu = None
-    if world == 1 and not args.no_cpu_baseline:
-        sys.path.insert(0, os.path.join(ROOT, "tests"))
-        import refpy  # parity oracle: the checker and the CPU baseline, never the product path
-        try:
-            cores = len(os.sched_getaffinity(0))
-        except AttributeError:
-            cores = os.cpu_count() or 1
-        cores = args.cpu_threads or min(16, cores)
-        pol = refpy.Policy(w.policy)
-        t1 = time.perf_counter()
-        rv, rr, rc = pol.classify(w.conns, w.arena, w.offsets, w.lengths, w.conn_ids, cores)
-        cpu_s = time.perf_counter() - t1
-        cpu = {"value": round(nu / cpu_s, 1), "unit": "verdicts/s", "cores": cores, "kind": "port",
-               "sample": f"the {nu} unique requests of the {args.workload} arena, one pass, oracle/ C restatement "
-                         f"on {cores} threads ({cpu_s:.2f} s wall, {w.arena.nbytes / 1e9:.2f} GB)",
-               "scanned_gbps": round(w.lengths.astype(np.int64).sum() / cpu_s / 1e9, 3)}
-        rv, rr, rc = (np.tile(a, tiles) for a in (rv, rr, rc))
-        mism = int(((verdict != rv) | (rule != rr) | (consumed != rc)).sum())
-        parity = {"checked": n, "mismatches": mism, "bit_exact": mism == 0}
-        if mism:
-            log(f"PARITY FAILURE: {mism} of {n} requests differ from the oracle")
-
+    total_requests = n * world * args.steps
+    verdicts_per_s = total_requests / elapsed
+    # algorithmic bytes per launch per GPU: payload + 25 B per request
+    alg = {k: (pbytes[k]["payload"] + 25 * pbytes[k]["requests"]) * tiles for k in ("http", "kafka", "memcache")}
+    n_other = pbytes["kafka"]["requests"] + pbytes["memcache"]["requests"]
+    alg["partition"] = (8 * nu + 4 * n_other) * tiles if stage_ms["partition"] > 0 else 0
+    step_alg = sum(alg[k] for k in ("http", "kafka", "memcache"))
+    kernels = {}
+    for k in Engine.STAGES:
+        if stage_ms[k] > 0:
+            g = alg[k] / (stage_ms[k] / 1e3) / 1e9
+            kernels[k] = {"kernel": KERNEL_NAMES[k], "ms": round(stage_ms[k], 4), "algorithmic_bytes": alg[k],
+                          "achieved_gbps": round(g, 1), "frac": round(g / HBM_PEAK_GBPS, 4)}
+    dom = max((k for k in kernels if k != "partition"), key=lambda k: kernels[k]["ms"], default=None)
     traffic = None
     tpath = os.path.join(ROOT, "profiles", f"traffic_{args.workload}.json")
-    if os.path.exists(tpath):
+    if dom and os.path.exists(tpath):
         try:
             with open(tpath) as f:
-                traffic = json.load(f).get("hbm_bytes_per_launch")
+                tj = json.load(f)
+            traffic = tj.get("kernels", {}).get(KERNEL_NAMES[dom], {}).get("hbm_bytes_per_launch")
+            if traffic is None and len(kernels) == 1:
+                traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
-
-    hist = np.bincount(verdict, minlength=5)
-    if args.workload == "cfg5":
-        line_extra = {"protocol_mix": {"http": int((w.conns["proto"][w.conn_ids] == 1).sum()),
-                                       "kafka": int((w.conns["proto"][w.conn_ids] == 2).sum()),
-                                       "memcache": int((w.conns["proto"][w.conn_ids] == 3).sum())}}
+    if dom:
+        achieved = alg[dom] / (stage_ms[dom] / 1e3) / 1e9
+        roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic, "kernel": KERNEL_NAMES[dom],
+                    "kernel_ms": round(stage_ms[dom], 4), "algorithmic_bytes_per_launch": alg[dom]}
     else:
-        line_extra = {}
+        roofline = None
+    step_gbps = step_alg / (kernel_ms / 1e3) / 1e9
+    hist = np.bincount(verdict, minlength=5)
     tot = totals.cpu().numpy()
     line = {
         "metric": METRIC,
@@ -228,19 +394,29 @@ def main():
         "dtype": "u8",
         "data": "synthetic",
         "config": {"workload": f"{wdesc}, {n} requests per GPU",
-                   "requests_per_gpu": n, "unique_requests": nu, "global_requests_per_step": n * world,
+                   "requests_per_gpu": n, "unique_requests": full.n, "unique_per_gpu": nu,
+                   "global_requests_per_step": n * world,
                    "mean_request_bytes": round(float(w.lengths.mean()), 1),
-                   "parallelism": f"dp{world}" + (" + RCCL counter all-reduce" if world > 1 else "")},
-        "scanned_gbps": round(scanned_gbps, 2),
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                     "kernel": kname, "kernel_ms": round(kernel_ms, 4),
-                     "algorithmic_bytes_per_launch": alg_bytes},
+                   "protocol_mix": {k: v["requests"] for k, v in pbytes.items()},
+                   "parallelism": f"dp{world}" + (" (connection-sharded stream) + RCCL counter all-reduce"
+                                                  if world > 1 else "")},
+        "scanned_gbps": round(step_alg * world * args.steps / elapsed / 1e9, 2),
+        "roofline": roofline,
+        "step_roofline": {"algorithmic_bytes_per_launch": step_alg, "kernel_ms": round(kernel_ms, 4),
+                          "achieved_gbps": round(step_gbps, 1), "frac": round(step_gbps / HBM_PEAK_GBPS, 4),
+                          "note": "all kernels of one l7g_classify call, one HIP event pair on the stream"},
+        "kernels": kernels,
         "cpu_baseline": cpu,
-        "parity": parity,
-        "verdict_hist_last_step": hist.tolist(),
+        "e2e": None if e2e is None else {
+            "verdicts_per_s": round(e2e["requests"] / e2e["s"], 1), "ms_per_pass": round(e2e["s"] * 1e3, 3),
+            "requests_per_pass": e2e["requests"], "pcie_gbps": round(e2e["bytes"] / e2e["s"] / 1e9, 2),
+            "mismatches": e2e["mismatches"],
+            "mode": "unique shard per GPU from pinned host memory: H2D arena + metadata, classify, D2H verdicts; "
+                    "8 chunks alternating over 2 streams"},
+        "parity": {"checked": checked, "mismatches": mism, "bit_exact": mism == 0,
+                   "scope": "every request of the last step on every rank vs the oracle"},
+        "verdict_hist_last_step_rank0": hist.tolist(),
         "counter_totals": {"allow_hits": int(tot[:nrules].sum()), "verdicts": tot[nrules:nrules + 5].tolist()},
-        **line_extra,
     }
     print(json.dumps(line), flush=True)
     if dist is not None:

@@ -17,22 +17,13 @@
 #include "regex/re_dfa.h"
 
 namespace l7 {
-hipError_t LaunchHttpClassify(const uint8_t *arena, uint64_t arena_len, const uint64_t *offs, const uint32_t *lens, const uint32_t *conn_ids,
-                              uint32_t n, const DevConn *conns, uint32_t nconns, const HttpTables &T, bool any_cold,
-                              uint8_t *verdict, int32_t *rule, uint32_t *consumed, uint64_t *counters,
-                              uint32_t ncounters, hipStream_t stream);
-hipError_t LaunchKafkaClassify(const uint8_t *arena, const uint64_t *offs, const uint32_t *lens, const uint32_t *conn_ids,
-                               uint32_t n, const DevConn *conns, uint32_t nconns, const KafkaTables &T,
-                               uint8_t *verdict, int32_t *rule, uint32_t *consumed, uint64_t *counters,
-                               uint32_t ncounters, const uint32_t *sel, const uint32_t *sel_count, hipStream_t stream);
-hipError_t LaunchMemcacheClassify(const uint8_t *arena, const uint64_t *offs, const uint32_t *lens,
-                                  const uint32_t *conn_ids, uint32_t n, const DevConn *conns, uint32_t nconns,
-                                  const McTables &T, uint8_t *verdict, int32_t *rule, uint32_t *consumed,
-                                  uint64_t *counters, uint32_t ncounters, const uint32_t *sel, const uint32_t *sel_count,
+hipError_t LaunchHttpClassify(const Batch &B, const HttpTables &T, bool any_cold, bool answer_other,
+                              hipStream_t stream);
+hipError_t LaunchKafkaClassify(const Batch &B, const KafkaTables &T, const uint32_t *sel, const uint32_t *sel_count,
+                               hipStream_t stream);
+hipError_t LaunchMemcacheClassify(const Batch &B, const McTables &T, const uint32_t *sel, const uint32_t *sel_count,
                                   hipStream_t stream);
-hipError_t LaunchPartition(const uint32_t *conn_ids, const uint32_t *lens, uint32_t n, const DevConn *conns,
-                           uint32_t nconns, uint32_t *sel_kafka, uint32_t *sel_mc, uint32_t *counts,
-                           hipStream_t stream);
+hipError_t LaunchPartition(const Batch &B, uint32_t *sel_kafka, uint32_t *sel_mc, uint32_t *counts, hipStream_t stream);
 hipError_t HttpPhaseTimes(uint64_t *out, bool reset);
 }  // namespace l7
 
@@ -66,9 +57,22 @@ struct l7g_engine {
     // protocol split (grow-only, stream-ordered): [counts(16) | L7_KAFKA_CLASSES x n Kafka idx | n memcached idx]
     uint32_t *d_sel = nullptr;
     size_t sel_cap = 0;
-    hipStream_t sel_stream = nullptr;
-    bool sel_used = false;
+    // Completion of the last l7g_classify's kernels (recorded on the caller's
+    // stream).  The engine waits on it -- never on the caller's stream, which
+    // may be gone by then -- before it rewrites or frees anything a launched
+    // kernel reads: the connection table, the table blob, the partition scratch.
+    hipEvent_t done_ev = nullptr;
+    bool launched = false;
+    // l7g_profile_*: timing events around each launch of the last call
+    bool profile = false;
+    hipEvent_t prof_ev[5] = {};
+    bool prof_ran[4] = {};
 };
+
+static hipError_t WaitLastClassify(l7g_engine *e) {
+    if (!e->launched) return hipSuccess;
+    return hipEventSynchronize(e->done_ev);
+}
 
 static void set_err(char *err, size_t errlen, const std::string &m) {
     if (!err || errlen == 0) return;
@@ -160,7 +164,7 @@ hipError_t Upload(l7g_engine *e) {
         uint8_t *d = nullptr;
         if ((rc = hipMalloc(&d, blob.size())) != hipSuccess) return rc;
         if ((rc = hipMemcpy(d, blob.data(), blob.size(), hipMemcpyHostToDevice)) != hipSuccess) { hipFree(d); return rc; }
-        if (e->d_blob) { hipDeviceSynchronize(); hipFree(e->d_blob); }
+        if (e->d_blob) { WaitLastClassify(e); hipFree(e->d_blob); }
         e->d_blob = d;
         e->blob_bytes = blob.size();
         HttpTables &T = e->ht;
@@ -185,9 +189,12 @@ hipError_t Upload(l7g_engine *e) {
         e->tables_dirty = false;
     }
     if (e->conns_dirty) {
+        // kernels of the previous batch may still read the table: it is
+        // rewritten (or freed) only once they have finished
+        if ((rc = WaitLastClassify(e)) != hipSuccess) return rc;
         size_t need = std::max<size_t>(e->conns.size(), 1);
         if (need > e->conns_cap) {
-            if (e->d_conns) { hipDeviceSynchronize(); hipFree(e->d_conns); e->d_conns = nullptr; }
+            if (e->d_conns) { hipFree(e->d_conns); e->d_conns = nullptr; }
             if ((rc = hipMalloc(&e->d_conns, need * sizeof(DevConn))) != hipSuccess) return rc;
             e->conns_cap = need;
         }
@@ -222,6 +229,11 @@ l7g_engine *l7g_engine_create(int device, char *err, size_t errlen) {
     if ((rc = hipSetDevice(device)) != hipSuccess) { set_err(err, errlen, hipGetErrorString(rc)); return nullptr; }
     auto *e = new l7g_engine();
     e->device = device;
+    if ((rc = hipEventCreateWithFlags(&e->done_ev, hipEventDisableTiming)) != hipSuccess) {
+        set_err(err, errlen, hipGetErrorString(rc));
+        delete e;
+        return nullptr;
+    }
     e->ps = std::make_unique<PolicySet>();
     e->hc = std::make_unique<HttpCompiler>(e->ps.get());
     e->kc = std::make_unique<KafkaCompiler>(e->ps.get());
@@ -237,6 +249,9 @@ void l7g_engine_destroy(l7g_engine *e) {
     if (e->d_blob) hipFree(e->d_blob);
     if (e->d_conns) hipFree(e->d_conns);
     if (e->d_sel) hipFree(e->d_sel);
+    if (e->done_ev) hipEventDestroy(e->done_ev);
+    for (hipEvent_t ev : e->prof_ev)
+        if (ev) hipEventDestroy(ev);
     if (e->s_arena) hipFree(e->s_arena);
     if (e->s_req) hipFree(e->s_req);
     if (e->sstream) hipStreamDestroy(e->sstream);
@@ -324,43 +339,68 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
     if (rc == hipSuccess) rc = Upload(e);
     if (rc != hipSuccess) return (int)rc;
     hipStream_t s = (hipStream_t)stream;
-    const uint32_t ncounters = counters ? (uint32_t)e->ps->nrules + 8 : 0;
-    // The kernels each classify only their own protocol's requests and skip
-    // the rest, so a mixed batch needs one launch per protocol present.  With
-    // more than one protocol the Kafka and memcached kernels walk index lists
-    // written by partition_kernel instead of the whole batch.
-    const uint32_t nconns = (uint32_t)e->conns.size();
-    // Kafka batches always go through the split: it also groups Kafka requests
-    // into L7_KAFKA_CLASSES length classes (one list of up to n entries each).
-    const bool mixed = (int)e->has_http + (int)e->has_kafka + (int)e->has_mc > 1;
+    Batch B{};
+    B.arena = arena;
+    B.arena_len = arena_len;
+    B.offs = off;
+    B.lens = len;
+    B.conn_ids = conn;
+    B.conns = e->d_conns;
+    B.verdict = verdict;
+    B.rule = rule;
+    B.consumed = consumed;
+    B.counters = counters;
+    B.n = n;
+    B.nconns = (uint32_t)e->conns.size();
+    B.ncounters = counters ? (uint32_t)e->ps->nrules + 8 : 0;
+    if (n == 0) return 0;
+    // The kernels each classify only their own protocol's requests, so a
+    // mixed batch needs one launch per protocol present.  Unless the batch can
+    // hold HTTP requests only, partition_kernel runs first: it writes the
+    // Kafka (by length class) and memcached index lists the other two kernels
+    // walk, and it answers the requests no classifier owns (unknown
+    // connection, no parser) itself.  An HTTP-only engine skips it; its HTTP
+    // kernel answers those.
+    const bool partitioned = e->has_kafka || e->has_mc;
     uint32_t *sel_k = nullptr, *sel_m = nullptr, *cnt = nullptr;
-    if ((mixed || e->has_kafka) && n > 0) {
+    if (partitioned) {
         const size_t need = 16 + (L7_KAFKA_CLASSES + 1) * (size_t)n;
-        if (e->sel_used && e->sel_stream != s) rc = hipStreamSynchronize(e->sel_stream);  // scratch reuse across streams
+        // the scratch may still be in use by the previous batch (any stream)
+        if (e->launched) rc = hipStreamWaitEvent(s, e->done_ev, 0);
         if (rc == hipSuccess && need > e->sel_cap) {
-            if (e->d_sel) { hipDeviceSynchronize(); hipFree(e->d_sel); e->d_sel = nullptr; e->sel_cap = 0; }
-            rc = hipMalloc(&e->d_sel, need * sizeof(uint32_t));
+            if (e->d_sel) {
+                rc = WaitLastClassify(e);
+                hipFree(e->d_sel);
+                e->d_sel = nullptr;
+                e->sel_cap = 0;
+            }
+            if (rc == hipSuccess) rc = hipMalloc(&e->d_sel, need * sizeof(uint32_t));
             if (rc == hipSuccess) e->sel_cap = need;
         }
         if (rc != hipSuccess) return (int)rc;
         cnt = e->d_sel;  // [0, L7_KAFKA_CLASSES) Kafka length classes, then memcached
         sel_k = e->d_sel + 16;
         sel_m = sel_k + L7_KAFKA_CLASSES * (size_t)n;
-        e->sel_stream = s;
-        e->sel_used = true;
         rc = hipMemsetAsync(cnt, 0, 16 * sizeof(uint32_t), s);
-        if (rc == hipSuccess) rc = LaunchPartition(conn, len, n, e->d_conns, nconns, sel_k, sel_m, cnt, s);
     }
-    if (rc == hipSuccess && (e->has_http || (!e->has_kafka && !e->has_mc)))
-        rc = LaunchHttpClassify(arena, arena_len, off, len, conn, n, e->d_conns, nconns, e->ht, e->any_cold,
-                                verdict, rule,
-                                consumed, counters, ncounters, s);
-    if (rc == hipSuccess && e->has_kafka)
-        rc = LaunchKafkaClassify(arena, off, len, conn, n, e->d_conns, nconns, e->kt, verdict, rule,
-                                 consumed, counters, ncounters, sel_k, cnt, s);
-    if (rc == hipSuccess && e->has_mc)
-        rc = LaunchMemcacheClassify(arena, off, len, conn, n, e->d_conns, nconns, e->mt, verdict,
-                                    rule, consumed, counters, ncounters, mixed ? sel_m : nullptr, mixed ? cnt + L7_KAFKA_CLASSES : nullptr, s);
+    // profiling: event k is recorded before stage k (partition, http, kafka, memcache), event 4 after the last
+    const bool prof = e->profile;
+    auto mark = [&](int k) {
+        if (prof && rc == hipSuccess) rc = hipEventRecord(e->prof_ev[k], s);
+    };
+    const bool run[4] = {partitioned, e->has_http || !partitioned, e->has_kafka, e->has_mc};
+    for (int k = 0; k < 4; k++) e->prof_ran[k] = run[k];
+    mark(0);
+    if (rc == hipSuccess && run[0]) rc = LaunchPartition(B, sel_k, sel_m, cnt, s);
+    mark(1);
+    if (rc == hipSuccess && run[1]) rc = LaunchHttpClassify(B, e->ht, e->any_cold, !partitioned, s);
+    mark(2);
+    if (rc == hipSuccess && run[2]) rc = LaunchKafkaClassify(B, e->kt, sel_k, cnt, s);
+    mark(3);
+    if (rc == hipSuccess && run[3]) rc = LaunchMemcacheClassify(B, e->mt, sel_m, cnt + L7_KAFKA_CLASSES, s);
+    mark(4);
+    if (rc == hipSuccess) rc = hipEventRecord(e->done_ev, s);
+    if (rc == hipSuccess) e->launched = true;
     return (int)rc;
 }
 
@@ -432,6 +472,26 @@ int l7g_stats(l7g_engine *e, l7g_stats_t *out) {
     out->mc_dfas = (uint32_t)M.dfas;
     out->mc_dfa_states = (uint32_t)M.dfa_states;
     return 0;
+}
+
+int l7g_profile_enable(l7g_engine *e, int on) {
+    std::lock_guard<std::mutex> g(e->mu);
+    if (e->device < 0) return (int)hipErrorNoDevice;
+    hipError_t rc = hipSetDevice(e->device);
+    for (hipEvent_t &ev : e->prof_ev)
+        if (rc == hipSuccess && !ev) rc = hipEventCreate(&ev);
+    if (rc == hipSuccess) e->profile = on != 0;
+    return (int)rc;
+}
+
+int l7g_profile_last(l7g_engine *e, float out_ms[4]) {
+    std::lock_guard<std::mutex> g(e->mu);
+    for (int k = 0; k < 4; k++) out_ms[k] = 0.f;
+    if (!e->profile || !e->launched) return (int)hipErrorNotReady;
+    hipError_t rc = hipEventSynchronize(e->prof_ev[4]);
+    for (int k = 0; k < 4 && rc == hipSuccess; k++)
+        if (e->prof_ran[k]) rc = hipEventElapsedTime(&out_ms[k], e->prof_ev[k], e->prof_ev[k + 1]);
+    return (int)rc;
 }
 
 int l7g_debug_phase_times(l7g_engine *e, uint64_t *out8, int reset) {

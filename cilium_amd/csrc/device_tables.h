@@ -5,6 +5,12 @@
 #pragma once
 #include <stdint.h>
 
+#if defined(__HIPCC__)
+#define L7_HD __host__ __device__
+#else
+#define L7_HD
+#endif
+
 namespace l7 {
 
 enum : uint8_t {
@@ -28,6 +34,30 @@ struct DevConn {
     uint8_t flags;     // memcached: L7G_CONN_MC_TEXT / _BINARY (0 = by first byte)
     uint8_t pad[2];
 };
+
+// One l7g_classify call as the kernels see it (passed by value): request i is
+// arena[offs[i] .. offs[i] + lens[i]) on connection conn_ids[i]; outputs are
+// indexed by i.  counters (may be null) = u64[ncounters]: per-rule allow hits,
+// then 8 per-verdict totals.
+struct Batch {
+    const uint8_t *arena;
+    uint64_t arena_len;
+    const uint64_t *offs;
+    const uint32_t *lens;
+    const uint32_t *conn_ids;
+    const DevConn *conns;
+    uint8_t *verdict;
+    int32_t *rule;
+    uint32_t *consumed;
+    uint64_t *counters;
+    uint32_t n, nconns, ncounters, pad;
+};
+
+// A request whose bytes leave [arena, arena + arena_len) is out of contract:
+// every kernel answers it UNSUPPORTED instead of reading past the arena.
+L7_HD inline bool l7_in_arena(uint64_t off, uint32_t len, uint64_t arena_len) {
+    return off <= arena_len && (uint64_t)len <= arena_len - off;
+}
 
 // ---------------- HTTP ----------------
 // Every HTTP rule set is one self-contained, 16-byte aligned "image": a

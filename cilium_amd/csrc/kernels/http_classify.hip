@@ -941,12 +941,14 @@ __device__ __forceinline__ void run_tile(Lane &L, const uint8_t *img, uint8_t *w
 //               plus entries on connections without an HTTP parser.
 // kHot = false: every other HTTP request (images read through L2); all of
 //               them when no hot kernel runs (T.hot_ruleset < 0).
+// answer_other: also answer the entries no classifier owns (unknown connection,
+// no parser) UNSUPPORTED; false when partition_kernel has answered them.
 template <bool kHot>
-__global__ __launch_bounds__(kBlock) void http_classify_kernel(
-    const uint8_t *__restrict__ arena, const uint64_t *__restrict__ offs, const uint32_t *__restrict__ lens,
-    const uint32_t *__restrict__ conn_ids, uint32_t n, const DevConn *__restrict__ conns, uint32_t nconns,
-    HttpTables T, uint8_t *__restrict__ out_verdict, int32_t *__restrict__ out_rule, uint32_t *__restrict__ out_consumed,
-    uint64_t *__restrict__ counters, uint32_t ncounters, uint64_t arena_len) {
+__global__ __launch_bounds__(kBlock) void http_classify_kernel(Batch B, HttpTables T, uint32_t answer_other) {
+    const uint8_t *__restrict__ arena = B.arena;
+    const uint32_t n = B.n, nconns = B.nconns;
+    uint64_t *__restrict__ counters = B.counters;
+    const uint32_t ncounters = B.ncounters;
     __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63, wave = tid >> 6;
@@ -967,7 +969,7 @@ __global__ __launch_bounds__(kBlock) void http_classify_kernel(
         for (uint32_t i = tid; i < 8 + kLdsRuleCounters; i += kBlock) s_cnt[i] = 0;
     __syncthreads();
 
-    const Out O{out_verdict, out_rule, out_consumed, s_cnt, counters, ncounters > 8 ? ncounters - 8 : 0};
+    const Out O{B.verdict, B.rule, B.consumed, s_cnt, counters, ncounters > 8 ? ncounters - 8 : 0};
     uint8_t *wave_lds = lds + wave * kWaveLds;
     const uint32_t ntiles = (n + 63) / 64;
     for (uint32_t tile = blockIdx.x * kWaves + wave; tile < ntiles; tile += gridDim.x * kWaves) {
@@ -983,18 +985,18 @@ __global__ __launch_bounds__(kBlock) void http_classify_kernel(
         L.a0 = L.pa = L.w = L.lena = 0;
         const uint8_t *img = kHot ? s_img : nullptr;
         if (L.idx < n) {
-            const uint32_t ci = conn_ids[L.idx];
-            const DevConn conn = ci < nconns ? conns[ci] : DevConn{-1, PROTO_NONE, 0, {0, 0}};
+            const uint32_t ci = B.conn_ids[L.idx];
+            const DevConn conn = ci < nconns ? B.conns[ci] : DevConn{-1, PROTO_NONE, 0, {0, 0}};
             // entries of other protocols belong to their own kernels; the HTTP
             // kernel answers entries whose connection is unknown or has no parser
             const bool mine = !(conn.proto == PROTO_KAFKA || conn.proto == PROTO_MEMCACHE);
             const bool http = mine && conn.proto == PROTO_HTTP && conn.ruleset >= 0 && (uint32_t)conn.ruleset < T.nrulesets;
             const bool is_hot = http && hot_ok && conn.ruleset == hot;
-            if (mine && !http && (kHot || !hot_ok)) L.owed = true;  // unsupported connection: answered as is
+            if (mine && !http && answer_other && (kHot || !hot_ok)) L.owed = true;  // unsupported connection: answered as is
             if (http && is_hot == kHot) {
-                const uint64_t off = offs[L.idx];
-                const uint32_t len = lens[L.idx];
-                if (off > arena_len || len > arena_len - off) {  // outside the arena: out of contract
+                const uint64_t off = B.offs[L.idx];
+                const uint32_t len = B.lens[L.idx];
+                if (!l7_in_arena(off, len, B.arena_len)) {  // outside the arena: out of contract
                     L.owed = true;
                 } else {
                 const uint64_t a = (uint64_t)(arena + off);
@@ -1024,11 +1026,9 @@ __global__ __launch_bounds__(kBlock) void http_classify_kernel(
 // Host-side launcher (called from the C-ABI): persistent grids of one
 // 512-thread workgroup per CU; the hot-rule-set kernel, then (only if some
 // HTTP connection uses another rule set) the general one.
-hipError_t LaunchHttpClassify(const uint8_t *arena, uint64_t arena_len, const uint64_t *offs, const uint32_t *lens,
-                              const uint32_t *conn_ids, uint32_t n, const DevConn *conns, uint32_t nconns,
-                              const HttpTables &T, bool any_cold, uint8_t *verdict, int32_t *rule, uint32_t *consumed,
-                              uint64_t *counters, uint32_t ncounters, hipStream_t stream) {
-    if (n == 0) return hipSuccess;
+hipError_t LaunchHttpClassify(const Batch &B, const HttpTables &T, bool any_cold, bool answer_other,
+                              hipStream_t stream) {
+    if (B.n == 0) return hipSuccess;
     static int num_cus = 0;
     if (num_cus == 0) {
         int dev = 0;
@@ -1036,16 +1036,15 @@ hipError_t LaunchHttpClassify(const uint8_t *arena, uint64_t arena_len, const ui
             hipDeviceGetAttribute(&num_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || num_cus <= 0)
             num_cus = 256;
     }
-    const uint32_t ntiles = (n + 63) / 64;
+    const uint32_t ntiles = (B.n + 63) / 64;
     uint32_t blocks = (ntiles + kWaves - 1) / kWaves;
     blocks = min(blocks, (uint32_t)num_cus);
     const bool hot = T.hot_ruleset >= 0;
+    const uint32_t other = answer_other ? 1u : 0u;
     if (hot)
-        hipLaunchKernelGGL(http_classify_kernel<true>, dim3(blocks), dim3(kBlock), 0, stream, arena, offs, lens, conn_ids,
-                           n, conns, nconns, T, verdict, rule, consumed, counters, ncounters, arena_len);
+        hipLaunchKernelGGL(http_classify_kernel<true>, dim3(blocks), dim3(kBlock), 0, stream, B, T, other);
     if (!hot || any_cold)
-        hipLaunchKernelGGL(http_classify_kernel<false>, dim3(blocks), dim3(kBlock), 0, stream, arena, offs, lens,
-                           conn_ids, n, conns, nconns, T, verdict, rule, consumed, counters, ncounters, arena_len);
+        hipLaunchKernelGGL(http_classify_kernel<false>, dim3(blocks), dim3(kBlock), 0, stream, B, T, other);
     return hipGetLastError();
 }
 

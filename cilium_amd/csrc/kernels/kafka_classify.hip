@@ -252,11 +252,12 @@ __device__ __forceinline__ uint32_t topic_first(const KafkaTables &T, const DevK
 }  // namespace
 
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) void kafka_classify_kernel(
-    const uint8_t *__restrict__ arena, const uint64_t *__restrict__ offs, const uint32_t *__restrict__ lens,
-    const uint32_t *__restrict__ conn_ids, uint32_t n, const DevConn *__restrict__ conns, uint32_t nconns,
-    KafkaTables T, uint8_t *__restrict__ out_verdict, int32_t *__restrict__ out_rule, uint32_t *__restrict__ out_consumed,
-    uint64_t *__restrict__ counters, uint32_t ncounters, const uint32_t *__restrict__ sel,
-    const uint32_t *__restrict__ sel_count) {
+    Batch B, KafkaTables T, const uint32_t *__restrict__ sel, const uint32_t *__restrict__ sel_count) {
+    const uint32_t n = B.n, nconns = B.nconns, ncounters = B.ncounters;
+    const uint8_t *__restrict__ arena = B.arena;
+    const uint32_t *__restrict__ conn_ids = B.conn_ids;
+    const DevConn *__restrict__ conns = B.conns;
+    uint64_t *__restrict__ counters = B.counters;
     static_assert(kBlock == 256, "one CRC table entry per thread");
     __shared__ uint32_t crctab[8 * 256];
     __shared__ uint32_t s_verdicts[8];
@@ -293,8 +294,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
         if (ci >= nconns) continue;
         const DevConn conn = conns[ci];
         if (conn.proto != PROTO_KAFKA) continue;
-        const uint8_t *b = arena + offs[idx];
-        const uint32_t len = lens[idx];
+        const uint64_t off = B.offs[idx];
+        const uint32_t len = B.lens[idx];
+        const uint8_t *b = arena + off;
         Cur cur;
         cur.line = ~(uintptr_t)0;
         uint8_t verdict = V_PARSE_ERROR;
@@ -302,6 +304,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
         uint32_t consumed = 0;
         // ---- proto.ReadReq
         do {
+            if (!l7_in_arena(off, len, B.arena_len)) { verdict = V_UNSUPPORTED; break; }
             if (len < 4) { verdict = V_INCOMPLETE; break; }
             const int32_t size = (int32_t)be_load(cur, b, 4);
             if (size <= 0) { verdict = V_PARSE_ERROR; break; }
@@ -463,9 +466,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
             }
             if (best != kInf) { verdict = V_ALLOW; rule = T.rules[rs.rule_first + best].gid; }
         } while (false);
-        out_verdict[idx] = verdict;
-        out_rule[idx] = rule;
-        out_consumed[idx] = consumed;
+        B.verdict[idx] = verdict;
+        B.rule[idx] = rule;
+        B.consumed[idx] = consumed;
         if (counters) {
             atomicAdd(&s_verdicts[verdict], 1u);  // per-verdict totals: one global atomic per block
             if (rule >= 0 && (uint32_t)rule < ncounters - 8) atomicAdd((unsigned long long *)&counters[rule], 1ull);
@@ -478,15 +481,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
     }
 }
 
-hipError_t LaunchKafkaClassify(const uint8_t *arena, const uint64_t *offs, const uint32_t *lens, const uint32_t *conn_ids,
-                               uint32_t n, const DevConn *conns, uint32_t nconns, const KafkaTables &T,
-                               uint8_t *verdict, int32_t *rule, uint32_t *consumed, uint64_t *counters,
-                               uint32_t ncounters, const uint32_t *sel, const uint32_t *sel_count, hipStream_t stream) {
-    if (n == 0) return hipSuccess;
-    uint32_t blocks = (n + kBlock - 1) / kBlock;
+hipError_t LaunchKafkaClassify(const Batch &B, const KafkaTables &T, const uint32_t *sel, const uint32_t *sel_count,
+                               hipStream_t stream) {
+    if (B.n == 0) return hipSuccess;
+    uint32_t blocks = (B.n + kBlock - 1) / kBlock;
     if (blocks > 8192) blocks = 8192;
-    hipLaunchKernelGGL(kafka_classify_kernel, dim3(blocks), dim3(kBlock), 0, stream, arena, offs, lens, conn_ids, n,
-                       conns, nconns, T, verdict, rule, consumed, counters, ncounters, sel, sel_count);
+    hipLaunchKernelGGL(kafka_classify_kernel, dim3(blocks), dim3(kBlock), 0, stream, B, T, sel, sel_count);
     return hipGetLastError();
 }
 

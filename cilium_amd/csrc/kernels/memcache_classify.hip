@@ -170,12 +170,13 @@ __device__ __forceinline__ void classify_cmd(const uint32_t cw[4], uint32_t clen
 
 }  // namespace
 
-__global__ __launch_bounds__(kBlock) void memcache_classify_kernel(
-    const uint8_t *__restrict__ arena, const uint64_t *__restrict__ offs, const uint32_t *__restrict__ lens,
-    const uint32_t *__restrict__ conn_ids, uint32_t n, const DevConn *__restrict__ conns, uint32_t nconns,
-    McTables T, uint8_t *__restrict__ out_verdict, int32_t *__restrict__ out_rule, uint32_t *__restrict__ out_consumed,
-    uint64_t *__restrict__ counters, uint32_t ncounters, const uint32_t *__restrict__ sel,
-    const uint32_t *__restrict__ sel_count) {
+__global__ __launch_bounds__(kBlock) void memcache_classify_kernel(Batch B, McTables T,
+                                                                   const uint32_t *__restrict__ sel,
+                                                                   const uint32_t *__restrict__ sel_count) {
+    const uint32_t n = B.n, nconns = B.nconns, ncounters = B.ncounters;
+    const uint32_t *__restrict__ conn_ids = B.conn_ids;
+    const DevConn *__restrict__ conns = B.conns;
+    uint64_t *__restrict__ counters = B.counters;
     __shared__ uint32_t s_verdicts[8];
     if (threadIdx.x < 8) s_verdicts[threadIdx.x] = 0;
     __syncthreads();
@@ -196,11 +197,13 @@ __global__ __launch_bounds__(kBlock) void memcache_classify_kernel(
             I.terminal = (h0 >> 8) & 0xFF;
             I.ndfa = (h0 >> 16) & 0xFF;
         }
-        const uint8_t *b = arena + offs[idx];
-        const uint32_t len = lens[idx];
+        const uint64_t off = B.offs[idx];
+        const uint32_t len = B.lens[idx];
+        const uint8_t *b = B.arena + off;
         uint8_t verdict = V_PARSE_ERROR;
         int32_t rule = -1;
         uint32_t consumed = 0;
+        const bool in_arena = l7_in_arena(off, len, B.arena_len);
         Keys K;
 #pragma unroll
         for (int c = 0; c < kMcMaxChunks; c++) K.all[c] = ~0ull;
@@ -209,7 +212,8 @@ __global__ __launch_bounds__(kBlock) void memcache_classify_kernel(
         bool staged = false;  // framing succeeded: match against the rules
         // More key DFAs than one pass walks: re-read the request once per
         // group of kMcMaxDfas (framing is identical in every pass).
-        for (uint32_t d0 = 0;; d0 += kMcMaxDfas) {
+        if (!in_arena) verdict = V_UNSUPPORTED;  // out of contract: nothing is read
+        for (uint32_t d0 = 0; in_arena; d0 += kMcMaxDfas) {
         I.d0 = d0;
         I.dn = I.ndfa - d0 < (uint32_t)kMcMaxDfas ? I.ndfa - d0 : (uint32_t)kMcMaxDfas;
         keys_reset(I, K);
@@ -327,9 +331,9 @@ __global__ __launch_bounds__(kBlock) void memcache_classify_kernel(
                 if (ok) { verdict = V_ALLOW; rule = ids[c * 64 + __builtin_ctzll(ok)]; break; }
             }
         } while (false);
-        out_verdict[idx] = verdict;
-        out_rule[idx] = rule;
-        out_consumed[idx] = consumed;
+        B.verdict[idx] = verdict;
+        B.rule[idx] = rule;
+        B.consumed[idx] = consumed;
         if (counters) {
             atomicAdd(&s_verdicts[verdict], 1u);  // per-verdict totals: one global atomic per block
             if (rule >= 0 && (uint32_t)rule < ncounters - 8) atomicAdd((unsigned long long *)&counters[rule], 1ull);
@@ -342,15 +346,12 @@ __global__ __launch_bounds__(kBlock) void memcache_classify_kernel(
     }
 }
 
-hipError_t LaunchMemcacheClassify(const uint8_t *arena, const uint64_t *offs, const uint32_t *lens,
-                                  const uint32_t *conn_ids, uint32_t n, const DevConn *conns, uint32_t nconns,
-                                  const McTables &T, uint8_t *verdict, int32_t *rule, uint32_t *consumed,
-                                  uint64_t *counters, uint32_t ncounters, const uint32_t *sel, const uint32_t *sel_count, hipStream_t stream) {
-    if (n == 0) return hipSuccess;
-    uint32_t blocks = (n + kBlock - 1) / kBlock;
+hipError_t LaunchMemcacheClassify(const Batch &B, const McTables &T, const uint32_t *sel, const uint32_t *sel_count,
+                                  hipStream_t stream) {
+    if (B.n == 0) return hipSuccess;
+    uint32_t blocks = (B.n + kBlock - 1) / kBlock;
     if (blocks > 8192) blocks = 8192;
-    hipLaunchKernelGGL(memcache_classify_kernel, dim3(blocks), dim3(kBlock), 0, stream, arena, offs, lens, conn_ids, n,
-                       conns, nconns, T, verdict, rule, consumed, counters, ncounters, sel, sel_count);
+    hipLaunchKernelGGL(memcache_classify_kernel, dim3(blocks), dim3(kBlock), 0, stream, B, T, sel, sel_count);
     return hipGetLastError();
 }
 

@@ -31,29 +31,36 @@ __device__ __forceinline__ uint8_t kafka_class(uint32_t len) {
 }
 }  // namespace
 
-// Lists: Kafka class c at sel_kafka + c * n, memcached at sel_mc; counts[c] entries each.
-__global__ __launch_bounds__(kBlock) void partition_kernel(const uint32_t *__restrict__ conn_ids,
-                                                           const uint32_t *__restrict__ lens, uint32_t n,
-                                                           const DevConn *__restrict__ conns, uint32_t nconns,
-                                                           uint32_t *__restrict__ sel_kafka,
+// Lists: Kafka class c at sel_kafka + c * n, memcached at sel_mc; counts[c]
+// entries each.  Requests no classifier owns (unknown connection index, a
+// connection without a parser) are answered here: UNSUPPORTED, rule -1,
+// consumed 0, so every request of the batch gets a verdict whichever
+// classifiers run (the HTTP kernel is then told not to answer them again).
+__global__ __launch_bounds__(kBlock) void partition_kernel(Batch B, uint32_t *__restrict__ sel_kafka,
                                                            uint32_t *__restrict__ sel_mc,
                                                            uint32_t *__restrict__ counts) {
+    const uint32_t n = B.n;
     __shared__ uint32_t s_off[kWaves][kClasses];
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint64_t start = (uint64_t)blockIdx.x * (kBlock * kPer);
     const uint64_t below = (1ull << lane) - 1;
     uint8_t p[kPer];  // class + 1, 0 = none
     uint32_t cnt[kClasses] = {};
+    uint32_t other = 0;
 #pragma unroll
     for (int r = 0; r < kPer; r++) {
         const uint64_t idx = start + (uint64_t)r * kBlock + threadIdx.x;
         uint8_t cls = 0;
         if (idx < n) {
-            const uint32_t ci = conn_ids[idx];
-            if (ci < nconns) {
-                const uint8_t proto = conns[ci].proto;
-                if (proto == PROTO_KAFKA) cls = 1 + kafka_class(lens[idx]);
-                else if (proto == PROTO_MEMCACHE) cls = 1 + kKafkaClasses;
+            const uint32_t ci = B.conn_ids[idx];
+            const uint8_t proto = ci < B.nconns ? B.conns[ci].proto : PROTO_NONE;
+            if (proto == PROTO_KAFKA) cls = 1 + kafka_class(B.lens[idx]);
+            else if (proto == PROTO_MEMCACHE) cls = 1 + kKafkaClasses;
+            else if (proto != PROTO_HTTP) {
+                B.verdict[idx] = V_UNSUPPORTED;
+                B.rule[idx] = -1;
+                B.consumed[idx] = 0;
+                other++;
             }
         }
         p[r] = cls;
@@ -62,6 +69,11 @@ __global__ __launch_bounds__(kBlock) void partition_kernel(const uint32_t *__res
     }
     if (lane == 0)
         for (int c = 0; c < kClasses; c++) s_off[wave][c] = cnt[c];
+    if (B.counters) {  // per-verdict total of the answered requests
+        for (int o = 32; o > 0; o >>= 1) other += __shfl_xor(other, o);
+        if (lane == 0 && other)
+            atomicAdd((unsigned long long *)&B.counters[B.ncounters - 8 + V_UNSUPPORTED], (unsigned long long)other);
+    }
     __syncthreads();
     if (threadIdx.x < kClasses) {
         const int c = threadIdx.x;
@@ -94,13 +106,10 @@ __global__ __launch_bounds__(kBlock) void partition_kernel(const uint32_t *__res
 }
 
 // counts[0..kClasses) must be zero on entry (the caller clears them on `stream`).
-hipError_t LaunchPartition(const uint32_t *conn_ids, const uint32_t *lens, uint32_t n, const DevConn *conns,
-                           uint32_t nconns, uint32_t *sel_kafka, uint32_t *sel_mc, uint32_t *counts,
-                           hipStream_t stream) {
-    if (n == 0) return hipSuccess;
-    const uint32_t blocks = (uint32_t)(((uint64_t)n + kBlock * kPer - 1) / (kBlock * kPer));
-    hipLaunchKernelGGL(partition_kernel, dim3(blocks), dim3(kBlock), 0, stream, conn_ids, lens, n, conns, nconns,
-                       sel_kafka, sel_mc, counts);
+hipError_t LaunchPartition(const Batch &B, uint32_t *sel_kafka, uint32_t *sel_mc, uint32_t *counts, hipStream_t stream) {
+    if (B.n == 0) return hipSuccess;
+    const uint32_t blocks = (uint32_t)(((uint64_t)B.n + kBlock * kPer - 1) / (kBlock * kPer));
+    hipLaunchKernelGGL(partition_kernel, dim3(blocks), dim3(kBlock), 0, stream, B, sel_kafka, sel_mc, counts);
     return hipGetLastError();
 }
 

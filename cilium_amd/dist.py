@@ -42,17 +42,29 @@ def allreduce_counters(counters, dist):
     return counters
 
 
-def shard_by_connection(conn_ids, lengths, nconns, world):
-    """Assign whole connections to ranks as contiguous connection ranges with
-    balanced payload bytes (a connection's stream stays on one GPU: framing
-    state, reply queues).  Returns (owner[nconns], request index list per rank)."""
+def shard_by_connection(conn_ids, lengths, nconns, world, conn_proto=None):
+    """Assign whole connections to ranks (a connection's stream stays on one
+    GPU: framing state, reply queues, Kafka close-on-error) so that every rank
+    gets an equal share of the payload bytes -- of each protocol separately
+    when conn_proto (protocol per connection) is given, since an HTTP byte, a
+    Kafka byte and a memcached byte do not cost the same device time.  Within
+    a protocol, ranks own contiguous connection-id ranges.  Returns
+    (owner[nconns], sorted request index array per rank)."""
     conn_ids = np.asarray(conn_ids, np.int64)
-    per_conn = np.bincount(conn_ids, weights=np.asarray(lengths, np.float64), minlength=nconns)
-    cum = np.cumsum(per_conn)
-    total = cum[-1] if nconns else 0.0
-    # connection c goes to the rank whose byte range holds its midpoint
-    mid = cum - per_conn / 2
-    owner = np.minimum((mid * world // max(total, 1.0)).astype(np.int64), world - 1) if nconns else np.zeros(0, np.int64)
-    owner = np.maximum.accumulate(owner)  # contiguous, non-decreasing ranges
-    req_owner = owner[conn_ids]
+    per_conn = np.bincount(conn_ids, weights=np.asarray(lengths, np.float64), minlength=nconns)[:nconns]
+    owner = np.zeros(nconns, np.int64)
+    groups = [np.arange(nconns)] if conn_proto is None else \
+        [np.nonzero(np.asarray(conn_proto) == p)[0] for p in np.unique(conn_proto)]
+    for g in groups:
+        if len(g) == 0:
+            continue
+        b = per_conn[g]
+        cum = np.cumsum(b)
+        total = cum[-1]
+        # connection c goes to the rank whose byte range holds its midpoint
+        mid = cum - b / 2
+        o = np.minimum((mid * world // max(total, 1.0)).astype(np.int64), world - 1)
+        owner[g] = np.maximum.accumulate(o)  # contiguous, non-decreasing ranges
+    valid = conn_ids < nconns
+    req_owner = np.where(valid, owner[np.minimum(conn_ids, max(nconns - 1, 0))], conn_ids % max(world, 1))
     return owner, [np.nonzero(req_owner == r)[0] for r in range(world)]

@@ -93,6 +93,22 @@ class Engine:
             raise RuntimeError(f"l7g_classify_host failed: HIP error {rc}")
         return v, r, c
 
+    STAGES = ("partition", "http", "kafka", "memcache")
+
+    def profile(self, on=True):
+        """Record HIP events around each kernel of every l7g_classify call."""
+        rc = self._lib.l7g_profile_enable(self._h, 1 if on else 0)
+        if rc != 0:
+            raise RuntimeError(f"l7g_profile_enable failed: HIP error {rc}")
+
+    def profile_last(self):
+        """Device ms per stage of the last classify call (profiling on)."""
+        out = np.zeros(4, np.float32)
+        rc = self._lib.l7g_profile_last(self._h, out.ctypes.data)
+        if rc != 0:
+            raise RuntimeError(f"l7g_profile_last failed: HIP error {rc}")
+        return dict(zip(self.STAGES, out.tolist()))
+
     def phase_times(self, reset=True):
         """Per-phase cycle totals of the HTTP kernel (timing build only), or None."""
         out = np.zeros(8, np.uint64)

@@ -617,6 +617,45 @@ def mixed_workload(n, seed=None):
     return Workload("cfg5", arena2, offs2, lens2, cids[perm], conns, pol, {"payload_bytes": payload})
 
 
+PROTO_NAMES = {PROTO_HTTP: "http", PROTO_KAFKA: "kafka", PROTO_MEMCACHE: "memcache"}
+
+
+def protocol_bytes(w):
+    """Per protocol: request count and the payload bytes its classifier must
+    read (every byte for HTTP and Kafka; for memcached the
+    command line, or the 24-byte header + extras + key).  Algorithmic bytes
+    of a protocol's kernel = payload + 25 per request."""
+    proto = w.conns["proto"][np.minimum(w.conn_ids, len(w.conns) - 1)] if len(w.conns) else np.zeros(w.n, np.uint8)
+    proto = np.where(w.conn_ids < len(w.conns), proto, 0)
+    out = {}
+    for p, name in PROTO_NAMES.items():
+        sel = np.nonzero(proto == p)[0]
+        if p == PROTO_MEMCACHE:
+            buf = w.arena
+            reqs = (bytes(buf[int(w.offsets[i]):int(w.offsets[i]) + int(w.lengths[i])]) for i in sel)
+            payload = mc_inspected_bytes(reqs)
+        else:
+            payload = int(w.lengths[sel].astype(np.int64).sum())
+        out[name] = {"requests": int(len(sel)), "payload": int(payload)}
+    return out
+
+
+def select(w, idx, name=None):
+    """The requests idx of w repacked into a compact arena of their own (one
+    rank's connection shard), in the same order."""
+    idx = np.asarray(idx, np.int64)
+    offs = w.offsets[idx].astype(np.int64)
+    lens = w.lengths[idx].astype(np.int64)
+    new_offs = np.zeros(len(idx), np.uint64)
+    if len(idx) > 1:
+        new_offs[1:] = np.cumsum(lens[:-1]).astype(np.uint64)
+    mv = memoryview(np.ascontiguousarray(w.arena))
+    arena = np.frombuffer(b"".join(mv[o:o + n] for o, n in zip(offs.tolist(), lens.tolist())), np.uint8)
+    meta = {}
+    return Workload(name or (w.name + "[shard]"), np.ascontiguousarray(arena), new_offs, w.lengths[idx].copy(),
+                    w.conn_ids[idx].copy(), w.conns, w.policy, meta)
+
+
 def tile_offsets(w, k):
     """Request metadata for k back-to-back copies of w's arena (copy j at byte
     offset j * len(arena)).  The arena itself is replicated on the device, so a

@@ -24,7 +24,8 @@
  *                                                                  proxylib/proxylib.go:97-110,
  *                                                                  proxylib/memcached/parser.go:186-202,
  *                                                                  proxylib/proxylib/policymap.go:210-236
- *   l7g_counters        Endpoint.UpdateProxyStatistics counters    pkg/endpoint/endpoint.go:2207-2233
+ *   counters argument   Endpoint.UpdateProxyStatistics counters    pkg/endpoint/endpoint.go:2207-2233
+ *   of l7g_classify     (per-rule allow hits + per-verdict totals, accumulated on the device)
  *
  * Verdict codes match the oracle (oracle/l7ref.h) and DESIGN.md.
  */
@@ -123,6 +124,13 @@ int l7g_classify_host(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, c
                       uint32_t *consumed);
 
 int l7g_stats(l7g_engine *e, l7g_stats_t *out);
+
+/* Measurement hook (bench.py): with profiling on, l7g_classify records HIP
+ * events on its stream around each kernel it launches; l7g_profile_last waits
+ * for the last call and returns the device time in ms of its four stages
+ * (partition, HTTP, Kafka, memcached; 0 = not launched).  Off by default. */
+int l7g_profile_enable(l7g_engine *e, int on);
+int l7g_profile_last(l7g_engine *e, float out_ms[4]);
 
 /* Profiling hook: per-phase cycle totals of the HTTP kernel (slots: 0 window
  * DMA, 1 parse, 2 long-value scan, 3 other, 4 rounds, 5 scanned values,
