@@ -20,9 +20,9 @@ namespace l7 {
 hipError_t LaunchHttpClassify(const Batch &B, const HttpTables &T, bool any_cold, bool answer_other,
                               hipStream_t stream);
 hipError_t LaunchKafkaClassify(const Batch &B, const KafkaTables &T, const uint32_t *sel, const uint32_t *sel_count,
-                               hipStream_t stream);
+                               bool answer_other, hipStream_t stream);
 hipError_t LaunchMemcacheClassify(const Batch &B, const McTables &T, const uint32_t *sel, const uint32_t *sel_count,
-                                  hipStream_t stream);
+                                  bool answer_other, hipStream_t stream);
 hipError_t LaunchPartition(const Batch &B, uint32_t *sel_kafka, uint32_t *sel_mc, uint32_t *counts, hipStream_t stream);
 hipError_t HttpPhaseTimes(uint64_t *out, bool reset);
 }  // namespace l7
@@ -355,13 +355,14 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
     B.ncounters = counters ? (uint32_t)e->ps->nrules + 8 : 0;
     if (n == 0) return 0;
     // The kernels each classify only their own protocol's requests, so a
-    // mixed batch needs one launch per protocol present.  Unless the batch can
-    // hold HTTP requests only, partition_kernel runs first: it writes the
-    // Kafka (by length class) and memcached index lists the other two kernels
-    // walk, and it answers the requests no classifier owns (unknown
-    // connection, no parser) itself.  An HTTP-only engine skips it; its HTTP
-    // kernel answers those.
-    const bool partitioned = e->has_kafka || e->has_mc;
+    // mixed batch needs one launch per protocol present.  When the engine
+    // serves more than one protocol, partition_kernel runs first: it writes
+    // the Kafka and memcached index lists those two kernels walk, and answers
+    // the requests no classifier owns (unknown connection, no parser) itself.
+    // A single-protocol engine skips it; its one kernel walks the whole batch
+    // and answers those requests.
+    const int nproto = (int)e->has_http + (int)e->has_kafka + (int)e->has_mc;
+    const bool partitioned = nproto > 1;
     uint32_t *sel_k = nullptr, *sel_m = nullptr, *cnt = nullptr;
     if (partitioned) {
         const size_t need = 16 + (L7_KAFKA_CLASSES + 1) * (size_t)n;
@@ -388,16 +389,17 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
     auto mark = [&](int k) {
         if (prof && rc == hipSuccess) rc = hipEventRecord(e->prof_ev[k], s);
     };
-    const bool run[4] = {partitioned, e->has_http || !partitioned, e->has_kafka, e->has_mc};
+    const bool run[4] = {partitioned, e->has_http || nproto == 0, e->has_kafka, e->has_mc};
     for (int k = 0; k < 4; k++) e->prof_ran[k] = run[k];
     mark(0);
     if (rc == hipSuccess && run[0]) rc = LaunchPartition(B, sel_k, sel_m, cnt, s);
     mark(1);
     if (rc == hipSuccess && run[1]) rc = LaunchHttpClassify(B, e->ht, e->any_cold, !partitioned, s);
     mark(2);
-    if (rc == hipSuccess && run[2]) rc = LaunchKafkaClassify(B, e->kt, sel_k, cnt, s);
+    if (rc == hipSuccess && run[2]) rc = LaunchKafkaClassify(B, e->kt, sel_k, cnt, !partitioned, s);
     mark(3);
-    if (rc == hipSuccess && run[3]) rc = LaunchMemcacheClassify(B, e->mt, sel_m, cnt + L7_KAFKA_CLASSES, s);
+    if (rc == hipSuccess && run[3])
+        rc = LaunchMemcacheClassify(B, e->mt, sel_m, cnt ? cnt + L7_KAFKA_CLASSES : nullptr, !partitioned, s);
     mark(4);
     if (rc == hipSuccess) rc = hipEventRecord(e->done_ev, s);
     if (rc == hipSuccess) e->launched = true;

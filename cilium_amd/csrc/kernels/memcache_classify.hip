@@ -170,9 +170,13 @@ __device__ __forceinline__ void classify_cmd(const uint32_t cw[4], uint32_t clen
 
 }  // namespace
 
+// sel: this protocol's request indices (partition_kernel, mixed batches), else
+// requests 0..n-1.  answer_other: answer entries on connections that are not
+// memcached (single-protocol engines, where partition_kernel does not run).
 __global__ __launch_bounds__(kBlock) void memcache_classify_kernel(Batch B, McTables T,
                                                                    const uint32_t *__restrict__ sel,
-                                                                   const uint32_t *__restrict__ sel_count) {
+                                                                   const uint32_t *__restrict__ sel_count,
+                                                                   uint32_t answer_other) {
     const uint32_t n = B.n, nconns = B.nconns, ncounters = B.ncounters;
     const uint32_t *__restrict__ conn_ids = B.conn_ids;
     const DevConn *__restrict__ conns = B.conns;
@@ -185,9 +189,16 @@ __global__ __launch_bounds__(kBlock) void memcache_classify_kernel(Batch B, McTa
     for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < m; i += gridDim.x * kBlock) {
         const uint32_t idx = sel ? sel[i] : i;
         const uint32_t ci = conn_ids[idx];
-        if (ci >= nconns) continue;
-        const DevConn conn = conns[ci];
-        if (conn.proto != PROTO_MEMCACHE || conn.ruleset < 0 || (uint32_t)conn.ruleset >= T.nrulesets) continue;
+        const DevConn conn = ci < nconns ? conns[ci] : DevConn{-1, PROTO_NONE, 0, {0, 0}};
+        if (conn.proto != PROTO_MEMCACHE || conn.ruleset < 0 || (uint32_t)conn.ruleset >= T.nrulesets) {
+            if (answer_other && conn.proto != PROTO_HTTP && conn.proto != PROTO_KAFKA) {  // no parser: UNSUPPORTED
+                B.verdict[idx] = V_UNSUPPORTED;
+                B.rule[idx] = -1;
+                B.consumed[idx] = 0;
+                if (counters) atomicAdd(&s_verdicts[V_UNSUPPORTED], 1u);
+            }
+            continue;
+        }
         const DevRuleset rs = T.rulesets[conn.ruleset];
         Image I;
         I.p = T.images + rs.image_off;
@@ -347,11 +358,12 @@ __global__ __launch_bounds__(kBlock) void memcache_classify_kernel(Batch B, McTa
 }
 
 hipError_t LaunchMemcacheClassify(const Batch &B, const McTables &T, const uint32_t *sel, const uint32_t *sel_count,
-                                  hipStream_t stream) {
+                                  bool answer_other, hipStream_t stream) {
     if (B.n == 0) return hipSuccess;
     uint32_t blocks = (B.n + kBlock - 1) / kBlock;
     if (blocks > 8192) blocks = 8192;
-    hipLaunchKernelGGL(memcache_classify_kernel, dim3(blocks), dim3(kBlock), 0, stream, B, T, sel, sel_count);
+    hipLaunchKernelGGL(memcache_classify_kernel, dim3(blocks), dim3(kBlock), 0, stream, B, T, sel, sel_count,
+                       answer_other ? 1u : 0u);
     return hipGetLastError();
 }
 

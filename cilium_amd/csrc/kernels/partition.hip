@@ -25,7 +25,9 @@ constexpr int kWaves = kBlock / 64;
 constexpr int kKafkaClasses = L7_KAFKA_CLASSES;
 constexpr int kClasses = kKafkaClasses + 1;
 
+static_assert(kKafkaClasses == 1 || kKafkaClasses == 8, "length classes");
 __device__ __forceinline__ uint8_t kafka_class(uint32_t len) {
+    if (kKafkaClasses == 1) return 0;
     return len < 192 ? 0 : len < 384 ? 1 : len < 640 ? 2 : len < 896 ? 3 : len < 1280 ? 4 : len < 2048 ? 5
          : len < 4096 ? 6 : 7;
 }

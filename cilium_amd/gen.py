@@ -178,10 +178,10 @@ def cfg4_workload(n, nids=512, rules_total=10000, seed=None, unknown_frac=0.02):
     source identity is uniform over the 512 (+2% unknown => deny)."""
     seed = SEED_BASE + 4 if seed is None else seed
     rng = np.random.default_rng(seed)
-    per = rules_total // nids
+    per, extra = divmod(rules_total, nids)  # the first `extra` identities get one more rule
     groups = []
     for g in range(nids):
-        ks = rng.integers(0, 4096, size=per)
+        ks = rng.integers(0, 4096, size=per + (1 if g < extra else 0))
         rules = [cfg2_rules(int(k), 1)[0] for k in ks]
         groups.append(api.port_rule(remote_policies=[256 + g], http=api.http_rules_from_api(rules)))
     pol = api.policy_set(api.network_policy("10.0.0.1", 3, ingress=[(80, groups)]))

@@ -38,7 +38,7 @@ def test_cfg4_full_size_parity_and_counters(engine, oracle, cfg4):
     engine.update_policy(w.policy)
     engine.set_connections(w.conns)
     nrules = engine.nrules
-    assert nrules >= 9_900
+    assert nrules == 10_000
     st = engine.stats()
     assert st["http_rulesets"] >= 512
     dev = torch.device("cuda", 0)
