@@ -39,16 +39,18 @@ EXPORTS = (
     "l7g_debug_regex", "l7g_debug_phase_times", "l7g_profile_enable", "l7g_profile_last",
 )
 
-_lib = None
+_libs = {}
 
 
-def load():
-    global _lib
-    if _lib is not None:
-        return _lib
-    if not os.path.exists(LIB_PATH):
-        raise RuntimeError(f"{LIB_PATH} is missing: run python -m cilium_amd.build (no CPU fallback exists)")
-    lib = C.CDLL(LIB_PATH)
+def load(path=None):
+    """The product library (or, for kernel experiments, a variant build of it
+    named by path: tools/exp_*.py)."""
+    path = path or LIB_PATH
+    if path in _libs:
+        return _libs[path]
+    if not os.path.exists(path):
+        raise RuntimeError(f"{path} is missing: run python -m cilium_amd.build (no CPU fallback exists)")
+    lib = C.CDLL(path)
     vp, sz, cp = C.c_void_p, C.c_size_t, C.c_char_p
     lib.l7g_engine_create.restype = vp
     lib.l7g_engine_create.argtypes = [C.c_int, cp, sz]
@@ -67,7 +69,7 @@ def load():
     lib.l7g_debug_phase_times.argtypes = [vp, vp, C.c_int]
     lib.l7g_profile_enable.argtypes = [vp, C.c_int]
     lib.l7g_profile_last.argtypes = [vp, vp]
-    _lib = lib
+    _libs[path] = lib
     return lib
 
 

@@ -253,37 +253,15 @@ __device__ __forceinline__ uint32_t topic_first(const KafkaTables &T, const DevK
     return kInf;
 }
 
-// ------------------------------------------------------------------ per-wave CRC queue
-struct Queue {
-    uint4 *items;     // {addr lo, addr hi, stored crc, len | lane << 26}
-    uint32_t *count;  // items claimed (may exceed kQueue: overflow)
-};
+// ------------------------------------------------------------------ exact decode (redo path)
+// The reference's decode of one request, sequential, CRC checked inline.
+// Lanes whose request the fast path cannot finish exactly (a message CRC that
+// does not match) take it; it is kept out of line.
+enum : int { RS_OK = 0, RS_ERROR = -1, RS_COMPRESSED = -2 };
 
-// Append a CRC work item for the calling lane; false if the queue is full.
-// Called in divergent code: the active lanes take consecutive slots.
-__device__ __forceinline__ bool queue_push(const Queue &Q, uint32_t lane, const uint8_t *p, uint32_t n, uint32_t crc) {
-    const uint64_t act = __ballot(1);
-    const uint32_t leader = (uint32_t)__builtin_ctzll(act);
-    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0));
-    uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(Q.count, (uint32_t)__builtin_popcountll(act));
-    base = (uint32_t)__shfl((int)base, (int)leader);
-    const uint32_t slot = base + rank;
-    if (slot >= kQueue || n >= (1u << 26)) return false;
-    const uint64_t a = (uint64_t)(uintptr_t)p;
-    Q.items[slot] = make_uint4((uint32_t)a, (uint32_t)(a >> 32), crc, n | lane << 26);
-    return true;
-}
-
-// ------------------------------------------------------------------ one request
-enum : int { RS_OK = 0, RS_ERROR = -1, RS_COMPRESSED = -2, RS_OVERFLOW = -3 };
-
-// readMessageSet on the shared position (messages.go:363-494).  kExact: check
-// each CRC here; else queue it (assumed to match) and read on.
-template <bool kExact>
+// readMessageSet on the shared position (messages.go:363-494)
 __device__ __forceinline__ int read_message_set(Cur &cur, const uint8_t *b, uint32_t &pos, uint32_t end, int32_t size,
-                                                int16_t version, const uint32_t *crctab, const Queue &Q,
-                                                uint32_t lane) {
+                                                int16_t version, const uint32_t *crctab) {
     if (size < 0) return RS_OK;
     if ((uint32_t)size > kMaxParseBuf) return RS_ERROR;
     KDec dec{b, pos, end, size, 0, &cur};
@@ -299,12 +277,7 @@ __device__ __forceinline__ int read_message_set(Cur &cur, const uint8_t *b, uint
         KDec md{b, at, at + (uint32_t)msize, -1, 0, &cur};
         uint32_t crc = (uint32_t)dec_int(md, 4);
         if (msize <= 4) break;
-        if (kExact) {
-            if (crc != crc32_ieee(crctab, cur, b + at + 4, (uint32_t)msize - 4)) break;  // stop, no drain
-        } else if (!queue_push(Q, lane, b + at + 4, (uint32_t)msize - 4, crc)) {
-            rc = RS_OVERFLOW;
-            break;
-        }
+        if (crc != crc32_ieee(crctab, cur, b + at + 4, (uint32_t)msize - 4)) break;  // stop, no drain
         (void)dec_int(md, 1);
         int8_t attr = (int8_t)dec_int(md, 1);
         if (version >= 1) (void)dec_int(md, 8);
@@ -325,33 +298,65 @@ struct Result {
     uint32_t consumed;
 };
 
-// proto.ReadReq + kafka.ReadRequest + canAccess/MatchesRule for one request.
-// Returns false (kExact = false only) if the CRC queue overflowed.
-template <bool kExact>
-__device__ __forceinline__ bool classify_one(const KafkaTables &T, const DevConn &conn, const uint8_t *b, uint32_t len,
-                             const uint32_t *crctab, const Queue &Q, uint32_t lane, Result &out) {
-    Cur cur;
-    cur.line = ~(uintptr_t)0;
+// MatchesRule (policy.go:200-225) from the raw topic count and the topic
+// completion index cmax (max over topics of the first rule that matches it)
+__device__ __forceinline__ void match_rules(const KafkaTables &T, const DevKafkaRuleset &rs, const ReqInfo &q,
+                                            uint32_t ntopics, uint32_t cmax, uint32_t rawlen, Result &out) {
+    out.consumed = rawlen;
+    out.verdict = V_DENY;
+    out.rule = -1;
+    if (!rs.any) return;  // rules.Kafka == nil => deny (pkg/proxy/kafka.go:139-142)
+    uint32_t best = kInf;
+    if (ntopics == 0) {
+        const int key = (q.kind >= 0 && q.kind < 64) ? q.kind : 64;
+        const uint32_t off = T.index[rs.bykey_off + 2 * key], cnt = T.index[rs.bykey_off + 2 * key + 1];
+        for (uint32_t i = 0; i < cnt; i++) {
+            uint32_t p = T.index[off + i];
+            if (rule_matches(T.rules[rs.rule_first + p], q)) { best = p; break; }
+        }
+    } else {
+        for (uint32_t i = 0; i < rs.ntopicless; i++) {
+            uint32_t p = T.index[rs.topicless_off + i];
+            if (p >= cmax) break;  // cannot beat topic completion
+            if (rule_matches(T.rules[rs.rule_first + p], q)) { best = p; break; }
+        }
+        if (best == kInf) best = cmax;
+    }
+    if (best != kInf) { out.verdict = V_ALLOW; out.rule = T.rules[rs.rule_first + best].gid; }
+}
+
+// proto.ReadReq framing checks; false = answered (out set), else rawlen / kind / version
+__device__ __forceinline__ bool frame_request(Cur &cur, const uint8_t *b, uint32_t len, Result &out, uint32_t &rawlen,
+                                              ReqInfo &q) {
     out.verdict = V_PARSE_ERROR;
     out.rule = -1;
     out.consumed = 0;
-    // ---- proto.ReadReq (messages.go:124-165), kafka.ReadRequest (request.go:186-229)
-    if (len < 4) { out.verdict = V_INCOMPLETE; return true; }
+    // proto.ReadReq (messages.go:124-165), kafka.ReadRequest (request.go:186-229)
+    if (len < 4) { out.verdict = V_INCOMPLETE; return false; }
     const int32_t size = (int32_t)be_load(cur, b, 4);
-    if (size <= 0) { out.verdict = V_PARSE_ERROR; return true; }
-    if (len < 6) { out.verdict = V_INCOMPLETE; return true; }
-    if ((uint64_t)(uint32_t)size + 4 > kMaxParseBuf) { out.verdict = V_PARSE_ERROR; return true; }
-    const uint32_t rawlen = (uint32_t)size + 4;
-    if (rawlen > len) { out.verdict = V_INCOMPLETE; return true; }
-    if (rawlen < 12) { out.verdict = V_PARSE_ERROR; return true; }
-    ReqInfo q;
+    if (size <= 0) { out.verdict = V_PARSE_ERROR; return false; }
+    if (len < 6) { out.verdict = V_INCOMPLETE; return false; }
+    if ((uint64_t)(uint32_t)size + 4 > kMaxParseBuf) { out.verdict = V_PARSE_ERROR; return false; }
+    rawlen = (uint32_t)size + 4;
+    if (rawlen > len) { out.verdict = V_INCOMPLETE; return false; }
+    if (rawlen < 12) { out.verdict = V_PARSE_ERROR; return false; }
     q.kind = (int16_t)be_load(cur, b + 4, 2);
     q.version = (int16_t)be_load(cur, b + 6, 2);
     q.typed = (q.kind == 0 || q.kind == 1 || q.kind == 2 || q.kind == 3 || q.kind == 8 || q.kind == 9) ? 1
             : (q.kind == 10 ? 2 : 0);
     q.client = -2;
+    return true;
+}
+
+__device__ __noinline__ void classify_exact(const KafkaTables &T, const DevConn &conn, const uint8_t *b, uint32_t len,
+                                            const uint32_t *crctab, Result &out) {
+    Cur cur;
+    cur.line = ~(uintptr_t)0;
+    uint32_t rawlen = 0;
+    ReqInfo q;
+    if (!frame_request(cur, b, len, out, rawlen, q)) return;
     const DevKafkaRuleset rs = T.rulesets[conn.ruleset];
-    uint32_t ntopics = 0, cmax = 0;  // raw topic count; max over topics of first matching rule
+    uint32_t ntopics = 0, cmax = 0;
     int rc = RS_OK;
     if (q.typed) {
         KDec d{b, 0, rawlen, -1, 0, &cur};
@@ -390,7 +395,7 @@ __device__ __forceinline__ bool classify_one(const KafkaTables &T, const DevConn
                     if (d.err) { rc = RS_ERROR; break; }
                     const int32_t ss = (int32_t)dec_int(d, 4);
                     if (d.err) { rc = RS_ERROR; break; }
-                    rc = read_message_set<kExact>(cur, b, d.pos, d.end, ss, ver, crctab, Q, lane);
+                    rc = read_message_set(cur, b, d.pos, d.end, ss, ver, crctab);
                     if (rc != RS_OK) break;
                 }
             }
@@ -473,61 +478,342 @@ __device__ __forceinline__ bool classify_one(const KafkaTables &T, const DevConn
         }
         if (rc == RS_OK && d.err) rc = RS_ERROR;
     }
-    if (rc == RS_OVERFLOW) return false;
-    if (rc == RS_ERROR) { out.verdict = V_PARSE_ERROR; return true; }
-    if (rc == RS_COMPRESSED) { out.verdict = V_UNSUPPORTED; return true; }
-    out.consumed = rawlen;
-    out.verdict = V_DENY;
-    if (!rs.any) return true;  // rules.Kafka == nil => deny (pkg/proxy/kafka.go:139-142)
-    // ---- MatchesRule (policy.go:200-225)
-    uint32_t best = kInf;
-    if (ntopics == 0) {
-        const int key = (q.kind >= 0 && q.kind < 64) ? q.kind : 64;
-        const uint32_t off = T.index[rs.bykey_off + 2 * key], cnt = T.index[rs.bykey_off + 2 * key + 1];
-        for (uint32_t i = 0; i < cnt; i++) {
-            uint32_t p = T.index[off + i];
-            if (rule_matches(T.rules[rs.rule_first + p], q)) { best = p; break; }
-        }
-    } else {
-        for (uint32_t i = 0; i < rs.ntopicless; i++) {
-            uint32_t p = T.index[rs.topicless_off + i];
-            if (p >= cmax) break;  // cannot beat topic completion
-            if (rule_matches(T.rules[rs.rule_first + p], q)) { best = p; break; }
-        }
-        if (best == kInf) best = cmax;
-    }
-    if (best != kInf) { out.verdict = V_ALLOW; out.rule = T.rules[rs.rule_first + best].gid; }
+    if (rc == RS_ERROR) { out.verdict = V_PARSE_ERROR; out.consumed = 0; return; }
+    if (rc == RS_COMPRESSED) { out.verdict = V_UNSUPPORTED; out.consumed = 0; return; }
+    match_rules(T, rs, q, ntopics, cmax, rawlen, out);
+}
+
+// ------------------------------------------------------------------ fast path: the decode as a program
+// The typed decoders are sequences of the same few field operations, so each
+// kind is a small program (kProg) that every lane interprets over its own
+// bytes.  A lane only touches memory for the integer fields it must look at
+// (array lengths, sizes, message headers): those come from a 32-byte window
+// of its request held in registers.  When a lane's next field lies outside its
+// window, the lane stops; the wave then refills every stopped lane's window
+// together (one pair of dwordx4 loads, all latencies overlapped) and the lanes
+// run on.  Strings and fixed-size fields nobody looks at are skipped by length
+// alone.  Two things are queued per wave instead of done in the walk:
+//   * message CRCs (checked by the wave together, see crc_pass);
+//   * topic names (looked up by the wave together, one topic per lane,
+//     see flush_topics) -- MatchesRule needs only the topic count and the max
+//     over topics of the first rule that matches each (cmax).
+enum : uint8_t {
+    P_END = 0,   // program done
+    P_SKIP,      // a: bytes of fixed-size ints read and dropped
+    P_SKIP_VGE,  // the same if version >= b
+    P_SKIP_VEQ,  // the same if version == b
+    P_STR,       // DecodeString, dropped
+    P_STR_VGE,   // the same if version >= b
+    P_CLIENT,    // DecodeString: the client id
+    P_TOPIC,     // DecodeString: a topic (GetTopics entry), counted even on error
+    P_TOPIC_OK,  // DecodeString: a topic, counted only without error
+    P_ARR,       // DecodeArrayLen (a: nullable), b: loop level; skips to after the matching P_NEXT if empty
+    P_NEXT,      // end of a loop body (b: level): next element (no decoder error) or fall through
+    P_PART,      // produce partition: id, set size, readMessageSet
+};
+struct POp {
+    uint8_t op, a, b, jump;  // jump: P_ARR -> index after its P_NEXT; P_NEXT -> body start
+};
+#define PO(o, a, b, j) {o, a, b, j}
+// kinds 0, 1, 2, 3, 8, 9, 10 at these offsets (messages.go decoders, see classify_exact)
+__constant__ POp kProg[] = {
+    // 0: Produce (:1591-1647)
+    PO(P_CLIENT, 0, 0, 0), PO(P_STR_VGE, 0, 3, 0), PO(P_SKIP, 6, 0, 0), PO(P_ARR, 0, 0, 9),
+    PO(P_TOPIC_OK, 0, 0, 0), PO(P_ARR, 0, 1, 8), PO(P_PART, 0, 0, 0), PO(P_NEXT, 0, 1, 6), PO(P_NEXT, 0, 0, 4),
+    PO(P_END, 0, 0, 0),
+    // 10: Fetch (:767-824)
+    PO(P_CLIENT, 0, 0, 0), PO(P_SKIP, 12, 0, 0), PO(P_SKIP_VGE, 4, 3, 0), PO(P_SKIP_VGE, 1, 4, 0),
+    PO(P_ARR, 0, 0, 22), PO(P_TOPIC, 0, 0, 0), PO(P_ARR, 0, 1, 21), PO(P_SKIP, 12, 0, 0), PO(P_SKIP_VGE, 8, 5, 0),
+    PO(P_SKIP, 4, 0, 0), PO(P_NEXT, 0, 1, 17), PO(P_NEXT, 0, 0, 15), PO(P_END, 0, 0, 0),
+    // 23: Offset (:1810-1858)
+    PO(P_CLIENT, 0, 0, 0), PO(P_SKIP, 4, 0, 0), PO(P_SKIP_VGE, 1, 2, 0), PO(P_ARR, 0, 0, 33), PO(P_TOPIC, 0, 0, 0),
+    PO(P_ARR, 0, 1, 32), PO(P_SKIP, 12, 0, 0), PO(P_SKIP_VEQ, 4, 0, 0), PO(P_NEXT, 0, 1, 29), PO(P_NEXT, 0, 0, 27),
+    PO(P_END, 0, 0, 0),
+    // 34: Metadata (:504-537)
+    PO(P_CLIENT, 0, 0, 0), PO(P_ARR, 1, 0, 38), PO(P_TOPIC_OK, 0, 0, 0), PO(P_NEXT, 0, 0, 36),
+    PO(P_SKIP_VGE, 1, 4, 0), PO(P_END, 0, 0, 0),
+    // 40: OffsetCommit (:1173-1228)
+    PO(P_CLIENT, 0, 0, 0), PO(P_STR, 0, 0, 0), PO(P_SKIP_VGE, 4, 1, 0), PO(P_STR_VGE, 0, 1, 0),
+    PO(P_SKIP_VGE, 8, 2, 0), PO(P_ARR, 0, 0, 53), PO(P_TOPIC, 0, 0, 0), PO(P_ARR, 0, 1, 52), PO(P_SKIP, 12, 0, 0),
+    PO(P_SKIP_VEQ, 8, 1, 0), PO(P_STR, 0, 0, 0), PO(P_NEXT, 0, 1, 48), PO(P_NEXT, 0, 0, 46), PO(P_END, 0, 0, 0),
+    // 54: OffsetFetch (:1389-1430)
+    PO(P_CLIENT, 0, 0, 0), PO(P_STR, 0, 0, 0), PO(P_ARR, 1, 0, 62), PO(P_TOPIC, 0, 0, 0), PO(P_ARR, 0, 1, 61),
+    PO(P_SKIP, 4, 0, 0), PO(P_NEXT, 0, 1, 59), PO(P_NEXT, 0, 0, 57), PO(P_END, 0, 0, 0),
+    // 63: ConsumerMetadata (:1033-1054)
+    PO(P_CLIENT, 0, 0, 0), PO(P_STR, 0, 0, 0), PO(P_SKIP_VGE, 1, 1, 0), PO(P_END, 0, 0, 0),
+};
+#undef PO
+constexpr uint32_t kProgLen = 67;
+static_assert(sizeof(kProg) == kProgLen * sizeof(POp), "program table");
+static_assert(kProgLen <= kBlock, "one thread per program entry");
+__device__ __forceinline__ uint32_t prog_start(int kind) {
+    return kind == 0 ? 0 : kind == 1 ? 10 : kind == 2 ? 23 : kind == 3 ? 34 : kind == 8 ? 40 : kind == 9 ? 54 : 63;
+}
+
+// message-set sub-states (readMessageSet, messages.go:363-494)
+enum : uint8_t { M_NONE = 0, M_HEAD, M_CRC, M_ATTR, M_TS, M_KEY, M_VALUE };
+
+// 32-byte register window of a lane's request
+struct Win {
+    uint64_t wa;  // address of w[0] (16-byte aligned); ~0: empty
+    uint32_t w[8];
+};
+__device__ __forceinline__ uint32_t wsel(const Win &W, uint32_t i) {
+    return i < 4 ? (i < 2 ? (i == 0 ? W.w[0] : W.w[1]) : (i == 2 ? W.w[2] : W.w[3]))
+                 : (i < 6 ? (i == 4 ? W.w[4] : W.w[5]) : (i == 6 ? W.w[6] : W.w[7]));
+}
+__device__ __forceinline__ bool win_has(const Win &W, uint64_t a, uint32_t n) { return a >= W.wa && a + n <= W.wa + 32; }
+// big-endian n-byte value (n = 1, 2, 4, 8) at a; win_has(W, a, n)
+__device__ __forceinline__ uint64_t win_be(const Win &W, uint64_t a, uint32_t n) {
+    const uint32_t k = (uint32_t)(a - W.wa), i = k >> 2, sh = k & 3;
+    const uint32_t w0 = wsel(W, i), w1 = wsel(W, min(i + 1, 7u)), w2 = wsel(W, min(i + 2, 7u));
+    const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, sh), hi = __builtin_amdgcn_alignbyte(w2, w1, sh);
+    const uint64_t be = (uint64_t)__builtin_bswap32(lo) << 32 | __builtin_bswap32(hi);
+    return be >> (64 - 8 * n);
+}
+
+struct Walk {
+    // outer decoder (bytes.Buffer over rawMsg) and readMessageSet's LimitReader decoder share pos
+    uint32_t pos, end;
+    bool err;            // outer decoder error (sticky)
+    // program
+    uint32_t pc;
+    int32_t cnt0, cnt1;  // remaining elements of the topic / partition loop
+    int rc;              // RS_OK / RS_ERROR / RS_COMPRESSED
+    bool done;
+    // readMessageSet
+    uint8_t ms;          // M_* sub-state
+    bool serr;           // set decoder error
+    uint64_t slim;       // set LimitReader end position
+    uint32_t at, mend, mpos;  // current message body [at, mend), message decoder position
+    bool merr;
+    int codec;
+    // findings
+    uint32_t ntopics;
+    uint32_t client_off, client_len;
+    // window request
+    bool need;
+    uint64_t need_a;     // address the window must start at (rounded down)
+    // queued work this step (pushed by the wave between steps)
+    bool has_crc, has_topic;
+    uint32_t crc_off, crc_len, crc_want, top_off, top_len;
+};
+
+// Read n bytes (an integer field) at position P below bound lim on a decoder
+// with sticky error E (io.ReadFull semantics: nothing left => EOF, a partial
+// read advances P).  Returns 0 = value read, 1 = error (value 0), 2 = the
+// window does not cover it (nothing changed).
+__device__ __forceinline__ int rd_int(const Win &W, const uint8_t *b, uint32_t &P, uint64_t lim, bool &E, uint32_t n,
+                                      uint64_t &v, Walk &S) {
+    v = 0;
+    if (E) return 1;
+    const uint64_t avail = lim > P ? lim - P : 0;
+    if (avail == 0) { E = true; return 1; }
+    if (avail < n) { P += (uint32_t)avail; E = true; return 1; }
+    const uint64_t a = (uint64_t)(uintptr_t)(b + P);
+    if (!win_has(W, a, n)) { S.need = true; S.need_a = a; return 2; }
+    v = win_be(W, a, n);
+    P += n;
+    return 0;
+}
+// io.ReadFull of n bytes that nobody looks at: bounds only
+__device__ __forceinline__ bool rd_skip(uint32_t &P, uint64_t lim, bool &E, uint32_t n) {
+    if (E || n == 0) return !E;
+    const uint64_t avail = lim > P ? lim - P : 0;
+    if (avail == 0) { E = true; return false; }
+    if (avail < n) { P += (uint32_t)avail; E = true; return false; }
+    P += n;
     return true;
 }
 
-// The exact decode (CRC checked inline), kept out of line: only lanes with a
-// mismatching CRC or an overflowed queue take it.
-__device__ __noinline__ void classify_exact(const KafkaTables &T, const DevConn &conn, const uint8_t *b, uint32_t len,
-                                            const uint32_t *crctab, Result &out) {
-    const Queue none{nullptr, nullptr};
-    classify_one<true>(T, conn, b, len, crctab, none, 0, out);
+// One step of a lane's walk; false when it must stop (window needed, work
+// queued, or done).
+__device__ __forceinline__ bool walk_step(Walk &S, const Win &W, const uint8_t *b, int ver, const POp *prog) {
+    uint64_t v;
+    if (S.ms != M_NONE) {
+        // ---- readMessageSet: one message per pass through these states
+        const uint64_t slim = min((uint64_t)S.end, S.slim);
+        if (S.ms == M_HEAD) {  // offset i64, size i32, body
+            const uint32_t P0 = S.pos;
+            bool e2 = S.serr;
+            uint64_t off;
+            int r = rd_int(W, b, S.pos, slim, e2, 8, off, S);
+            if (r == 2) return false;
+            if (r == 0) {
+                // size immediately follows: both in the window or refetch from the offset
+                r = rd_int(W, b, S.pos, slim, e2, 4, v, S);
+                if (r == 2) { S.pos = P0; S.need_a = (uint64_t)(uintptr_t)(b + P0); return false; }
+            }
+            S.serr = e2;
+            const int32_t msize = (int32_t)(uint32_t)v;
+            if (r != 0 || msize <= 0) { S.ms = M_NONE; return true; }  // set done
+            if ((uint32_t)msize > kMaxParseBuf) { S.rc = RS_ERROR; S.done = true; return false; }
+            const uint32_t at = S.pos;
+            if (!rd_skip(S.pos, slim, S.serr, (uint32_t)msize)) { S.ms = M_NONE; return true; }
+            if (msize <= 4) { S.ms = M_NONE; return true; }  // crc only: appended, set stops
+            S.at = at;
+            S.mend = at + (uint32_t)msize;
+            S.mpos = at;
+            S.merr = false;
+            S.ms = M_CRC;
+            return true;
+        }
+        if (S.ms == M_CRC) {  // crc u32 (the body holds > 4 bytes), queued for the wave's CRC pass
+            const int r = rd_int(W, b, S.mpos, S.mend, S.merr, 4, v, S);
+            if (r == 2) return false;
+            S.has_crc = true;
+            S.crc_off = S.at + 4;
+            S.crc_len = S.mend - S.at - 4;
+            S.crc_want = (uint32_t)v;
+            S.ms = M_ATTR;
+            return false;  // the wave pushes the item
+        }
+        if (S.ms == M_ATTR) {  // magic i8, attributes i8
+            const uint32_t P0 = S.mpos;
+            int r = rd_int(W, b, S.mpos, S.mend, S.merr, 1, v, S);
+            if (r == 2) return false;
+            uint64_t attr = 0;
+            if (r == 0) {
+                r = rd_int(W, b, S.mpos, S.mend, S.merr, 1, attr, S);
+                if (r == 2) { S.mpos = P0; S.need_a = (uint64_t)(uintptr_t)(b + P0); return false; }
+            }
+            S.codec = (int)(attr & 3);
+            S.ms = ver >= 1 ? M_TS : M_KEY;
+            if (S.ms == M_KEY && S.codec == 3) { S.ms = M_NONE; }  // `return nil, err` with err == nil
+            return true;
+        }
+        if (S.ms == M_TS) {  // timestamp i64 (version >= 1)
+            const int r = rd_int(W, b, S.mpos, S.mend, S.merr, 8, v, S);
+            if (r == 2) return false;
+            S.ms = S.codec == 3 ? M_NONE : M_KEY;
+            return true;
+        }
+        // M_KEY / M_VALUE: DecodeBytes (i32 length, < 1 => nil, > max => error)
+        const int r = rd_int(W, b, S.mpos, S.mend, S.merr, 4, v, S);
+        if (r == 2) return false;
+        if (r == 0) {
+            const int32_t sl = (int32_t)(uint32_t)v;
+            if (sl >= 1) {
+                if ((uint32_t)sl > kMaxParseBuf) S.merr = true;
+                else rd_skip(S.mpos, S.mend, S.merr, (uint32_t)sl);
+            }
+        }
+        if (S.ms == M_KEY) { S.ms = M_VALUE; return true; }
+        if (S.merr) { S.rc = RS_ERROR; S.done = true; return false; }
+        if (S.codec != 0) { S.rc = RS_COMPRESSED; S.done = true; return false; }
+        S.ms = M_HEAD;  // next message
+        return true;
+    }
+    const POp o = prog[S.pc];
+    switch (o.op) {
+    case P_END:
+        S.done = true;
+        return false;
+    case P_SKIP_VGE:
+    case P_SKIP_VEQ:
+    case P_SKIP:
+        if (o.op == P_SKIP || (o.op == P_SKIP_VGE ? ver >= o.b : ver == o.b)) rd_skip(S.pos, S.end, S.err, o.a);
+        S.pc++;
+        return true;
+    case P_STR_VGE:
+    case P_STR:
+    case P_CLIENT:
+    case P_TOPIC:
+    case P_TOPIC_OK: {
+        if (o.op == P_STR_VGE && ver < o.b) { S.pc++; return true; }
+        // DecodeString: i16 length, < 1 => "", then the bytes
+        const int r = rd_int(W, b, S.pos, S.end, S.err, 2, v, S);
+        if (r == 2) return false;
+        const int32_t sl = (int16_t)(uint16_t)v;
+        uint32_t so = 0, sn = 0;
+        if (r == 0 && sl >= 1) {
+            const uint32_t at = S.pos;
+            if (rd_skip(S.pos, S.end, S.err, (uint32_t)sl)) { so = at; sn = (uint32_t)sl; }
+        }
+        S.pc++;
+        if (o.op == P_CLIENT) {
+            if (!S.err) { S.client_off = so; S.client_len = sn; }
+        } else if (o.op == P_TOPIC || (o.op == P_TOPIC_OK && !S.err)) {
+            S.has_topic = true;
+            S.top_off = so;
+            S.top_len = sn;
+            S.ntopics++;
+            return false;  // the wave queues the topic
+        }
+        return true;
+    }
+    case P_ARR: {
+        const int r = rd_int(W, b, S.pos, S.end, S.err, 4, v, S);
+        if (r == 2) return false;
+        int32_t l = (int32_t)(uint32_t)v;  // 0 after an error
+        if (l < 0) {
+            if (!o.a) { S.rc = RS_ERROR; S.done = true; return false; }  // ErrInvalidArrayLen
+            l = 0;  // null array
+        }
+        if ((uint32_t)l > kMaxParseBuf) { S.rc = RS_ERROR; S.done = true; return false; }
+        if (o.b == 0) S.cnt0 = l; else S.cnt1 = l;
+        S.pc = (l > 0 && !S.err) ? S.pc + 1 : o.jump;
+        return true;
+    }
+    case P_NEXT: {
+        int32_t &c = o.b == 0 ? S.cnt0 : S.cnt1;
+        c--;
+        S.pc = (c > 0 && !S.err) ? o.jump : S.pc + 1;
+        return true;
+    }
+    default: {  // P_PART: partition id i32, set size i32 (errors are fatal), readMessageSet
+        const uint32_t P0 = S.pos;
+        int r = rd_int(W, b, S.pos, S.end, S.err, 4, v, S);
+        if (r == 2) return false;
+        if (r == 0) {
+            r = rd_int(W, b, S.pos, S.end, S.err, 4, v, S);
+            if (r == 2) { S.pos = P0; S.need_a = (uint64_t)(uintptr_t)(b + P0); return false; }
+        }
+        if (r != 0) { S.rc = RS_ERROR; S.done = true; return false; }
+        const int32_t ss = (int32_t)(uint32_t)v;
+        S.pc++;
+        if (ss < 0) return true;  // null set
+        if ((uint32_t)ss > kMaxParseBuf) { S.rc = RS_ERROR; S.done = true; return false; }
+        S.slim = (uint64_t)S.pos + (uint32_t)ss;
+        S.serr = false;
+        S.ms = M_HEAD;
+        return true;
+    }
+    }
 }
 
-// ------------------------------------------------------------------ CRC pass
-// All lanes of the wave check the queued message CRCs together.  Lane t
-// starts on item t; 64 bytes per step; a lane whose message is done takes the
-// next unclaimed item (claims in lane order, by ballot).  Returns the mask of
-// request lanes with a mismatching CRC.
+// ------------------------------------------------------------------ per-wave queues
+struct WaveLds {
+    // CRC work items: request offset, length | lane << 26, stored CRC
+    uint32_t *c_off, *c_len, *c_want;
+    // topic names: request offset, length | lane << 26
+    uint32_t *t_off, *t_len;
+    // per request lane
+    const uint8_t **base;  // request start
+    uint32_t *cmax;        // max over its topics of the first matching rule (atomicMax)
+    int32_t *rs;           // rule set
+    int32_t *client;       // interned client id (-2 none)
+    int32_t *kind, *ver;
+};
+constexpr uint32_t kCrcQ = 256;   // CRC items per wave
+constexpr uint32_t kTopQ = 128;   // topics per wave
+
+// CRC pass over items [0, n): lane t starts on item t, 64 bytes per step; a
+// lane whose message is done takes the next unclaimed item.  ORs the request
+// lanes with a mismatching CRC into bad.
 struct CrcLane {
-    uint64_t a;       // next aligned address
+    uint64_t a;       // next address
     uint32_t rem;     // bytes left
     uint32_t want;    // stored CRC
     uint32_t owner;   // request lane
     uint32_t c;       // running CRC state
     bool have;
 };
-
-__device__ __forceinline__ void crc_load(CrcLane &L, const Queue &Q, uint32_t i, const uint32_t *tab) {
-    const uint4 e = Q.items[i];
-    L.a = (uint64_t)e.x | (uint64_t)e.y << 32;
-    L.want = e.z;
-    L.rem = e.w & ((1u << 26) - 1);
-    L.owner = e.w >> 26;
+__device__ __forceinline__ void crc_load(CrcLane &L, const WaveLds &Q, uint32_t i, const uint32_t *tab) {
+    L.owner = Q.c_len[i] >> 26;
+    L.rem = Q.c_len[i] & ((1u << 26) - 1);
+    L.want = Q.c_want[i];
+    L.a = (uint64_t)(uintptr_t)Q.base[L.owner] + Q.c_off[i];
     L.c = 0xFFFFFFFFu;
     // bytes up to 16-byte alignment
     const uint32_t k = (uint32_t)(L.a & 15);
@@ -543,8 +829,7 @@ __device__ __forceinline__ void crc_load(CrcLane &L, const Queue &Q, uint32_t i,
     }
     L.have = true;
 }
-
-__device__ __forceinline__ uint64_t crc_pass(const Queue &Q, uint32_t nitems, const uint32_t *tab, uint32_t lane) {
+__device__ __forceinline__ uint64_t crc_pass(const WaveLds &Q, uint32_t nitems, const uint32_t *tab, uint32_t lane) {
     uint64_t bad = 0;
     uint32_t next = 64;  // next unclaimed item (wave-uniform)
     CrcLane L;
@@ -581,13 +866,11 @@ __device__ __forceinline__ uint64_t crc_pass(const Queue &Q, uint32_t nitems, co
                 L.have = false;
             }
         }
-        // lanes without an item claim the next ones
         const uint64_t idle = __ballot(!L.have);
         const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0));
         if (!L.have && next + rank < nitems) crc_load(L, Q, next + rank, tab);
         next += (uint32_t)__builtin_popcountll(idle);
     }
-    // OR the lanes' findings over the wave
     uint32_t lo = (uint32_t)bad, hi = (uint32_t)(bad >> 32);
     for (int o = 32; o > 0; o >>= 1) {
         lo |= (uint32_t)__shfl_xor((int)lo, o);
@@ -596,20 +879,46 @@ __device__ __forceinline__ uint64_t crc_pass(const Queue &Q, uint32_t nitems, co
     return (uint64_t)hi << 32 | lo;
 }
 
+// Topic lookups for queued names [0, n): one name per lane.  Each name's
+// first matching rule position (kInf: none) is max-ed into its request lane.
+__device__ __forceinline__ void flush_topics(const KafkaTables &T, const WaveLds &Q, uint32_t n, uint32_t lane) {
+    for (uint32_t i = lane; i < n; i += 64) {
+        const uint32_t owner = Q.t_len[i] >> 26, tl = Q.t_len[i] & ((1u << 26) - 1);
+        const uint8_t *b = Q.base[owner];
+        ReqInfo q;
+        q.kind = Q.kind[owner];
+        q.version = Q.ver[owner];
+        q.typed = 1;
+        q.client = Q.client[owner];
+        Cur cur;
+        cur.line = ~(uintptr_t)0;
+        const int32_t tid = tl > 0 ? str_lookup(T.topic_hash, T.topic_mask, T.strings, cur, b + Q.t_off[i], tl) : -1;
+        const DevKafkaRuleset rs = T.rulesets[Q.rs[owner]];
+        const uint32_t e = topic_first(T, rs, q, tid);
+        atomicMax(&Q.cmax[owner], e);
+    }
+}
+
 }  // namespace
 
 // sel: this protocol's request indices (partition_kernel, mixed batches; the
 // first sel_count[0] entries), else requests 0..n-1.  answer_other: answer
 // entries on connections that are not Kafka (single-protocol engines, where
 // partition_kernel does not run).
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) void kafka_classify_kernel(
-    Batch B, KafkaTables T, const uint32_t *__restrict__ sel, const uint32_t *__restrict__ sel_count,
-    uint32_t answer_other) {
+__global__ __launch_bounds__(kBlock) void kafka_classify_kernel(Batch B, KafkaTables T,
+                                                                const uint32_t *__restrict__ sel,
+                                                                const uint32_t *__restrict__ sel_count,
+                                                                uint32_t answer_other) {
     __shared__ uint32_t crctab[8 * 256];
-    __shared__ uint4 s_items[kWaves][kQueue];
-    __shared__ uint32_t s_qn[kWaves];
+    __shared__ uint32_t s_c[kWaves][3][kCrcQ];
+    __shared__ uint32_t s_t[kWaves][2][kTopQ];
+    __shared__ const uint8_t *s_base[kWaves][64];
+    __shared__ uint32_t s_cmax[kWaves][64];
+    __shared__ int32_t s_req[kWaves][4][64];
     __shared__ uint32_t s_verdicts[8];
+    __shared__ POp s_prog[kProgLen];
     const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    if (t < kProgLen) s_prog[t] = kProg[t];
     {
         uint32_t c = t;
         for (int k = 0; k < 8; k++) c = (c & 1) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
@@ -622,7 +931,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
             __syncthreads();
         }
     }
-    const Queue Q{s_items[wave], &s_qn[wave]};
+    const WaveLds Q{s_c[wave][0], s_c[wave][1], s_c[wave][2], s_t[wave][0], s_t[wave][1], s_base[wave],
+                    s_cmax[wave], s_req[wave][0], s_req[wave][1], s_req[wave][2], s_req[wave][3]};
     const uint32_t m = sel ? sel_count[0] : B.n;
     const uint32_t ntiles = (m + 63) / 64;
     uint32_t vcount[5] = {0, 0, 0, 0, 0};
@@ -646,21 +956,135 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
                 if (!l7_in_arena(off, len, B.arena_len)) mine = false;  // out of contract: UNSUPPORTED
             }
         }
-        if (lane == 0) *Q.count = 0;
-        __builtin_amdgcn_wave_barrier();
         const uint8_t *b = B.arena + off;
-        // 1. speculative walk (CRCs queued)
-        bool redo = false;
-        if (mine) redo = !classify_one<false>(T, conn, b, len, crctab, Q, lane, r);
-        // 2. CRC pass over the queue
-        __builtin_amdgcn_wave_barrier();
-        const uint32_t nq = min(*(volatile uint32_t *)Q.count, kQueue);
-        if (nq) {
-            const uint64_t bad = crc_pass(Q, nq, crctab, lane);
-            redo |= mine && ((bad >> lane) & 1);
+        // ---- framing (ReadReq) and the request header
+        uint32_t rawlen = 0;
+        ReqInfo q{0, 0, 0, -2};
+        bool walk = false;
+        if (mine) {
+            Cur cur;
+            cur.line = ~(uintptr_t)0;
+            walk = frame_request(cur, b, len, r, rawlen, q);
         }
-        // 3. exact redo of the lanes a CRC (or the queue) decided against
-        if (redo) classify_exact(T, conn, b, len, crctab, r);
+        Walk S;
+        S.pos = 12;
+        S.end = rawlen;
+        S.err = false;
+        S.pc = prog_start(q.kind);
+        S.cnt0 = S.cnt1 = 0;
+        S.rc = RS_OK;
+        S.done = !walk || !q.typed;  // untyped kinds: request = nil, nothing to decode
+        S.ms = M_NONE;
+        S.serr = S.merr = false;
+        S.slim = 0;
+        S.at = S.mend = S.mpos = 0;
+        S.codec = 0;
+        S.ntopics = 0;
+        S.client_off = S.client_len = 0;
+        S.need = !S.done;
+        S.need_a = (uint64_t)(uintptr_t)(b + 12);
+        S.has_crc = S.has_topic = false;
+        Win W;
+        W.wa = ~0ull;
+        Q.base[lane] = b;
+        Q.cmax[lane] = 0;
+        Q.rs[lane] = conn.ruleset;
+        Q.kind[lane] = q.kind;
+        Q.ver[lane] = q.version;
+        uint32_t nc = 0, nt = 0;  // queued CRC items / topics (wave-uniform)
+        uint64_t bad = 0;         // request lanes with a mismatching CRC
+        bool client_done = false;
+        const uint64_t req_end = (uint64_t)(uintptr_t)b + len;
+        while (__any(!S.done)) {
+            // refill the windows of the lanes that stopped on one (all loads in flight together)
+            if (!S.done && S.need) {
+                W.wa = S.need_a & ~(uint64_t)15;
+                const uint4 v0 = *reinterpret_cast<const uint4 *>(W.wa);
+                uint4 v1 = make_uint4(0, 0, 0, 0);
+                if (W.wa + 16 < req_end) v1 = *reinterpret_cast<const uint4 *>(W.wa + 16);
+                W.w[0] = v0.x; W.w[1] = v0.y; W.w[2] = v0.z; W.w[3] = v0.w;
+                W.w[4] = v1.x; W.w[5] = v1.y; W.w[6] = v1.z; W.w[7] = v1.w;
+                S.need = false;
+            }
+            // run until a window, a queue slot or the end is needed
+            if (!S.done && !S.need && !S.has_crc && !S.has_topic)
+                while (walk_step(S, W, b, q.version, s_prog)) {}
+            // the client id: once every lane has read it (its first field)
+            if (!client_done && !__any(!S.done && S.pc == prog_start(q.kind) && S.ms == M_NONE)) {
+                client_done = true;
+                int32_t cid = -2;
+                if (walk && q.typed && S.client_len > 0) {
+                    Cur cur;
+                    cur.line = ~(uintptr_t)0;
+                    cid = str_lookup(T.client_hash, T.client_mask, T.strings, cur, b + S.client_off, S.client_len);
+                    if (cid < 0) cid = -2;
+                }
+                q.client = cid;
+                Q.client[lane] = cid;
+            }
+            // queue this round's CRC items and topics (prefix by ballot; no atomics)
+            const uint64_t mc = __ballot(S.has_crc), mt = __ballot(S.has_topic);
+            const uint32_t rc = __builtin_amdgcn_mbcnt_hi((uint32_t)(mc >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mc, 0));
+            const uint32_t rt = __builtin_amdgcn_mbcnt_hi((uint32_t)(mt >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mt, 0));
+            const uint32_t pc_ = (uint32_t)__builtin_popcountll(mc), pt_ = (uint32_t)__builtin_popcountll(mt);
+            if (nc + pc_ > kCrcQ) {  // flush the CRC queue first
+                __builtin_amdgcn_wave_barrier();
+                bad |= crc_pass(Q, nc, crctab, lane);
+                __builtin_amdgcn_wave_barrier();
+                nc = 0;
+            }
+            if ((nt + pt_ > kTopQ) && client_done) {
+                __builtin_amdgcn_wave_barrier();
+                flush_topics(T, Q, nt, lane);
+                __builtin_amdgcn_wave_barrier();
+                nt = 0;
+            }
+            if (S.has_crc) {
+                Q.c_off[nc + rc] = S.crc_off;
+                Q.c_len[nc + rc] = S.crc_len | lane << 26;
+                Q.c_want[nc + rc] = S.crc_want;
+                if (S.crc_len >= (1u << 26)) bad |= 1ull << lane;  // cannot be queued: exact redo
+                S.has_crc = false;
+            }
+            nc += pc_;
+            if (S.has_topic && (nt + pt_ <= kTopQ)) {
+                Q.t_off[nt + rt] = S.top_off;
+                Q.t_len[nt + rt] = S.top_len | lane << 26;
+                S.has_topic = false;
+            }
+            if (nt + pt_ <= kTopQ) nt += pt_;
+            __builtin_amdgcn_wave_barrier();
+        }
+        // ---- the rest of the queues
+        __builtin_amdgcn_wave_barrier();
+        if (nc) bad |= crc_pass(Q, nc, crctab, lane);
+        if (nt) flush_topics(T, Q, nt, lane);
+        __builtin_amdgcn_wave_barrier();
+        // OR of the per-lane `bad` findings (each lane only saw its own CRC lanes' owners)
+        {
+            uint32_t lo = (uint32_t)bad, hi = (uint32_t)(bad >> 32);
+            for (int o = 32; o > 0; o >>= 1) {
+                lo |= (uint32_t)__shfl_xor((int)lo, o);
+                hi |= (uint32_t)__shfl_xor((int)hi, o);
+            }
+            bad = (uint64_t)hi << 32 | lo;
+        }
+        if (walk) {
+            if ((bad >> lane) & 1) {
+                classify_exact(T, conn, b, len, crctab, r);
+            } else if (S.rc == RS_ERROR || (S.rc == RS_OK && S.err)) {
+                r.verdict = V_PARSE_ERROR;
+                r.rule = -1;
+                r.consumed = 0;
+            } else if (S.rc == RS_COMPRESSED) {
+                r.verdict = V_UNSUPPORTED;
+                r.rule = -1;
+                r.consumed = 0;
+            } else {
+                const DevKafkaRuleset rs = T.rulesets[conn.ruleset];
+                match_rules(T, rs, q, q.typed == 1 ? S.ntopics : 0, Q.cmax[lane], rawlen, r);
+            }
+        }
         if (answer) {
             B.verdict[idx] = r.verdict;
             B.rule[idx] = r.rule;

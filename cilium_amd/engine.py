@@ -20,8 +20,8 @@ class PolicyError(ValueError):
 
 
 class Engine:
-    def __init__(self, device=0):
-        self._lib = _lib.load()
+    def __init__(self, device=0, lib_path=None):
+        self._lib = _lib.load(lib_path)
         err = C.create_string_buffer(512)
         h = self._lib.l7g_engine_create(device, err, 512)
         if not h:

@@ -303,6 +303,105 @@ def k_metadata(version, corr, client, topics):
     return k_request(3, version, corr, client, b)
 
 
+def k_offset(version, corr, client, topics):
+    """ListOffsets (kind 2): topics: list of (name, [partition ids])"""
+    b = struct.pack(">i", -1)
+    if version >= 2:
+        b += b"\x00"
+    b += struct.pack(">i", len(topics))
+    for name, parts in topics:
+        b += k_str(name) + struct.pack(">i", len(parts))
+        for pid in parts:
+            b += struct.pack(">iq", pid, -1)
+            if version == 0:
+                b += struct.pack(">i", 1)
+    return k_request(2, version, corr, client, b)
+
+
+def k_offset_commit(version, corr, client, group, topics):
+    """OffsetCommit (kind 8): topics: list of (name, [partition ids])"""
+    b = k_str(group)
+    if version >= 1:
+        b += struct.pack(">i", 3) + k_str("member-1")
+    if version >= 2:
+        b += struct.pack(">q", 60000)
+    b += struct.pack(">i", len(topics))
+    for name, parts in topics:
+        b += k_str(name) + struct.pack(">i", len(parts))
+        for pid in parts:
+            b += struct.pack(">iq", pid, 42)
+            if version == 1:
+                b += struct.pack(">q", 1234)
+            b += k_str("meta")
+    return k_request(8, version, corr, client, b)
+
+
+def k_offset_fetch(version, corr, client, group, topics):
+    """OffsetFetch (kind 9): topics None (null array) or list of (name, [partition ids])"""
+    b = k_str(group)
+    if topics is None:
+        b += struct.pack(">i", -1)
+    else:
+        b += struct.pack(">i", len(topics))
+        for name, parts in topics:
+            b += k_str(name) + struct.pack(">i", len(parts)) + b"".join(struct.pack(">i", p) for p in parts)
+    return k_request(9, version, corr, client, b)
+
+
+def k_consumer_metadata(version, corr, client, group):
+    b = k_str(group)
+    if version >= 1:
+        b += b"\x00"
+    return k_request(10, version, corr, client, b)
+
+
+def kafka_all_kinds(n, seed):
+    """Every kind the reference decodes (0, 1, 2, 3, 8, 9, 10) plus untyped
+    ones, at every version the decoders distinguish, with 0-5 topics of
+    1-3 partitions (parity coverage for the decode program of each kind)."""
+    rng = np.random.default_rng(seed)
+    topics = kafka_topics()
+    D = _Draws(rng, 64 * n + 1024)
+    out = []
+
+    def tps(with_parts=True):
+        k = D.int(0, 6)
+        return [(topics[D.int(0, 1000)] if D.uniform() < 0.9 else "", [D.int(0, 8) for _ in range(D.int(1, 4))])
+                for _ in range(k)]
+
+    for i in range(n):
+        client = f"client-{D.int(0, 16):02d}" if D.uniform() < 0.95 else ""
+        k = D.int(0, 9)
+        if k == 0:
+            v = D.int(0, 4)
+            t = [(name, [(p, [k_message(D.bytes(D.int(0, 90)), version=v) for _ in range(D.int(0, 3))])
+                         for p in parts]) for name, parts in tps()]
+            out.append(k_produce(v, i, client, t, txn="tx" if v >= 3 and D.uniform() < 0.5 else None))
+        elif k == 1:
+            out.append(k_fetch(D.int(0, 6), i, client, tps()))
+        elif k == 2:
+            out.append(k_offset(D.int(0, 3), i, client, tps()))
+        elif k == 3:
+            out.append(k_metadata(D.int(0, 6), i, client, None if D.uniform() < 0.2 else [n for n, _ in tps()]))
+        elif k == 4:
+            out.append(k_offset_commit(D.int(0, 4), i, client, "grp", tps()))
+        elif k == 5:
+            out.append(k_offset_fetch(D.int(0, 4), i, client, "grp", None if D.uniform() < 0.2 else tps()))
+        elif k == 6:
+            out.append(k_consumer_metadata(D.int(0, 2), i, client, "grp"))
+        elif k == 7:
+            out.append(k_request(int(rng.choice([4, 5, 6, 7, 11, 12, 18, 19, 36])), D.int(0, 3), i, client, b"\x00" * D.int(0, 12)))
+        else:  # truncated or size-edited frames of the above kinds
+            r = bytearray(k_offset_commit(D.int(0, 4), i, client, "grp", tps()) if D.uniform() < 0.5
+                          else k_offset(D.int(0, 3), i, client, tps()))
+            cut = D.int(12, len(r) + 1)
+            r = r[:cut]
+            if D.uniform() < 0.5:
+                r[0:4] = struct.pack(">i", len(r) - 4)
+            out.append(bytes(r))
+    return out
+
+
 def kafka_topics():
     return [f"topic-{i:04d}" for i in range(1000)]
 
@@ -320,37 +419,66 @@ def cfg3_policy():
     return api.policy_set(api.network_policy("10.0.0.1", 3, ingress=[(9092, [api.port_rule(kafka=cfg3_rules())])]))
 
 
+class _Draws:
+    """Scalar draws from pre-generated uniforms (numpy per-call overhead
+    dominated the per-request generators)."""
+
+    def __init__(self, rng, n):
+        self.u = rng.random(n).tolist()
+        self.k = 0
+        self.pool = rng.integers(0, 256, size=1 << 22, dtype=np.uint8).tobytes()
+        self.pk = 0
+
+    def uniform(self):
+        if self.k >= len(self.u):
+            self.k = 0
+        v = self.u[self.k]
+        self.k += 1
+        return v
+
+    def int(self, lo, hi):
+        """uniform integer in [lo, hi)"""
+        return lo + int(self.uniform() * (hi - lo))
+
+    def bytes(self, n):
+        if self.pk + n > len(self.pool):
+            self.pk = 0
+        b = self.pool[self.pk:self.pk + n]
+        self.pk += n + 1
+        return b
+
+
 def kafka_requests(n, seed):
     rng = np.random.default_rng(seed)
     topics = kafka_topics()
     kind = rng.choice(3, p=[0.5, 0.4, 0.1], size=n)
+    D = _Draws(rng, 64 * n + 1024)
     out = []
 
     def pick_topic():
-        if rng.random() < 0.9:
-            return topics[int(rng.integers(0, 1000))]
-        return f"other-{int(rng.integers(0, 1000)):04d}"
+        if D.uniform() < 0.9:
+            return topics[D.int(0, 1000)]
+        return f"other-{D.int(0, 1000):04d}"
 
     for i in range(n):
-        client = f"client-{int(rng.integers(0, 16)):02d}"
+        client = f"client-{D.int(0, 16):02d}"
         if kind[i] == 0:
-            v = int(rng.integers(0, 3))
+            v = D.int(0, 3)
             tps = []
-            for _ in range(int(rng.integers(1, 4))):
-                msgs = [k_message(bytes(rng.integers(0, 256, size=int(rng.integers(64, 513)), dtype=np.uint8)),
-                                  key=None if rng.random() < 0.5 else b"k%d" % i, version=v)
-                        for _ in range(int(rng.integers(1, 5)))]
+            for _ in range(D.int(1, 4)):
+                msgs = [k_message(D.bytes(D.int(64, 513)), key=None if D.uniform() < 0.5 else b"k%d" % i, version=v)
+                        for _ in range(D.int(1, 5))]
                 tps.append((pick_topic(), [(0, msgs)]))
             out.append(k_produce(v, i, client, tps))
         elif kind[i] == 1:
-            v = int(rng.integers(0, 6))
-            tps = [(pick_topic(), [int(rng.integers(0, 8))]) for _ in range(int(rng.integers(1, 5)))]
+            v = D.int(0, 6)
+            tps = [(pick_topic(), [D.int(0, 8)]) for _ in range(D.int(1, 5))]
             out.append(k_fetch(v, i, client, tps))
         else:
-            sub = int(rng.integers(0, 3))
+            sub = D.int(0, 3)
             if sub == 0:
-                tl = None if rng.random() < 0.3 else [pick_topic() for _ in range(int(rng.integers(0, 4)))]
-                out.append(k_metadata(int(rng.integers(0, 6)), i, client, tl))
+                tl = None if D.uniform() < 0.3 else [pick_topic() for _ in range(D.int(0, 4))]
+                out.append(k_metadata(D.int(0, 6), i, client, tl))
             elif sub == 1:
                 out.append(k_request(18, 0, i, client, b""))  # ApiVersions
             else:
@@ -400,9 +528,12 @@ def kafka_adversarial(n, seed):
     return out
 
 
-def kafka_workload(n, nconns=256, seed=None, adversarial=False):
+def kafka_workload(n, nconns=256, seed=None, adversarial=False, all_kinds=False):
     seed = SEED_BASE + 3 if seed is None else seed
-    reqs = kafka_adversarial(n, seed) if adversarial else kafka_requests(n, seed)
+    if all_kinds:
+        reqs = kafka_all_kinds(n, seed)
+    else:
+        reqs = kafka_adversarial(n, seed) if adversarial else kafka_requests(n, seed)
     arena, offs, lens = pack(reqs)
     rng = np.random.default_rng(seed + 1)
     conn_ids = rng.integers(0, nconns, size=n).astype(np.uint32)

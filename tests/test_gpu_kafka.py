@@ -53,3 +53,14 @@ def test_mixed_http_kafka_batch(engine, oracle):
     w = gen.Workload("mixed", arena, offs[perm], lens[perm], cids[perm], conns, pol)
     got, ref = both(engine, oracle, w)
     assert_same(got, ref, w)
+
+
+def test_kafka_all_kinds_parity(engine, oracle):
+    """Every decoder the reference has (Produce, Fetch, ListOffsets, Metadata,
+    OffsetCommit, OffsetFetch, ConsumerMetadata) at every version its fields
+    depend on, empty / null topic arrays, empty topic names, truncated and
+    size-edited frames, untyped kinds."""
+    w = gen.kafka_workload(30000, seed=99, all_kinds=True)
+    got, ref = both(engine, oracle, w)
+    assert_same(got, ref, w)
+    assert len(set(got[0].tolist())) >= 4

@@ -1,0 +1,61 @@
+"""Kafka kernel experiment (GPU box): cfg3 at N requests through the product
+library and variant builds side by side (libl7gpu_<name>.so, built with
+`python -m cilium_amd.build --variant NAME -DX`).  Prints per-variant kernel
+time (HIP events around the launch, median of 10) and parity vs the oracle.
+
+usage: python tools/exp_kafka.py N variant...   ("prod" = libl7gpu.so)
+"""
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def main():
+    import torch
+    import refpy
+    from cilium_amd import Engine, gen
+    n = int(sys.argv[1])
+    names = sys.argv[2:] or ["prod"]
+    wl = os.environ.get("EXP_WORKLOAD", "cfg3")
+    t0 = time.time()
+    w = gen.kafka_workload(n) if wl == "cfg3" else gen.mixed_workload(n)
+    print(f"{wl}: {n} requests, {w.arena.nbytes / 1e6:.1f} MB, generated in {time.time() - t0:.1f}s", flush=True)
+    ref = refpy.classify_workload(w, 16)
+    dev = torch.device("cuda", 0)
+    d = [torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in
+         (w.arena, w.offsets.view(np.int64), w.lengths.view(np.int32), w.conn_ids.view(np.int32))]
+    outs = [torch.empty(n, dtype=t, device=dev) for t in (torch.uint8, torch.int32, torch.int32)]
+    s = torch.cuda.current_stream()
+    for name in names:
+        path = os.path.join(ROOT, "cilium_amd", "libl7gpu.so" if name == "prod" else f"libl7gpu_{name}.so")
+        eng = Engine(0, lib_path=path)
+        eng.update_policy(w.policy)
+        eng.set_connections(w.conns)
+        eng.profile(True)
+        ms = []
+        for it in range(13):
+            eng.classify_device(d[0].data_ptr(), d[0].numel(), d[1].data_ptr(), d[2].data_ptr(), d[3].data_ptr(), n,
+                                *[o.data_ptr() for o in outs], stream=s.cuda_stream)
+            p = eng.profile_last()
+            if it >= 3:
+                ms.append(p)
+        torch.cuda.synchronize()
+        got = (outs[0].cpu().numpy(), outs[1].cpu().numpy(), outs[2].cpu().numpy().view(np.uint32))
+        mism = int(((got[0] != ref[0]) | (got[1] != ref[1]) | (got[2] != ref[2])).sum())
+        med = {k: float(np.median([m[k] for m in ms])) for k in ms[0] if ms[0][k] > 0}
+        gb = (w.lengths.astype(np.int64).sum() + 25 * n) / 1e9
+        kms = med.get("kafka", 0.0)
+        print(f"{name:12s} " + " ".join(f"{k}={v:.3f}ms" for k, v in med.items()) +
+              (f"  kafka {gb / (kms / 1e3):.0f} GB/s frac {gb / (kms / 1e3) / 8000:.3f}" if kms else "") +
+              f"  mismatches={mism}", flush=True)
+        eng.close()
+
+
+if __name__ == "__main__":
+    main()
