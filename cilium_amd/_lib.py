@@ -37,6 +37,7 @@ EXPORTS = (
     "l7g_engine_create", "l7g_engine_destroy", "l7g_policy_update", "l7g_policy_index",
     "l7g_policy_nrules", "l7g_conns_set", "l7g_conn_update", "l7g_classify", "l7g_classify_host", "l7g_stats",
     "l7g_debug_regex", "l7g_debug_phase_times", "l7g_profile_enable", "l7g_profile_last",
+    "l7g_debug_kafka_phase_times",
 )
 
 _libs = {}
@@ -67,6 +68,7 @@ def load(path=None):
     lib.l7g_stats.argtypes = [vp, C.POINTER(Stats)]
     lib.l7g_debug_regex.argtypes = [cp, sz, C.c_int, cp, sz, cp, sz]
     lib.l7g_debug_phase_times.argtypes = [vp, vp, C.c_int]
+    lib.l7g_debug_kafka_phase_times.argtypes = [vp, vp, C.c_int]
     lib.l7g_profile_enable.argtypes = [vp, C.c_int]
     lib.l7g_profile_last.argtypes = [vp, vp]
     _libs[path] = lib

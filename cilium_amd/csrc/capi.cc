@@ -25,6 +25,7 @@ hipError_t LaunchMemcacheClassify(const Batch &B, const McTables &T, const uint3
                                   bool answer_other, hipStream_t stream);
 hipError_t LaunchPartition(const Batch &B, uint32_t *sel_kafka, uint32_t *sel_mc, uint32_t *counts, hipStream_t stream);
 hipError_t HttpPhaseTimes(uint64_t *out, bool reset);
+hipError_t KafkaPhaseTimes(uint64_t *out, bool reset);
 }  // namespace l7
 
 using namespace l7;
@@ -500,6 +501,12 @@ int l7g_debug_phase_times(l7g_engine *e, uint64_t *out8, int reset) {
     if (!e || e->device < 0) return (int)hipErrorNoDevice;
     hipSetDevice(e->device);
     return (int)HttpPhaseTimes(out8, reset != 0);
+}
+
+int l7g_debug_kafka_phase_times(l7g_engine *e, uint64_t *out8, int reset) {
+    if (!e || e->device < 0) return (int)hipErrorNoDevice;
+    hipSetDevice(e->device);
+    return (int)KafkaPhaseTimes(out8, reset != 0);
 }
 
 int l7g_debug_regex(const char *pat, size_t patlen, int anchored, const uint8_t *s, size_t slen, char *err,

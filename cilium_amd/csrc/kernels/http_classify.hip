@@ -92,7 +92,9 @@ __device__ unsigned long long g_phase[8];
 #endif
 
 enum : uint32_t {
-    M_METHOD, M_TARGET, M_VERSION, M_LINE, M_NAME, M_OWS, M_VALUE, M_SKIP, M_LF, M_ENDLF, M_DONE
+    M_METHOD, M_TARGET, M_VERSION, M_LINE, M_NAME, M_OWS, M_VALUE, M_SKIP, M_LF, M_ENDLF, M_DONE,
+    // chunked body (Transfer-Encoding: chunked), after the verdict is known
+    M_CHSIZE, M_CHEXT, M_CHLF, M_CHDATA, M_CHDCR, M_CHDLF, M_TRL, M_TRLSCAN, M_TRLLF, M_TRLEND
 };
 constexpr uint32_t kNoSlot = 0xFF;
 
@@ -204,9 +206,9 @@ struct Lane {
     uint32_t slot;      // slot of the current header value (kNoSlot: none)
     uint32_t nstate;    // name DFA state
     uint32_t ninfo;     // NI_* flags of the current header name
-    bool have_cl, have_te, cl_bad, cl_ws, in_ows;
-    uint32_t ndig;
-    uint64_t clv, cl;
+    bool have_cl, chunked, cl_bad, cl_ws, in_ows;
+    uint32_t ndig;      // Content-Length digits; Transfer-Encoding: bytes of "chunked" matched (0xFF: no)
+    uint64_t clv, cl;   // clv: Content-Length value; in the chunked body: the chunk size
     // DFA of the current slot (kDfasPerPass == 1); dtrans == 0: none
     uint32_t dcls, dtrans, dmask, dncls, st, saved;
     uint32_t dabs;      // states >= dabs (and 0) are absorbing
@@ -264,7 +266,7 @@ __device__ __forceinline__ void frame_reset(const Img<kLds> &I, Lane &L) {
     L.mode = M_METHOD;
     L.mark = L.a0;
     L.present = 0;
-    L.have_cl = L.have_te = false;
+    L.have_cl = L.chunked = false;
     L.cl = 0;
     slot_begin(I, L, SLOT_METHOD);
 }
@@ -279,12 +281,24 @@ __device__ __forceinline__ void finish(Lane &L, uint8_t v, int32_t rule = -1) {
 }
 
 // Headers complete (framing succeeded for this pass): next pass or verdict.
+// The verdict of a request whose body is chunked: the chunks (and trailers)
+// are walked after it to find where the request ends.
+__device__ __forceinline__ void verdict_then_body(Lane &L, uint8_t v, int32_t rule) {
+    if (!L.chunked) {
+        finish(L, v, rule);
+        return;
+    }
+    L.verdict = v;
+    L.rule = rule;
+    L.mode = M_CHSIZE;
+    L.mark = L.pa;
+    L.clv = 0;
+}
+
 template <bool kLds>
 __device__ __forceinline__ void headers_done(const Img<kLds> &I, Lane &L) {
-    const uint64_t total = (uint64_t)(L.pa - L.a0) + L.cl;
-    if (L.have_te) {
-        finish(L, V_UNSUPPORTED);
-    } else if (total > 0xFFFFFFFFull) {
+    const uint64_t total = L.chunked ? (uint64_t)(L.pa - L.a0) : (uint64_t)(L.pa - L.a0) + L.cl;
+    if (total > 0xFFFFFFFFull) {
         finish(L, V_PARSE_ERROR);
     } else if (total > (uint64_t)(L.lena - L.a0)) {
         finish(L, V_INCOMPLETE);
@@ -311,14 +325,14 @@ __device__ __forceinline__ void headers_done(const Img<kLds> &I, Lane &L) {
             for (int c = kChunksPerPass - 1; c >= 0; c--)
                 if ((uint32_t)c < nc && L.acc[c]) hit = (int32_t)(64 * (L.cg + c) + (uint32_t)__builtin_ctzll(L.acc[c]));
             if (hit >= 0) {
-                finish(L, V_ALLOW, (int32_t)I.u32(HDR_U32(I, rule_off) + 4 * (uint32_t)hit));
+                verdict_then_body(L, V_ALLOW, (int32_t)I.u32(HDR_U32(I, rule_off) + 4 * (uint32_t)hit));
             } else if (L.cg + kChunksPerPass < nchunks) {  // next chunk group
                 L.cg += kChunksPerPass;
                 L.dg = 0;
                 acc_init(I, L);
                 frame_reset(I, L);
             } else {
-                finish(L, (uint8_t)HDR_U8(I, terminal));
+                verdict_then_body(L, (uint8_t)HDR_U8(I, terminal), -1);
             }
         }
     }
@@ -333,7 +347,7 @@ __device__ __forceinline__ bool line_done(const Img<kLds> &I, Lane &L) {
         L.have_cl = true;
         L.cl = L.clv;
     }
-    if (L.ninfo & NI_TE) L.have_te = true;
+    if ((L.ninfo & NI_TE) && L.ndig == 7) L.chunked = true;  // the value is "chunked" (case-insensitive)
     if (L.slot != kNoSlot) {
         slot_end(I, L);
         L.present |= 1u << L.slot;
@@ -535,7 +549,7 @@ __device__ __forceinline__ void parse_window(const Img<kLds> &I, Lane &L, Cursor
                 if (c != ' ' && c != '\t') break;
             }
             if (L.pa < lim) {
-                if (L.slot == kNoSlot && !(L.ninfo & NI_CL)) {
+                if (L.slot == kNoSlot && !(L.ninfo & (NI_CL | NI_TE))) {
                     L.mode = M_SKIP;
                 } else {
                     L.mode = M_VALUE;
@@ -552,7 +566,7 @@ __device__ __forceinline__ void parse_window(const Img<kLds> &I, Lane &L, Cursor
                 }
             }
         }
-        if (L.mode == M_VALUE && !(L.ninfo & NI_CL)) {  // a value some rule looks at: DFA walk only
+        if (L.mode == M_VALUE && !(L.ninfo & (NI_CL | NI_TE))) {  // a value some rule looks at: DFA walk only
             // software pipeline as for the target: byte p+1 and its class are
             // read while the transition on byte p is in flight
             uint32_t c = 0;
@@ -591,23 +605,27 @@ __device__ __forceinline__ void parse_window(const Img<kLds> &I, Lane &L, Cursor
                 }
             }
         }
-        if (L.mode == M_VALUE) {  // Content-Length (and possibly a rule's DFA on it)
+        if (L.mode == M_VALUE) {  // Content-Length / Transfer-Encoding (and possibly a rule's DFA on it)
             uint32_t c = 0;
+            const bool te = (L.ninfo & NI_TE) != 0;
             for (; L.pa < lim; L.pa++) {
                 c = C.at(L.pa);
                 if ((c < 0x20 && c != '\t') || c == 0x7F) break;  // CR ends it; other CTLs are errors
                 const bool ws = c == ' ' || c == '\t';
                 if (ws && !L.in_ows) L.saved = L.st;
                 L.in_ows = ws;
-                L.cl_ws |= ws;
                 if (!ws) {
-                    if (c - '0' < 10u && !L.cl_ws) {
+                    if (te) {  // "chunked", case-insensitive, then trailing OWS only
+                        const uint32_t want = (uint32_t)(0x64656B6E756863ull >> (8 * min(L.ndig, 7u))) & 0xFF;
+                        L.ndig = (!L.cl_ws && L.ndig < 7 && (c | 0x20) == want) ? L.ndig + 1 : 0xFF;
+                    } else if (c - '0' < 10u && !L.cl_ws) {
                         L.clv = L.clv * 10 + (c - '0');
                         L.ndig++;
                     } else {
                         L.cl_bad = true;
                     }
                 }
+                L.cl_ws |= ws;
                 dfa_step(I, L, c);
             }
             if (L.pa < lim) {
@@ -658,6 +676,86 @@ __device__ __forceinline__ void parse_window(const Img<kLds> &I, Lane &L, Cursor
                 if (line_done(I, L)) L.mode = M_LINE;
                 else finish(L, V_PARSE_ERROR);
             }
+        }
+    }
+    // ---- chunked body: chunk = 1*HEXDIG [";" ext] CRLF data CRLF; size 0 ends
+    // the chunks, then trailer lines up to an empty line (oracle/http_ref.c)
+    while (L.mode > M_DONE && L.pa < lim) {
+        const uint32_t c = C.at(L.pa);
+        switch (L.mode) {
+        case M_CHSIZE: {
+            const uint32_t d = c - '0' < 10u ? c - '0' : (c | 0x20) - 'a' < 6u ? (c | 0x20) - 'a' + 10 : 0xFF;
+            if (d != 0xFF) {
+                L.clv = L.clv * 16 + d;
+                L.pa++;
+                if (L.clv > 0xFFFFFFFFull) finish(L, V_PARSE_ERROR);
+            } else if (L.pa == L.mark) {
+                finish(L, V_PARSE_ERROR);
+            } else if (c == ';') {
+                L.pa++;
+                L.mode = M_CHEXT;
+            } else if (c == '\r') {
+                L.pa++;
+                L.mode = M_CHLF;
+            } else {
+                finish(L, V_PARSE_ERROR);
+            }
+            break;
+        }
+        case M_CHEXT:
+            if (c == '\n') finish(L, V_PARSE_ERROR);
+            else if (c == '\r') L.mode = M_CHLF;
+            L.pa++;
+            break;
+        case M_CHLF:
+            if (c != '\n') { finish(L, V_PARSE_ERROR); break; }
+            L.pa++;
+            L.mode = L.clv ? M_CHDATA : M_TRL;
+            break;
+        case M_CHDATA:  // skip the data by its length
+            if ((uint64_t)(L.pa - L.a0) + L.clv > 0xFFFFFFFFull) {
+                finish(L, V_PARSE_ERROR);
+            } else if ((uint64_t)L.pa + L.clv > L.lena) {
+                L.pa = L.lena;
+                finish(L, V_INCOMPLETE);
+            } else {
+                L.pa += (uint32_t)L.clv;
+                L.mode = M_CHDCR;
+            }
+            break;
+        case M_CHDCR:
+            if (c != '\r') { finish(L, V_PARSE_ERROR); break; }
+            L.pa++;
+            L.mode = M_CHDLF;
+            break;
+        case M_CHDLF:
+            if (c != '\n') { finish(L, V_PARSE_ERROR); break; }
+            L.pa++;
+            L.mode = M_CHSIZE;
+            L.mark = L.pa;
+            L.clv = 0;
+            break;
+        case M_TRL:
+            if (c == '\n') { finish(L, V_PARSE_ERROR); break; }
+            L.mode = c == '\r' ? M_TRLEND : M_TRLSCAN;
+            L.pa++;
+            break;
+        case M_TRLSCAN:
+            if (c == '\n') finish(L, V_PARSE_ERROR);
+            else if (c == '\r') L.mode = M_TRLLF;
+            L.pa++;
+            break;
+        case M_TRLLF:
+            if (c != '\n') { finish(L, V_PARSE_ERROR); break; }
+            L.pa++;
+            L.mode = M_TRL;
+            break;
+        default:  // M_TRLEND
+            if (c != '\n') { finish(L, V_PARSE_ERROR); break; }
+            L.pa++;
+            finish(L, L.verdict, L.rule);
+            L.consumed = L.pa - L.a0;
+            break;
         }
     }
 }

@@ -43,6 +43,22 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr int kWaves = kBlock / 64;
+
+// Optional per-phase cycle accounting (-DL7G_KX_TIMING, experiment builds):
+// 0 framing, 1 walk loop, 2 CRC pass, 3 topic lookups, 4 verdict + output,
+// 5 walk iterations, 6 window refills, 7 tiles.
+#ifdef L7G_KX_TIMING
+__device__ unsigned long long g_kx_phase[8];
+#define KX_DECL uint64_t kx_t = __builtin_amdgcn_s_memtime(); uint64_t kx_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define KX_MARK(slot) do { const uint64_t kx_n = __builtin_amdgcn_s_memtime(); kx_acc[slot] += kx_n - kx_t; kx_t = kx_n; } while (0)
+#define KX_COUNT(slot, v) (kx_acc[slot] += (v))
+#define KX_FLUSH(lane) do { if ((lane) == 0) for (int kx_i = 0; kx_i < 8; kx_i++) atomicAdd(&g_kx_phase[kx_i], (unsigned long long)kx_acc[kx_i]); } while (0)
+#else
+#define KX_DECL
+#define KX_MARK(slot) do {} while (0)
+#define KX_COUNT(slot, v) do {} while (0)
+#define KX_FLUSH(lane) do {} while (0)
+#endif
 constexpr uint32_t kQueue = 192;  // CRC work items per wave (16 B each)
 constexpr uint32_t kMaxParseBuf = 6553500;
 constexpr uint32_t kInf = 0xFFFFFFFFu;
@@ -53,18 +69,21 @@ constexpr uint32_t kInf = 0xFFFFFFFFu;
 // the arena's 16-byte rounding; see include/l7gpu.h).
 struct Cur {
     uintptr_t line;  // address of the cached chunk (~0 = none)
-    uint32_t w[4];
+    uint32_t w0, w1, w2, w3;  // scalars, not an array: a selected array element would put Cur in scratch
 };
 __device__ __forceinline__ void cur_fill(Cur &c, uintptr_t a) {
     const uintptr_t ln = a & ~(uintptr_t)15;
     if (ln != c.line) {
         const uint4 v = *reinterpret_cast<const uint4 *>(ln);
-        c.w[0] = v.x; c.w[1] = v.y; c.w[2] = v.z; c.w[3] = v.w;
+        c.w0 = v.x; c.w1 = v.y; c.w2 = v.z; c.w3 = v.w;
         c.line = ln;
     }
 }
+// (values are copied out before they are selected: a select between struct
+// members becomes a select between their addresses, i.e. a scratch array)
 __device__ __forceinline__ uint32_t cur_word(const Cur &c, uint32_t k) {
-    return k < 8 ? (k < 4 ? c.w[0] : c.w[1]) : (k < 12 ? c.w[2] : c.w[3]);
+    const uint32_t a = c.w0, b = c.w1, d = c.w2, e = c.w3;
+    return k < 8 ? (k < 4 ? a : b) : (k < 12 ? d : e);
 }
 __device__ __forceinline__ uint32_t cur_byte(Cur &c, const uint8_t *p) {
     const uintptr_t a = (uintptr_t)p;
@@ -76,8 +95,9 @@ __device__ __forceinline__ uint32_t cur_byte(Cur &c, const uint8_t *p) {
 __device__ __forceinline__ uint32_t cur_le32(Cur &c, uintptr_t a) {
     cur_fill(c, a);
     const uint32_t k = (uint32_t)(a & 15), i = k >> 2;
-    const uint32_t lo = i == 0 ? c.w[0] : i == 1 ? c.w[1] : i == 2 ? c.w[2] : c.w[3];
-    const uint32_t hi = i == 0 ? c.w[1] : i == 1 ? c.w[2] : c.w[3];
+    const uint32_t w0 = c.w0, w1 = c.w1, w2 = c.w2, w3 = c.w3;
+    const uint32_t lo = i == 0 ? w0 : i == 1 ? w1 : i == 2 ? w2 : w3;
+    const uint32_t hi = i == 0 ? w1 : i == 1 ? w2 : w3;
     return __builtin_amdgcn_alignbyte(hi, lo, k & 3);
 }
 // big-endian n-byte field (n = 1, 2, 4, 8)
@@ -167,7 +187,8 @@ __device__ __forceinline__ uint32_t crc_byte(const uint32_t *tab, uint32_t c, ui
     return tab[(c ^ b) & 0xFF] ^ (c >> 8);
 }
 __device__ __forceinline__ uint32_t word_of(const uint4 &v, uint32_t q) {
-    return q < 8 ? (q < 4 ? v.x : v.y) : (q < 12 ? v.z : v.w);
+    const uint32_t x = v.x, y = v.y, z = v.z, w = v.w;  // values, not member addresses (see cur_word)
+    return q < 8 ? (q < 4 ? x : y) : (q < 12 ? z : w);
 }
 // one lane, one buffer (exact redo path)
 __device__ uint32_t crc32_ieee(const uint32_t *tab, Cur &cur, const uint8_t *p, uint32_t n) {
@@ -348,7 +369,7 @@ __device__ __forceinline__ bool frame_request(Cur &cur, const uint8_t *b, uint32
     return true;
 }
 
-__device__ __noinline__ void classify_exact(const KafkaTables &T, const DevConn &conn, const uint8_t *b, uint32_t len,
+__device__ __forceinline__ void classify_exact(const KafkaTables &T, const DevConn &conn, const uint8_t *b, uint32_t len,
                                             const uint32_t *crctab, Result &out) {
     Cur cur;
     cur.line = ~(uintptr_t)0;
@@ -510,6 +531,8 @@ enum : uint8_t {
     P_ARR,       // DecodeArrayLen (a: nullable), b: loop level; skips to after the matching P_NEXT if empty
     P_NEXT,      // end of a loop body (b: level): next element (no decoder error) or fall through
     P_PART,      // produce partition: id, set size, readMessageSet
+    P_ARRSK,     // DecodeArrayLen of fixed-size elements nobody looks at: the loop is one skip of
+                 // count * (a + extra) bytes (b: extra = 1: 8 if version >= 5, 2: 4 if version == 0)
 };
 struct POp {
     uint8_t op, a, b, jump;  // jump: P_ARR -> index after its P_NEXT; P_NEXT -> body start
@@ -523,134 +546,155 @@ __constant__ POp kProg[] = {
     PO(P_END, 0, 0, 0),
     // 10: Fetch (:767-824)
     PO(P_CLIENT, 0, 0, 0), PO(P_SKIP, 12, 0, 0), PO(P_SKIP_VGE, 4, 3, 0), PO(P_SKIP_VGE, 1, 4, 0),
-    PO(P_ARR, 0, 0, 22), PO(P_TOPIC, 0, 0, 0), PO(P_ARR, 0, 1, 21), PO(P_SKIP, 12, 0, 0), PO(P_SKIP_VGE, 8, 5, 0),
-    PO(P_SKIP, 4, 0, 0), PO(P_NEXT, 0, 1, 17), PO(P_NEXT, 0, 0, 15), PO(P_END, 0, 0, 0),
-    // 23: Offset (:1810-1858)
-    PO(P_CLIENT, 0, 0, 0), PO(P_SKIP, 4, 0, 0), PO(P_SKIP_VGE, 1, 2, 0), PO(P_ARR, 0, 0, 33), PO(P_TOPIC, 0, 0, 0),
-    PO(P_ARR, 0, 1, 32), PO(P_SKIP, 12, 0, 0), PO(P_SKIP_VEQ, 4, 0, 0), PO(P_NEXT, 0, 1, 29), PO(P_NEXT, 0, 0, 27),
-    PO(P_END, 0, 0, 0),
-    // 34: Metadata (:504-537)
-    PO(P_CLIENT, 0, 0, 0), PO(P_ARR, 1, 0, 38), PO(P_TOPIC_OK, 0, 0, 0), PO(P_NEXT, 0, 0, 36),
+    PO(P_ARR, 0, 0, 18), PO(P_TOPIC, 0, 0, 0), PO(P_ARRSK, 16, 1, 0), PO(P_NEXT, 0, 0, 15), PO(P_END, 0, 0, 0),
+    // 19: Offset (:1810-1858)
+    PO(P_CLIENT, 0, 0, 0), PO(P_SKIP, 4, 0, 0), PO(P_SKIP_VGE, 1, 2, 0), PO(P_ARR, 0, 0, 26), PO(P_TOPIC, 0, 0, 0),
+    PO(P_ARRSK, 12, 2, 0), PO(P_NEXT, 0, 0, 23), PO(P_END, 0, 0, 0),
+    // 27: Metadata (:504-537)
+    PO(P_CLIENT, 0, 0, 0), PO(P_ARR, 1, 0, 31), PO(P_TOPIC_OK, 0, 0, 0), PO(P_NEXT, 0, 0, 29),
     PO(P_SKIP_VGE, 1, 4, 0), PO(P_END, 0, 0, 0),
-    // 40: OffsetCommit (:1173-1228)
+    // 33: OffsetCommit (:1173-1228)
     PO(P_CLIENT, 0, 0, 0), PO(P_STR, 0, 0, 0), PO(P_SKIP_VGE, 4, 1, 0), PO(P_STR_VGE, 0, 1, 0),
-    PO(P_SKIP_VGE, 8, 2, 0), PO(P_ARR, 0, 0, 53), PO(P_TOPIC, 0, 0, 0), PO(P_ARR, 0, 1, 52), PO(P_SKIP, 12, 0, 0),
-    PO(P_SKIP_VEQ, 8, 1, 0), PO(P_STR, 0, 0, 0), PO(P_NEXT, 0, 1, 48), PO(P_NEXT, 0, 0, 46), PO(P_END, 0, 0, 0),
-    // 54: OffsetFetch (:1389-1430)
-    PO(P_CLIENT, 0, 0, 0), PO(P_STR, 0, 0, 0), PO(P_ARR, 1, 0, 62), PO(P_TOPIC, 0, 0, 0), PO(P_ARR, 0, 1, 61),
-    PO(P_SKIP, 4, 0, 0), PO(P_NEXT, 0, 1, 59), PO(P_NEXT, 0, 0, 57), PO(P_END, 0, 0, 0),
-    // 63: ConsumerMetadata (:1033-1054)
+    PO(P_SKIP_VGE, 8, 2, 0), PO(P_ARR, 0, 0, 46), PO(P_TOPIC, 0, 0, 0), PO(P_ARR, 0, 1, 45), PO(P_SKIP, 12, 0, 0),
+    PO(P_SKIP_VEQ, 8, 1, 0), PO(P_STR, 0, 0, 0), PO(P_NEXT, 0, 1, 41), PO(P_NEXT, 0, 0, 39), PO(P_END, 0, 0, 0),
+    // 47: OffsetFetch (:1389-1430)
+    PO(P_CLIENT, 0, 0, 0), PO(P_STR, 0, 0, 0), PO(P_ARR, 1, 0, 53), PO(P_TOPIC, 0, 0, 0), PO(P_ARRSK, 4, 0, 0),
+    PO(P_NEXT, 0, 0, 50), PO(P_END, 0, 0, 0),
+    // 54: ConsumerMetadata (:1033-1054)
     PO(P_CLIENT, 0, 0, 0), PO(P_STR, 0, 0, 0), PO(P_SKIP_VGE, 1, 1, 0), PO(P_END, 0, 0, 0),
 };
 #undef PO
-constexpr uint32_t kProgLen = 67;
+constexpr uint32_t kProgLen = 58;
 static_assert(sizeof(kProg) == kProgLen * sizeof(POp), "program table");
 static_assert(kProgLen <= kBlock, "one thread per program entry");
 __device__ __forceinline__ uint32_t prog_start(int kind) {
-    return kind == 0 ? 0 : kind == 1 ? 10 : kind == 2 ? 23 : kind == 3 ? 34 : kind == 8 ? 40 : kind == 9 ? 54 : 63;
+    return kind == 0 ? 0 : kind == 1 ? 10 : kind == 2 ? 19 : kind == 3 ? 27 : kind == 8 ? 33 : kind == 9 ? 47 : 54;
 }
 
 // message-set sub-states (readMessageSet, messages.go:363-494)
-enum : uint8_t { M_NONE = 0, M_HEAD, M_CRC, M_ATTR, M_TS, M_KEY, M_VALUE };
+enum : uint8_t { M_NONE = 0, M_HEAD, M_CRC, M_KEY, M_VALUE };
 
-// 32-byte register window of a lane's request
+// 32-byte register window of a lane's request, as four 64-bit words
 struct Win {
-    uint64_t wa;  // address of w[0] (16-byte aligned); ~0: empty
-    uint32_t w[8];
+    uint64_t wa;  // address of q0's first byte (16-byte aligned)
+    uint64_t q0, q1, q2, q3;  // scalars: an indexed array would live in scratch
 };
-__device__ __forceinline__ uint32_t wsel(const Win &W, uint32_t i) {
-    return i < 4 ? (i < 2 ? (i == 0 ? W.w[0] : W.w[1]) : (i == 2 ? W.w[2] : W.w[3]))
-                 : (i < 6 ? (i == 4 ? W.w[4] : W.w[5]) : (i == 6 ? W.w[6] : W.w[7]));
-}
 __device__ __forceinline__ bool win_has(const Win &W, uint64_t a, uint32_t n) { return a >= W.wa && a + n <= W.wa + 32; }
-// big-endian n-byte value (n = 1, 2, 4, 8) at a; win_has(W, a, n)
-__device__ __forceinline__ uint64_t win_be(const Win &W, uint64_t a, uint32_t n) {
-    const uint32_t k = (uint32_t)(a - W.wa), i = k >> 2, sh = k & 3;
-    const uint32_t w0 = wsel(W, i), w1 = wsel(W, min(i + 1, 7u)), w2 = wsel(W, min(i + 2, 7u));
-    const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, sh), hi = __builtin_amdgcn_alignbyte(w2, w1, sh);
-    const uint64_t be = (uint64_t)__builtin_bswap32(lo) << 32 | __builtin_bswap32(hi);
-    return be >> (64 - 8 * n);
+// big-endian value of the vn (1..8) bytes at a; win_has(W, a, vn)
+__device__ __forceinline__ uint64_t win_be(const Win &W, uint64_t a, uint32_t vn) {
+    const uint32_t k = (uint32_t)(a - W.wa), i = k >> 3, sh = (k & 7) * 8;
+    const uint64_t x0 = W.q0, x1 = W.q1, x2 = W.q2, x3 = W.q3;
+    const uint64_t lo = i == 0 ? x0 : i == 1 ? x1 : i == 2 ? x2 : x3;
+    const uint64_t hi = i == 0 ? x1 : i == 1 ? x2 : x3;
+    const uint64_t le = sh ? (lo >> sh) | (hi << (64 - sh)) : lo;  // the 8 bytes at a, little-endian
+    const uint64_t be = (uint64_t)__builtin_bswap32((uint32_t)le) << 32 | __builtin_bswap32((uint32_t)(le >> 32));
+    return be >> (64 - 8 * vn);
 }
 
 struct Walk {
-    // outer decoder (bytes.Buffer over rawMsg) and readMessageSet's LimitReader decoder share pos
-    uint32_t pos, end;
-    bool err;            // outer decoder error (sticky)
+    // outer decoder (bytes.Buffer over rawMsg) and readMessageSet's LimitReader
+    // decoder share pos; the message decoder has its own (mpos)
+    uint32_t pos, end, mpos, mend, slim;
+    bool err, serr, merr;  // sticky decoder errors
     // program
     uint32_t pc;
     int32_t cnt0, cnt1;  // remaining elements of the topic / partition loop
     int rc;              // RS_OK / RS_ERROR / RS_COMPRESSED
     bool done;
-    // readMessageSet
-    uint8_t ms;          // M_* sub-state
-    bool serr;           // set decoder error
-    uint64_t slim;       // set LimitReader end position
-    uint32_t at, mend, mpos;  // current message body [at, mend), message decoder position
-    bool merr;
+    uint32_t ms;         // M_* sub-state (readMessageSet)
+    uint32_t at;         // current message body start
     int codec;
     // findings
     uint32_t ntopics;
     uint32_t client_off, client_len;
     // window request
     bool need;
-    uint64_t need_a;     // address the window must start at (rounded down)
-    // queued work this step (pushed by the wave between steps)
+    uint32_t need_pos;   // request position the window must cover
+    // queued work (pushed by the wave at the end of the round)
     bool has_crc, has_topic;
     uint32_t crc_off, crc_len, crc_want, top_off, top_len;
 };
 
-// Read n bytes (an integer field) at position P below bound lim on a decoder
-// with sticky error E (io.ReadFull semantics: nothing left => EOF, a partial
-// read advances P).  Returns 0 = value read, 1 = error (value 0), 2 = the
-// window does not cover it (nothing changed).
-__device__ __forceinline__ int rd_int(const Win &W, const uint8_t *b, uint32_t &P, uint64_t lim, bool &E, uint32_t n,
-                                      uint64_t &v, Walk &S) {
-    v = 0;
-    if (E) return 1;
-    const uint64_t avail = lim > P ? lim - P : 0;
-    if (avail == 0) { E = true; return 1; }
-    if (avail < n) { P += (uint32_t)avail; E = true; return 1; }
-    const uint64_t a = (uint64_t)(uintptr_t)(b + P);
-    if (!win_has(W, a, n)) { S.need = true; S.need_a = a; return 2; }
-    v = win_be(W, a, n);
-    P += n;
-    return 0;
-}
-// io.ReadFull of n bytes that nobody looks at: bounds only
-__device__ __forceinline__ bool rd_skip(uint32_t &P, uint64_t lim, bool &E, uint32_t n) {
+// io.ReadFull of n bytes that nobody looks at: bounds only (sticky error E,
+// a short read advances P to the bound)
+__device__ __forceinline__ bool rd_skip(uint32_t &P, uint32_t lim, bool &E, uint32_t n) {
     if (E || n == 0) return !E;
-    const uint64_t avail = lim > P ? lim - P : 0;
+    const uint32_t avail = lim > P ? lim - P : 0;
     if (avail == 0) { E = true; return false; }
-    if (avail < n) { P += (uint32_t)avail; E = true; return false; }
+    if (avail < n) { P += avail; E = true; return false; }
     P += n;
     return true;
 }
 
-// One step of a lane's walk; false when it must stop (window needed, work
-// queued, or done).
+// One step of a lane's walk: one field (or a fixed group of fields with the
+// same error outcome) read through one common path.  false = stop (window
+// needed, an item pending already, or done).
 __device__ __forceinline__ bool walk_step(Walk &S, const Win &W, const uint8_t *b, int ver, const POp *prog) {
-    uint64_t v;
-    if (S.ms != M_NONE) {
-        // ---- readMessageSet: one message per pass through these states
-        const uint64_t slim = min((uint64_t)S.end, S.slim);
-        if (S.ms == M_HEAD) {  // offset i64, size i32, body
-            const uint32_t P0 = S.pos;
-            bool e2 = S.serr;
-            uint64_t off;
-            int r = rd_int(W, b, S.pos, slim, e2, 8, off, S);
-            if (r == 2) return false;
-            if (r == 0) {
-                // size immediately follows: both in the window or refetch from the offset
-                r = rd_int(W, b, S.pos, slim, e2, 4, v, S);
-                if (r == 2) { S.pos = P0; S.need_a = (uint64_t)(uintptr_t)(b + P0); return false; }
+    // ---- A. what the step reads: n bytes on decoder dec (0 outer, 1 set, 2 message),
+    //         the value is the last vn of them
+    POp o{0, 0, 0, 0};
+    uint32_t dec = 0, n = 0, vn = 0;
+    const uint32_t ms = S.ms;
+    if (ms != M_NONE) {
+        // readMessageSet (messages.go:363-494): offset i64 + size i32 (one
+        // outcome: any short read ends the set), crc u32, magic + attributes,
+        // timestamp i64 (version >= 1), key / value i32 lengths
+        dec = ms == M_HEAD ? 1 : 2;
+        // M_CRC: crc u32 + magic i8 + attributes i8 (the body holds >= 5 bytes;
+        // a missing attributes byte is a short read of the message decoder)
+        n = ms == M_HEAD ? 12 : ms == M_CRC ? min(6u, S.mend - S.mpos) : 4;
+        vn = ms == M_HEAD ? 4 : n;
+    } else {
+        o = prog[S.pc];
+        if (o.op == P_STR || o.op == P_STR_VGE || o.op == P_CLIENT || o.op == P_TOPIC || o.op == P_TOPIC_OK) {
+            if (o.op != P_STR_VGE || ver >= o.b) n = vn = 2;  // DecodeString: i16 length
+        } else if (o.op == P_ARR || o.op == P_ARRSK) {
+            n = vn = 4;  // DecodeArrayLen: i32
+        } else if (o.op == P_PART) {
+            n = 8;  // partition id i32 + set size i32 (either short read is fatal)
+            vn = 4;
+        }
+    }
+    // ---- B. the read (io.ReadFull semantics: nothing left => EOF, a partial
+    //         read advances the position; errors are sticky)
+    uint32_t P = dec == 2 ? S.mpos : S.pos;
+    const uint32_t lim = dec == 0 ? S.end : dec == 1 ? min(S.end, S.slim) : S.mend;
+    bool E = dec == 0 ? S.err : dec == 1 ? S.serr : S.merr;
+    uint64_t v = 0;
+    bool ok = true;  // value read
+    if (n) {
+        if (E) {
+            ok = false;
+        } else {
+            const uint32_t avail = lim > P ? lim - P : 0;
+            if (avail < n) {
+                P += avail;
+                E = true;
+                ok = false;
+            } else {
+                const uint64_t a = (uint64_t)(uintptr_t)(b + P);
+                if (!win_has(W, a, n)) {
+                    S.need = true;
+                    S.need_pos = P;
+                    return false;
+                }
+                v = win_be(W, a + n - vn, vn);
+                P += n;
             }
-            S.serr = e2;
+        }
+        if (dec == 2) { S.mpos = P; S.merr = E; }
+        else if (dec == 1) { S.pos = P; S.serr = E; }
+        else { S.pos = P; S.err = E; }
+    }
+    // ---- C. what the value means
+    if (ms != M_NONE) {
+        if (ms == M_HEAD) {
             const int32_t msize = (int32_t)(uint32_t)v;
-            if (r != 0 || msize <= 0) { S.ms = M_NONE; return true; }  // set done
+            if (!ok || msize <= 0) { S.ms = M_NONE; return true; }  // the set ends
             if ((uint32_t)msize > kMaxParseBuf) { S.rc = RS_ERROR; S.done = true; return false; }
             const uint32_t at = S.pos;
-            if (!rd_skip(S.pos, slim, S.serr, (uint32_t)msize)) { S.ms = M_NONE; return true; }
-            if (msize <= 4) { S.ms = M_NONE; return true; }  // crc only: appended, set stops
+            if (!rd_skip(S.pos, min(S.end, S.slim), S.serr, (uint32_t)msize)) { S.ms = M_NONE; return true; }
+            if (msize <= 4) { S.ms = M_NONE; return true; }  // crc only: appended, the set stops
             S.at = at;
             S.mend = at + (uint32_t)msize;
             S.mpos = at;
@@ -658,53 +702,32 @@ __device__ __forceinline__ bool walk_step(Walk &S, const Win &W, const uint8_t *
             S.ms = M_CRC;
             return true;
         }
-        if (S.ms == M_CRC) {  // crc u32 (the body holds > 4 bytes), queued for the wave's CRC pass
-            const int r = rd_int(W, b, S.mpos, S.mend, S.merr, 4, v, S);
-            if (r == 2) return false;
+        if (ms == M_CRC) {  // the body holds > 4 bytes: the crc is there; queue the check
+            if (S.has_crc) { S.mpos -= n; return false; }  // one item per lane per round
             S.has_crc = true;
             S.crc_off = S.at + 4;
             S.crc_len = S.mend - S.at - 4;
-            S.crc_want = (uint32_t)v;
-            S.ms = M_ATTR;
-            return false;  // the wave pushes the item
-        }
-        if (S.ms == M_ATTR) {  // magic i8, attributes i8
-            const uint32_t P0 = S.mpos;
-            int r = rd_int(W, b, S.mpos, S.mend, S.merr, 1, v, S);
-            if (r == 2) return false;
-            uint64_t attr = 0;
-            if (r == 0) {
-                r = rd_int(W, b, S.mpos, S.mend, S.merr, 1, attr, S);
-                if (r == 2) { S.mpos = P0; S.need_a = (uint64_t)(uintptr_t)(b + P0); return false; }
-            }
-            S.codec = (int)(attr & 3);
-            S.ms = ver >= 1 ? M_TS : M_KEY;
-            if (S.ms == M_KEY && S.codec == 3) { S.ms = M_NONE; }  // `return nil, err` with err == nil
+            S.crc_want = (uint32_t)(v >> (8 * (n - 4)));
+            if (n < 6) S.merr = true;  // attributes missing: short read (codec 0)
+            S.codec = n == 6 ? (int)(v & 3) : 0;
+            if (ver >= 1) rd_skip(S.mpos, S.mend, S.merr, 8);  // timestamp i64
+            S.ms = S.codec == 3 ? M_NONE : M_KEY;  // codec 3: `return nil, nil`
             return true;
         }
-        if (S.ms == M_TS) {  // timestamp i64 (version >= 1)
-            const int r = rd_int(W, b, S.mpos, S.mend, S.merr, 8, v, S);
-            if (r == 2) return false;
-            S.ms = S.codec == 3 ? M_NONE : M_KEY;
-            return true;
-        }
-        // M_KEY / M_VALUE: DecodeBytes (i32 length, < 1 => nil, > max => error)
-        const int r = rd_int(W, b, S.mpos, S.mend, S.merr, 4, v, S);
-        if (r == 2) return false;
-        if (r == 0) {
+        // M_KEY / M_VALUE: DecodeBytes (< 1 => nil, > max => error, else the bytes)
+        if (ok) {
             const int32_t sl = (int32_t)(uint32_t)v;
             if (sl >= 1) {
                 if ((uint32_t)sl > kMaxParseBuf) S.merr = true;
                 else rd_skip(S.mpos, S.mend, S.merr, (uint32_t)sl);
             }
         }
-        if (S.ms == M_KEY) { S.ms = M_VALUE; return true; }
+        if (ms == M_KEY) { S.ms = M_VALUE; return true; }
         if (S.merr) { S.rc = RS_ERROR; S.done = true; return false; }
         if (S.codec != 0) { S.rc = RS_COMPRESSED; S.done = true; return false; }
         S.ms = M_HEAD;  // next message
         return true;
     }
-    const POp o = prog[S.pc];
     switch (o.op) {
     case P_END:
         S.done = true;
@@ -715,18 +738,52 @@ __device__ __forceinline__ bool walk_step(Walk &S, const Win &W, const uint8_t *
         if (o.op == P_SKIP || (o.op == P_SKIP_VGE ? ver >= o.b : ver == o.b)) rd_skip(S.pos, S.end, S.err, o.a);
         S.pc++;
         return true;
-    case P_STR_VGE:
-    case P_STR:
-    case P_CLIENT:
-    case P_TOPIC:
-    case P_TOPIC_OK: {
+    case P_ARR: {
+        int32_t l = (int32_t)(uint32_t)v;  // 0 after an error
+        if (l < 0) {
+            if (!o.a) { S.rc = RS_ERROR; S.done = true; return false; }  // ErrInvalidArrayLen
+            l = 0;  // null array
+        }
+        if ((uint32_t)l > kMaxParseBuf) { S.rc = RS_ERROR; S.done = true; return false; }
+        if (o.b == 0) S.cnt0 = l; else S.cnt1 = l;
+        S.pc = (l > 0 && !S.err) ? S.pc + 1 : o.jump;
+        return true;
+    }
+    case P_ARRSK: {
+        const int32_t l = (int32_t)(uint32_t)v;  // 0 after an error
+        if (l < 0 || (uint32_t)l > kMaxParseBuf) { S.rc = RS_ERROR; S.done = true; return false; }
+        const uint32_t sz = o.a + (o.b == 1 ? (ver >= 5 ? 8u : 0u) : o.b == 2 ? (ver == 0 ? 4u : 0u) : 0u);
+        if (l > 0) rd_skip(S.pos, S.end, S.err, (uint32_t)l * sz);  // <= 6,553,500 * 24: no overflow
+        S.pc++;
+        return true;
+    }
+    case P_NEXT: {
+        const int32_t c = (o.b == 0 ? S.cnt0 : S.cnt1) - 1;
+        if (o.b == 0) S.cnt0 = c; else S.cnt1 = c;
+        S.pc = (c > 0 && !S.err) ? o.jump : S.pc + 1;
+        return true;
+    }
+    case P_PART: {
+        if (!ok) { S.rc = RS_ERROR; S.done = true; return false; }
+        const int32_t ss = (int32_t)(uint32_t)v;
+        S.pc++;
+        if (ss < 0) return true;  // null set
+        if ((uint32_t)ss > kMaxParseBuf) { S.rc = RS_ERROR; S.done = true; return false; }
+        S.slim = S.pos + (uint32_t)ss;
+        S.serr = false;
+        S.ms = M_HEAD;
+        return true;
+    }
+    default: {  // strings: P_STR, P_STR_VGE, P_CLIENT, P_TOPIC, P_TOPIC_OK
         if (o.op == P_STR_VGE && ver < o.b) { S.pc++; return true; }
-        // DecodeString: i16 length, < 1 => "", then the bytes
-        const int r = rd_int(W, b, S.pos, S.end, S.err, 2, v, S);
-        if (r == 2) return false;
+        const bool topic = o.op == P_TOPIC || o.op == P_TOPIC_OK;
+        if (topic && S.has_topic) {  // one topic per lane per round: this step again next round
+            if (ok) S.pos -= 2;  // (after a failed read the sticky error makes the redo identical)
+            return false;
+        }
         const int32_t sl = (int16_t)(uint16_t)v;
         uint32_t so = 0, sn = 0;
-        if (r == 0 && sl >= 1) {
+        if (ok && sl >= 1) {
             const uint32_t at = S.pos;
             if (rd_skip(S.pos, S.end, S.err, (uint32_t)sl)) { so = at; sn = (uint32_t)sl; }
         }
@@ -738,45 +795,7 @@ __device__ __forceinline__ bool walk_step(Walk &S, const Win &W, const uint8_t *
             S.top_off = so;
             S.top_len = sn;
             S.ntopics++;
-            return false;  // the wave queues the topic
         }
-        return true;
-    }
-    case P_ARR: {
-        const int r = rd_int(W, b, S.pos, S.end, S.err, 4, v, S);
-        if (r == 2) return false;
-        int32_t l = (int32_t)(uint32_t)v;  // 0 after an error
-        if (l < 0) {
-            if (!o.a) { S.rc = RS_ERROR; S.done = true; return false; }  // ErrInvalidArrayLen
-            l = 0;  // null array
-        }
-        if ((uint32_t)l > kMaxParseBuf) { S.rc = RS_ERROR; S.done = true; return false; }
-        if (o.b == 0) S.cnt0 = l; else S.cnt1 = l;
-        S.pc = (l > 0 && !S.err) ? S.pc + 1 : o.jump;
-        return true;
-    }
-    case P_NEXT: {
-        int32_t &c = o.b == 0 ? S.cnt0 : S.cnt1;
-        c--;
-        S.pc = (c > 0 && !S.err) ? o.jump : S.pc + 1;
-        return true;
-    }
-    default: {  // P_PART: partition id i32, set size i32 (errors are fatal), readMessageSet
-        const uint32_t P0 = S.pos;
-        int r = rd_int(W, b, S.pos, S.end, S.err, 4, v, S);
-        if (r == 2) return false;
-        if (r == 0) {
-            r = rd_int(W, b, S.pos, S.end, S.err, 4, v, S);
-            if (r == 2) { S.pos = P0; S.need_a = (uint64_t)(uintptr_t)(b + P0); return false; }
-        }
-        if (r != 0) { S.rc = RS_ERROR; S.done = true; return false; }
-        const int32_t ss = (int32_t)(uint32_t)v;
-        S.pc++;
-        if (ss < 0) return true;  // null set
-        if ((uint32_t)ss > kMaxParseBuf) { S.rc = RS_ERROR; S.done = true; return false; }
-        S.slim = (uint64_t)S.pos + (uint32_t)ss;
-        S.serr = false;
-        S.ms = M_HEAD;
         return true;
     }
     }
@@ -795,8 +814,8 @@ struct WaveLds {
     int32_t *client;       // interned client id (-2 none)
     int32_t *kind, *ver;
 };
-constexpr uint32_t kCrcQ = 256;   // CRC items per wave
-constexpr uint32_t kTopQ = 128;   // topics per wave
+constexpr uint32_t kCrcQ = 320;   // CRC items per wave (cfg3: ~160 per 64 requests)
+constexpr uint32_t kTopQ = 320;   // topics per wave (cfg3: ~140 per 64 requests)
 
 // CRC pass over items [0, n): lane t starts on item t, 64 bytes per step; a
 // lane whose message is done takes the next unclaimed item.  ORs the request
@@ -837,18 +856,33 @@ __device__ __forceinline__ uint64_t crc_pass(const WaveLds &Q, uint32_t nitems, 
     L.a = 0;
     L.rem = L.want = L.owner = L.c = 0;
     if (lane < nitems) crc_load(L, Q, lane, tab);
+    // 64-byte blocks are software-pipelined: the next block of the lane's
+    // message is loaded while the current one is hashed
+    uint4 pf0 = make_uint4(0, 0, 0, 0), pf1 = pf0, pf2 = pf0, pf3 = pf0;
+    bool haspf = false;
     while (__any(L.have)) {
         if (L.have) {
             if (L.rem >= 64) {
-                const uint4 *p = reinterpret_cast<const uint4 *>(L.a);
-                uint4 v[4];
-#pragma unroll
-                for (int j = 0; j < 4; j++) v[j] = p[j];
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    L.c = crc_step8(tab, L.c, v[j].x, v[j].y);
-                    L.c = crc_step8(tab, L.c, v[j].z, v[j].w);
+                uint4 v0, v1, v2, v3;
+                if (haspf) {
+                    v0 = pf0; v1 = pf1; v2 = pf2; v3 = pf3;
+                } else {
+                    const uint4 *p = reinterpret_cast<const uint4 *>(L.a);
+                    v0 = p[0]; v1 = p[1]; v2 = p[2]; v3 = p[3];
                 }
+                haspf = L.rem >= 128;  // the next block lies inside the message
+                if (haspf) {
+                    const uint4 *q = reinterpret_cast<const uint4 *>(L.a + 64);
+                    pf0 = q[0]; pf1 = q[1]; pf2 = q[2]; pf3 = q[3];
+                }
+                L.c = crc_step8(tab, L.c, v0.x, v0.y);
+                L.c = crc_step8(tab, L.c, v0.z, v0.w);
+                L.c = crc_step8(tab, L.c, v1.x, v1.y);
+                L.c = crc_step8(tab, L.c, v1.z, v1.w);
+                L.c = crc_step8(tab, L.c, v2.x, v2.y);
+                L.c = crc_step8(tab, L.c, v2.z, v2.w);
+                L.c = crc_step8(tab, L.c, v3.x, v3.y);
+                L.c = crc_step8(tab, L.c, v3.z, v3.w);
                 L.a += 64;
                 L.rem -= 64;
             } else {  // tail: < 64 bytes from an aligned address
@@ -868,7 +902,10 @@ __device__ __forceinline__ uint64_t crc_pass(const WaveLds &Q, uint32_t nitems, 
         }
         const uint64_t idle = __ballot(!L.have);
         const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0));
-        if (!L.have && next + rank < nitems) crc_load(L, Q, next + rank, tab);
+        if (!L.have && next + rank < nitems) {
+            crc_load(L, Q, next + rank, tab);
+            haspf = false;
+        }
         next += (uint32_t)__builtin_popcountll(idle);
     }
     uint32_t lo = (uint32_t)bad, hi = (uint32_t)(bad >> 32);
@@ -936,7 +973,9 @@ __global__ __launch_bounds__(kBlock) void kafka_classify_kernel(Batch B, KafkaTa
     const uint32_t m = sel ? sel_count[0] : B.n;
     const uint32_t ntiles = (m + 63) / 64;
     uint32_t vcount[5] = {0, 0, 0, 0, 0};
+    KX_DECL
     for (uint32_t tile = blockIdx.x * kWaves + wave; tile < ntiles; tile += gridDim.x * kWaves) {
+        KX_COUNT(7, 1);
         const uint32_t i = tile * 64 + lane;
         uint32_t idx = 0;
         bool mine = false, answer = false;
@@ -982,7 +1021,7 @@ __global__ __launch_bounds__(kBlock) void kafka_classify_kernel(Batch B, KafkaTa
         S.ntopics = 0;
         S.client_off = S.client_len = 0;
         S.need = !S.done;
-        S.need_a = (uint64_t)(uintptr_t)(b + 12);
+        S.need_pos = 12;
         S.has_crc = S.has_topic = false;
         Win W;
         W.wa = ~0ull;
@@ -992,22 +1031,27 @@ __global__ __launch_bounds__(kBlock) void kafka_classify_kernel(Batch B, KafkaTa
         Q.kind[lane] = q.kind;
         Q.ver[lane] = q.version;
         uint32_t nc = 0, nt = 0;  // queued CRC items / topics (wave-uniform)
-        uint64_t bad = 0;         // request lanes with a mismatching CRC
+        bool ovf = false;         // a queue was full: exact redo
         bool client_done = false;
         const uint64_t req_end = (uint64_t)(uintptr_t)b + len;
+        KX_MARK(0);
         while (__any(!S.done)) {
+            KX_COUNT(5, 1);
+            KX_COUNT(6, __builtin_popcountll(__ballot(!S.done && S.need)));
             // refill the windows of the lanes that stopped on one (all loads in flight together)
             if (!S.done && S.need) {
-                W.wa = S.need_a & ~(uint64_t)15;
+                W.wa = (uint64_t)(uintptr_t)(b + S.need_pos) & ~(uint64_t)15;
                 const uint4 v0 = *reinterpret_cast<const uint4 *>(W.wa);
                 uint4 v1 = make_uint4(0, 0, 0, 0);
                 if (W.wa + 16 < req_end) v1 = *reinterpret_cast<const uint4 *>(W.wa + 16);
-                W.w[0] = v0.x; W.w[1] = v0.y; W.w[2] = v0.z; W.w[3] = v0.w;
-                W.w[4] = v1.x; W.w[5] = v1.y; W.w[6] = v1.z; W.w[7] = v1.w;
+                W.q0 = (uint64_t)v0.x | (uint64_t)v0.y << 32;
+                W.q1 = (uint64_t)v0.z | (uint64_t)v0.w << 32;
+                W.q2 = (uint64_t)v1.x | (uint64_t)v1.y << 32;
+                W.q3 = (uint64_t)v1.z | (uint64_t)v1.w << 32;
                 S.need = false;
             }
-            // run until a window, a queue slot or the end is needed
-            if (!S.done && !S.need && !S.has_crc && !S.has_topic)
+            // run until a window is needed, a second item is pending, or the end
+            if (!S.done && !S.need)
                 while (walk_step(S, W, b, q.version, s_prog)) {}
             // the client id: once every lane has read it (its first field)
             if (!client_done && !__any(!S.done && S.pc == prog_start(q.kind) && S.ms == M_NONE)) {
@@ -1022,55 +1066,46 @@ __global__ __launch_bounds__(kBlock) void kafka_classify_kernel(Batch B, KafkaTa
                 q.client = cid;
                 Q.client[lane] = cid;
             }
-            // queue this round's CRC items and topics (prefix by ballot; no atomics)
+            // queue this round's CRC items and topics (prefix by ballot; no atomics).
+            // A lane whose item does not fit stops and is decoded again exactly.
             const uint64_t mc = __ballot(S.has_crc), mt = __ballot(S.has_topic);
             const uint32_t rc = __builtin_amdgcn_mbcnt_hi((uint32_t)(mc >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mc, 0));
             const uint32_t rt = __builtin_amdgcn_mbcnt_hi((uint32_t)(mt >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mt, 0));
-            const uint32_t pc_ = (uint32_t)__builtin_popcountll(mc), pt_ = (uint32_t)__builtin_popcountll(mt);
-            if (nc + pc_ > kCrcQ) {  // flush the CRC queue first
-                __builtin_amdgcn_wave_barrier();
-                bad |= crc_pass(Q, nc, crctab, lane);
-                __builtin_amdgcn_wave_barrier();
-                nc = 0;
-            }
-            if ((nt + pt_ > kTopQ) && client_done) {
-                __builtin_amdgcn_wave_barrier();
-                flush_topics(T, Q, nt, lane);
-                __builtin_amdgcn_wave_barrier();
-                nt = 0;
-            }
             if (S.has_crc) {
-                Q.c_off[nc + rc] = S.crc_off;
-                Q.c_len[nc + rc] = S.crc_len | lane << 26;
-                Q.c_want[nc + rc] = S.crc_want;
-                if (S.crc_len >= (1u << 26)) bad |= 1ull << lane;  // cannot be queued: exact redo
+                if (nc + rc < kCrcQ && S.crc_len < (1u << 26)) {
+                    Q.c_off[nc + rc] = S.crc_off;
+                    Q.c_len[nc + rc] = S.crc_len | lane << 26;
+                    Q.c_want[nc + rc] = S.crc_want;
+                } else {
+                    ovf = true;
+                    S.done = true;
+                }
                 S.has_crc = false;
             }
-            nc += pc_;
-            if (S.has_topic && (nt + pt_ <= kTopQ)) {
-                Q.t_off[nt + rt] = S.top_off;
-                Q.t_len[nt + rt] = S.top_len | lane << 26;
+            if (S.has_topic) {
+                if (nt + rt < kTopQ) {
+                    Q.t_off[nt + rt] = S.top_off;
+                    Q.t_len[nt + rt] = S.top_len | lane << 26;
+                } else {
+                    ovf = true;
+                    S.done = true;
+                }
                 S.has_topic = false;
             }
-            if (nt + pt_ <= kTopQ) nt += pt_;
-            __builtin_amdgcn_wave_barrier();
+            nc = min(nc + (uint32_t)__builtin_popcountll(mc), kCrcQ);
+            nt = min(nt + (uint32_t)__builtin_popcountll(mt), kTopQ);
         }
-        // ---- the rest of the queues
+        // ---- the queued work: message CRCs, topic lookups
         __builtin_amdgcn_wave_barrier();
-        if (nc) bad |= crc_pass(Q, nc, crctab, lane);
+        KX_MARK(1);
+        uint64_t bad = 0;  // request lanes with a mismatching CRC
+        if (nc) bad = crc_pass(Q, nc, crctab, lane);
+        KX_MARK(2);
         if (nt) flush_topics(T, Q, nt, lane);
         __builtin_amdgcn_wave_barrier();
-        // OR of the per-lane `bad` findings (each lane only saw its own CRC lanes' owners)
-        {
-            uint32_t lo = (uint32_t)bad, hi = (uint32_t)(bad >> 32);
-            for (int o = 32; o > 0; o >>= 1) {
-                lo |= (uint32_t)__shfl_xor((int)lo, o);
-                hi |= (uint32_t)__shfl_xor((int)hi, o);
-            }
-            bad = (uint64_t)hi << 32 | lo;
-        }
+        KX_MARK(3);
         if (walk) {
-            if ((bad >> lane) & 1) {
+            if (ovf || ((bad >> lane) & 1)) {
                 classify_exact(T, conn, b, len, crctab, r);
             } else if (S.rc == RS_ERROR || (S.rc == RS_OK && S.err)) {
                 r.verdict = V_PARSE_ERROR;
@@ -1096,7 +1131,9 @@ __global__ __launch_bounds__(kBlock) void kafka_classify_kernel(Batch B, KafkaTa
             }
         }
         __builtin_amdgcn_wave_barrier();
+        KX_MARK(4);
     }
+    KX_FLUSH(lane);
     if (B.counters) {
         for (int v = 0; v < 5; v++)
             if (vcount[v]) atomicAdd(&s_verdicts[v], vcount[v]);
@@ -1116,5 +1153,18 @@ hipError_t LaunchKafkaClassify(const Batch &B, const KafkaTables &T, const uint3
                        answer_other ? 1u : 0u);
     return hipGetLastError();
 }
+
+#ifdef L7G_KX_TIMING
+hipError_t KafkaPhaseTimes(uint64_t *out, bool reset) {
+    hipError_t rc = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_kx_phase), sizeof(unsigned long long) * 8);
+    if (rc == hipSuccess && reset) {
+        static const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        rc = hipMemcpyToSymbol(HIP_SYMBOL(g_kx_phase), z, sizeof z);
+    }
+    return rc;
+}
+#else
+hipError_t KafkaPhaseTimes(uint64_t *, bool) { return hipErrorNotSupported; }
+#endif
 
 }  // namespace l7

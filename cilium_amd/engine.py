@@ -109,6 +109,13 @@ class Engine:
             raise RuntimeError(f"l7g_profile_last failed: HIP error {rc}")
         return dict(zip(self.STAGES, out.tolist()))
 
+    def kafka_phase_times(self, reset=True):
+        """Per-phase cycle totals of the Kafka kernel (-DL7G_KX_TIMING build only), or None."""
+        out = np.zeros(8, np.uint64)
+        if self._lib.l7g_debug_kafka_phase_times(self._h, out.ctypes.data, 1 if reset else 0) != 0:
+            return None
+        return out
+
     def phase_times(self, reset=True):
         """Per-phase cycle totals of the HTTP kernel (timing build only), or None."""
         out = np.zeros(8, np.uint64)

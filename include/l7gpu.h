@@ -138,6 +138,10 @@ int l7g_profile_last(l7g_engine *e, float out_ms[4]);
  * (libl7gpu_timing.so, -DL7G_PHASE_TIMING) records them; the product build
  * returns hipErrorNotSupported. */
 int l7g_debug_phase_times(l7g_engine *e, uint64_t *out8, int reset);
+/* The same for the Kafka kernel (-DL7G_KX_TIMING builds; slots: 0 framing,
+ * 1 walk, 2 CRC pass, 3 topic lookups, 4 verdict + output, 5 walk rounds,
+ * 6 window refills, 7 tiles). */
+int l7g_debug_kafka_phase_times(l7g_engine *e, uint64_t *out8, int reset);
 
 /* Test hook: compile one Go regexp with the product's DFA compiler and run
  * the compiled tables on the host.  Returns 1 match, 0 no match, -1 compile

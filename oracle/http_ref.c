@@ -81,7 +81,7 @@ static int http_frame(const uint8_t *b, uint32_t len, http_msg *m) {
     NEED(1); if (b[i] != '\r') return L7_PARSE_ERROR; i++;
     NEED(1); if (b[i] != '\n') return L7_PARSE_ERROR; i++;
 
-    int have_cl = 0, have_te = 0; uint64_t cl = 0;
+    int have_cl = 0, chunked = 0; uint64_t cl = 0;
     for (;;) {
         NEED(1);
         uint8_t c = b[i];
@@ -120,7 +120,10 @@ static int http_frame(const uint8_t *b, uint32_t len, http_msg *m) {
             cl = 0;
             for (uint32_t k = vs; k < ve; k++) { if (b[k] < '0' || b[k] > '9') return L7_PARSE_ERROR; cl = cl * 10 + (b[k] - '0'); }
         } else if (name_is(b, (int32_t)ns, (int32_t)(ne - ns), "transfer-encoding")) {
-            have_te = 1;
+            /* http_parser (Envoy's HTTP/1 codec at the pinned commit) sets
+             * F_CHUNKED when a Transfer-Encoding value is "chunked"; any
+             * other value leaves the body framed by Content-Length. */
+            if (name_is(b, (int32_t)vs, (int32_t)(ve - vs), "chunked")) chunked = 1;
         }
         if (m->nh == m->caph) { m->caph = m->caph ? 2 * m->caph : 16; m->h = realloc(m->h, sizeof(hdr_t) * m->caph); }
         m->h[m->nh++] = (hdr_t){(int32_t)ns, (int32_t)(ne - ns), (int32_t)vs, (int32_t)(ve - vs)};
@@ -128,14 +131,51 @@ static int http_frame(const uint8_t *b, uint32_t len, http_msg *m) {
             m->info.host_off = (int32_t)vs; m->info.host_len = (int32_t)(ve - vs);
         }
     }
-#undef NEED
     m->info.nheaders = m->nh;
-    if (have_te) return L7_UNSUPPORTED;
+    if (chunked) {
+        /* chunked body: chunk = 1*HEXDIG [";" ext] CRLF data CRLF,
+         * last chunk size 0, then trailer lines up to an empty line */
+        for (;;) {
+            uint32_t st = i;
+            uint64_t size = 0;
+            for (;;) {
+                NEED(1);
+                uint8_t c = b[i];
+                int d = c >= '0' && c <= '9' ? c - '0' : (c | 0x20) >= 'a' && (c | 0x20) <= 'f' ? (c | 0x20) - 'a' + 10 : -1;
+                if (d < 0) break;
+                size = size * 16 + (uint64_t)d;
+                if (size > 0xFFFFFFFFull) return L7_PARSE_ERROR;
+                i++;
+            }
+            if (i == st) return L7_PARSE_ERROR;
+            if (b[i] == ';') {
+                i++;
+                for (;;) { NEED(1); if (b[i] == '\r' || b[i] == '\n') break; i++; }
+            }
+            if (b[i] != '\r') return L7_PARSE_ERROR;
+            i++; NEED(1); if (b[i] != '\n') return L7_PARSE_ERROR; i++;
+            if (size == 0) break;
+            if ((uint64_t)i + size > 0xFFFFFFFFull) return L7_PARSE_ERROR;
+            if ((uint64_t)i + size > len) return L7_INCOMPLETE;
+            i += (uint32_t)size;
+            NEED(1); if (b[i] != '\r') return L7_PARSE_ERROR; i++;
+            NEED(1); if (b[i] != '\n') return L7_PARSE_ERROR; i++;
+        }
+        for (;;) {  /* trailer section */
+            NEED(1);
+            if (b[i] == '\r') { i++; NEED(1); if (b[i] != '\n') return L7_PARSE_ERROR; i++; break; }
+            for (;;) { NEED(1); if (b[i] == '\r') break; if (b[i] == '\n') return L7_PARSE_ERROR; i++; }
+            i++; NEED(1); if (b[i] != '\n') return L7_PARSE_ERROR; i++;
+        }
+        m->info.consumed = i;
+        return L7_ALLOW; /* "ok" */
+    }
     uint64_t total = (uint64_t)i + cl;
     if (total > 0xFFFFFFFFull) return L7_PARSE_ERROR;
     if (total > len) return L7_INCOMPLETE;
     m->info.consumed = (uint32_t)total;
     return L7_ALLOW; /* "ok" */
+#undef NEED
 }
 
 int ref_http_parse(const uint8_t *buf, uint32_t len, ref_http_info_t *info) {

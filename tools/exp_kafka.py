@@ -54,6 +54,13 @@ def main():
         print(f"{name:12s} " + " ".join(f"{k}={v:.3f}ms" for k, v in med.items()) +
               (f"  kafka {gb / (kms / 1e3):.0f} GB/s frac {gb / (kms / 1e3) / 8000:.3f}" if kms else "") +
               f"  mismatches={mism}", flush=True)
+        ph = eng.kafka_phase_times()
+        if ph is not None:
+            tot = float(ph[:5].sum()) or 1.0
+            print("   phases: " + " ".join(f"{k}={ph[i] / tot:.3f}" for i, k in
+                                           enumerate(["frame", "walk", "crc", "topics", "out"])) +
+                  f"  rounds/tile={ph[5] / max(ph[7], 1):.1f} refills/tile={ph[6] / max(ph[7], 1):.1f}"
+                  f" cycles/tile={tot / max(ph[7], 1):.0f}", flush=True)
         eng.close()
 
 
