@@ -18,9 +18,8 @@ enum : uint8_t {
 };
 enum : uint8_t { PROTO_NONE = 0, PROTO_HTTP = 1, PROTO_KAFKA = 2, PROTO_MEMCACHE = 3 };
 
-// partition_kernel's Kafka request lists (one per length class; the v2 Kafka
-// kernel balances message sizes itself, so one list in request order)
-#define L7_KAFKA_CLASSES 1
+// partition_kernel groups Kafka requests into this many length classes
+#define L7_KAFKA_CLASSES 8
 
 // Header slots recorded by the HTTP framer.
 enum : int { SLOT_METHOD = 0, SLOT_PATH = 1, SLOT_AUTHORITY = 2, SLOT_CUSTOM0 = 3 };

@@ -228,6 +228,53 @@ def http_adversarial(n, seed):
     return out
 
 
+def http_chunked(n, seed):
+    """Requests with Transfer-Encoding (DESIGN.md §4 chunked-body contract):
+    valid chunked bodies (0-5 chunks, hex sizes in either case, chunk
+    extensions, trailers), TE values that are and are not "chunked", TE with
+    Content-Length, then truncations and byte edits anywhere in the framing."""
+    rng = np.random.default_rng(seed)
+    D = _Draws(rng, 64 * n + 1024)
+    heads = http_requests(n, seed + 1)
+    te_vals = [b"chunked", b"Chunked", b"CHUNKED", b"chunked  ", b"chunked\t", b"gzip", b"gzip, chunked",
+               b"chunkedx", b"chun ked", b"identity"]
+    out = []
+    for i in range(n):
+        h = heads[i]
+        h = h[:h.index(b"X-Pad:")]  # request line + Host / UA / Accept / X-Token
+        te = te_vals[D.int(0, len(te_vals))] if D.uniform() < 0.5 else b"chunked"
+        h += b"Transfer-Encoding: " + te + b"\r\n"
+        if D.uniform() < 0.15:
+            h += b"Content-Length: %d\r\n" % D.int(0, 20)
+        if D.uniform() < 0.05:
+            h += b"Transfer-Encoding: " + te_vals[D.int(0, len(te_vals))] + b"\r\n"
+        body = b""
+        for _ in range(D.int(0, 6)):
+            size = D.int(1, 300)
+            hx = (b"%x" if D.uniform() < 0.5 else b"%X") % size
+            if D.uniform() < 0.1:
+                hx = b"0" * D.int(1, 3) + hx
+            ext = b";name=val" if D.uniform() < 0.2 else b""
+            body += hx + ext + b"\r\n" + D.bytes(size) + b"\r\n"
+        body += b"0" + (b";last" if D.uniform() < 0.1 else b"") + b"\r\n"
+        if D.uniform() < 0.3:
+            body += b"X-Trailer: t%d\r\n" % i
+        body += b"\r\n"
+        r = bytearray(h + b"\r\n" + body)
+        if D.uniform() < 0.2:
+            r += b"GET / HTTP/1.1\r\n\r\n"  # a pipelined next request
+        op = D.int(0, 10)
+        if op == 0:
+            r = r[:D.int(len(h), len(r) + 1)]
+        elif op == 1 and len(r) > len(h) + 2:
+            p = D.int(len(h) + 2, len(r))
+            r[p] = [0x0D, 0x0A, 0x3B, 0x47, 0x20, 0x00, 0x30][D.int(0, 7)]
+        elif op == 2:
+            r = r.replace(b"\r\n0\r\n", b"\r\nfffffffff\r\n", 1)
+        out.append(bytes(r))
+    return out
+
+
 # ------------------------------------------------------------------ Kafka wire encoder
 # Restates the optiopay/kafka proto encoders the reference's decoders expect
 # (vendor/github.com/optiopay/kafka/proto/messages.go: *Req.Bytes).
