@@ -96,7 +96,24 @@ def cpu_info():
         usable = len(os.sched_getaffinity(0))
     except AttributeError:
         usable = os.cpu_count() or 1
-    return {"nproc": os.cpu_count(), "usable_cores": usable, "model": model}
+    # the process's CPU share: a cgroup quota caps what the affinity mask shows
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max", "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"):
+        try:
+            with open(path) as f:
+                parts = f.read().split()
+            if path.endswith("cpu.max") and parts and parts[0] != "max":
+                quota = int(parts[0]) / int(parts[1])
+            elif path.endswith("quota_us") and parts and int(parts[0]) > 0:
+                with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                    quota = int(parts[0]) / int(f.read())
+        except (OSError, ValueError, IndexError):
+            continue
+        if quota:
+            break
+    share = max(1, min(usable, int(quota))) if quota else usable
+    return {"nproc": os.cpu_count(), "usable_cores": share, "affinity_cores": usable, "cgroup_cpu_quota": quota,
+            "model": model}
 
 
 def e2e_pipeline(torch, eng, w, dev, nchunks=8, reps=3):
@@ -282,7 +299,7 @@ def main():
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import refpy  # parity oracle: the checker and the CPU baseline, never the product path
     cinfo = cpu_info()
-    threads = args.cpu_threads or min(cinfo["usable_cores"], 128)
+    threads = args.cpu_threads or cinfo["usable_cores"]  # every core of the process's CPU share
     verdict = d_v.cpu().numpy()
     rule = d_r.cpu().numpy()
     consumed = d_c.cpu().numpy().view(np.uint32)
@@ -338,7 +355,8 @@ def main():
                          f"core: the first {m1} requests ({cpu_1_s:.2f} s)",
                "scanned_gbps": round(float(w.lengths.astype(np.int64).sum()) / cpu_all_s / 1e9, 3),
                "single_core_verdicts_per_s": round(m1 / cpu_1_s, 1),
-               "nproc": cinfo["nproc"], "usable_cores": cinfo["usable_cores"], "cpu_model": cinfo["model"]}
+               "nproc": cinfo["nproc"], "usable_cores": cinfo["usable_cores"], "affinity_cores": cinfo["affinity_cores"],
+               "cgroup_cpu_quota": cinfo["cgroup_cpu_quota"], "cpu_model": cinfo["model"]}
 
     if rank != 0:
         if dist is not None:

@@ -37,7 +37,7 @@ EXPORTS = (
     "l7g_engine_create", "l7g_engine_destroy", "l7g_policy_update", "l7g_policy_index",
     "l7g_policy_nrules", "l7g_conns_set", "l7g_conn_update", "l7g_classify", "l7g_classify_host", "l7g_stats",
     "l7g_debug_regex", "l7g_debug_phase_times", "l7g_profile_enable", "l7g_profile_last",
-    "l7g_debug_kafka_phase_times",
+    "l7g_debug_kafka_phase_times", "l7g_kafka_deny_response",
 )
 
 _libs = {}
@@ -69,6 +69,7 @@ def load(path=None):
     lib.l7g_debug_regex.argtypes = [cp, sz, C.c_int, cp, sz, cp, sz]
     lib.l7g_debug_phase_times.argtypes = [vp, vp, C.c_int]
     lib.l7g_debug_kafka_phase_times.argtypes = [vp, vp, C.c_int]
+    lib.l7g_kafka_deny_response.argtypes = [cp, sz, vp, sz, C.POINTER(C.c_size_t)]
     lib.l7g_profile_enable.argtypes = [vp, C.c_int]
     lib.l7g_profile_last.argtypes = [vp, vp]
     _libs[path] = lib
@@ -87,3 +88,19 @@ def debug_regex(pattern, data, anchored=True):
     if r < 0:
         raise ValueError(err.value.decode(errors="replace"))
     return bool(r)
+
+
+def kafka_deny_response(req):
+    """The bytes the Kafka proxy answers a denied request with
+    (CreateResponse(ErrTopicAuthorizationFailed)), or None (untyped kind /
+    undecodable request: no response)."""
+    lib = load()
+    cap = 4 * len(req) + 256
+    out = C.create_string_buffer(cap)
+    n = C.c_size_t(0)
+    rc = lib.l7g_kafka_deny_response(req, len(req), out, cap, C.byref(n))
+    if rc == -1:
+        return None
+    if rc != 0:
+        raise RuntimeError(f"l7g_kafka_deny_response: {rc}")
+    return out.raw[:n.value]

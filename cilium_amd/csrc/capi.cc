@@ -99,16 +99,19 @@ bool ResolveOne(l7g_engine *e, size_t i, std::string *err) {
     c = DevConn{-1, PROTO_NONE, 0, {0, 0}};
     c.proto = a.proto;
     c.flags = (uint8_t)(a.flags & 3);
+    const bool proxylib = (a.flags & L7G_CONN_PROXYLIB) != 0;
     if (a.proto == PROTO_HTTP) {
-        // remote identity: ingress = source, egress = destination (cilium_l7policy.cc:144-150)
-        uint64_t remote = a.ingress ? a.src_id : a.dst_id;
-        c.ruleset = e->hc->RulesetFor(a.policy, a.ingress != 0, a.port, remote, err);
+        // remote identity: Envoy's HTTP filter uses the source on ingress and the
+        // destination on egress (cilium_l7policy.cc:144-150); proxylib matches
+        // the connection's SrcId in both directions (connection.go:176-179)
+        uint64_t remote = (a.ingress || proxylib) ? a.src_id : a.dst_id;
+        c.ruleset = e->hc->RulesetFor(a.policy, a.ingress != 0, a.port, remote, proxylib, err);
         if (c.ruleset < 0) return false;
         e->has_http = true;
     } else if (a.proto == PROTO_KAFKA) {
         // Kafka rules are selected by the source identity in both directions
         // (pkg/proxy/kafka.go:327,357)
-        c.ruleset = e->kc->RulesetFor(a.policy, a.ingress != 0, a.port, a.src_id, err);
+        c.ruleset = e->kc->RulesetFor(a.policy, a.ingress != 0, a.port, a.src_id, proxylib, err);
         if (c.ruleset < 0) return false;
         e->has_kafka = true;
     } else if (a.proto == PROTO_MEMCACHE) {

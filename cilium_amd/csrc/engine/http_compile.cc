@@ -67,10 +67,28 @@ std::unique_ptr<re::Node> PatternAst(const Pat &p, std::string *err) {
 
 }  // namespace
 
-int HttpCompiler::RulesetFor(int policy, bool ingress, uint32_t port, uint64_t remote, std::string *err) {
+int HttpCompiler::RulesetFor(int policy, bool ingress, uint32_t port, uint64_t remote, bool proxylib,
+                             std::string *err) {
     std::vector<const HttpRule *> items;
     uint8_t terminal = V_DENY;
-    if (policy >= 0 && policy < (int)ps_->policies.size()) {
+    if (proxylib && policy >= 0 && policy < (int)ps_->policies.size()) {
+        // proxylib "http" parser: PortNetworkPolicies.Matches (policymap.go:208-236)
+        // -- exact port then port 0, entries proxylib installs only, no entry => drop
+        const PortPolicy *ex, *wc;
+        ps_->policies[policy].Lookup(ingress, port, &ex, &wc);
+        bool decided = false;
+        for (const PortPolicy *pp : {ex, wc}) {
+            if (!pp || !pp->px_installed) continue;
+            if (!pp->px_have_l7 || pp->rules.empty()) { terminal = V_ALLOW; decided = true; break; }  // :173-186
+            for (auto &r : pp->rules) {
+                if (!r.RemoteOk(remote)) continue;
+                if (r.NumL7() == 0) { terminal = V_ALLOW; decided = true; break; }  // empty L7 set (:106-108)
+                if (r.type == PortRule::Http)
+                    for (auto &h : r.http) items.push_back(&h);
+            }
+            if (decided) break;
+        }
+    } else if (!proxylib && policy >= 0 && policy < (int)ps_->policies.size()) {
         const NetworkPolicy &np = ps_->policies[policy];
         const PortPolicy *ex, *wc;
         np.Lookup(ingress, port, &ex, &wc);

@@ -32,7 +32,9 @@ public:
     explicit HttpCompiler(const PolicySet *ps) : ps_(ps) {}
     // Returns the rule set index for a connection, compiling it on first use.
     // policy < 0: unknown policy (NetworkPolicyMap::Allowed => deny).
-    int RulesetFor(int policy, bool ingress, uint32_t port, uint64_t remote, std::string *err);
+    // proxylib: the proxylib "http" parser's policymap semantics (no port entry
+    // => drop, installed entries only) instead of Envoy's NetworkPolicyMap
+    int RulesetFor(int policy, bool ingress, uint32_t port, uint64_t remote, bool proxylib, std::string *err);
     const HttpImage &image() const { return img_; }
     int max_dfa_states = 4096;
 

@@ -50,7 +50,8 @@ KafkaCompiler::KafkaCompiler(const PolicySet *ps) : ps_(ps) {
     img_.ntopics = topic_id_.size();
 }
 
-int KafkaCompiler::RulesetFor(int policy, bool ingress, uint32_t port, uint64_t src_id, std::string *err) {
+int KafkaCompiler::RulesetFor(int policy, bool ingress, uint32_t port, uint64_t src_id, bool proxylib,
+                              std::string *err) {
     (void)err;
     std::vector<const KafkaRule *> rules;
     bool any = false;
@@ -60,6 +61,21 @@ int KafkaCompiler::RulesetFor(int policy, bool ingress, uint32_t port, uint64_t 
         ps_->policies[policy].Lookup(ingress, port, &ex, &wc);
         for (const PortPolicy *pp : {ex, wc}) {
             if (!pp) continue;
+            if (proxylib) {
+                // proxylib "kafka" parser: the installed entries of PortNetworkPolicies
+                // (policymap.go:150-236); a port without L7 rules, or a group whose L7
+                // set is empty, lets everything through; the groups' Kafka rules
+                // are evaluated together as one MatchesRule list (the
+                // GetRelevantRules view of pkg/policy/l4.go:118-141)
+                if (!pp->px_installed) continue;
+                if (!pp->px_have_l7 || pp->rules.empty()) { rules.push_back(&kWildcard); any = true; continue; }
+                for (auto &r : pp->rules) {
+                    if (!r.RemoteOk(src_id)) continue;
+                    if (r.NumL7() == 0) { rules.push_back(&kWildcard); any = true; }
+                    else if (r.type == PortRule::Kafka) { for (auto &k : r.kafka) rules.push_back(&k); any = true; }
+                }
+                continue;
+            }
             for (auto &r : pp->rules) {
                 if (!r.RemoteOk(src_id)) continue;
                 if (r.type == PortRule::Kafka) { for (auto &k : r.kafka) rules.push_back(&k); any = true; }

@@ -39,7 +39,8 @@ struct KafkaImage {
 class KafkaCompiler {
 public:
     explicit KafkaCompiler(const PolicySet *ps);
-    int RulesetFor(int policy, bool ingress, uint32_t port, uint64_t src_id, std::string *err);
+    // proxylib: the proxylib "kafka" parser's view of the port entries
+    int RulesetFor(int policy, bool ingress, uint32_t port, uint64_t src_id, bool proxylib, std::string *err);
     const KafkaImage &image() const { return img_; }
 
 private:

@@ -18,13 +18,13 @@ int McCompiler::RulesetFor(int policy, bool ingress, uint32_t port, uint64_t rem
         ps_->policies[policy].Lookup(ingress, port, &ex, &wc);
         bool decided = false;
         for (const PortPolicy *pp : {ex, wc}) {
-            if (!pp || !pp->mc_installed) continue;
+            if (!pp || !pp->px_installed) continue;
             // !HaveL7Rules or no rules at all: matches (policymap.go:173-186)
-            if (!pp->mc_have_l7 || pp->rules.empty()) { terminal = V_ALLOW; decided = true; break; }
+            if (!pp->px_have_l7 || pp->rules.empty()) { terminal = V_ALLOW; decided = true; break; }
             for (auto &r : pp->rules) {
                 if (!r.RemoteOk(remote)) continue;
-                if (r.mc.empty()) { terminal = V_ALLOW; decided = true; break; }  // empty L7 set (:106-108)
-                for (auto &m : r.mc) items.push_back(&m);
+                if (r.NumL7() == 0) { terminal = V_ALLOW; decided = true; break; }  // empty L7 set (:106-108)
+                for (auto &m : r.mc) items.push_back(&m);  // HTTP / Kafka rules never match a memcached request
             }
             if (decided) break;
         }

@@ -22,6 +22,11 @@ bool PortRule::RemoteOk(uint64_t id) const {
     return std::binary_search(remotes.begin(), remotes.end(), id);
 }
 
+bool ProxylibParserRegistered(const std::string &name) {
+    return name.empty() || name == "memcache" || name == "PortNetworkPolicyRule_HttpRules" ||
+           name == "PortNetworkPolicyRule_KafkaRules";
+}
+
 std::string PortRule::ParserName() const {
     if (!l7proto.empty()) return l7proto;
     switch (type) {
@@ -259,6 +264,7 @@ struct Loader {
                 if (pr->type == Value::Num && pr->inum != 0) p.tcp = false;
             }
             mc_stop = false;
+            std::string first_parser;
             if (auto *rs = pj.get("rules"); rs && rs->isArr())
                 for (auto &rj : rs->arr) {
                     p.rules.emplace_back();
@@ -266,8 +272,14 @@ struct Loader {
                     if (!rule(rj, &r)) return false;
                     if (r.type == PortRule::Http) p.has_http = true;
                     std::string pn = r.ParserName();
-                    if (!pn.empty() && pn != "memcache") { mc_stop = true; p.mc_installed = false; }
-                    if (!mc_stop && !r.mc.empty()) p.mc_have_l7 = true;
+                    // proxylib stops parsing a port at the first unregistered parser
+                    // (policymap.go:118-131): later memcache rules are never parsed
+                    if (!ProxylibParserRegistered(pn)) { mc_stop = true; p.px_installed = false; }
+                    if (!pn.empty()) {
+                        if (first_parser.empty()) first_parser = pn;
+                        else if (pn != first_parser) p.px_installed = false;  // mismatching L7 types
+                    }
+                    if (!mc_stop && r.NumL7() > 0) p.px_have_l7 = true;
                 }
             if (p.tcp)
                 for (auto &q : *out) if (q.tcp && q.port == p.port) return fail("PortNetworkPolicy: Duplicate port number");

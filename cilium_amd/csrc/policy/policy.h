@@ -63,7 +63,13 @@ struct PortRule {
     // (proxylib/proxylib/policymap.go:68-75)
     std::string ParserName() const;
     bool RemoteOk(uint64_t id) const;
+    // parsed L7 rules of this group (proxylib's len(L7Rules)): memcache rules,
+    // HTTP rules or Kafka rules
+    size_t NumL7() const { return type == Http ? http.size() : type == Kafka ? kafka.size() : mc.size(); }
 };
+// L7 rule parsers the proxylib view registers (policymap.go:42-45): "memcache",
+// "PortNetworkPolicyRule_HttpRules", "PortNetworkPolicyRule_KafkaRules".
+bool ProxylibParserRegistered(const std::string &name);
 
 struct PortPolicy {
     uint32_t port = 0;
@@ -71,10 +77,12 @@ struct PortPolicy {
     std::vector<PortRule> rules;
     bool has_http = false;
     // proxylib view (policymap.go:113-148): the entry is installed only if every
-    // rule's parser is registered ("memcache" or none); HaveL7Rules = some
-    // rule has parsed L7 rules.
-    bool mc_installed = true;
-    bool mc_have_l7 = false;
+    // rule's parser is registered and they agree (the reference NACKs the
+    // proxylib update on "Mismatching L7 types on the same port" :135-140; here
+    // the port is left out of the proxylib view, as for an unregistered parser);
+    // HaveL7Rules = some rule has parsed L7 rules.
+    bool px_installed = true;
+    bool px_have_l7 = false;
 };
 
 struct NetworkPolicy {

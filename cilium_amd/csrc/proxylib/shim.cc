@@ -4,15 +4,33 @@
 //   OnNewConnection            proxylib/proxylib.go:57-74, connection.go:65-101
 //   OnData                     proxylib/proxylib.go:98-108, connection.go:104-174
 //   Close                      proxylib/proxylib.go:112-116
-// and the "memcache" parser (proxylib/memcached/parser.go:186-202 with
-// text/parser.go:72-330 and binary/parser.go:58-205).  Every request-direction
-// parser step asks the device for the frame's verdict (l7g_classify_host on
-// the connection's slot of the engine's connection table): the kernel frames
-// the request, tokenises it and evaluates the policy; the host keeps what
-// proxylib keeps per connection — the parser chosen by the first byte, the
-// text reply-intent queue, the binary inject queue and request/reply counts —
-// and drives the op loop and inject buffers exactly as connection.go does.
+// and three parsers (the registry of parserfactory.go:68-71):
+//   "memcache"  proxylib/memcached/parser.go:186-202 with text/parser.go:72-330
+//               and binary/parser.go:58-205;
+//   "http"      HTTP/1 requests with Envoy's cilium.l7policy verdict
+//               (envoy/cilium_l7policy.cc:127-182): allowed => PASS, denied =>
+//               DROP and a 403 "Access denied" reply injected (:171-177);
+//   "kafka"     Kafka requests with the in-agent proxy's verdict
+//               (pkg/proxy/kafka.go:117-153, 249-261): allowed => PASS, denied
+//               => DROP and the CreateResponse(ErrTopicAuthorizationFailed)
+//               reply injected (kafka_response.cc).
+// HTTP and Kafka connections use proxylib's policymap semantics
+// (L7G_CONN_PROXYLIB: no port entry => drop, SrcId as the remote).
+//
+// The device gives the verdicts.  Each OnData call in the request direction
+// first proposes where the frames in its input start (a cheap host scan: the
+// Kafka size prefix, the memcached binary header, the HTTP header block and
+// Content-Length, the memcached text line and data length) and classifies all
+// of them in ONE l7g_classify_host launch; the op loop then takes each frame's
+// verdict from that batch.  A proposal the device's consumed length does not
+// confirm is simply not used: the frame at the real position is classified on
+// its own, so the scan only saves launches, it never decides anything.  The
+// host keeps what proxylib keeps per connection -- the memcached parser chosen
+// by the first byte, the text reply-intent queue, the binary inject queue and
+// request/reply counts -- and drives the op loop and inject buffers exactly as
+// connection.go does.
 #include <atomic>
+#include <cctype>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -90,8 +108,76 @@ long FindCRLF(const std::string &d, size_t from = 0) {
 }
 
 const char kDeniedText[] = "CLIENT_ERROR access denied\r\n";  // text/parser.go:327
+// Envoy's local reply for a denied HTTP request: sendLocalReply(Forbidden,
+// denied_403_body = "Access denied" + CRLF) (envoy/cilium_l7policy.cc:90-96,171-177)
+const char kDenied403[] =
+    "HTTP/1.1 403 Forbidden\r\ncontent-length: 15\r\ncontent-type: text/plain\r\n\r\nAccess denied\r\n";
 const uint8_t kDeniedBinary[37] = {0x81, 0, 0, 0, 0, 0, 0, 8, 0, 0, 0, 0x0d, 0, 0, 0, 0, 0, 0, 0,
                                    0,    0, 0, 0, 0, 'a', 'c', 'c', 'e', 's', 's', ' ', 'd', 'e', 'n', 'i', 'e', 'd'};
+
+}  // namespace
+namespace l7 {
+bool KafkaDenyResponse(const uint8_t *req, size_t len, std::string *out);
+}
+namespace {
+
+enum Kind { K_MEMCACHE, K_HTTP, K_KAFKA };
+
+struct Cached {
+    uint8_t v;
+    int32_t rule;
+    uint32_t consumed;
+};
+
+// ---------------------------------------------------------------- frame proposals
+// Where the next frame would start if the one at p is complete; 0 = unknown.
+// Only proposals: the device decides, and a wrong guess costs one extra launch.
+size_t NextKafka(const std::string &d, size_t p) {
+    if (d.size() - p < 4) return 0;
+    const uint8_t *b = (const uint8_t *)d.data() + p;
+    const int32_t size = (int32_t)((uint32_t)b[0] << 24 | (uint32_t)b[1] << 16 | (uint32_t)b[2] << 8 | b[3]);
+    if (size <= 0 || (uint64_t)size + 4 > d.size() - p) return 0;
+    return p + 4 + (size_t)size;
+}
+size_t NextMcBinary(const std::string &d, size_t p) {
+    if (d.size() - p < 24) return 0;
+    const uint8_t *b = (const uint8_t *)d.data() + p;
+    const uint64_t body = (uint32_t)b[8] << 24 | (uint32_t)b[9] << 16 | (uint32_t)b[10] << 8 | b[11];
+    return body + 24 <= d.size() - p ? p + 24 + (size_t)body : 0;
+}
+size_t NextMcText(const std::string &d, size_t p) {
+    const size_t lf = d.find("\r\n", p);
+    if (lf == std::string::npos) return 0;
+    auto tok = Fields((const uint8_t *)d.data() + p, lf - p);
+    size_t next = lf + 2;
+    if (!tok.empty() && (tok[0] == "set" || tok[0] == "add" || tok[0] == "replace" || tok[0] == "append" ||
+                         tok[0] == "prepend" || tok[0] == "cas")) {
+        if (tok.size() < 5) return 0;
+        char *end = nullptr;
+        const long long n = strtoll(tok[4].c_str(), &end, 10);
+        if (!end || *end || n < 0) return 0;
+        next += (size_t)n + 2;
+    }
+    return next <= d.size() ? next : 0;
+}
+size_t NextHttp(const std::string &d, size_t p) {
+    const size_t he = d.find("\r\n\r\n", p);
+    if (he == std::string::npos) return 0;
+    uint64_t cl = 0;
+    for (size_t ls = d.find("\r\n", p) + 2; ls < he; ) {  // header lines
+        const size_t le = d.find("\r\n", ls);
+        const size_t colon = d.find(':', ls);
+        if (colon != std::string::npos && colon < le) {
+            std::string name = d.substr(ls, colon - ls);
+            for (auto &ch : name) ch = (char)tolower((unsigned char)ch);
+            if (name == "transfer-encoding") return 0;  // chunked or not: leave it to the device
+            if (name == "content-length") cl = strtoull(d.c_str() + colon + 1, nullptr, 10);
+        }
+        ls = le + 2;
+    }
+    const uint64_t next = he + 4 + cl;
+    return next <= d.size() ? (size_t)next : 0;
+}
 
 // ---------------------------------------------------------------- connection
 struct Connection {
@@ -102,6 +188,11 @@ struct Connection {
     std::string policy, proto;
     GoSlice *orig = nullptr, *reply = nullptr;
     uint32_t slot = 0;
+    Kind kind = K_MEMCACHE;
+    // verdicts of this OnData call's proposed frames, by offset from the start
+    // of the call's input; `base` = input bytes already consumed in this call
+    std::map<uint64_t, Cached> batch;
+    uint64_t base = 0;
     // memcache parser state
     int mode = 0;  // 0 none yet, L7G_CONN_MC_TEXT, L7G_CONN_MC_BINARY
     struct Intent { std::string command; bool denied; };
@@ -126,18 +217,106 @@ struct Connection {
         a.policy = l7g_policy_index(ins->eng, policy.data(), policy.size());
         a.port = port;
         a.ingress = ingress ? 1 : 0;
-        a.proto = L7G_PROTO_MEMCACHE;
-        a.flags = (uint16_t)mode;
+        a.proto = kind == K_HTTP ? L7G_PROTO_HTTP : kind == K_KAFKA ? L7G_PROTO_KAFKA : L7G_PROTO_MEMCACHE;
+        a.flags = kind == K_MEMCACHE ? (uint16_t)mode : (uint16_t)L7G_CONN_PROXYLIB;
         a.src_id = src;
         a.dst_id = dst;
         return a;
     }
-    // Device verdict for the request at the start of `data` (one kernel lane).
+    // Device verdict for the request at the start of `data`: from this call's
+    // batch if it proposed a frame there, else one kernel lane on its own.
     bool Verdict(const std::string &data, uint8_t *v, int32_t *rule, uint32_t *consumed) {
+        auto it = batch.find(base);
+        if (it != batch.end()) {
+            *v = it->second.v;
+            *rule = it->second.rule;
+            *consumed = it->second.consumed;
+            return true;
+        }
         uint64_t off = 0;
         uint32_t len = (uint32_t)data.size(), cid = slot;
         return l7g_classify_host(ins->eng, (const uint8_t *)data.data(), data.size(), &off, &len, &cid, 1, v, rule,
                                  consumed) == 0;
+    }
+    // Propose the frames of a request-direction input and classify them all in
+    // one launch (at most `max` frames).
+    bool Prefetch(const std::string &d, size_t max) {
+        batch.clear();
+        if (d.empty() || max == 0) return true;
+        if (kind == K_MEMCACHE && mode == 0) return true;  // the parser is chosen by the first byte first
+        std::vector<uint64_t> offs;
+        std::vector<uint32_t> lens, cids;
+        for (size_t p = 0; p < d.size() && offs.size() < max;) {
+            offs.push_back(p);
+            lens.push_back((uint32_t)(d.size() - p));
+            cids.push_back(slot);
+            const size_t q = kind == K_KAFKA ? NextKafka(d, p)
+                           : kind == K_HTTP ? NextHttp(d, p)
+                           : mode == L7G_CONN_MC_BINARY ? NextMcBinary(d, p) : NextMcText(d, p);
+            if (q <= p) break;
+            p = q;
+        }
+        if (offs.size() < 2) return true;  // one frame: classified when it is reached
+        const size_t n = offs.size();
+        std::vector<uint8_t> v(n);
+        std::vector<int32_t> r(n);
+        std::vector<uint32_t> c(n);
+        if (l7g_classify_host(ins->eng, (const uint8_t *)d.data(), d.size(), offs.data(), lens.data(), cids.data(),
+                              (uint32_t)n, v.data(), r.data(), c.data()) != 0)
+            return false;
+        for (size_t i = 0; i < n; i++) batch[offs[i]] = Cached{v[i], r[i], c[i]};
+        return true;
+    }
+
+    // ---- "http": a request's verdict from its headers (cilium_l7policy.cc:127-182)
+    int64_t HttpOnData(bool r, const std::vector<std::string> &in, int64_t *n, bool *err) {
+        std::string d;
+        for (auto &b : in) d += b;
+        if (r) {  // responses pass; a denial's 403 was injected when the request was dropped
+            if (d.empty()) { *n = 0; return NOP; }
+            *n = (int64_t)d.size();
+            return FILTEROP_PASS;
+        }
+        if (d.empty()) { *n = 0; return NOP; }
+        uint8_t v;
+        int32_t rule;
+        uint32_t cons;
+        if (!Verdict(d, &v, &rule, &cons)) { *err = true; *n = 0; return FILTEROP_ERROR; }
+        if (v == L7G_INCOMPLETE) { *n = 1; return FILTEROP_MORE; }
+        if (v != L7G_ALLOW && v != L7G_DENY) { *n = FILTEROP_ERROR_INVALID_FRAME_TYPE; return FILTEROP_ERROR; }
+        *n = cons;
+        if (v == L7G_ALLOW) return FILTEROP_PASS;
+        Inject(true, kDenied403, sizeof kDenied403 - 1);
+        return FILTEROP_DROP;
+    }
+
+    // ---- "kafka": proto.ReadReq framing, canAccess verdict, deny response
+    int64_t KafkaOnData(bool r, const std::vector<std::string> &in, int64_t *n, bool *err) {
+        std::string d;
+        for (auto &b : in) d += b;
+        if (r) {  // responses pass; a denial's error response was injected with the drop
+            if (d.empty()) { *n = 0; return NOP; }
+            *n = (int64_t)d.size();
+            return FILTEROP_PASS;
+        }
+        if (d.empty()) { *n = 0; return NOP; }
+        uint8_t v;
+        int32_t rule;
+        uint32_t cons;
+        if (!Verdict(d, &v, &rule, &cons)) { *err = true; *n = 0; return FILTEROP_ERROR; }
+        if (v == L7G_INCOMPLETE) {  // the size prefix tells how much is missing
+            if (d.size() < 4) { *n = 4 - (int64_t)d.size(); return FILTEROP_MORE; }
+            const uint8_t *b = (const uint8_t *)d.data();
+            const uint64_t size = (uint32_t)b[0] << 24 | (uint32_t)b[1] << 16 | (uint32_t)b[2] << 8 | b[3];
+            *n = size + 4 > d.size() ? (int64_t)(size + 4 - d.size()) : 1;
+            return FILTEROP_MORE;
+        }
+        if (v != L7G_ALLOW && v != L7G_DENY) { *n = FILTEROP_ERROR_INVALID_FRAME_TYPE; return FILTEROP_ERROR; }
+        *n = cons;
+        if (v == L7G_ALLOW) return FILTEROP_PASS;
+        std::string resp;
+        if (l7::KafkaDenyResponse((const uint8_t *)d.data(), cons, &resp)) Inject(true, resp.data(), resp.size());
+        return FILTEROP_DROP;
     }
 
     // ---- text parser (text/parser.go:72-262)
@@ -274,8 +453,11 @@ struct Connection {
         return FILTEROP_PASS;
     }
 
-    // memcache.Parser.OnData (memcached/parser.go:186-202)
+    // the connection's parser
     int64_t ParserOnData(bool r, const std::vector<std::string> &in, bool first_nonempty, int64_t *n, bool *err) {
+        if (kind == K_HTTP) return HttpOnData(r, in, n, err);
+        if (kind == K_KAFKA) return KafkaOnData(r, in, n, err);
+        // memcache.Parser.OnData (memcached/parser.go:186-202)
         if (mode == 0) {
             if (!first_nonempty) { *n = 0; return NOP; }
             mode = (uint8_t)in[0][0] >= 128 ? L7G_CONN_MC_BINARY : L7G_CONN_MC_TEXT;
@@ -388,7 +570,11 @@ FilterResult OnNewConnection(uint64_t instance_id, GoString proto, uint64_t conn
     auto ins = FindInstance(instance_id);
     if (!ins) return FILTER_INVALID_INSTANCE;
     std::string p = Str(proto);
-    if (p != "memcache") return FILTER_UNKNOWN_PARSER;
+    Kind kind;
+    if (p == "memcache") kind = K_MEMCACHE;
+    else if (p == "http") kind = K_HTTP;
+    else if (p == "kafka") kind = K_KAFKA;
+    else return FILTER_UNKNOWN_PARSER;
     uint32_t port;
     if (!DstPort(Str(dst_addr), &port)) return FILTER_INVALID_ADDRESS;
     auto c = std::make_shared<Connection>();
@@ -400,6 +586,7 @@ FilterResult OnNewConnection(uint64_t instance_id, GoString proto, uint64_t conn
     c->port = port;
     c->policy = Str(policy_name);
     c->proto = p;
+    c->kind = kind;
     c->orig = orig_buf;
     c->reply = reply_buf;
     {
@@ -440,6 +627,13 @@ FilterResult OnData(uint64_t connection_id, uint8_t reply, uint8_t end_stream, G
     const GoSlice *bufs = (const GoSlice *)data->data;
     for (GoInt i = 0; i < data->len; i++) in.emplace_back((const char *)bufs[i].data, (size_t)bufs[i].len);
     int64_t *op = (int64_t *)ops->data;
+    c->base = 0;
+    c->batch.clear();
+    if (!reply) {  // the request frames of this call: one device launch
+        std::string all;
+        for (auto &b : in) all += b;
+        if (!c->Prefetch(all, (size_t)(ops->cap - ops->len))) return FILTER_UNKNOWN_ERROR;
+    }
     try {
         while (ops->len < ops->cap) {  // connection.go:138-172
             int64_t n = 0;
@@ -454,6 +648,7 @@ FilterResult OnData(uint64_t connection_id, uint8_t reply, uint8_t end_stream, G
             ops->len++;
             if (o == FILTEROP_MORE) break;
             if (o == FILTEROP_PASS || o == FILTEROP_DROP) {  // advanceInput (connection.go:104-116)
+                c->base += (uint64_t)n;
                 int64_t k = n;
                 while (k > 0 && !in.empty()) {
                     if ((size_t)k < in[0].size()) { in[0].erase(0, (size_t)k); k = 0; }
@@ -463,8 +658,10 @@ FilterResult OnData(uint64_t connection_id, uint8_t reply, uint8_t end_stream, G
             if (o == FILTEROP_INJECT && c->InjectFull(reply != 0)) break;
         }
     } catch (const Panic &) {
+        c->batch.clear();
         return FILTER_PARSER_ERROR;
     }
+    c->batch.clear();
     return FILTER_OK;
 }
 

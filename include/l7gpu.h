@@ -50,8 +50,12 @@ enum {
 };
 
 /* memcached: proxylib picks the text or binary parser from the first byte a
- * connection carries and keeps it (proxylib/memcached/parser.go:186-202). */
-enum { L7G_CONN_MC_TEXT = 1, L7G_CONN_MC_BINARY = 2 };
+ * connection carries and keeps it (proxylib/memcached/parser.go:186-202).
+ * L7G_CONN_PROXYLIB: an HTTP or Kafka connection served by the proxylib
+ * "http" / "kafka" parser: proxylib's policymap semantics apply (no port entry
+ * => DENY, SrcId is the remote in both directions; policymap.go:208-236,
+ * connection.go:176-179) instead of Envoy's / the in-agent Kafka proxy's. */
+enum { L7G_CONN_MC_TEXT = 1, L7G_CONN_MC_BINARY = 2, L7G_CONN_PROXYLIB = 4 };
 
 /* Connection attributes (20 bytes; identical layout to the oracle's ref_conn_t). */
 typedef struct {

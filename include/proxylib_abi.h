@@ -10,8 +10,15 @@
  * reply bookkeeping and inject buffers stay on the host exactly as in
  * proxylib/proxylib/connection.go:118-174.
  *
- * Registered parsers: "memcache" (proxylib/memcached).  Any other proto name
- * => FILTER_UNKNOWN_PARSER.  Policies: the NPDS stream (xds-path) is replaced
+ * Registered parsers: "memcache" (proxylib/memcached), "http" and "kafka"
+ * (the Envoy-filter protocols run through proxylib's policymap semantics:
+ * policymap.go:150-236 -- installed entries only, no port entry => drop, SrcId
+ * as the remote in both directions).  HTTP: a denied request is DROPped and
+ * the 403 of the HTTP filter injected on the reply side; Kafka: a denied
+ * request is DROPped and CreateResponse(ErrTopicAuthorizationFailed) injected
+ * (pkg/proxy/kafka.go:249-261).  Every complete request frame of one OnData
+ * call is decided in ONE device launch.  Any other proto name =>
+ * FILTER_UNKNOWN_PARSER.  Policies: the NPDS stream (xds-path) is replaced
  * by l7g_proxylib_policy_update (same cilium.NetworkPolicy shape as JSON).
  */
 #ifndef L7G_PROXYLIB_ABI_H
@@ -77,6 +84,15 @@ void Close(uint64_t connection_id);
 int l7g_proxylib_policy_update(uint64_t instance_id, const char *json, size_t len, char *err, size_t errlen);
 /* Number of open connections (all instances). */
 uint64_t l7g_proxylib_connections(void);
+
+/* The Kafka deny response for one request frame: what pkg/proxy/kafka.go:
+ * 249-261 sends for a denied request -- req.CreateResponse(proto.
+ * ErrTopicAuthorizationFailed) (pkg/kafka/request.go:158-182,
+ * response.go:81-315) in the request's kind/version encoding.  Host code.
+ * Returns 0 (out[0..*outlen) written), -1 (no response: an untyped kind or an
+ * undecodable request, request == nil in the reference), -2 (cap too small;
+ * *outlen says how much is needed). */
+int l7g_kafka_deny_response(const uint8_t *req, size_t len, uint8_t *out, size_t cap, size_t *outlen);
 
 #ifdef __cplusplus
 }

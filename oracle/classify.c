@@ -264,8 +264,9 @@ static int load_ports(ld *l, const jnode *arr, ref_port **out, int *nout) {
                 if (load_rule(l, rs->items[k], &ps[i].rules[k]) < 0) return -1;
                 if (ps[i].rules[k].l7type == L7T_HTTP) ps[i].has_http = 1;
                 const ref_pnp_rule *pr = &ps[i].rules[k];
+                /* unregistered parser: any l7_proto but "memcache", or generic L7 rules */
                 if ((pr->l7proto && *pr->l7proto && strcmp(pr->l7proto, "memcache")) ||
-                    ((!pr->l7proto || !*pr->l7proto) && pr->l7type != L7T_NONE))
+                    ((!pr->l7proto || !*pr->l7proto) && pr->l7type == L7T_L7))
                     l->mc_stop = 1;
             }
         }
@@ -339,6 +340,42 @@ int ref_port_lookup(const ref_netpolicy *np, int ingress, uint32_t port, const r
         if (ps[i].port == 0 && port != 0) *wild = &ps[i];
     }
     return *exact || *wild;
+}
+
+static const char *px_parser(const ref_pnp_rule *r) {  /* policymap.go:68-75 */
+    if (r->l7proto && *r->l7proto) return r->l7proto;
+    switch (r->l7type) {
+    case L7T_HTTP: return "PortNetworkPolicyRule_HttpRules";
+    case L7T_KAFKA: return "PortNetworkPolicyRule_KafkaRules";
+    case L7T_L7: return "PortNetworkPolicyRule_L7Rules";
+    default: return "";
+    }
+}
+
+int ref_px_nl7(const ref_pnp_rule *r) {
+    if (r->l7type == L7T_HTTP) return r->nhttp;
+    if (r->l7type == L7T_KAFKA) return r->nkafka;
+    if (r->l7type == L7T_L7 && r->l7proto && !strcmp(r->l7proto, "memcache")) return r->nl7;
+    return 0;
+}
+
+int ref_px_installed(const ref_port *pp) {
+    const char *first = NULL;
+    for (int r = 0; r < pp->nrules; r++) {
+        const char *n = px_parser(&pp->rules[r]);
+        if (!*n) continue;
+        if (strcmp(n, "memcache") && strcmp(n, "PortNetworkPolicyRule_HttpRules") &&
+            strcmp(n, "PortNetworkPolicyRule_KafkaRules"))
+            return 0;  /* no such parser: port skipped (:128-134, 200-203) */
+        if (!first) first = n;
+        else if (strcmp(first, n)) return 0;  /* mismatching L7 types (:135-140; the reference NACKs) */
+    }
+    return 1;
+}
+
+int ref_px_have_l7(const ref_port *pp) {
+    for (int r = 0; r < pp->nrules; r++) if (ref_px_nl7(&pp->rules[r]) > 0) return 1;
+    return 0;
 }
 
 int ref_remote_ok(const ref_pnp_rule *r, uint64_t id) {

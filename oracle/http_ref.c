@@ -269,6 +269,36 @@ void ref_http_verdict(const ref_policy *pol, const ref_conn_t *c, const uint8_t 
     o->consumed = m.info.consumed;
     if (c->policy < 0 || c->policy >= pol->np) { o->verdict = L7_DENY; free(m.h); return; }
     const ref_netpolicy *np = &pol->p[c->policy];
+    if (c->flags & L7_CONN_PROXYLIB) {
+        /* the proxylib "http" parser: Instance.PolicyMatches -> PortNetworkPolicies.Matches
+         * (proxylib/proxylib/policymap.go:150-236): SrcId is the remote in both
+         * directions (connection.go:176-179), installed entries only, no entry => drop */
+        const ref_port *ex, *wc;
+        ref_port_lookup(np, c->ingress, c->port, &ex, &wc);
+        const ref_port *cands[2] = {ex, wc};
+        o->verdict = L7_DENY;
+        for (int k = 0; k < 2; k++) {
+            const ref_port *pp = cands[k];
+            if (!pp || !ref_px_installed(pp)) continue;
+            if (!ref_px_have_l7(pp) || pp->nrules == 0) { o->verdict = L7_ALLOW; break; }
+            int hit = 0;
+            for (int r = 0; r < pp->nrules && !hit; r++) {
+                const ref_pnp_rule *pr = &pp->rules[r];
+                if (!ref_remote_ok(pr, c->src_id)) continue;
+                if (ref_px_nl7(pr) == 0) { hit = 1; break; }
+                if (pr->l7type != L7T_HTTP) continue;
+                for (int q = 0; q < pr->nhttp; q++) {
+                    const ref_http_rule *hr = &pr->http[q];
+                    int all = 1;
+                    for (int j = 0; j < hr->n && all; j++) all = hmatch(buf, &m, &hr->m[j]);
+                    if (all) { hit = 1; o->rule = hr->id; break; }
+                }
+            }
+            if (hit) { o->verdict = L7_ALLOW; break; }
+        }
+        free(m.h);
+        return;
+    }
     uint64_t remote = c->ingress ? c->src_id : c->dst_id;
     const ref_port *ex, *wc;
     ref_port_lookup(np, c->ingress, c->port, &ex, &wc);

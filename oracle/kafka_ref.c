@@ -349,9 +349,28 @@ void ref_kafka_verdict(const ref_policy *pol, const ref_conn_t *c, const uint8_t
     const ref_kafka_rule **rules = NULL; int nr = 0, cap = 0, any = 0;
     static const ref_kafka_rule WILDCARD = {0, 1, 0, 0, NULL, 0, NULL, 0, -1};
     const ref_port *cands[2] = {ex, wc};
+    const int px = (c->flags & L7_CONN_PROXYLIB) != 0;
     for (int k = 0; k < 2; k++) {
         const ref_port *pp = cands[k];
         if (!pp) continue;
+        if (px) {
+            /* the proxylib "kafka" parser: installed entries only; a port without
+             * L7 rules or a group with an empty L7 set admits everything; the
+             * groups' Kafka rules form one MatchesRule list */
+            if (!ref_px_installed(pp)) continue;
+            int all_ok = !ref_px_have_l7(pp) || pp->nrules == 0;
+            for (int r = 0; r < pp->nrules || all_ok; r++) {
+                const ref_pnp_rule *pr = all_ok ? NULL : &pp->rules[r];
+                if (pr && !ref_remote_ok(pr, c->src_id)) continue;
+                int wild = all_ok || ref_px_nl7(pr) == 0;
+                int add = wild ? 1 : (pr->l7type == L7T_KAFKA ? pr->nkafka : 0);
+                if (nr + add > cap) { cap = (nr + add) * 2 + 8; rules = realloc(rules, sizeof(*rules) * cap); }
+                if (wild) { rules[nr++] = &WILDCARD; any = 1; }
+                else if (pr->l7type == L7T_KAFKA) { for (int i = 0; i < pr->nkafka; i++) rules[nr++] = &pr->kafka[i]; any = 1; }
+                if (all_ok) break;
+            }
+            continue;
+        }
         for (int r = 0; r < pp->nrules; r++) {
             const ref_pnp_rule *pr = &pp->rules[r];
             if (!ref_remote_ok(pr, c->src_id)) continue;

@@ -43,7 +43,7 @@ void ref_policy_free(ref_policy *p);
 /* memcached parser selection (proxylib/memcached/parser.go:186-202): the
  * first byte a connection carries picks text or binary for its lifetime.
  * 0 = not chosen yet (this buffer's first byte decides). */
-enum { L7_CONN_MC_TEXT = 1, L7_CONN_MC_BINARY = 2 };
+enum { L7_CONN_MC_TEXT = 1, L7_CONN_MC_BINARY = 2, L7_CONN_PROXYLIB = 4 };
 
 typedef struct {
     int32_t policy;     /* index of the NetworkPolicy in the loaded set, -1 = unknown */

@@ -196,34 +196,17 @@ static int mc_rule_matches(const ref_mc_rule *r, const mc_meta *m) {
 /* PortNetworkPolicyRules.Matches (policymap.go:150-171) */
 static int mc_port_rules_match(const ref_port *pp, uint64_t remote, const mc_meta *m, int32_t *rule) {
     *rule = -1;
-    int have_l7 = 0;
-    for (int r = 0; r < pp->nrules; r++) if (pp->rules[r].l7type == L7T_L7 && pp->rules[r].nl7 > 0) have_l7 = 1;
-    if (!have_l7) return 1;
+    if (!ref_px_have_l7(pp)) return 1;
     if (pp->nrules == 0) return 1;
     for (int r = 0; r < pp->nrules; r++) {
         const ref_pnp_rule *pr = &pp->rules[r];
         if (!ref_remote_ok(pr, remote)) continue;
-        int n = pr->l7type == L7T_L7 ? pr->nl7 : 0;
-        if (n == 0) return 1;
-        for (int k = 0; k < n; k++)
+        if (ref_px_nl7(pr) == 0) return 1;  /* empty L7 set matches any payload */
+        if (pr->l7type != L7T_L7) continue;  /* HTTP / Kafka rules never match a memcached request */
+        for (int k = 0; k < pr->nl7; k++)
             if (mc_rule_matches(&pr->l7[k], m)) { *rule = pr->l7[k].id; return 1; }
     }
     return 0;
-}
-
-/* A port entry proxylib installs for this parser: every rule's L7 parser name
- * must be registered (policymap.go:58-89,118-148); only "memcache" is. */
-static int mc_port_installed(const ref_port *pp) {
-    for (int r = 0; r < pp->nrules; r++) {
-        const ref_pnp_rule *pr = &pp->rules[r];
-        const char *name = pr->l7proto;
-        if (!name || !*name) {
-            if (pr->l7type == L7T_NONE) continue;
-            return 0;  /* PortNetworkPolicyRule_{Http,Kafka,L7}Rules: no such parser */
-        }
-        if (strcmp(name, "memcache") != 0) return 0;
-    }
-    return 1;
 }
 
 void ref_memcache_verdict(const ref_policy *pol, const ref_conn_t *c, const uint8_t *b, uint32_t len, ref_out_t *o) {
@@ -305,7 +288,7 @@ void ref_memcache_verdict(const ref_policy *pol, const ref_conn_t *c, const uint
         const ref_port *cands[2] = {ex, wc};
         for (int k = 0; k < 2; k++) {
             int32_t rule;
-            if (!cands[k] || !mc_port_installed(cands[k])) continue;
+            if (!cands[k] || !ref_px_installed(cands[k])) continue;
             if (mc_port_rules_match(cands[k], c->src_id, &m, &rule)) { o->verdict = L7_ALLOW; o->rule = rule; break; }
         }
     }

@@ -71,5 +71,11 @@ const void *ref_mc_group(const char *name, size_t n);
 
 int ref_port_lookup(const ref_netpolicy *np, int ingress, uint32_t port, const ref_port **exact, const ref_port **wild);
 int ref_remote_ok(const ref_pnp_rule *r, uint64_t id);
+/* proxylib's view of a port entry (proxylib/proxylib/policymap.go:58-206) with
+ * the rule parsers "memcache", PortNetworkPolicyRule_HttpRules and
+ * PortNetworkPolicyRule_KafkaRules registered */
+int ref_px_nl7(const ref_pnp_rule *r);          /* len(L7Rules) of a rule */
+int ref_px_installed(const ref_port *pp);       /* entry kept in PortNetworkPolicies */
+int ref_px_have_l7(const ref_port *pp);         /* HaveL7Rules */
 
 #endif

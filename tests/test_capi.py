@@ -21,7 +21,7 @@ def declared(header):
 
 def test_library_exports_header_symbols():
     lib = _lib.load()
-    names = declared("l7gpu.h")
+    names = declared("l7gpu.h") + declared("proxylib_abi.h")
     assert "l7g_classify" in names and "l7g_policy_update" in names
     for name in names:
         assert hasattr(lib, name), name

@@ -42,7 +42,9 @@ def test_no_gpu_no_module(monkeypatch):
 @pytest.mark.parametrize("proto,dst,exp", [
     ("memcache", "2.2.2.2:80", P.OK),
     ("memcache", "[::1]:11211", P.OK),
-    ("http", "2.2.2.2:80", P.UNKNOWN_PARSER),
+    ("http", "2.2.2.2:80", P.OK),
+    ("kafka", "2.2.2.2:9092", P.OK),
+    ("cassandra-not-here", "2.2.2.2:80", P.UNKNOWN_PARSER),
     ("memcache", "2.2.2.2", P.INVALID_ADDRESS),
     ("memcache", "2.2.2.2:0", P.INVALID_ADDRESS),
     ("memcache", "2.2.2.2:http", P.INVALID_ADDRESS),
