@@ -30,14 +30,15 @@ class Stats(C.Structure):
         "kafka_rulesets", "kafka_rules", "kafka_topics")] + [
         ("table_bytes", C.c_uint64), ("http_image_bytes", C.c_uint64), ("hot_ruleset", C.c_int32),
         ("hot_image_bytes", C.c_uint32)] + [
-        (n, C.c_uint32) for n in ("mc_rulesets", "mc_rules", "mc_dfas", "mc_dfa_states")]
+        (n, C.c_uint32) for n in ("mc_rulesets", "mc_rules", "mc_dfas", "mc_dfa_states", "http_nfas", "mc_nfas")] + [
+        ("nfa_pool_bytes", C.c_uint64)]
 
 
 EXPORTS = (
     "l7g_engine_create", "l7g_engine_destroy", "l7g_policy_update", "l7g_policy_index",
     "l7g_policy_nrules", "l7g_conns_set", "l7g_conn_update", "l7g_classify", "l7g_classify_host", "l7g_stats",
     "l7g_debug_regex", "l7g_debug_phase_times", "l7g_profile_enable", "l7g_profile_last",
-    "l7g_debug_kafka_phase_times", "l7g_kafka_deny_response",
+    "l7g_debug_kafka_phase_times", "l7g_kafka_deny_response", "l7g_debug_regex_nfa",
 )
 
 _libs = {}
@@ -67,6 +68,7 @@ def load(path=None):
     lib.l7g_classify_host.argtypes = [vp, vp, C.c_uint64, vp, vp, vp, C.c_uint32, vp, vp, vp]
     lib.l7g_stats.argtypes = [vp, C.POINTER(Stats)]
     lib.l7g_debug_regex.argtypes = [cp, sz, C.c_int, cp, sz, cp, sz]
+    lib.l7g_debug_regex_nfa.argtypes = [cp, sz, C.c_int, cp, sz, cp, sz]
     lib.l7g_debug_phase_times.argtypes = [vp, vp, C.c_int]
     lib.l7g_debug_kafka_phase_times.argtypes = [vp, vp, C.c_int]
     lib.l7g_kafka_deny_response.argtypes = [cp, sz, vp, sz, C.POINTER(C.c_size_t)]
@@ -76,15 +78,17 @@ def load(path=None):
     return lib
 
 
-def debug_regex(pattern, data, anchored=True):
-    """Compile `pattern` with the product's Go-regexp DFA compiler and run the
-    compiled tables on `data` (host walk of the device tables; test hook).
-    Returns True/False, or raises ValueError with Go's compile error text."""
+def debug_regex(pattern, data, anchored=True, nfa=False):
+    """Compile `pattern` with the product's Go-regexp DFA compiler (nfa=True:
+    the bit-parallel NFA fallback) and run the compiled tables on `data` (host
+    walk of the device tables; test hook).  Returns True/False, or raises
+    ValueError with Go's compile error text."""
     lib = load()
     p = pattern.encode() if isinstance(pattern, str) else pattern
     d = data.encode() if isinstance(data, str) else data
     err = C.create_string_buffer(512)
-    r = lib.l7g_debug_regex(p, len(p), 1 if anchored else 0, d, len(d), err, 512)
+    fn = lib.l7g_debug_regex_nfa if nfa else lib.l7g_debug_regex
+    r = fn(p, len(p), 1 if anchored else 0, d, len(d), err, 512)
     if r < 0:
         raise ValueError(err.value.decode(errors="replace"))
     return bool(r)

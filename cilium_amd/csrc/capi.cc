@@ -13,7 +13,9 @@
 #include "engine/http_compile.h"
 #include "engine/kafka_compile.h"
 #include "engine/mc_compile.h"
+#include "engine/nfa_pool.h"
 #include "policy/policy.h"
+#include "regex/nfa_walk.h"
 #include "regex/re_dfa.h"
 
 namespace l7 {
@@ -23,6 +25,7 @@ hipError_t LaunchKafkaClassify(const Batch &B, const KafkaTables &T, const uint3
                                bool answer_other, hipStream_t stream);
 hipError_t LaunchMemcacheClassify(const Batch &B, const McTables &T, const uint32_t *sel, const uint32_t *sel_count,
                                   bool answer_other, hipStream_t stream);
+hipError_t LaunchHttpNfa(const Batch &B, const HttpTables &T, hipStream_t stream);
 hipError_t LaunchPartition(const Batch &B, uint32_t *sel_kafka, uint32_t *sel_mc, uint32_t *counts, hipStream_t stream);
 hipError_t HttpPhaseTimes(uint64_t *out, bool reset);
 hipError_t KafkaPhaseTimes(uint64_t *out, bool reset);
@@ -58,6 +61,9 @@ struct l7g_engine {
     // protocol split (grow-only, stream-ordered): [counts(16) | L7_KAFKA_CLASSES x n Kafka idx | n memcached idx]
     uint32_t *d_sel = nullptr;
     size_t sel_cap = 0;
+    // NFA pre-pass results, u64 per request (grow-only, stream-ordered as d_sel)
+    uint64_t *d_nfa = nullptr;
+    size_t nfa_cap = 0;
     // Completion of the last l7g_classify's kernels (recorded on the caller's
     // stream).  The engine waits on it -- never on the caller's stream, which
     // may be gone by then -- before it rewrites or frees anything a launched
@@ -159,7 +165,7 @@ hipError_t Upload(l7g_engine *e) {
     if (e->tables_dirty) {
         std::vector<uint8_t> blob;
         const HttpImage &H = e->hc->image();
-        size_t o_rs = Put(blob, H.rulesets), o_img = Put(blob, H.images);
+        size_t o_rs = Put(blob, H.rulesets), o_img = Put(blob, H.images), o_nfa = Put(blob, H.nfa_pool);
         const KafkaImage &K = e->kc->image();
         size_t k_rs = Put(blob, K.rulesets), k_r = Put(blob, K.rules), k_idx = Put(blob, K.index),
                k_th = Put(blob, K.topic_hash), k_ch = Put(blob, K.client_hash), k_s = Put(blob, K.strings);
@@ -176,6 +182,8 @@ hipError_t Upload(l7g_engine *e) {
         T.images = d + o_img;
         T.nrulesets = (uint32_t)H.rulesets.size();
         T.hot_ruleset = e->hot_ruleset;
+        T.nfa_pool = H.nfa_pool.empty() ? nullptr : d + o_nfa;
+        T.nfa_bits = nullptr;
         KafkaTables &KT = e->kt;
         KT.rulesets = (const DevKafkaRuleset *)(d + k_rs);
         KT.rules = (const DevKafkaRule *)(d + k_r);
@@ -253,6 +261,7 @@ void l7g_engine_destroy(l7g_engine *e) {
     if (e->d_blob) hipFree(e->d_blob);
     if (e->d_conns) hipFree(e->d_conns);
     if (e->d_sel) hipFree(e->d_sel);
+    if (e->d_nfa) hipFree(e->d_nfa);
     if (e->done_ev) hipEventDestroy(e->done_ev);
     for (hipEvent_t ev : e->prof_ev)
         if (ev) hipEventDestroy(ev);
@@ -388,6 +397,24 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
         sel_m = sel_k + L7_KAFKA_CLASSES * (size_t)n;
         rc = hipMemsetAsync(cnt, 0, 16 * sizeof(uint32_t), s);
     }
+    // rule sets with NFA-fallback matchers: the pre-pass writes one u64 per request
+    HttpTables ht = e->ht;
+    const bool nfa = e->ht.nfa_pool != nullptr && (e->has_http || nproto == 0);
+    if (nfa && rc == hipSuccess) {
+        if (!partitioned && e->launched) rc = hipStreamWaitEvent(s, e->done_ev, 0);
+        if (rc == hipSuccess && n > e->nfa_cap) {
+            if (e->d_nfa) {
+                rc = WaitLastClassify(e);
+                hipFree(e->d_nfa);
+                e->d_nfa = nullptr;
+                e->nfa_cap = 0;
+            }
+            if (rc == hipSuccess) rc = hipMalloc(&e->d_nfa, (size_t)n * sizeof(uint64_t));
+            if (rc == hipSuccess) e->nfa_cap = n;
+        }
+        if (rc != hipSuccess) return (int)rc;
+        ht.nfa_bits = e->d_nfa;
+    }
     // profiling: event k is recorded before stage k (partition, http, kafka, memcache), event 4 after the last
     const bool prof = e->profile;
     auto mark = [&](int k) {
@@ -398,7 +425,8 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
     mark(0);
     if (rc == hipSuccess && run[0]) rc = LaunchPartition(B, sel_k, sel_m, cnt, s);
     mark(1);
-    if (rc == hipSuccess && run[1]) rc = LaunchHttpClassify(B, e->ht, e->any_cold, !partitioned, s);
+    if (rc == hipSuccess && run[1] && nfa) rc = LaunchHttpNfa(B, ht, s);
+    if (rc == hipSuccess && run[1]) rc = LaunchHttpClassify(B, ht, e->any_cold, !partitioned, s);
     mark(2);
     if (rc == hipSuccess && run[2]) rc = LaunchKafkaClassify(B, e->kt, sel_k, cnt, !partitioned, s);
     mark(3);
@@ -477,6 +505,8 @@ int l7g_stats(l7g_engine *e, l7g_stats_t *out) {
     out->mc_rules = (uint32_t)M.rules;
     out->mc_dfas = (uint32_t)M.dfas;
     out->mc_dfa_states = (uint32_t)M.dfa_states;
+    out->http_nfas = (uint32_t)H.nfas;
+    out->nfa_pool_bytes = H.nfa_pool.size();
     return 0;
 }
 
@@ -522,6 +552,19 @@ int l7g_debug_regex(const char *pat, size_t patlen, int anchored, const uint8_t 
     if (!re::BuildDFA(ps, 1 << 16, &d, &m)) { set_err(err, errlen, m); return -1; }
     auto acc = re::RunDFA(d, s, slen);
     return (int)(acc[0] & 1);
+}
+
+int l7g_debug_regex_nfa(const char *pat, size_t patlen, int anchored, const uint8_t *s, size_t slen, char *err,
+                        size_t errlen) {
+    std::string m;
+    auto ast = re::Parse(std::string(pat, patlen), &m);
+    if (!ast) { set_err(err, errlen, m); return -1; }
+    re::BitNfa n;
+    if (!re::BuildBitNfa({ast.get(), anchored != 0}, kNfaMaxWords * 64, &n, &m)) { set_err(err, errlen, m); return -1; }
+    std::vector<uint8_t> pool;
+    const uint64_t off = AppendDevNfa(n, &pool, &m);
+    if (off == ~0ull) { set_err(err, errlen, m); return -1; }
+    return nfa_run(pool.data(), off, s, (uint32_t)slen) ? 1 : 0;
 }
 
 }  // extern "C"

@@ -98,7 +98,7 @@ struct DevHdrName {        // 12 B: a custom header name the rule set looks at
     uint16_t pad;
     uint32_t name_off;     // lower-cased bytes
 };
-struct ImgHeader {         // 64 B, at offset 0 of every image
+struct ImgHeader {         // 80 B, at offset 0 of every image
     uint8_t nchunks;
     uint8_t nhdr;
     uint8_t terminal;      // verdict when no rule matches (V_ALLOW => rule -1)
@@ -119,8 +119,39 @@ struct ImgHeader {         // 64 B, at offset 0 of every image
     uint32_t name_info_off;   // u8[name_states]: NI_* flags
     uint16_t name_ncls;
     uint16_t name_states;
+    uint32_t nfa_off;      // DevNfaRef[nnfa]
+    uint8_t nnfa;
+    uint8_t pad2[11];
 };
-static_assert(sizeof(ImgHeader) == 64, "ImgHeader layout");
+static_assert(sizeof(ImgHeader) == 80, "ImgHeader layout");
+
+// Bit-parallel rune NFA (the fallback for a pattern whose DFA alone exceeds
+// the state budget; re_dfa.h BitNfa, walked by regex/nfa_walk.h).  One DevNfa
+// per distinct pattern, in a pool shared by all rule sets; all offsets are
+// bytes from the pool start.  t_off: the follow sets tabulated per condition
+// class k, per 8-position chunk j of the state and per value v of that chunk:
+// u64[K][8W][256][W] (T[k][j][v] = OR of Follow_k(8j + b) for the bits b of v).
+constexpr int kNfaMaxWords = 16;  // <= 1024 positions
+struct DevNfa {            // 128 B
+    uint32_t m, W, K, nivl;
+    uint64_t t_off;
+    uint64_t ivl_off;      // u32[nivl]: first rune of each interval (sorted; [0] = 0)
+    uint64_t b_off;        // u64[nivl][W]: positions whose class holds the interval
+    uint64_t acc_off;      // u64[K][W]
+    uint64_t ascii_off;    // u16[128]: interval of each ASCII rune
+    uint8_t condmap[64];   // NC_* condition bits -> class
+};
+// An HTTP rule set's NFA-evaluated matcher (one per distinct pattern): the
+// pre-pass (http_nfa_kernel) runs the NFA over the slot's value and sets bit
+// k of the request's u64; the framing kernel then ANDs mask row 0 (rejected)
+// or 1 (accepted) into the rule accumulators when the slot is present.
+constexpr int kMaxNfaPerRuleset = 64;
+struct DevNfaRef {         // 16 B
+    uint64_t nfa;          // DevNfa offset in the pool
+    uint32_t mask_off;     // u64[2][nchunks] in the image
+    uint8_t slot;
+    uint8_t pad[3];
+};
 
 struct DevRuleset {        // 8 B
     uint32_t image_off;    // into HttpTables::images (16-byte aligned)
@@ -132,6 +163,8 @@ struct HttpTables {
     const uint8_t *images;
     uint32_t nrulesets;
     int32_t hot_ruleset;   // rule set whose image is staged in LDS (-1: none)
+    const uint8_t *nfa_pool;   // DevNfa pool (null: no rule set has NFA matchers)
+    uint64_t *nfa_bits;        // per request: bit k = NFA matcher k of its rule set accepted
 };
 
 // ---------------- Kafka ----------------

@@ -6,6 +6,7 @@
 #include <memory>
 
 #include "../regex/re_dfa.h"
+#include "nfa_pool.h"
 
 namespace l7 {
 
@@ -289,6 +290,8 @@ int HttpCompiler::Compile(const std::vector<const HttpRule *> &rules, uint8_t te
     H.terminal = terminal;
     struct Built { int slot; re::DFA d; std::vector<uint64_t> masks; uint32_t absorb; };
     std::vector<Built> built;
+    struct NfaRef { int slot; uint64_t nfa; int pat; std::vector<uint64_t> masks; };
+    std::vector<NfaRef> nfas;
     for (auto &kv : by_slot) {
         const int slot = kv.first;
         H.ref_slots |= (uint16_t)(1u << slot);
@@ -312,22 +315,62 @@ int HttpCompiler::Compile(const std::vector<const HttpRule *> &rules, uint8_t te
             asts.push_back(a.get());
             owned.push_back(std::move(a));
         }
-        // build DFAs, halving the pattern set until each fits the budget
+        // build DFAs, halving the pattern set until each fits the budget; a
+        // pattern over the budget on its own goes to the NFA fallback
         std::vector<std::vector<int>> groups;
         std::vector<re::DFA> dfas;
+        std::vector<int> nfa_pats;
         std::function<bool(std::vector<int>)> build = [&](std::vector<int> sub) -> bool {
             std::vector<re::Pattern> ps;
             for (int p : sub) ps.push_back({asts[p], true});
             re::DFA d;
             std::string e;
             if (re::BuildDFA(ps, max_dfa_states, &d, &e)) { groups.push_back(sub); dfas.push_back(std::move(d)); return true; }
-            if (sub.size() == 1) { *err = "regex too complex for the DFA budget: " + pats[sub[0]].value; return false; }
+            if (sub.size() == 1) { nfa_pats.push_back(sub[0]); return true; }
             std::vector<int> a(sub.begin(), sub.begin() + sub.size() / 2), b(sub.begin() + sub.size() / 2, sub.end());
             return build(a) && build(b);
         };
         std::vector<int> allp;
         for (size_t p = 0; p < pats.size(); p++) allp.push_back((int)p);
         if (!build(allp)) return -1;
+        for (int p : nfa_pats) {
+            std::string e;
+            auto it = nfa_cache_.find(pats[p].value);
+            if (it == nfa_cache_.end()) {
+                re::BitNfa n;
+                if (re::BuildBitNfa({asts[p], true}, kNfaMaxWords * 64, &n, &e)) {
+                    const uint64_t off = AppendDevNfa(n, &img_.nfa_pool, err);
+                    if (off == ~0ull) return -1;
+                    it = nfa_cache_.emplace(pats[p].value, off).first;
+                    img_.nfas++;
+                }
+            }
+            if (it != nfa_cache_.end()) {
+                nfas.push_back({slot, it->second, p, {}});
+                continue;
+            }
+            // too many positions for the NFA: one large DFA if it fits
+            re::DFA d;
+            std::string e2;
+            if (!re::BuildDFA({{asts[p], true}}, max_single_dfa_states, &d, &e2)) {
+                *err = "regex too complex for the device (" + e + "; DFA over " +
+                       std::to_string(max_single_dfa_states) + " states): " + pats[p].value;
+                return -1;
+            }
+            groups.push_back({p});
+            dfas.push_back(std::move(d));
+        }
+        // mask rows of the NFA matchers: [rejected, accepted] x chunks
+        for (auto &nf : nfas) {
+            if (nf.slot != slot || !nf.masks.empty()) continue;
+            nf.masks.resize(2 * nchunks);
+            for (int a = 0; a < 2; a++) {
+                uint64_t *m = &nf.masks[a * nchunks];
+                for (size_t c = 0; c < nchunks; c++) m[c] = all[c];
+                for (auto &rp : rm_pat)
+                    if (rp.second == nf.pat && (a == 1) == pats[rp.second].invert) m[rp.first >> 6] &= ~bit(rp.first);
+            }
+        }
         H.max_slot_dfas = (uint8_t)std::max<size_t>(H.max_slot_dfas, dfas.size());
         for (size_t g = 0; g < dfas.size(); g++) {
             Built b{slot, std::move(dfas[g]), {}, 0};
@@ -350,6 +393,8 @@ int HttpCompiler::Compile(const std::vector<const HttpRule *> &rules, uint8_t te
         }
     }
     if (built.size() > 255) { *err = "rule set needs more than 255 DFAs"; return -1; }
+    if (nfas.size() > (size_t)kMaxNfaPerRuleset) { *err = "rule set needs more than 64 NFA matchers"; return -1; }
+    H.nnfa = (uint8_t)nfas.size();
     H.ndfa = (uint8_t)built.size();
     // slot directory (built is ordered by slot)
     for (int s = 0, k = 0; s <= kNumSlots; s++) {
@@ -377,6 +422,15 @@ int HttpCompiler::Compile(const std::vector<const HttpRule *> &rules, uint8_t te
         h.name_off = (uint32_t)names.size();
         names.insert(names.end(), nm.begin(), nm.end());
         hn.push_back(h);
+    }
+    {
+        std::vector<DevNfaRef> refs(nfas.size());
+        for (size_t k = 0; k < nfas.size(); k++) {
+            refs[k].nfa = nfas[k].nfa;
+            refs[k].slot = (uint8_t)nfas[k].slot;
+            refs[k].mask_off = Append(img, nfas[k].masks.data(), nfas[k].masks.size());
+        }
+        H.nfa_off = Append(img, refs.data(), refs.size());
     }
     H.hdr_off = Append(img, hn.data(), hn.size());
     uint32_t names_off = Append(img, names.data(), names.size());

@@ -24,7 +24,8 @@ namespace l7 {
 struct HttpImage {
     std::vector<DevRuleset> rulesets;
     std::vector<uint8_t> images;
-    size_t chunks = 0, dfas = 0, dfa_states = 0;
+    std::vector<uint8_t> nfa_pool;  // DevNfa tables (device_tables.h), shared by all rule sets
+    size_t chunks = 0, dfas = 0, dfa_states = 0, nfas = 0;
 };
 
 class HttpCompiler {
@@ -37,11 +38,16 @@ public:
     int RulesetFor(int policy, bool ingress, uint32_t port, uint64_t remote, bool proxylib, std::string *err);
     const HttpImage &image() const { return img_; }
     int max_dfa_states = 4096;
+    // A pattern whose DFA alone exceeds max_dfa_states is evaluated by the
+    // bit-parallel NFA (<= kNfaMaxWords * 64 positions), else by one DFA of up
+    // to max_single_dfa_states; beyond both the policy is rejected.
+    int max_single_dfa_states = 65535;
 
 private:
     const PolicySet *ps_;
     HttpImage img_;
     std::map<std::pair<std::vector<int>, int>, int> cache_;  // (rule ids, terminal) -> ruleset
+    std::map<std::string, uint64_t> nfa_cache_;              // regex -> DevNfa offset in the pool
     int Compile(const std::vector<const HttpRule *> &rules, uint8_t terminal, std::string *err);
 };
 

@@ -1,0 +1,68 @@
+// Device layout of bit-parallel NFAs (product code): BitNfa (re_dfa.h) ->
+// DevNfa + its tables appended to a pool (device_tables.h).
+#pragma once
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../device_tables.h"
+#include "../regex/re_dfa.h"
+
+namespace l7 {
+
+// Appends n's device tables to pool (16-byte aligned); returns the DevNfa
+// offset, or ~0ull with *err when the pool would pass 4 GiB.
+inline uint64_t AppendDevNfa(const re::BitNfa &n, std::vector<uint8_t> *pool, std::string *err) {
+    const size_t W = (size_t)n.W, K = (size_t)n.K;
+    auto align = [&](size_t bytes) {
+        size_t off = (pool->size() + 15) & ~(size_t)15;
+        pool->resize(off + bytes, 0);
+        return off;
+    };
+    const size_t t_bytes = K * 8 * W * 256 * W * 8, niv = n.ivl_lo.size();
+    if (pool->size() + t_bytes + niv * (W * 8 + 4) + K * W * 8 + 512 > (1ull << 32)) {
+        *err = "NFA tables exceed 4 GiB";
+        return ~0ull;
+    }
+    DevNfa d{};
+    const size_t doff = align(sizeof(DevNfa));
+    d.m = (uint32_t)n.m;
+    d.W = (uint32_t)W;
+    d.K = (uint32_t)K;
+    d.nivl = (uint32_t)niv;
+    memcpy(d.condmap, n.condmap, sizeof d.condmap);
+    d.t_off = align(t_bytes);
+    {
+        uint64_t *T = (uint64_t *)(pool->data() + d.t_off);
+        for (size_t k = 0; k < K; k++)
+            for (size_t j = 0; j < 8 * W; j++) {
+                uint64_t *tab = T + (k * 8 * W + j) * 256 * W;  // [v][W]
+                for (size_t v = 1; v < 256; v++) {
+                    const size_t b = (size_t)__builtin_ctz((unsigned)v), p = 8 * j + b;
+                    const uint64_t *rest = tab + (v & (v - 1)) * W;
+                    uint64_t *dst = tab + v * W;
+                    for (size_t u = 0; u < W; u++)
+                        dst[u] = rest[u] | (p < (size_t)n.m ? n.follow[(k * n.m + p) * W + u] : 0);
+                }
+            }
+    }
+    d.ivl_off = align(niv * 4);
+    memcpy(pool->data() + d.ivl_off, n.ivl_lo.data(), niv * 4);
+    d.b_off = align(niv * W * 8);
+    memcpy(pool->data() + d.b_off, n.b.data(), niv * W * 8);
+    d.ascii_off = align(128 * 2);
+    {
+        uint16_t *a = (uint16_t *)(pool->data() + d.ascii_off);
+        for (size_t r = 0, iv = 0; r < 128; r++) {
+            while (iv + 1 < niv && (size_t)n.ivl_lo[iv + 1] <= r) iv++;
+            a[r] = (uint16_t)iv;
+        }
+    }
+    d.acc_off = align(K * W * 8);
+    memcpy(pool->data() + d.acc_off, n.acc.data(), K * W * 8);
+    memcpy(pool->data() + doff, &d, sizeof d);
+    align(16);  // aligned tail: 16-byte reads of the last table stay inside
+    return doff;
+}
+
+}  // namespace l7

@@ -296,7 +296,7 @@ __device__ __forceinline__ void verdict_then_body(Lane &L, uint8_t v, int32_t ru
 }
 
 template <bool kLds>
-__device__ __forceinline__ void headers_done(const Img<kLds> &I, Lane &L) {
+__device__ __forceinline__ void headers_done(const Img<kLds> &I, Lane &L, const uint64_t *nfa_bits) {
     const uint64_t total = L.chunked ? (uint64_t)(L.pa - L.a0) : (uint64_t)(L.pa - L.a0) + L.cl;
     if (total > 0xFFFFFFFFull) {
         finish(L, V_PARSE_ERROR);
@@ -319,6 +319,22 @@ __device__ __forceinline__ void headers_done(const Img<kLds> &I, Lane &L) {
 #pragma unroll
                 for (int c = 0; c < kChunksPerPass; c++)
                     if ((uint32_t)c < nc) L.acc[c] &= I.u64(HDR_U32(I, absent_off) + 8 * (s * nchunks + L.cg + c));
+            }
+            // matchers the NFA pre-pass evaluated (present slots; an absent one
+            // is covered by the absent masks above)
+            const uint32_t nnfa = HDR_U8(I, nnfa);
+            if (nnfa) {
+                const uint64_t bits = nfa_bits[L.idx];
+                const uint32_t refs = HDR_U32(I, nfa_off);
+                for (uint32_t k = 0; k < nnfa; k++) {
+                    const uint32_t ref = refs + k * (uint32_t)sizeof(DevNfaRef);
+                    if (!((L.present >> I.u8(ref + offsetof(DevNfaRef, slot))) & 1)) continue;
+                    const uint32_t mo = I.u32(ref + offsetof(DevNfaRef, mask_off)) +
+                                        8 * ((uint32_t)((bits >> k) & 1) * nchunks + L.cg);
+#pragma unroll
+                    for (int c = 0; c < kChunksPerPass; c++)
+                        if ((uint32_t)c < nc) L.acc[c] &= I.u64(mo + 8 * c);
+                }
             }
             int32_t hit = -1;
 #pragma unroll
@@ -390,7 +406,7 @@ __device__ __forceinline__ uint32_t find_stop(const Cursor &C, uint32_t pa, uint
 // Consumes [L.pa, min(window end, request end)).  Every loop has a single
 // exit; errors set the mode to M_DONE so later blocks fall through.
 template <bool kLds>
-__device__ __forceinline__ void parse_window(const Img<kLds> &I, Lane &L, Cursor &C) {
+__device__ __forceinline__ void parse_window(const Img<kLds> &I, Lane &L, Cursor &C, const uint64_t *nfa_bits) {
     const uint32_t lim = min(L.w + kWin, L.lena);
     C.w = L.w;
     const uint32_t ncls_name = HDR_U16(I, name_ncls);
@@ -495,7 +511,7 @@ __device__ __forceinline__ void parse_window(const Img<kLds> &I, Lane &L, Cursor
                 finish(L, V_PARSE_ERROR);
             } else {
                 L.pa++;
-                headers_done(I, L);  // done, or a new pass from the request start
+                headers_done(I, L, nfa_bits);  // done, or a new pass from the request start
             }
         }
         if (L.mode == M_NAME) {  // 1*tchar ":"  (obs-fold SP/HT is not a tchar)
@@ -946,12 +962,12 @@ __device__ __forceinline__ void map_skip(Lane &L, const TileMap &T) {
 // those four bytes (M_SKIP -> M_LF -> line_done -> M_LINE -> M_ENDLF ->
 // headers_done), without another window.
 template <bool kLds>
-__device__ __forceinline__ void finish_tail(const Img<kLds> &I, Lane &L) {
+__device__ __forceinline__ void finish_tail(const Img<kLds> &I, Lane &L, const uint64_t *nfa_bits) {
     L.tail = false;
     L.pa += 4;
     if (line_done(I, L)) {
         L.mode = M_LINE;
-        headers_done(I, L);
+        headers_done(I, L, nfa_bits);
     } else {
         finish(L, V_PARSE_ERROR);
     }
@@ -964,6 +980,7 @@ struct Out {
     uint32_t *s_cnt;
     uint64_t *counters;
     uint32_t nrules;
+    const uint64_t *nfa_bits;  // NFA pre-pass results (HttpTables::nfa_bits)
 };
 
 __device__ __forceinline__ void emit(const Lane &L, const Out &O) {
@@ -1010,13 +1027,13 @@ __device__ __forceinline__ void run_tile(Lane &L, const uint8_t *img, uint8_t *w
         dma_windows(wave_lds, packed, lane);
         PH_MARK(0);
         if (!L.done) {
-            parse_window(I, L, C);
+            parse_window(I, L, C, O.nfa_bits);
             if (!L.done && !L.scan && L.pa >= L.lena) finish(L, V_INCOMPLETE);
         }
         PH_MARK(1);
         PH_COUNT(5, __builtin_popcountll(__ballot(L.scan)));
         map_skip(L, TM);
-        if (L.tail) finish_tail(I, L);
+        if (L.tail) finish_tail(I, L, O.nfa_bits);
         PH_MARK(2);
         if (L.done && L.owed) {
             emit(L, O);
@@ -1067,7 +1084,7 @@ __global__ __launch_bounds__(kBlock) void http_classify_kernel(Batch B, HttpTabl
         for (uint32_t i = tid; i < 8 + kLdsRuleCounters; i += kBlock) s_cnt[i] = 0;
     __syncthreads();
 
-    const Out O{B.verdict, B.rule, B.consumed, s_cnt, counters, ncounters > 8 ? ncounters - 8 : 0};
+    const Out O{B.verdict, B.rule, B.consumed, s_cnt, counters, ncounters > 8 ? ncounters - 8 : 0, T.nfa_bits};
     uint8_t *wave_lds = lds + wave * kWaveLds;
     const uint32_t ntiles = (n + 63) / 64;
     for (uint32_t tile = blockIdx.x * kWaves + wave; tile < ntiles; tile += gridDim.x * kWaves) {

@@ -3,6 +3,7 @@
 #include "re_dfa.h"
 
 #include <algorithm>
+#include <cstring>
 #include <map>
 #include <unordered_map>
 
@@ -41,7 +42,7 @@ inline bool IsWordByte(int b) {
     return (b >= '0' && b <= '9') || (b >= 'A' && b <= 'Z') || (b >= 'a' && b <= 'z') || b == '_';
 }
 
-enum class K : uint8_t { Byte, Split, Assert, Match };
+enum class K : uint8_t { Byte, Split, Assert, Match, Rune /* rune mode: one whole rune of rsets[rset] */ };
 struct BTr { uint8_t lo, hi, guard; int to; };
 struct NState {
     K k = K::Byte;
@@ -49,6 +50,7 @@ struct NState {
     uint8_t cond = 0;
     int acc = -1;   // Match_k / Done_k: pattern id
     int done = -1;  // Match_k of an unanchored pattern: its sticky Done_k state
+    int rset = -1;  // K::Rune: its rune class
     std::vector<BTr> tr;
 };
 
@@ -93,6 +95,10 @@ class Nfa {
 public:
     std::vector<NState> st;
     bool uses_line = false, uses_word = false;
+    // rune mode (BuildBitNfa): a class is one K::Rune state matching a decoded
+    // rune instead of a UTF-8 byte trie; byte-level ops are not available
+    bool rune_mode = false, byte_ops = false;
+    std::vector<RuneSet> rsets;
 
     int New(K k) { st.emplace_back(); st.back().k = k; return (int)st.size() - 1; }
     int Compile(const Node *x, int next);
@@ -103,6 +109,13 @@ private:
 };
 
 int Nfa::CompileClass(const RuneSet &c, int next) {
+    if (rune_mode) {
+        int r = New(K::Rune);
+        st[r].rset = (int)rsets.size();
+        st[r].out = next;
+        rsets.push_back(c);
+        return r;
+    }
     int e = New(K::Byte);
     std::vector<Seq> seqs;
     for (auto &r : c.r) Utf8Split(r.first, r.second, seqs);
@@ -159,6 +172,7 @@ int Nfa::Compile(const Node *x, int next) {
         return s;
     }
     case Op::ByteString: {
+        byte_ops |= rune_mode;
         int pc = next;
         for (int i = (int)x->bytes.size() - 1; i >= 0; i--) {
             int s = New(K::Byte);
@@ -169,6 +183,7 @@ int Nfa::Compile(const Node *x, int next) {
         return pc;
     }
     case Op::AnyBytes: {  // [\x00-\xff]* over raw bytes
+        byte_ops |= rune_mode;
         int s = New(K::Split);
         int b = New(K::Byte);
         st[b].tr.push_back({0x00, 0xFF, G_NONE, s});
@@ -457,6 +472,135 @@ bool BuildDFA(const std::vector<Pattern> &pats, int max_states, DFA *out, std::s
         for (int c = 0; c < out->ncls; c++) out->next[(size_t)blk[s] * out->ncls + c] = (uint16_t)blk[trans[s][rep[c]]];
     }
     if (nb > 65535) { if (err) *err = "DFA too large"; return false; }
+    return true;
+}
+
+bool BuildBitNfa(const Pattern &p, int max_positions, BitNfa *out, std::string *err) {
+    Nfa nfa;
+    nfa.rune_mode = true;
+    RuneSet any;
+    any.add(0, 0x10FFFF);
+    const int mt = nfa.New(K::Match);
+    nfa.st[mt].acc = 0;
+    if (!p.anchored) {  // Go regexp.Match: a sticky "done" state after the first match
+        int d = nfa.CompileClass(any, -1);
+        nfa.st[d].out = d;
+        nfa.st[d].acc = 0;
+        nfa.st[mt].done = d;
+    }
+    const int entry = nfa.Compile(p.ast, mt);
+    if (nfa.byte_ops) {
+        if (err) *err = "byte-level matcher in the NFA fallback";
+        return false;
+    }
+    int start = entry;
+    if (!p.anchored) {  // search loop over whole runes, as in BuildDFA
+        int s0 = nfa.New(K::Split);
+        int loop = nfa.CompileClass(any, s0);
+        nfa.st[s0].out = loop;
+        nfa.st[s0].out1 = entry;
+        start = s0;
+    }
+    // ---- positions: the rune states; 0 = virtual start
+    const int ns = (int)nfa.st.size();
+    std::vector<int> pos_of(ns, -1), to_of{start}, rset_of{-1};
+    for (int q = 0; q < ns; q++)
+        if (nfa.st[q].k == K::Rune) {
+            pos_of[q] = (int)to_of.size();
+            to_of.push_back(nfa.st[q].out);
+            rset_of.push_back(nfa.st[q].rset);
+        }
+    const int m = (int)to_of.size();
+    if (m > max_positions) {
+        if (err) *err = "regex needs " + std::to_string(m) + " NFA positions (limit " + std::to_string(max_positions) + ")";
+        return false;
+    }
+    const int W = (m + 63) / 64;
+    // ---- empty-width condition classes: the achievable conditions reduced
+    // to the bits some assertion of the pattern tests
+    uint8_t relevant = 0;
+    for (auto &st : nfa.st)
+        if (st.k == K::Assert) relevant |= st.cond;
+    auto cond_for = [](uint8_t prev, int b) -> uint8_t {  // as in BuildDFA
+        uint8_t c = 0;
+        if (prev & P_START) c |= C_BOT | C_BOL;
+        if (prev & P_NL) c |= C_BOL;
+        bool pw = (prev & P_WORD) != 0;
+        if (b < 0) { c |= C_EOT | C_EOL; c |= pw ? C_WB : C_NWB; }
+        else { if (b == '\n') c |= C_EOL; c |= (pw != IsWordByte(b)) ? C_WB : C_NWB; }
+        return c;
+    };
+    std::vector<uint8_t> cls_cond;  // class -> reduced condition
+    memset(out->condmap, 0, sizeof out->condmap);
+    for (uint8_t prev : {(uint8_t)P_START, (uint8_t)0, (uint8_t)P_NL, (uint8_t)P_WORD})
+        for (int b : {-1, (int)'\n', (int)'a', (int)' '}) {
+            const uint8_t raw = cond_for(prev, b), red = raw & relevant;
+            int k = (int)(std::find(cls_cond.begin(), cls_cond.end(), red) - cls_cond.begin());
+            if (k == (int)cls_cond.size()) cls_cond.push_back(red);
+            out->condmap[raw & 63] = (uint8_t)k;
+        }
+    const int K = (int)cls_cond.size();
+    // ---- follow sets and acceptance per class (epsilon closure of each target)
+    out->m = m;
+    out->W = W;
+    out->K = K;
+    out->follow.assign((size_t)K * m * W, 0);
+    out->acc.assign((size_t)K * W, 0);
+    std::vector<int> mark(ns, -1), stack;
+    int epoch = 0;
+    for (int k = 0; k < K; k++) {
+        const uint8_t cond = cls_cond[k];
+        std::vector<int> memo_to(ns, -1);  // target state -> position whose row is already computed
+        for (int pp = 0; pp < m; pp++) {
+            uint64_t *row = &out->follow[((size_t)k * m + pp) * W];
+            const int to = to_of[pp];
+            if (memo_to[to] >= 0) {
+                const uint64_t *src = &out->follow[((size_t)k * m + memo_to[to]) * W];
+                std::copy(src, src + W, row);
+                if ((out->acc[(size_t)k * W + memo_to[to] / 64] >> (memo_to[to] % 64)) & 1)
+                    out->acc[(size_t)k * W + pp / 64] |= 1ull << (pp % 64);
+                continue;
+            }
+            memo_to[to] = pp;
+            epoch++;
+            bool accepts = false;
+            stack.assign(1, to);
+            while (!stack.empty()) {
+                int q = stack.back(); stack.pop_back();
+                if (mark[q] == epoch) continue;
+                mark[q] = epoch;
+                const NState &st = nfa.st[q];
+                switch (st.k) {
+                case K::Split: stack.push_back(st.out1); stack.push_back(st.out); break;
+                case K::Assert: if ((st.cond & cond) == st.cond) stack.push_back(st.out); break;
+                case K::Match: accepts = true; if (st.done >= 0) stack.push_back(st.done); break;
+                case K::Rune: {
+                    if (st.acc >= 0) accepts = true;
+                    const int e = pos_of[q];
+                    row[e / 64] |= 1ull << (e % 64);
+                    break;
+                }
+                case K::Byte: break;  // an empty class: matches nothing
+                }
+            }
+            if (accepts) out->acc[(size_t)k * W + pp / 64] |= 1ull << (pp % 64);
+        }
+    }
+    // ---- rune intervals on which every position's class is constant
+    std::vector<int32_t> cuts{0, 0x110000};
+    for (auto &rs : nfa.rsets)
+        for (auto &r : rs.r) { cuts.push_back(r.first); cuts.push_back(r.second + 1); }
+    std::sort(cuts.begin(), cuts.end());
+    cuts.erase(std::unique(cuts.begin(), cuts.end()), cuts.end());
+    cuts.pop_back();  // 0x110000 closes the last interval
+    out->ivl_lo.assign(cuts.begin(), cuts.end());
+    const size_t niv = cuts.size();
+    out->b.assign(niv * W, 0);
+    for (int pp = 1; pp < m; pp++)
+        for (auto &r : nfa.rsets[rset_of[pp]].r)
+            for (size_t iv = std::lower_bound(cuts.begin(), cuts.end(), r.first) - cuts.begin();
+                 iv < niv && cuts[iv] <= r.second; iv++)
+                out->b[iv * W + pp / 64] |= 1ull << (pp % 64);
     return true;
 }
 

@@ -42,6 +42,34 @@ struct DFA {
 // max_states; callers split the pattern set and retry.
 bool BuildDFA(const std::vector<Pattern> &pats, int max_states, DFA *out, std::string *err);
 
+// Bit-parallel Glushkov automaton of ONE pattern, over runes: the fallback
+// for a pattern whose DFA alone exceeds the state budget (its NFA has few
+// positions even when the subset construction explodes, e.g.
+// (a|b)*a(a|b){14}).
+//
+// Positions are the pattern's rune-class occurrences (one per class, however
+// many UTF-8 sequences it spans); position 0 is the virtual start.  The input
+// is decoded like utf8.DecodeRune (an invalid byte is U+FFFD of width 1), so
+// Go's rune semantics need no byte-level guards here.  A state set S is a
+// bitset over positions; reading rune r at the boundary whose empty-width
+// condition class is k:
+//     S' = Follow_k(S) & B[interval of r]
+// where Follow_k(p) is every position reachable from p through the epsilon
+// closure under k, and B[iv] the positions whose class holds the rune
+// interval iv.  The input is accepted iff S & Acc_k(end) != 0.
+struct BitNfa {
+    int m = 0;                    // positions (incl. the virtual start)
+    int W = 0;                    // u64 words per state set
+    int K = 0;                    // empty-width condition classes
+    uint8_t condmap[64] = {0};    // NC_* condition bits (nfa_walk.h) -> class
+    std::vector<uint64_t> follow; // [K][m][W]
+    std::vector<uint64_t> acc;    // [K][W]
+    std::vector<int32_t> ivl_lo;  // rune intervals [ivl_lo[i], ivl_lo[i+1]) (last ends at 0x110000)
+    std::vector<uint64_t> b;      // [interval][W]
+};
+// false (and *err) when the pattern needs more than max_positions positions.
+bool BuildBitNfa(const Pattern &p, int max_positions, BitNfa *out, std::string *err);
+
 // Reference walk over the compiled tables (used by tests and by the host-side
 // table validator; the product's matching runs on the GPU).
 std::vector<uint64_t> RunDFA(const DFA &d, const uint8_t *s, size_t n);

@@ -76,6 +76,9 @@ typedef struct {
     int32_t hot_ruleset;        /* HTTP rule set staged in LDS, -1 none */
     uint32_t hot_image_bytes;
     uint32_t mc_rulesets, mc_rules, mc_dfas, mc_dfa_states;
+    uint32_t http_nfas;         /* distinct patterns on the bit-parallel NFA fallback */
+    uint32_t mc_nfas;
+    uint64_t nfa_pool_bytes;    /* their device tables */
 } l7g_stats_t;
 
 /* Engine bound to one HIP device.  err receives a message on failure.
@@ -152,6 +155,11 @@ int l7g_debug_kafka_phase_times(l7g_engine *e, uint64_t *out8, int reset);
  * error (err set).  anchored: 1 = full match, 0 = Go regexp.Match. */
 int l7g_debug_regex(const char *pat, size_t patlen, int anchored, const uint8_t *s, size_t slen, char *err,
                     size_t errlen);
+/* The same through the bit-parallel NFA fallback (the DevNfa tables and the
+ * walk the device pre-pass runs); -1 also when the pattern needs more than
+ * 1024 NFA positions. */
+int l7g_debug_regex_nfa(const char *pat, size_t patlen, int anchored, const uint8_t *s, size_t slen, char *err,
+                        size_t errlen);
 
 #ifdef __cplusplus
 }

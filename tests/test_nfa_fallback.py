@@ -1,0 +1,15 @@
+"""The bit-parallel NFA fallback at policy-compile time (CPU, host-only
+engine): rule sets whose regexes exceed the DFA state budget on their own
+compile -- none is rejected -- and the patterns go to the NFA pool."""
+import cilium_amd
+import nfa_cases
+
+
+def test_blowup_rules_compile_onto_the_nfa():
+    e = cilium_amd.Engine(-1)
+    e.update_policy(nfa_cases.policy())
+    e.set_connections(nfa_cases.conns())
+    st = e.stats()
+    assert st["http_nfas"] == 5  # PATH, HOST, TOKEN, INV, BIG; GET/PUT/POST and /static/.* stay DFAs
+    assert st["nfa_pool_bytes"] > 0
+    assert st["http_dfas"] >= 1

@@ -30,11 +30,12 @@ BAD = ["*", "a**", "a++", "(", ")", "[a", "a{2,1}", "a{1001}", "\\1", "\\8", "(?
        "\\p{Foo}", "[[:foo:]]", "\\x{110000}", "a|*", "(?P<>a)", "(?P<a-b>c)", "[z-a]", "\\", "(?i"]
 
 
+@pytest.mark.parametrize("nfa", [False, True])
 @pytest.mark.parametrize("pat,data", CURATED)
-def test_curated_product_vs_oracle(oracle, pat, data):
+def test_curated_product_vs_oracle(oracle, pat, data, nfa):
     ref = oracle.Regex(pat)
     for anchored in (True, False):
-        assert ca.debug_regex(pat, data, anchored) == ref.match(data, anchored), (pat, data, anchored)
+        assert ca.debug_regex(pat, data, anchored, nfa) == ref.match(data, anchored), (pat, data, anchored)
 
 
 @pytest.mark.parametrize("pat", BAD)
@@ -67,7 +68,8 @@ def rand_pattern(rng, depth=0):
     return s
 
 
-def test_random_product_vs_oracle(oracle):
+@pytest.mark.parametrize("nfa", [False, True])
+def test_random_product_vs_oracle(oracle, nfa):
     rng = random.Random(1234)
     checked = 0
     for _ in range(600):
@@ -82,7 +84,7 @@ def test_random_product_vs_oracle(oracle):
         for _ in range(6):
             data = b"".join(rng.choice(INPUT_CHARS) for _ in range(rng.randint(0, 8)))
             for anchored in (True, False):
-                assert ca.debug_regex(pat, data, anchored) == ref.match(data, anchored), (pat, data, anchored)
+                assert ca.debug_regex(pat, data, anchored, nfa) == ref.match(data, anchored), (pat, data, anchored)
                 checked += 1
     assert checked > 3000
 
@@ -105,3 +107,28 @@ def test_oracle_vs_python_re_ascii(oracle):
             data = bytes(rng.choice(b"abc/.1 xA_\n") for _ in range(rng.randint(0, 8)))
             assert ref.match(data, True) == bool(cre.fullmatch(data)), (pat, data)
             assert ref.match(data, False) == bool(cre.search(data)), (pat, data)
+
+
+# Patterns whose DFA explodes (the reason the NFA fallback exists): the NFA
+# agrees with the oracle's Pike VM on them, at sizes the DFA cannot reach.
+BLOWUP = ["(a|b)*a(a|b){14}", "(a|b)*a(a|b){20}", ".*a.{12}", "(?s).*x[^y]{10}z", "[ab]*a[ab]{9}\\b",
+          "(.*/)?api/v[0-9]+/.{8}", "(?m)^.*(a|\\x{FFFD}).{6}$"]
+
+
+@pytest.mark.parametrize("pat", BLOWUP)
+def test_blowup_patterns_nfa_vs_oracle(oracle, pat):
+    ref = oracle.Regex(pat)
+    rng = random.Random(hash(pat) & 0xFFFF)
+    alphabet = [b"a", b"b", b"x", b"y", b"z", b"/", b"1", "é".encode(), b"\xe2\x82", b"\n", b" "]
+    for i in range(300):
+        n = rng.randint(0, 40)
+        data = b"".join(rng.choice(alphabet) for _ in range(n))
+        if i % 3 == 0:
+            data = b"api/v1/" + data
+        for anchored in (True, False):
+            assert ca.debug_regex(pat, data, anchored, nfa=True) == ref.match(data, anchored), (pat, data, anchored)
+
+
+def test_nfa_position_limit():
+    with pytest.raises(ValueError, match="NFA positions"):
+        ca.debug_regex(".{1000}.{100}", b"", True, nfa=True)
