@@ -170,7 +170,7 @@ hipError_t Upload(l7g_engine *e) {
         size_t k_rs = Put(blob, K.rulesets), k_r = Put(blob, K.rules), k_idx = Put(blob, K.index),
                k_th = Put(blob, K.topic_hash), k_ch = Put(blob, K.client_hash), k_s = Put(blob, K.strings);
         const McImage &M = e->mc->image();
-        size_t m_rs = Put(blob, M.rulesets), m_img = Put(blob, M.images);
+        size_t m_rs = Put(blob, M.rulesets), m_img = Put(blob, M.images), m_nfa = Put(blob, M.nfa_pool);
         uint8_t *d = nullptr;
         if ((rc = hipMalloc(&d, blob.size())) != hipSuccess) return rc;
         if ((rc = hipMemcpy(d, blob.data(), blob.size(), hipMemcpyHostToDevice)) != hipSuccess) { hipFree(d); return rc; }
@@ -198,6 +198,7 @@ hipError_t Upload(l7g_engine *e) {
         MT.rulesets = (const DevRuleset *)(d + m_rs);
         MT.images = d + m_img;
         MT.nrulesets = (uint32_t)M.rulesets.size();
+        MT.nfa_pool = M.nfa_pool.empty() ? nullptr : d + m_nfa;
         e->tables_dirty = false;
     }
     if (e->conns_dirty) {
@@ -506,7 +507,8 @@ int l7g_stats(l7g_engine *e, l7g_stats_t *out) {
     out->mc_dfas = (uint32_t)M.dfas;
     out->mc_dfa_states = (uint32_t)M.dfa_states;
     out->http_nfas = (uint32_t)H.nfas;
-    out->nfa_pool_bytes = H.nfa_pool.size();
+    out->mc_nfas = (uint32_t)M.nfas;
+    out->nfa_pool_bytes = H.nfa_pool.size() + M.nfa_pool.size();
     return 0;
 }
 

@@ -236,7 +236,9 @@ struct McImgHeader {       // 64 B, at offset 0 of every memcache image
     uint32_t rule_off;     // i32[nchunks * 64]: global rule ids
     uint32_t dfa_off;      // DevDfa[ndfa] (mask rows: u64[nstates][nchunks])
     uint32_t owned_off;    // u64[ndfa][nchunks]: rules whose key predicate DFA d evaluates
-    uint32_t pad1[8];
+    uint32_t nfa_off;      // DevNfaRef[nnfa] (mask_off: u64[nchunks] rules whose predicate NFA k is)
+    uint32_t nnfa;
+    uint32_t pad1[6];
 };
 static_assert(sizeof(McImgHeader) == 64, "McImgHeader layout");
 
@@ -245,6 +247,7 @@ struct McTables {
     const uint8_t *images;
     uint32_t nrulesets;
     uint32_t pad;
+    const uint8_t *nfa_pool;   // DevNfa pool (null: no keyRegex on the NFA fallback)
 };
 
 // FNV-1a over lower-cased ASCII (header names are tchar, i.e. ASCII)

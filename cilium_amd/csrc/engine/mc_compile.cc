@@ -7,6 +7,7 @@
 
 #include "../regex/re_dfa.h"
 #include "mc_groups.h"
+#include "nfa_pool.h"
 
 namespace l7 {
 
@@ -79,7 +80,7 @@ int McCompiler::Compile(const std::vector<const McRule *> &rules, uint8_t termin
     const McGroup *groups = McGroups(&ngroups);
     std::vector<uint64_t> text((size_t)kMcTextRows * nch, 0), ops((size_t)256 * nch, 0), empty(nch, 0), nopred(nch, 0);
     // key predicates: (rule, pattern) with the effective predicate of Rule.Matches
-    struct Pat { std::unique_ptr<re::Node> own; const re::Node *ast; bool anchored; };
+    struct Pat { std::unique_ptr<re::Node> own; const re::Node *ast; bool anchored; std::string src; };
     std::vector<Pat> pats;
     std::vector<std::pair<size_t, int>> rule_pat;
     for (size_t r = 0; r < nr; r++) {
@@ -98,7 +99,7 @@ int McCompiler::Compile(const std::vector<const McRule *> &rules, uint8_t termin
             const re::Node *p = a.get();
             pats.push_back({std::move(a), p, true});
         } else if (m.key_re) {
-            pats.push_back({nullptr, m.key_re.get(), false});  // regexp.Match: unanchored
+            pats.push_back({nullptr, m.key_re.get(), false, m.key_re_src});  // regexp.Match: unanchored
         } else {
             nopred[r >> 6] |= bit(r);
             continue;
@@ -109,13 +110,14 @@ int McCompiler::Compile(const std::vector<const McRule *> &rules, uint8_t termin
     // DFAs over the key predicates, halving the pattern set until each fits
     std::vector<std::vector<int>> parts;
     std::vector<re::DFA> dfas;
+    std::vector<int> nfa_pats;
     std::function<bool(std::vector<int>)> build = [&](std::vector<int> sub) -> bool {
         std::vector<re::Pattern> ps;
         for (int p : sub) ps.push_back({pats[p].ast, pats[p].anchored});
         re::DFA d;
         std::string e;
         if (re::BuildDFA(ps, max_dfa_states, &d, &e)) { parts.push_back(sub); dfas.push_back(std::move(d)); return true; }
-        if (sub.size() == 1) { *err = "memcache key pattern too complex for the DFA budget"; return false; }
+        if (sub.size() == 1) { nfa_pats.push_back(sub[0]); return true; }  // over the budget alone: the NFA
         std::vector<int> a(sub.begin(), sub.begin() + sub.size() / 2), b(sub.begin() + sub.size() / 2, sub.end());
         return build(a) && build(b);
     };
@@ -124,7 +126,35 @@ int McCompiler::Compile(const std::vector<const McRule *> &rules, uint8_t termin
         for (size_t p = 0; p < pats.size(); p++) allp.push_back((int)p);
         if (!build(allp)) return -1;
     }
+    std::vector<std::pair<int, uint64_t>> nfas;  // (pattern, DevNfa offset)
+    for (int p : nfa_pats) {
+        std::string e;
+        auto it = nfa_cache_.find(pats[p].src);
+        if (it == nfa_cache_.end() && !pats[p].anchored) {
+            re::BitNfa nf;
+            if (re::BuildBitNfa({pats[p].ast, false}, kNfaMaxWords * 64, &nf, &e)) {
+                const uint64_t off = AppendDevNfa(nf, &img_.nfa_pool, err);
+                if (off == ~0ull) return -1;
+                it = nfa_cache_.emplace(pats[p].src, off).first;
+                img_.nfas++;
+            }
+        }
+        if (it != nfa_cache_.end()) {
+            nfas.emplace_back(p, it->second);
+            continue;
+        }
+        re::DFA d;
+        std::string e2;
+        if (!re::BuildDFA({{pats[p].ast, pats[p].anchored}}, max_single_dfa_states, &d, &e2)) {
+            *err = "memcache key pattern too complex for the device (" + e + "; DFA over " +
+                   std::to_string(max_single_dfa_states) + " states): " + pats[p].src;
+            return -1;
+        }
+        parts.push_back({p});
+        dfas.push_back(std::move(d));
+    }
     if (dfas.size() > 255) { *err = "memcache key patterns need more than 255 DFAs"; return -1; }
+    if (nfas.size() > (size_t)kMaxNfaPerRuleset) { *err = "memcache rule set needs more than 64 NFA matchers"; return -1; }
     H.ndfa = (uint8_t)dfas.size();
 
     std::vector<uint8_t> img(sizeof(McImgHeader));
@@ -143,6 +173,18 @@ int McCompiler::Compile(const std::vector<const McRule *> &rules, uint8_t termin
             if (std::find(parts[k].begin(), parts[k].end(), rp.second) != parts[k].end())
                 owned[k * nch + (rp.first >> 6)] |= bit(rp.first);
     H.owned_off = Append(img, owned.data(), owned.size());
+    {
+        std::vector<DevNfaRef> refs(nfas.size());
+        for (size_t k = 0; k < nfas.size(); k++) {
+            std::vector<uint64_t> own(nch, 0);
+            for (auto &rp : rule_pat)
+                if (rp.second == nfas[k].first) own[rp.first >> 6] |= bit(rp.first);
+            refs[k].nfa = nfas[k].second;
+            refs[k].mask_off = Append(img, own.data(), own.size());
+        }
+        H.nfa_off = Append(img, refs.data(), refs.size());
+        H.nnfa = (uint32_t)nfas.size();
+    }
     size_t states = 0;
     for (size_t k = 0; k < dfas.size(); k++) {
         const re::DFA &d = dfas[k];

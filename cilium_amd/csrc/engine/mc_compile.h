@@ -23,7 +23,8 @@ namespace l7 {
 struct McImage {
     std::vector<DevRuleset> rulesets;
     std::vector<uint8_t> images;
-    size_t rules = 0, dfas = 0, dfa_states = 0;
+    std::vector<uint8_t> nfa_pool;  // DevNfa tables of keyRegex patterns over the DFA budget
+    size_t rules = 0, dfas = 0, dfa_states = 0, nfas = 0;
 };
 
 class McCompiler {
@@ -33,11 +34,13 @@ public:
     int RulesetFor(int policy, bool ingress, uint32_t port, uint64_t remote, std::string *err);
     const McImage &image() const { return img_; }
     int max_dfa_states = 4096;
+    int max_single_dfa_states = 65535;  // a pattern the NFA cannot take (see HttpCompiler)
 
 private:
     const PolicySet *ps_;
     McImage img_;
     std::map<std::pair<std::vector<int>, int>, int> cache_;
+    std::map<std::string, uint64_t> nfa_cache_;  // keyRegex -> DevNfa offset in the pool
     int Compile(const std::vector<const McRule *> &rules, uint8_t terminal, std::string *err);
 };
 

@@ -25,6 +25,7 @@
 
 #include "../device_tables.h"
 #include "../engine/mc_groups.h"
+#include "../regex/nfa_walk.h"
 
 namespace l7 {
 
@@ -104,6 +105,8 @@ struct Image {
     const uint8_t *p;
     uint32_t nch, ndfa, terminal;
     uint32_t d0, dn;  // DFAs [d0, d0+dn) are walked in the current pass over the request
+    uint32_t nnfa;    // keyRegex matchers on the NFA fallback (evaluated in the first pass)
+    const uint8_t *nfa_pool;
 };
 
 __device__ __forceinline__ const uint64_t *u64at(const Image &I, uint32_t off) { return (const uint64_t *)(I.p + off); }
@@ -137,8 +140,24 @@ __device__ __forceinline__ void keys_step(const Image &I, Keys &K, uint32_t c) {
 
 // A key ended: AND its pass mask into K.all.  In this pass a rule passes if
 // its predicate is not evaluated by the pass's DFAs (no predicate, or another
-// pass owns it) or one of the pass's DFAs accepts the key.
-__device__ __forceinline__ void keys_end(const Image &I, Keys &K) {
+// pass owns it) or one of the pass's DFAs accepts the key.  The first pass
+// also runs the NFA-fallback matchers over the key bytes b[k0, k1): a rule
+// whose predicate one of them is fails if it rejects the key.
+__device__ __forceinline__ void keys_nfa(const Image &I, Keys &K, const uint8_t *b, uint32_t k0, uint32_t k1) {
+    const DevNfaRef *refs = (const DevNfaRef *)(I.p + hdr32(I, MC_OFF(nfa_off)));
+    for (uint32_t k = 0; k < I.nnfa; k++) {
+        const DevNfaRef ref = refs[k];
+        if (nfa_run(I.nfa_pool, ref.nfa, b + k0, k1 - k0)) continue;
+        const uint64_t *own = u64at(I, ref.mask_off);
+#pragma unroll
+        for (int c = 0; c < kMcMaxChunks; c++)
+            if ((uint32_t)c < I.nch) K.all[c] &= ~own[c];
+    }
+}
+
+template <bool kNfa>
+__device__ __forceinline__ void keys_end(const Image &I, Keys &K, const uint8_t *b, uint32_t k0, uint32_t k1) {
+    if (kNfa && I.nnfa && I.d0 == 0) keys_nfa(I, K, b, k0, k1);
     const uint64_t *owned = u64at(I, hdr32(I, MC_OFF(owned_off)));
 #pragma unroll
     for (int c = 0; c < kMcMaxChunks; c++) {
@@ -173,6 +192,9 @@ __device__ __forceinline__ void classify_cmd(const uint32_t cw[4], uint32_t clen
 // sel: this protocol's request indices (partition_kernel, mixed batches), else
 // requests 0..n-1.  answer_other: answer entries on connections that are not
 // memcached (single-protocol engines, where partition_kernel does not run).
+// kNfa: the variant that also runs NFA-fallback key matchers (launched only
+// when some memcache rule set has them; the other keeps its registers).
+template <bool kNfa>
 __global__ __launch_bounds__(kBlock) void memcache_classify_kernel(Batch B, McTables T,
                                                                    const uint32_t *__restrict__ sel,
                                                                    const uint32_t *__restrict__ sel_count,
@@ -208,6 +230,8 @@ __global__ __launch_bounds__(kBlock) void memcache_classify_kernel(Batch B, McTa
             I.terminal = (h0 >> 8) & 0xFF;
             I.ndfa = (h0 >> 16) & 0xFF;
         }
+        I.nnfa = hdr32(I, MC_OFF(nnfa));
+        I.nfa_pool = T.nfa_pool;
         const uint64_t off = B.offs[idx];
         const uint32_t len = B.lens[idx];
         const uint8_t *b = B.arena + off;
@@ -247,7 +271,7 @@ __global__ __launch_bounds__(kBlock) void memcache_classify_kernel(Batch B, McTa
                 cmdmask = u64at(I, hdr32(I, MC_OFF(op_off))) + (size_t)b[1] * I.nch;
                 Reader R{b, ~0ull, 0, 0, 0, 0};
                 for (uint32_t i = 24 + extras, e = 24 + extras + keylen; i < e; i++) keys_step(I, K, rd(R, i));
-                keys_end(I, K);
+                keys_end<kNfa>(I, K, b, 24 + extras, 24 + extras + keylen);
                 frame = (uint32_t)(body + 24u);  // uint32 arithmetic, then int()
             } else {
                 // ---- text command line
@@ -259,6 +283,7 @@ __global__ __launch_bounds__(kBlock) void memcache_classify_kernel(Batch B, McTa
                 int fr = F_NONE;
                 uint32_t cmd_id = kMcOther;
                 bool key_tok = false;         // current token is a key
+                uint32_t kstart = 0;          // its first byte
                 bool a_ok = false, a_bad = false, a_neg = false;  // strconv.Atoi(tokens[4])
                 uint32_t a_n = 0;
                 uint64_t a_v = 0;
@@ -269,7 +294,7 @@ __global__ __launch_bounds__(kBlock) void memcache_classify_kernel(Batch B, McTa
                     if (sp) {
                         if (in_tok) {  // token nt-1 ended
                             if (nt == 1) classify_cmd(cw, clen, fr, cmd_id);
-                            if (key_tok) keys_end(I, K);
+                            if (key_tok) keys_end<kNfa>(I, K, b, kstart, i);
                             in_tok = false;
                         }
                         i += sp;
@@ -280,6 +305,7 @@ __global__ __launch_bounds__(kBlock) void memcache_classify_kernel(Batch B, McTa
                         nt++;
                         key_tok = (fr == F_GET && nt >= 2) || (fr == F_GAT && nt >= 3) ||
                                   ((fr == F_STORAGE || fr == F_KEY1) && nt == 2);
+                        kstart = i;
                     }
                     if (nt == 1) {
                         if (clen < 16) cw[clen >> 2] |= c << ((clen & 3) * 8);
@@ -308,7 +334,7 @@ __global__ __launch_bounds__(kBlock) void memcache_classify_kernel(Batch B, McTa
                 }
                 if (in_tok) {
                     if (nt == 1) classify_cmd(cw, clen, fr, cmd_id);
-                    if (key_tok) keys_end(I, K);
+                    if (key_tok) keys_end<kNfa>(I, K, b, kstart, lf);
                 }
                 if (nt == 0) break;  // tokens[0] panics
                 if (fr == F_BAD) break;  // ERROR, 0
@@ -362,8 +388,12 @@ hipError_t LaunchMemcacheClassify(const Batch &B, const McTables &T, const uint3
     if (B.n == 0) return hipSuccess;
     uint32_t blocks = (B.n + kBlock - 1) / kBlock;
     if (blocks > 8192) blocks = 8192;
-    hipLaunchKernelGGL(memcache_classify_kernel, dim3(blocks), dim3(kBlock), 0, stream, B, T, sel, sel_count,
-                       answer_other ? 1u : 0u);
+    if (T.nfa_pool)
+        hipLaunchKernelGGL(memcache_classify_kernel<true>, dim3(blocks), dim3(kBlock), 0, stream, B, T, sel, sel_count,
+                           answer_other ? 1u : 0u);
+    else
+        hipLaunchKernelGGL(memcache_classify_kernel<false>, dim3(blocks), dim3(kBlock), 0, stream, B, T, sel, sel_count,
+                           answer_other ? 1u : 0u);
     return hipGetLastError();
 }
 

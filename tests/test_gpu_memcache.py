@@ -142,3 +142,52 @@ def test_cfg5_mixed_tiled_parity(engine, oracle):
     for g, r in zip(got, ref):
         assert np.array_equal(np.asarray(g).reshape(3, -1), np.broadcast_to(np.asarray(r).reshape(1, -1), (3, w.n)))
     assert w.algorithmic_bytes() < int(w.lengths.astype(np.int64).sum()) + 25 * w.n
+
+
+def mc_nfa_policy():
+    rules = [{"command": "get", "keyRegex": "(a|b)*a(a|b){14}"},
+             {"command": "delete", "keyRegex": "x[^y]{12}z"},
+             {"command": "get", "keyRegex": "^k:\\d+$"},
+             {"command": "set", "keyRegex": "é(.){10}$"}]
+    return api.policy_set(api.network_policy("mc", 1, ingress=[(gen.MC_PORT, [api.port_rule(l7proto="memcache", l7=rules)])]))
+
+
+def mc_nfa_requests(n, seed):
+    rng = np.random.default_rng(seed)
+
+    def ab(k, hit):
+        s = bytearray(rng.choice([ord("a"), ord("b")], size=k).astype(np.uint8).tobytes())
+        if k >= 15:
+            s[-15] = ord("a") if hit else ord("b")
+        return bytes(s)
+
+    reqs = []
+    for i in range(n):
+        kind = i % 5
+        if kind == 0:
+            keys = [b"pre" + ab(int(rng.integers(10, 30)), bool(rng.integers(0, 2))) for _ in range(int(rng.integers(1, 4)))]
+            reqs.append(b"get " + b" ".join(keys) + b"\r\n")
+        elif kind == 1:
+            mid = rng.choice(list(b"abyz"), size=int(rng.integers(10, 14))).astype(np.uint8).tobytes()
+            reqs.append(b"delete x" + mid + b"z\r\n")
+        elif kind == 2:
+            reqs.append(b"get k:%d" % i + (b" " + ab(20, True) if i % 3 else b"") + b"\r\n")
+        elif kind == 3:
+            key = "é".encode() + rng.choice(list(b"ab\xc3\xa9"), size=int(rng.integers(8, 14))).astype(np.uint8).tobytes()
+            reqs.append(b"set " + key + b" 0 0 1\r\nx\r\n")
+        else:  # binary GET (opcode 0)
+            reqs.append(gen.mc_bin(0, key=ab(int(rng.integers(14, 24)), bool(rng.integers(0, 2)))))
+    return reqs
+
+
+def test_memcache_nfa_fallback_parity(engine, oracle):
+    """keyRegex patterns over the DFA budget (Go regexp.Match, unanchored) run
+    as bit-parallel NFAs at each key's end; every key must match."""
+    reqs = mc_nfa_requests(6000, 11)
+    conns = gen.make_conns(2, 0, gen.MC_PORT, True, PROTO_MEMCACHE, [1, 2])
+    w = wl_from_reqs(reqs, mc_nfa_policy(), conns, np.arange(len(reqs)) % 2)
+    got, ref = both(engine, oracle, w)
+    assert_same(got, ref, w)
+    assert engine.stats()["mc_nfas"] >= 2
+    assert len(set(got[1][got[0] == ALLOW].tolist())) == 4
+    assert (got[0] == DENY).sum() > 500
