@@ -50,7 +50,7 @@ def _compile(src, obj, newest_header, defines=()):
     if src.endswith(".hip"):
         cmd = [HIPCC] + COMMON + HIP_FLAGS + list(defines) + ["-c", src, "-o", obj]
     else:  # host-only C++: plain g++ against the HIP runtime headers
-        cmd = ["g++"] + COMMON + ["-I/opt/rocm/include", "-D__HIP_PLATFORM_AMD__", "-c", src, "-o", obj]
+        cmd = ["g++"] + COMMON + ["-I/opt/rocm/include", "-D__HIP_PLATFORM_AMD__"] + list(defines) + ["-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")

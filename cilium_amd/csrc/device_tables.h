@@ -196,6 +196,20 @@ struct DevStrSlot {        // 16 B open-addressing slot (topics, client ids)
     uint16_t used;
     int32_t id;
 };
+// Topic / client-id hash of the Kafka string tables (host compiler and
+// kernel): the string's 32-bit little-endian words, the last one zero-padded,
+// then its length.  Strings sit 4-byte aligned and zero-padded in `strings`,
+// so the kernel compares them a word at a time.
+constexpr uint32_t kWHashSeed = 0x811C9DC5u;
+L7_HD inline uint32_t l7_whash_step(uint32_t h, uint32_t w) {
+    h = (h ^ w) * 0x9E3779B1u;
+    return h ^ (h >> 15);
+}
+L7_HD inline uint32_t l7_whash_final(uint32_t h, uint32_t n) {
+    h = (h ^ n) * 0x85EBCA6Bu;
+    return h ^ (h >> 13);
+}
+
 struct KafkaTables {
     const DevKafkaRuleset *rulesets;
     const DevKafkaRule *rules;

@@ -5,9 +5,13 @@
 namespace l7 {
 
 uint32_t KafkaStrHash(const uint8_t *s, size_t n) {
-    uint32_t h = kFnvBasis;
-    for (size_t i = 0; i < n; i++) h = (h ^ s[i]) * 16777619u;
-    return h;
+    uint32_t h = kWHashSeed;
+    for (size_t i = 0; i < n; i += 4) {
+        uint32_t w = 0;
+        for (size_t k = 0; k < 4 && i + k < n; k++) w |= (uint32_t)s[i + k] << (8 * k);
+        h = l7_whash_step(h, w);
+    }
+    return l7_whash_final(h, (uint32_t)n);
 }
 
 namespace {
@@ -30,8 +34,10 @@ void BuildHash(const std::unordered_map<std::string, int> &ids, std::vector<uint
         d.len = (uint16_t)s.size();
         d.used = 1;
         d.id = (int32_t)id;
+        strings.resize((strings.size() + 3) & ~(size_t)3, 0);  // 4-byte aligned, zero-padded
         d.str_off = (uint32_t)strings.size();
         strings.insert(strings.end(), s.begin(), s.end());
+        strings.resize((strings.size() + 3) & ~(size_t)3, 0);
     }
 }
 }  // namespace

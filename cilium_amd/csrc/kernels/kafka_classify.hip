@@ -19,6 +19,7 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr uint32_t kMaxParseBuf = 6553500;
+constexpr int kCrcSlices = 8;
 constexpr uint32_t kInf = 0xFFFFFFFFu;
 
 // Per-lane byte cursor: the decoders walk their request forward, so each lane
@@ -76,7 +77,23 @@ __device__ __forceinline__ uint32_t kread(KDec &d, uint32_t n) {
     if (take < n) d.err = 2;
     return at;
 }
+// Big-endian n-byte field (n = 1, 2, 4 or 8).  A field inside the cached
+// 16-byte chunk is cut out of two adjacent words (v_alignbyte) and byte-
+// swapped (v_perm); one straddling two chunks is read byte by byte.
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_amdgcn_perm(0, x, 0x00010203u); }
 __device__ __forceinline__ uint64_t be_load(Cur &c, const uint8_t *p, int n) {
+    const uintptr_t a = (uintptr_t)p;
+    const uint32_t k = (uint32_t)(a & 15);
+    if (n <= 4 && k + (uint32_t)n <= 16) {
+        cur_fill(c, a);
+        const uint32_t w0 = c.w0, w1 = c.w1, w2 = c.w2, w3 = c.w3;
+        const uint32_t i = k >> 2;
+        const uint32_t lo = i == 0 ? w0 : i == 1 ? w1 : i == 2 ? w2 : w3;
+        const uint32_t hi = i == 0 ? w1 : i == 1 ? w2 : i == 2 ? w3 : 0u;
+        const uint32_t v = bswap32(__builtin_amdgcn_alignbyte(hi, lo, k & 3));  // bytes k..k+3, big-endian
+        return n == 4 ? v : v >> (32 - 8 * n);
+    }
+    if (n == 8) return (be_load(c, p, 4) << 32) | be_load(c, p + 4, 4);
     uint64_t v = 0;
     for (int i = 0; i < n; i++) v = (v << 8) | cur_byte(c, p + i);
     return v;
@@ -87,6 +104,11 @@ __device__ __forceinline__ int64_t dec_int(KDec &d, int n) {
     if (d.err) return 0;
     uint64_t v = be_load(*d.c, d.b + at, n);
     return n == 1 ? (int64_t)(int8_t)v : n == 2 ? (int64_t)(int16_t)v : n == 4 ? (int64_t)(int32_t)v : (int64_t)v;
+}
+// A field whose value is not needed: only the read (and its errors) matter.
+__device__ __forceinline__ void dec_skip(KDec &d, int n) {
+    if (d.err) return;
+    kread(d, (uint32_t)n);
 }
 // DecodeString -> (off, len); len < 1 => ""
 __device__ __forceinline__ void dec_string(KDec &d, uint32_t &off, uint32_t &len) {
@@ -160,7 +182,7 @@ __device__ __forceinline__ int read_message_set(Cur &cur, const uint8_t *b, uint
     KDec dec{b, pos, end, size, 0, &cur};
     int rc = 0;
     for (;;) {
-        (void)dec_int(dec, 8);
+        dec_skip(dec, 8);
         if (dec.err) break;
         int32_t msize = (int32_t)dec_int(dec, 4);
         if (dec.err || msize <= 0) break;
@@ -171,9 +193,9 @@ __device__ __forceinline__ int read_message_set(Cur &cur, const uint8_t *b, uint
         uint32_t crc = (uint32_t)dec_int(md, 4);
         if (msize <= 4) break;
         if (crc != crc32_ieee(crctab, cur, b + at + 4, (uint32_t)msize - 4)) break;  // stop, no drain
-        (void)dec_int(md, 1);
+        dec_skip(md, 1);
         int8_t attr = (int8_t)dec_int(md, 1);
-        if (version >= 1) (void)dec_int(md, 8);
+        if (version >= 1) dec_skip(md, 8);
         int codec = attr & 3;
         if (codec == 3) break;  // `return nil, err` with err == nil
         dec_bytes(md);
@@ -185,18 +207,47 @@ __device__ __forceinline__ int read_message_set(Cur &cur, const uint8_t *b, uint
     return rc;
 }
 
+// 4 bytes at p as a little-endian word (bytes past a string's end are masked
+// off by the caller)
+__device__ __forceinline__ uint32_t le_load4(Cur &c, const uint8_t *p) {
+    const uintptr_t a = (uintptr_t)p;
+    const uint32_t k = (uint32_t)(a & 15);
+    if (k <= 12) {
+        cur_fill(c, a);
+        const uint32_t w0 = c.w0, w1 = c.w1, w2 = c.w2, w3 = c.w3;
+        const uint32_t i = k >> 2;
+        const uint32_t lo = i == 0 ? w0 : i == 1 ? w1 : i == 2 ? w2 : w3;
+        const uint32_t hi = i == 0 ? w1 : i == 1 ? w2 : i == 2 ? w3 : 0u;
+        return __builtin_amdgcn_alignbyte(hi, lo, k & 3);
+    }
+    uint32_t v = 0;
+    for (int i = 0; i < 4; i++) v |= cur_byte(c, p + i) << (8 * i);
+    return v;
+}
+
+// Interned id of the request string s[0, n) (topic or client id), -1 if the
+// rule tables do not know it: word hash (l7_whash_*), linear probing, then a
+// word-wise compare against the 4-byte aligned, zero-padded table string.
 __device__ __forceinline__ int32_t str_lookup(const DevStrSlot *tab, uint32_t mask, const uint8_t *strings, Cur &cur,
-                              const uint8_t *s, uint32_t n) {
-    uint32_t h = kFnvBasis;
-    for (uint32_t i = 0; i < n; i++) h = (h ^ cur_byte(cur, s + i)) * 16777619u;
+                                              const uint8_t *s, uint32_t n) {
+    uint32_t h = kWHashSeed;
+    for (uint32_t i = 0; i < n; i += 4) {
+        const uint32_t r = n - i;
+        const uint32_t keep = r >= 4 ? 0xFFFFFFFFu : (1u << (8 * r)) - 1u;
+        h = l7_whash_step(h, le_load4(cur, s + i) & keep);
+    }
+    h = l7_whash_final(h, n);
     for (uint32_t slot = h & mask;; slot = (slot + 1) & mask) {
         const DevStrSlot e = tab[slot];
         if (!e.used) return -1;
         if (e.hash == h && e.len == n) {
+            const uint32_t *t = reinterpret_cast<const uint32_t *>(strings + e.str_off);
             bool eq = true;
-            Cur tc;
-            tc.line = ~(uintptr_t)0;
-            for (uint32_t i = 0; i < n && eq; i++) eq = cur_byte(tc, strings + e.str_off + i) == cur_byte(cur, s + i);
+            for (uint32_t i = 0; i < n && eq; i += 4) {
+                const uint32_t r = n - i;
+                const uint32_t keep = r >= 4 ? 0xFFFFFFFFu : (1u << (8 * r)) - 1u;
+                eq = t[i >> 2] == (le_load4(cur, s + i) & keep);
+            }
             if (eq) return e.id;
         }
     }
@@ -267,7 +318,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
     const DevConn *__restrict__ conns = B.conns;
     uint64_t *__restrict__ counters = B.counters;
     static_assert(kBlock == 256, "one CRC table entry per thread");
-    __shared__ uint32_t crctab[8 * 256];
+    __shared__ uint32_t crctab[kCrcSlices * 256];
     __shared__ uint32_t s_verdicts[8];
     {
         const uint32_t t = threadIdx.x;
@@ -276,7 +327,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
         crctab[t] = c;
         if (t < 8) s_verdicts[t] = 0;
         __syncthreads();
-        for (int k = 1; k < 8; k++) {
+        for (int k = 1; k < kCrcSlices; k++) {
             const uint32_t prev = crctab[(k - 1) * 256 + t];
             crctab[k * 256 + t] = (prev >> 8) ^ crctab[prev & 0xFF];
             __syncthreads();
@@ -336,9 +387,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
             if (q.typed) {
                 KDec d{b, 0, rawlen, -1, 0, &cur};
                 bool bad = false;
-                (void)dec_int(d, 4); (void)dec_int(d, 2);
+                dec_skip(d, 4); dec_skip(d, 2);
                 const int16_t ver = (int16_t)dec_int(d, 2);
-                (void)dec_int(d, 4);
+                dec_skip(d, 4);
                 uint32_t co, cl;
                 dec_string(d, co, cl);
                 if (!d.err && cl > 0) q.client = str_lookup(T.client_hash, T.client_mask, T.strings, cur, b + co, cl);
@@ -356,7 +407,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                 switch (q.kind) {
                 case 0:  // Produce
                     if (ver >= 3) dec_string(d, o, l);
-                    (void)dec_int(d, 2); (void)dec_int(d, 4);
+                    dec_skip(d, 2); dec_skip(d, 4);
                     nt = dec_arraylen(d, false, bad);
                     if (bad) { rc = -1; break; }
                     for (int64_t t = 0; t < nt && rc == 0; t++) {
@@ -366,7 +417,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                         np = dec_arraylen(d, false, bad);
                         if (bad) { rc = -1; break; }
                         for (int64_t p = 0; p < np; p++) {
-                            (void)dec_int(d, 4);
+                            dec_skip(d, 4);
                             if (d.err) { rc = -1; break; }
                             const int32_t ss = (int32_t)dec_int(d, 4);
                             if (d.err) { rc = -1; break; }
@@ -376,9 +427,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                     }
                     break;
                 case 1:  // Fetch
-                    (void)dec_int(d, 4); (void)dec_int(d, 4); (void)dec_int(d, 4);
-                    if (ver >= 3) (void)dec_int(d, 4);
-                    if (ver >= 4) (void)dec_int(d, 1);
+                    dec_skip(d, 4); dec_skip(d, 4); dec_skip(d, 4);
+                    if (ver >= 3) dec_skip(d, 4);
+                    if (ver >= 4) dec_skip(d, 1);
                     nt = dec_arraylen(d, false, bad);
                     if (bad) { rc = -1; break; }
                     for (int64_t t = 0; t < nt && !d.err; t++) {
@@ -387,15 +438,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                         np = dec_arraylen(d, false, bad);
                         if (bad) { rc = -1; break; }
                         for (int64_t p = 0; p < np && !d.err; p++) {
-                            (void)dec_int(d, 4); (void)dec_int(d, 8);
-                            if (ver >= 5) (void)dec_int(d, 8);
-                            (void)dec_int(d, 4);
+                            dec_skip(d, 4); dec_skip(d, 8);
+                            if (ver >= 5) dec_skip(d, 8);
+                            dec_skip(d, 4);
                         }
                     }
                     break;
                 case 2:  // Offset
-                    (void)dec_int(d, 4);
-                    if (ver >= 2) (void)dec_int(d, 1);
+                    dec_skip(d, 4);
+                    if (ver >= 2) dec_skip(d, 1);
                     nt = dec_arraylen(d, false, bad);
                     if (bad) { rc = -1; break; }
                     for (int64_t t = 0; t < nt && !d.err; t++) {
@@ -404,8 +455,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                         np = dec_arraylen(d, false, bad);
                         if (bad) { rc = -1; break; }
                         for (int64_t p = 0; p < np && !d.err; p++) {
-                            (void)dec_int(d, 4); (void)dec_int(d, 8);
-                            if (ver == 0) (void)dec_int(d, 4);
+                            dec_skip(d, 4); dec_skip(d, 8);
+                            if (ver == 0) dec_skip(d, 4);
                         }
                     }
                     break;
@@ -413,12 +464,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                     nt = dec_arraylen(d, true, bad);
                     if (bad) { rc = -1; break; }
                     for (int64_t t = 0; t < nt && !d.err; t++) { dec_string(d, o, l); if (!d.err) on_topic(o, l); }
-                    if (ver >= 4) (void)dec_int(d, 1);
+                    if (ver >= 4) dec_skip(d, 1);
                     break;
                 case 8:  // OffsetCommit
                     dec_string(d, o, l);
-                    if (ver >= 1) { (void)dec_int(d, 4); dec_string(d, o, l); }
-                    if (ver >= 2) (void)dec_int(d, 8);
+                    if (ver >= 1) { dec_skip(d, 4); dec_string(d, o, l); }
+                    if (ver >= 2) dec_skip(d, 8);
                     nt = dec_arraylen(d, false, bad);
                     if (bad) { rc = -1; break; }
                     for (int64_t t = 0; t < nt && !d.err; t++) {
@@ -427,8 +478,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                         np = dec_arraylen(d, false, bad);
                         if (bad) { rc = -1; break; }
                         for (int64_t p = 0; p < np && !d.err; p++) {
-                            (void)dec_int(d, 4); (void)dec_int(d, 8);
-                            if (ver == 1) (void)dec_int(d, 8);
+                            dec_skip(d, 4); dec_skip(d, 8);
+                            if (ver == 1) dec_skip(d, 8);
                             uint32_t o2, l2;
                             dec_string(d, o2, l2);
                         }
@@ -443,12 +494,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                         on_topic(o, l);
                         np = dec_arraylen(d, false, bad);
                         if (bad) { rc = -1; break; }
-                        for (int64_t p = 0; p < np && !d.err; p++) (void)dec_int(d, 4);
+                        for (int64_t p = 0; p < np && !d.err; p++) dec_skip(d, 4);
                     }
                     break;
                 case 10:  // ConsumerMetadata
                     dec_string(d, o, l);
-                    if (ver >= 1) (void)dec_int(d, 1);
+                    if (ver >= 1) dec_skip(d, 1);
                     break;
                 }
                 if (rc == 0 && d.err) rc = -1;

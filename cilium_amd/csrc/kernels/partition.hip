@@ -5,10 +5,11 @@
 // stream (cfg5) most of their lanes would only discover "not my protocol" and
 // idle while the others decode.  This kernel writes, for each of those two
 // protocols, the list of request indices that belong to it; the classifiers
-// then walk only their own list.  Kafka requests are further grouped by length
-// class, so a wave of the one-lane-per-request Kafka kernel holds requests of
-// similar size and no longer waits on one long produce request among short
-// fetches (a wave runs as long as its longest lane).  One block owns 4096 consecutive requests
+// then walk only their own list.  Kafka requests are further grouped by kind
+// and length class, so a wave of the one-lane-per-request Kafka kernel holds
+// requests that take the same decode path for about as long, and no longer
+// waits on one long produce request among short fetches (a wave runs as long
+// as its longest lane, and divergent paths run one after the other).  One block owns 4096 consecutive requests
 // (16 per lane, protocol kept in registers between the count and the write
 // pass) and takes its slot range with one atomic per protocol.
 #include <hip/hip_runtime.h>
@@ -26,10 +27,15 @@ constexpr int kKafkaClasses = L7_KAFKA_CLASSES;
 constexpr int kClasses = kKafkaClasses + 1;
 
 static_assert(kKafkaClasses == 1 || kKafkaClasses == 8, "length classes");
-__device__ __forceinline__ uint8_t kafka_class(uint32_t len) {
+// Kafka list class: the decode path a lane takes is set by the request kind
+// and, for produce, by how many message bytes it hashes, so fetch requests,
+// the other kinds, and produce requests by length each get lists of their own.
+__device__ __forceinline__ uint8_t kafka_class(const uint8_t *b, uint32_t len) {
     if (kKafkaClasses == 1) return 0;
-    return len < 192 ? 0 : len < 384 ? 1 : len < 640 ? 2 : len < 896 ? 3 : len < 1280 ? 4 : len < 2048 ? 5
-         : len < 4096 ? 6 : 7;
+    const uint32_t kind = len >= 6 ? (uint32_t)b[4] << 8 | b[5] : 0xFFFF;
+    if (kind == 1) return 0;
+    if (kind != 0) return 1;
+    return len < 384 ? 2 : len < 640 ? 3 : len < 896 ? 4 : len < 1280 ? 5 : len < 2048 ? 6 : 7;
 }
 }  // namespace
 
@@ -56,7 +62,11 @@ __global__ __launch_bounds__(kBlock) void partition_kernel(Batch B, uint32_t *__
         if (idx < n) {
             const uint32_t ci = B.conn_ids[idx];
             const uint8_t proto = ci < B.nconns ? B.conns[ci].proto : PROTO_NONE;
-            if (proto == PROTO_KAFKA) cls = 1 + kafka_class(B.lens[idx]);
+            if (proto == PROTO_KAFKA) {
+                const uint32_t len = B.lens[idx];
+                const uint64_t off = B.offs[idx];
+                cls = 1 + kafka_class(B.arena + off, l7_in_arena(off, len, B.arena_len) ? len : 0);
+            }
             else if (proto == PROTO_MEMCACHE) cls = 1 + kKafkaClasses;
             else if (proto != PROTO_HTTP) {
                 B.verdict[idx] = V_UNSUPPORTED;
