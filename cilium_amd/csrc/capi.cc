@@ -25,6 +25,9 @@ hipError_t LaunchKafkaClassify(const Batch &B, const KafkaTables &T, const uint3
                                bool answer_other, hipStream_t stream);
 hipError_t LaunchMemcacheClassify(const Batch &B, const McTables &T, const uint32_t *sel, const uint32_t *sel_count,
                                   bool answer_other, hipStream_t stream);
+hipError_t LaunchCounters(const uint8_t *verdict, const int32_t *rule, uint32_t n, uint32_t nrules,
+                          uint64_t *counters, uint32_t *scratch, hipStream_t stream);
+size_t CountersScratchBytes();
 hipError_t LaunchHttpNfa(const Batch &B, const HttpTables &T, hipStream_t stream);
 hipError_t LaunchPartition(const Batch &B, uint32_t *sel_kafka, uint32_t *sel_mc, uint32_t *counts, hipStream_t stream);
 hipError_t HttpPhaseTimes(uint64_t *out, bool reset);
@@ -64,6 +67,8 @@ struct l7g_engine {
     // NFA pre-pass results, u64 per request (grow-only, stream-ordered as d_sel)
     uint64_t *d_nfa = nullptr;
     size_t nfa_cap = 0;
+    // counter histogram scratch (kernels/counters.hip), allocated on first use
+    uint32_t *d_hist = nullptr;
     // Completion of the last l7g_classify's kernels (recorded on the caller's
     // stream).  The engine waits on it -- never on the caller's stream, which
     // may be gone by then -- before it rewrites or frees anything a launched
@@ -263,6 +268,7 @@ void l7g_engine_destroy(l7g_engine *e) {
     if (e->d_conns) hipFree(e->d_conns);
     if (e->d_sel) hipFree(e->d_sel);
     if (e->d_nfa) hipFree(e->d_nfa);
+    if (e->d_hist) hipFree(e->d_hist);
     if (e->done_ev) hipEventDestroy(e->done_ev);
     for (hipEvent_t ev : e->prof_ev)
         if (ev) hipEventDestroy(ev);
@@ -363,10 +369,8 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
     B.verdict = verdict;
     B.rule = rule;
     B.consumed = consumed;
-    B.counters = counters;
     B.n = n;
     B.nconns = (uint32_t)e->conns.size();
-    B.ncounters = counters ? (uint32_t)e->ps->nrules + 8 : 0;
     if (n == 0) return 0;
     // The kernels each classify only their own protocol's requests, so a
     // mixed batch needs one launch per protocol present.  When the engine
@@ -436,6 +440,16 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
     if (rc == hipSuccess && run[3])
         rc = LaunchMemcacheClassify(B, e->mt, sel_m, cnt ? cnt + L7_KAFKA_CLASSES : nullptr, !partitioned, s);
     mark(4);
+    // per-rule allow hits and per-verdict totals, from the outputs
+    if (rc == hipSuccess && counters) {
+        if (!e->d_hist) {
+            if (e->launched) rc = hipStreamWaitEvent(s, e->done_ev, 0);
+            if (rc == hipSuccess) rc = hipMalloc(&e->d_hist, CountersScratchBytes());
+        } else if (e->launched && !partitioned && !nfa) {
+            rc = hipStreamWaitEvent(s, e->done_ev, 0);  // the scratch may still be read by the previous call
+        }
+        if (rc == hipSuccess) rc = LaunchCounters(verdict, rule, n, (uint32_t)e->ps->nrules, counters, e->d_hist, s);
+    }
     if (rc == hipSuccess) rc = hipEventRecord(e->done_ev, s);
     if (rc == hipSuccess) e->launched = true;
     return (int)rc;

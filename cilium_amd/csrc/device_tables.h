@@ -37,8 +37,8 @@ struct DevConn {
 
 // One l7g_classify call as the kernels see it (passed by value): request i is
 // arena[offs[i] .. offs[i] + lens[i]) on connection conn_ids[i]; outputs are
-// indexed by i.  counters (may be null) = u64[ncounters]: per-rule allow hits,
-// then 8 per-verdict totals.
+// indexed by i.  (The call's counters are histogrammed from verdict / rule
+// after the classifiers: kernels/counters.hip.)
 struct Batch {
     const uint8_t *arena;
     uint64_t arena_len;
@@ -49,8 +49,7 @@ struct Batch {
     uint8_t *verdict;
     int32_t *rule;
     uint32_t *consumed;
-    uint64_t *counters;
-    uint32_t n, nconns, ncounters, pad;
+    uint32_t n, nconns;
 };
 
 // A request whose bytes leave [arena, arena + arena_len) is out of contract:
@@ -73,7 +72,7 @@ L7_HD inline bool l7_in_arena(uint64_t off, uint32_t len, uint64_t arena_len) {
 // rules whose matcher on that slot holds if the value ends in that state.
 constexpr int kChunksPerPass = 4;       // chunk accumulators the kernel keeps in registers
 constexpr int kDfasPerPass = 1;         // DFAs per slot walked in one framing pass
-constexpr uint32_t kLdsImageBytes = 28 * 1024;  // LDS budget for the hot rule-set image
+constexpr uint32_t kLdsImageBytes = 32 * 1024;  // LDS budget for the hot rule-set image
 
 // Header-name recognition: every image carries a small DFA over the
 // lower-cased name bytes that spells out the names the framer must know

@@ -1,0 +1,97 @@
+// Per-rule allow hits and per-verdict totals of one l7g_classify call
+// (product code), counted after the classifiers from their outputs.
+//
+// The classifiers used to bump the counters themselves: one device-scope
+// atomic per allowed request on its rule's counter.  Device-scope atomics on
+// MI355X are performed past the (per-XCD, non-coherent) L2s, and a few
+// thousand hot counters shared by every CU serialise there: on the 100M-entry
+// mixed stream they cost ~15 ms per call, more than the Kafka kernel.  Here
+// the outputs are re-read once (5 B per request, streamed) instead:
+//   1. histogram_kernel: each workgroup histograms a contiguous slice of
+//      rule[] into LDS (u32 bins; verdicts through wave ballots, not atomics)
+//      and stores its bins to a [workgroup][bin] scratch matrix -- plain,
+//      coalesced stores, no global atomics;
+//   2. reduce_kernel: one thread per bin sums its column and adds the sum to
+//      the caller's u64 counter (one writer per counter, stream-ordered).
+// Rule sets with more bins than fit in LDS are counted in bin ranges, one
+// histogram pass per range.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "../device_tables.h"
+
+namespace l7 {
+
+namespace {
+
+constexpr int kHistBlock = 1024;
+constexpr uint32_t kHistBins = 16384;  // u32 bins per LDS pass (64 KiB)
+constexpr uint32_t kHistBlocks = 256;  // workgroups (one per CU)
+
+// rule bins [lo, lo + nb) of this pass; verdict bins counted only when lo == 0
+__global__ __launch_bounds__(kHistBlock) void histogram_kernel(const uint8_t *__restrict__ verdict,
+                                                               const int32_t *__restrict__ rule, uint32_t n,
+                                                               uint32_t lo, uint32_t nb, uint32_t *__restrict__ scratch,
+                                                               uint32_t stride) {
+    __shared__ uint32_t bins[kHistBins + 8];
+    for (uint32_t i = threadIdx.x; i < nb + 8; i += kHistBlock) bins[i] = 0;
+    __syncthreads();
+    const uint32_t per = (n + gridDim.x - 1) / gridDim.x;
+    const uint32_t b0 = blockIdx.x * per, b1 = min(n, b0 + per);
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t vc[5] = {0, 0, 0, 0, 0};
+    for (uint32_t i0 = b0; i0 < b1; i0 += kHistBlock) {
+        const uint32_t i = i0 + threadIdx.x;
+        const bool in = i < b1;
+        const int32_t r = in ? rule[i] : -1;
+        if ((uint32_t)(r - (int32_t)lo) < nb) atomicAdd(&bins[r - lo], 1u);
+        if (lo == 0) {
+            const uint32_t v = in ? verdict[i] : 0xFF;
+#pragma unroll
+            for (uint32_t k = 0; k < 5; k++) vc[k] += (uint32_t)__popcll(__ballot(v == k));
+        }
+    }
+    if (lo == 0 && lane == 0)
+        for (uint32_t k = 0; k < 5; k++)
+            if (vc[k]) atomicAdd(&bins[nb + k], vc[k]);
+    __syncthreads();
+    uint32_t *dst = scratch + (size_t)blockIdx.x * stride;
+    for (uint32_t i = threadIdx.x; i < nb + 8; i += kHistBlock) dst[i] = bins[i];
+}
+
+__global__ void reduce_kernel(const uint32_t *__restrict__ scratch, uint32_t nblocks, uint32_t stride, uint32_t lo,
+                              uint32_t nb, uint32_t nrules, uint64_t *__restrict__ counters) {
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool verdict_bin = lo == 0 && b >= nb && b < nb + 8;
+    if (b >= nb && !verdict_bin) return;
+    uint64_t s = 0;
+    for (uint32_t k = 0; k < nblocks; k++) s += scratch[(size_t)k * stride + b];
+    if (!s) return;
+    if (verdict_bin) counters[nrules + (b - nb)] += s;
+    else counters[lo + b] += s;
+}
+
+}  // namespace
+
+// Bytes of scratch LaunchCounters needs.
+size_t CountersScratchBytes() { return (size_t)kHistBlocks * (kHistBins + 8) * sizeof(uint32_t); }
+
+// counters: u64[nrules + 8] (rules, then verdicts), accumulated into.
+hipError_t LaunchCounters(const uint8_t *verdict, const int32_t *rule, uint32_t n, uint32_t nrules,
+                          uint64_t *counters, uint32_t *scratch, hipStream_t stream) {
+    if (n == 0 || !counters) return hipSuccess;
+    const uint32_t nblocks = std::min<uint32_t>(kHistBlocks, (n + kHistBlock - 1) / kHistBlock);
+    const uint32_t stride = kHistBins + 8;
+    for (uint32_t lo = 0; lo == 0 || lo < nrules; lo += kHistBins) {
+        const uint32_t nb = std::min<uint32_t>(kHistBins, nrules - lo);
+        hipLaunchKernelGGL(histogram_kernel, dim3(nblocks), dim3(kHistBlock), 0, stream, verdict, rule, n, lo, nb,
+                           scratch, stride);
+        const uint32_t nbins = nb + (lo == 0 ? 8 : 0);
+        hipLaunchKernelGGL(reduce_kernel, dim3((nbins + 255) / 256), dim3(256), 0, stream, scratch, nblocks, stride,
+                           lo, nb, nrules, counters);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace l7

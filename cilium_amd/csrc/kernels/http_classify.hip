@@ -32,7 +32,7 @@
 // values stop being walked once their DFA state is absorbing.
 //
 // One 512-thread workgroup per CU: 8 waves x 16 KiB windows + the hot rule
-// set's image (<= 28 KiB) + rule counters = 160 KiB of LDS.
+// set's image (<= 32 KiB) = 160 KiB of LDS.
 //
 // Grammar, error precedence and policy semantics: Envoy's HTTP/1 codec +
 // cilium.l7policy (envoy/cilium_l7policy.cc:127-182,
@@ -61,10 +61,8 @@ constexpr int kBlock = 64 * kWaves;
 constexpr uint32_t kWin = L7G_HTTP_WIN;        // bytes per lane window
 constexpr uint32_t kWinChunks = kWin / 16;
 constexpr uint32_t kWaveLds = 64 * kWin;       // 16 KiB per wave
-constexpr int kLdsRuleCounters = 1016;
 constexpr uint32_t kOffImg = kWaves * kWaveLds;
-constexpr uint32_t kOffCnt = kOffImg + kLdsImageBytes;
-constexpr uint32_t kLdsBytes = kOffCnt + (8 + kLdsRuleCounters) * 4;
+constexpr uint32_t kLdsBytes = kOffImg + kLdsImageBytes;
 static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
 constexpr uint32_t kLanesPerWin = kWinChunks;  // DMA: one lane per 16-byte chunk of a window
 constexpr uint32_t kWinPerInst = 64 / kLanesPerWin;
@@ -977,9 +975,6 @@ struct Out {
     uint8_t *verdict;
     int32_t *rule;
     uint32_t *consumed;
-    uint32_t *s_cnt;
-    uint64_t *counters;
-    uint32_t nrules;
     const uint64_t *nfa_bits;  // NFA pre-pass results (HttpTables::nfa_bits)
 };
 
@@ -987,13 +982,6 @@ __device__ __forceinline__ void emit(const Lane &L, const Out &O) {
     O.verdict[L.idx] = L.verdict;
     O.rule[L.idx] = L.rule;
     O.consumed[L.idx] = L.consumed;
-    if (O.counters) {
-        atomicAdd(&O.s_cnt[L.verdict], 1u);
-        if (L.rule >= 0 && (uint32_t)L.rule < O.nrules) {
-            if (L.rule < kLdsRuleCounters) atomicAdd(&O.s_cnt[8 + L.rule], 1u);
-            else atomicAdd((unsigned long long *)&O.counters[L.rule], 1ull);
-        }
-    }
 }
 
 // All rounds of one tile.
@@ -1062,29 +1050,24 @@ template <bool kHot>
 __global__ __launch_bounds__(kBlock) void http_classify_kernel(Batch B, HttpTables T, uint32_t answer_other) {
     const uint8_t *__restrict__ arena = B.arena;
     const uint32_t n = B.n, nconns = B.nconns;
-    uint64_t *__restrict__ counters = B.counters;
-    const uint32_t ncounters = B.ncounters;
     __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63, wave = tid >> 6;
     uint8_t *s_img = lds + kOffImg;
-    uint32_t *s_cnt = (uint32_t *)(lds + kOffCnt);
 
     const int32_t hot = T.hot_ruleset;
     const bool hot_ok = hot >= 0 && (uint32_t)hot < T.nrulesets && T.rulesets[hot].image_len <= kLdsImageBytes;
     if (kHot && !hot_ok) return;
-    // stage the hot rule set's image; zero the counters
+    // stage the hot rule set's image
     if (kHot) {
         const DevRuleset r = T.rulesets[hot];
         const uint4 *src = (const uint4 *)(T.images + r.image_off);
         const uint32_t n16 = (r.image_len + 15) / 16;
         for (uint32_t i = tid; i < n16; i += kBlock) ((uint4 *)s_img)[i] = src[i];
     }
-    if (counters)
-        for (uint32_t i = tid; i < 8 + kLdsRuleCounters; i += kBlock) s_cnt[i] = 0;
     __syncthreads();
 
-    const Out O{B.verdict, B.rule, B.consumed, s_cnt, counters, ncounters > 8 ? ncounters - 8 : 0, T.nfa_bits};
+    const Out O{B.verdict, B.rule, B.consumed, T.nfa_bits};
     uint8_t *wave_lds = lds + wave * kWaveLds;
     const uint32_t ntiles = (n + 63) / 64;
     for (uint32_t tile = blockIdx.x * kWaves + wave; tile < ntiles; tile += gridDim.x * kWaves) {
@@ -1125,16 +1108,6 @@ __global__ __launch_bounds__(kBlock) void http_classify_kernel(Batch B, HttpTabl
             }
         }
         run_tile<kHot>(L, img, wave_lds, lane, O);
-    }
-    if (counters) {
-        __syncthreads();
-        const uint32_t nrules = O.nrules;
-        for (uint32_t i = tid; i < 8 + kLdsRuleCounters; i += kBlock) {
-            const uint32_t v = s_cnt[i];
-            if (!v) continue;
-            if (i < 8) atomicAdd((unsigned long long *)&counters[nrules + i], (unsigned long long)v);
-            else if (i - 8 < nrules) atomicAdd((unsigned long long *)&counters[i - 8], (unsigned long long)v);
-        }
     }
 }
 

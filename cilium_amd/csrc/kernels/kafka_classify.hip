@@ -312,20 +312,17 @@ __device__ __forceinline__ uint32_t topic_first(const KafkaTables &T, const DevK
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) void kafka_classify_kernel(
     Batch B, KafkaTables T, const uint32_t *__restrict__ sel, const uint32_t *__restrict__ sel_count,
     uint32_t answer_other) {
-    const uint32_t n = B.n, nconns = B.nconns, ncounters = B.ncounters;
+    const uint32_t n = B.n, nconns = B.nconns;
     const uint8_t *__restrict__ arena = B.arena;
     const uint32_t *__restrict__ conn_ids = B.conn_ids;
     const DevConn *__restrict__ conns = B.conns;
-    uint64_t *__restrict__ counters = B.counters;
     static_assert(kBlock == 256, "one CRC table entry per thread");
     __shared__ uint32_t crctab[kCrcSlices * 256];
-    __shared__ uint32_t s_verdicts[8];
     {
         const uint32_t t = threadIdx.x;
         uint32_t c = t;
         for (int k = 0; k < 8; k++) c = (c & 1) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
         crctab[t] = c;
-        if (t < 8) s_verdicts[t] = 0;
         __syncthreads();
         for (int k = 1; k < kCrcSlices; k++) {
             const uint32_t prev = crctab[(k - 1) * 256 + t];
@@ -531,15 +528,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
         B.verdict[idx] = verdict;
         B.rule[idx] = rule;
         B.consumed[idx] = consumed;
-        if (counters) {
-            atomicAdd(&s_verdicts[verdict], 1u);  // per-verdict totals: one global atomic per block
-            if (rule >= 0 && (uint32_t)rule < ncounters - 8) atomicAdd((unsigned long long *)&counters[rule], 1ull);
-        }
-    }
-    if (counters) {
-        __syncthreads();
-        if (threadIdx.x < 8 && s_verdicts[threadIdx.x])
-            atomicAdd((unsigned long long *)&counters[ncounters - 8 + threadIdx.x], (unsigned long long)s_verdicts[threadIdx.x]);
     }
 }
 

@@ -199,13 +199,9 @@ __global__ __launch_bounds__(kBlock) void memcache_classify_kernel(Batch B, McTa
                                                                    const uint32_t *__restrict__ sel,
                                                                    const uint32_t *__restrict__ sel_count,
                                                                    uint32_t answer_other) {
-    const uint32_t n = B.n, nconns = B.nconns, ncounters = B.ncounters;
+    const uint32_t n = B.n, nconns = B.nconns;
     const uint32_t *__restrict__ conn_ids = B.conn_ids;
     const DevConn *__restrict__ conns = B.conns;
-    uint64_t *__restrict__ counters = B.counters;
-    __shared__ uint32_t s_verdicts[8];
-    if (threadIdx.x < 8) s_verdicts[threadIdx.x] = 0;
-    __syncthreads();
     // sel: this protocol's request indices from partition_kernel (mixed batches), else all n
     const uint32_t m = sel ? *sel_count : n;
     for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < m; i += gridDim.x * kBlock) {
@@ -217,7 +213,6 @@ __global__ __launch_bounds__(kBlock) void memcache_classify_kernel(Batch B, McTa
                 B.verdict[idx] = V_UNSUPPORTED;
                 B.rule[idx] = -1;
                 B.consumed[idx] = 0;
-                if (counters) atomicAdd(&s_verdicts[V_UNSUPPORTED], 1u);
             }
             continue;
         }
@@ -371,15 +366,6 @@ __global__ __launch_bounds__(kBlock) void memcache_classify_kernel(Batch B, McTa
         B.verdict[idx] = verdict;
         B.rule[idx] = rule;
         B.consumed[idx] = consumed;
-        if (counters) {
-            atomicAdd(&s_verdicts[verdict], 1u);  // per-verdict totals: one global atomic per block
-            if (rule >= 0 && (uint32_t)rule < ncounters - 8) atomicAdd((unsigned long long *)&counters[rule], 1ull);
-        }
-    }
-    if (counters) {
-        __syncthreads();
-        if (threadIdx.x < 8 && s_verdicts[threadIdx.x])
-            atomicAdd((unsigned long long *)&counters[ncounters - 8 + threadIdx.x], (unsigned long long)s_verdicts[threadIdx.x]);
     }
 }
 

@@ -54,7 +54,6 @@ __global__ __launch_bounds__(kBlock) void partition_kernel(Batch B, uint32_t *__
     const uint64_t below = (1ull << lane) - 1;
     uint8_t p[kPer];  // class + 1, 0 = none
     uint32_t cnt[kClasses] = {};
-    uint32_t other = 0;
 #pragma unroll
     for (int r = 0; r < kPer; r++) {
         const uint64_t idx = start + (uint64_t)r * kBlock + threadIdx.x;
@@ -72,7 +71,6 @@ __global__ __launch_bounds__(kBlock) void partition_kernel(Batch B, uint32_t *__
                 B.verdict[idx] = V_UNSUPPORTED;
                 B.rule[idx] = -1;
                 B.consumed[idx] = 0;
-                other++;
             }
         }
         p[r] = cls;
@@ -81,11 +79,6 @@ __global__ __launch_bounds__(kBlock) void partition_kernel(Batch B, uint32_t *__
     }
     if (lane == 0)
         for (int c = 0; c < kClasses; c++) s_off[wave][c] = cnt[c];
-    if (B.counters) {  // per-verdict total of the answered requests
-        for (int o = 32; o > 0; o >>= 1) other += __shfl_xor(other, o);
-        if (lane == 0 && other)
-            atomicAdd((unsigned long long *)&B.counters[B.ncounters - 8 + V_UNSUPPORTED], (unsigned long long)other);
-    }
     __syncthreads();
     if (threadIdx.x < kClasses) {
         const int c = threadIdx.x;
