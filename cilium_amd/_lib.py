@@ -38,7 +38,7 @@ EXPORTS = (
     "l7g_engine_create", "l7g_engine_destroy", "l7g_policy_update", "l7g_policy_index",
     "l7g_policy_nrules", "l7g_conns_set", "l7g_conn_update", "l7g_classify", "l7g_classify_host", "l7g_stats",
     "l7g_debug_regex", "l7g_debug_phase_times", "l7g_profile_enable", "l7g_profile_last",
-    "l7g_debug_kafka_phase_times", "l7g_kafka_deny_response", "l7g_debug_regex_nfa",
+    "l7g_debug_kafka_phase_times", "l7g_kafka_deny_response", "l7g_debug_regex_nfa", "l7g_policy_update_proto",
 )
 
 _libs = {}
@@ -58,6 +58,7 @@ def load(path=None):
     lib.l7g_engine_create.argtypes = [C.c_int, cp, sz]
     lib.l7g_engine_destroy.argtypes = [vp]
     lib.l7g_policy_update.argtypes = [vp, cp, sz, cp, sz]
+    lib.l7g_policy_update_proto.argtypes = [vp, cp, sz, cp, sz]
     lib.l7g_policy_index.restype = C.c_int32
     lib.l7g_policy_index.argtypes = [vp, cp, sz]
     lib.l7g_policy_nrules.restype = C.c_int32

@@ -14,6 +14,7 @@
 #include "engine/kafka_compile.h"
 #include "engine/mc_compile.h"
 #include "engine/nfa_pool.h"
+#include "policy/npds_proto.h"
 #include "policy/policy.h"
 #include "regex/nfa_walk.h"
 #include "regex/re_dfa.h"
@@ -278,11 +279,28 @@ void l7g_engine_destroy(l7g_engine *e) {
     delete e;
 }
 
+static int PolicySwap(l7g_engine *e, std::unique_ptr<PolicySet> ps, char *err, size_t errlen);
+
 int l7g_policy_update(l7g_engine *e, const char *json, size_t len, char *err, size_t errlen) {
     std::lock_guard<std::mutex> g(e->mu);
     auto ps = std::make_unique<PolicySet>();
     std::string m;
     if (!LoadPolicySet(json, len, ps.get(), &m)) { set_err(err, errlen, m); return -1; }
+    return PolicySwap(e, std::move(ps), err, errlen);
+}
+
+int l7g_policy_update_proto(l7g_engine *e, const uint8_t *buf, size_t len, char *err, size_t errlen) {
+    std::lock_guard<std::mutex> g(e->mu);
+    auto ps = std::make_unique<PolicySet>();
+    std::string m;
+    if (!LoadPolicySetProto(buf, len, ps.get(), &m)) { set_err(err, errlen, m); return -1; }
+    return PolicySwap(e, std::move(ps), err, errlen);
+}
+
+// Swap in a loaded policy version; on a compile failure the previous version
+// stays in force (an NPDS NACK).  Caller holds e->mu.
+static int PolicySwap(l7g_engine *e, std::unique_ptr<PolicySet> ps, char *err, size_t errlen) {
+    std::string m;
     auto hc = std::make_unique<HttpCompiler>(ps.get());
     auto kc = std::make_unique<KafkaCompiler>(ps.get());
     auto mc = std::make_unique<McCompiler>(ps.get());

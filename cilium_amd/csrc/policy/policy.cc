@@ -294,6 +294,10 @@ struct Loader {
 bool LoadPolicySet(const char *js, size_t n, PolicySet *out, std::string *err) {
     json::Value root;
     if (!json::Parse(js, n, &root, err)) return false;
+    return LoadPolicySetTree(root, out, err);
+}
+
+bool LoadPolicySetTree(const json::Value &root, PolicySet *out, std::string *err) {
     const json::Value *arr = root.isObj() ? root.get("policies") : &root;
     if (!arr || !arr->isArr()) { if (err) *err = "expected a list of policies"; return false; }
     Loader L;

@@ -100,5 +100,9 @@ struct PolicySet {
 };
 
 bool LoadPolicySet(const char *json, size_t n, PolicySet *out, std::string *err);
+namespace json { struct Value; }
+// The same from a parsed tree ({"policies": [...]} or a bare list): the JSON
+// path and the NPDS protobuf path (npds_proto.h) both end here.
+bool LoadPolicySetTree(const json::Value &root, PolicySet *out, std::string *err);
 
 }  // namespace l7

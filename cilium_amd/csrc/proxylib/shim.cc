@@ -681,15 +681,19 @@ void Close(uint64_t connection_id) {
     c->ins->free_slots.push_back(c->slot);
 }
 
-int l7g_proxylib_policy_update(uint64_t instance_id, const char *json, size_t len, char *err, size_t errlen) {
+}  // extern "C"
+
+// A policy version for one instance (JSON or NPDS protobuf), then every
+// connection of the instance re-resolved: policy names may map to new indices.
+template <class Update>
+static int InstancePolicyUpdate(uint64_t instance_id, Update update, char *err, size_t errlen) {
     auto ins = FindInstance(instance_id);
     if (!ins) {
         if (err && errlen) snprintf(err, errlen, "unknown instance %llu", (unsigned long long)instance_id);
         return -1;
     }
     std::lock_guard<std::mutex> g(ins->mu);
-    if (l7g_policy_update(ins->eng, json, len, err, errlen) != 0) return -1;
-    // policy names may map to new indices: re-resolve this instance's connections
+    if (update(ins->eng) != 0) return -1;
     std::shared_lock<std::shared_mutex> gc(g_conn_mu);
     for (auto &kv : g_conns) {
         Connection &c = *kv.second;
@@ -698,6 +702,18 @@ int l7g_proxylib_policy_update(uint64_t instance_id, const char *json, size_t le
         if (l7g_conn_update(ins->eng, c.slot, &a, err, errlen) != 0) return -1;
     }
     return 0;
+}
+
+extern "C" {
+
+int l7g_proxylib_policy_update(uint64_t instance_id, const char *json, size_t len, char *err, size_t errlen) {
+    return InstancePolicyUpdate(
+        instance_id, [&](l7g_engine *e) { return l7g_policy_update(e, json, len, err, errlen); }, err, errlen);
+}
+
+int l7g_proxylib_policy_update_proto(uint64_t instance_id, const uint8_t *buf, size_t len, char *err, size_t errlen) {
+    return InstancePolicyUpdate(
+        instance_id, [&](l7g_engine *e) { return l7g_policy_update_proto(e, buf, len, err, errlen); }, err, errlen);
 }
 
 uint64_t l7g_proxylib_connections(void) {

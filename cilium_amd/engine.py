@@ -48,6 +48,13 @@ class Engine:
         if self._lib.l7g_policy_update(self._h, b, len(b), err, 1024) != 0:
             raise PolicyError(err.value.decode(errors="replace"))
 
+    def update_policy_proto(self, buf):
+        """A serialized NPDS DiscoveryResponse (cilium.NetworkPolicy resources)."""
+        b = bytes(buf)
+        err = C.create_string_buffer(1024)
+        if self._lib.l7g_policy_update_proto(self._h, b, len(b), err, 1024) != 0:
+            raise PolicyError(err.value.decode(errors="replace"))
+
     def policy_index(self, name):
         b = name.encode()
         return self._lib.l7g_policy_index(self._h, b, len(b))

@@ -47,6 +47,8 @@ def lib():
         L.Close.argtypes = [C.c_uint64]
         L.l7g_proxylib_policy_update.restype = C.c_int
         L.l7g_proxylib_policy_update.argtypes = [C.c_uint64, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t]
+        L.l7g_proxylib_policy_update_proto.restype = C.c_int
+        L.l7g_proxylib_policy_update_proto.argtypes = [C.c_uint64, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t]
         L.l7g_proxylib_connections.restype = C.c_uint64
         _bound = L
     return _bound
@@ -116,3 +118,11 @@ def on_data(conn_id, reply, buffers, max_ops, end_stream=False):
     ops = GoSlice(C.cast(ops_mem, C.c_void_p), 0, max_ops)
     res = lib().OnData(conn_id, 1 if reply else 0, 1 if end_stream else 0, C.byref(data), C.byref(ops))
     return res, [(int(ops_mem[2 * i]), int(ops_mem[2 * i + 1])) for i in range(ops.len)]
+
+
+def policy_update_proto(mid, buf):
+    """NPDS wire form: a serialized DiscoveryResponse of cilium.NetworkPolicy."""
+    b = bytes(buf)
+    err = C.create_string_buffer(1024)
+    if lib().l7g_proxylib_policy_update_proto(mid, b, len(b), err, 1024) != 0:
+        raise ValueError(err.value.decode(errors="replace"))

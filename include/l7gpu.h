@@ -91,6 +91,13 @@ void l7g_engine_destroy(l7g_engine *e);
 /* Atomically replaces the policy set (0 = ok).  On error the previous policy
  * set stays in force (like an NPDS NACK).  Existing connections are re-resolved. */
 int l7g_policy_update(l7g_engine *e, const char *json, size_t len, char *err, size_t errlen);
+/* The same policy delivery as the NPDS stream carries it: buf is a serialized
+ * envoy.api.v2.DiscoveryResponse whose resources are google.protobuf.Any of
+ * type.googleapis.com/cilium.NetworkPolicy (envoy/cilium/npds.proto:31-182),
+ * decoded by the library's own proto3 wire-format reader.  Same atomic swap and
+ * NACK as l7g_policy_update; a response the JSON path would express the same
+ * way compiles to identical tables. */
+int l7g_policy_update_proto(l7g_engine *e, const uint8_t *buf, size_t len, char *err, size_t errlen);
 int32_t l7g_policy_index(l7g_engine *e, const char *name, size_t len);
 int32_t l7g_policy_nrules(l7g_engine *e);
 

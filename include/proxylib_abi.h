@@ -82,6 +82,9 @@ void Close(uint64_t connection_id);
  * cilium.NetworkPolicy list as JSON, swapped atomically; 0 = ok, else the
  * previous policies stay in force and err says why (an NPDS NACK). */
 int l7g_proxylib_policy_update(uint64_t instance_id, const char *json, size_t len, char *err, size_t errlen);
+/* The same from the NPDS wire form (a serialized DiscoveryResponse; see
+ * l7g_policy_update_proto in l7gpu.h). */
+int l7g_proxylib_policy_update_proto(uint64_t instance_id, const uint8_t *buf, size_t len, char *err, size_t errlen);
 /* Number of open connections (all instances). */
 uint64_t l7g_proxylib_connections(void);
 
