@@ -38,7 +38,8 @@ EXPORTS = (
     "l7g_engine_create", "l7g_engine_destroy", "l7g_policy_update", "l7g_policy_index",
     "l7g_policy_nrules", "l7g_conns_set", "l7g_conn_update", "l7g_classify", "l7g_classify_host", "l7g_stats",
     "l7g_debug_regex", "l7g_debug_phase_times", "l7g_profile_enable", "l7g_profile_last",
-    "l7g_debug_kafka_phase_times", "l7g_kafka_deny_response", "l7g_debug_regex_nfa", "l7g_policy_update_proto",
+    "l7g_debug_kafka_phase_times", "l7g_kafka_deny_response", "l7g_debug_regex_nfa", "l7g_policy_update_proto", "l7g_kafka_corr_create", "l7g_kafka_corr_destroy",
+    "l7g_kafka_corr_requests", "l7g_kafka_corr_responses", "l7g_kafka_corr_gc", "l7g_kafka_corr_size",
 )
 
 _libs = {}
@@ -72,6 +73,14 @@ def load(path=None):
     lib.l7g_debug_regex_nfa.argtypes = [cp, sz, C.c_int, cp, sz, cp, sz]
     lib.l7g_debug_phase_times.argtypes = [vp, vp, C.c_int]
     lib.l7g_debug_kafka_phase_times.argtypes = [vp, vp, C.c_int]
+    lib.l7g_kafka_corr_create.restype = vp
+    lib.l7g_kafka_corr_destroy.argtypes = [vp]
+    lib.l7g_kafka_corr_requests.argtypes = [vp, vp, vp, vp, C.c_uint32, vp]
+    lib.l7g_kafka_corr_responses.argtypes = [vp, vp, vp, vp, C.c_uint32, vp]
+    lib.l7g_kafka_corr_gc.restype = C.c_uint64
+    lib.l7g_kafka_corr_gc.argtypes = [vp, C.c_uint64]
+    lib.l7g_kafka_corr_size.restype = C.c_uint64
+    lib.l7g_kafka_corr_size.argtypes = [vp]
     lib.l7g_kafka_deny_response.argtypes = [cp, sz, vp, sz, C.POINTER(C.c_size_t)]
     lib.l7g_profile_enable.argtypes = [vp, C.c_int]
     lib.l7g_profile_last.argtypes = [vp, vp]
@@ -109,3 +118,41 @@ def kafka_deny_response(req):
     if rc != 0:
         raise RuntimeError(f"l7g_kafka_deny_response: {rc}")
     return out.raw[:n.value]
+
+
+class KafkaCorrelationCache:
+    """One client connection's correlation cache (l7g_kafka_corr_*): batches
+    of frames given as (arena: writable uint8 numpy array, offsets, lengths)."""
+
+    def __init__(self):
+        self._lib = load()
+        self._h = self._lib.l7g_kafka_corr_create()
+
+    def __del__(self):
+        try:
+            self._lib.l7g_kafka_corr_destroy(self._h)
+        except Exception:
+            pass
+
+    def requests(self, arena, offs, lens):
+        import numpy as np
+        o = np.ascontiguousarray(offs, np.uint64)
+        n = np.ascontiguousarray(lens, np.uint32)
+        ids = np.zeros(len(o), np.uint32)
+        self._lib.l7g_kafka_corr_requests(self._h, arena.ctypes.data, o.ctypes.data, n.ctypes.data, len(o), ids.ctypes.data)
+        return ids
+
+    def responses(self, arena, offs, lens):
+        import numpy as np
+        o = np.ascontiguousarray(offs, np.uint64)
+        n = np.ascontiguousarray(lens, np.uint32)
+        found = np.zeros(len(o), np.uint8)
+        self._lib.l7g_kafka_corr_responses(self._h, arena.ctypes.data, o.ctypes.data, n.ctypes.data, len(o),
+                                           found.ctypes.data)
+        return found.astype(bool)
+
+    def gc(self, lifetime_ms):
+        return int(self._lib.l7g_kafka_corr_gc(self._h, lifetime_ms))
+
+    def __len__(self):
+        return int(self._lib.l7g_kafka_corr_size(self._h))

@@ -157,6 +157,28 @@ int l7g_debug_phase_times(l7g_engine *e, uint64_t *out8, int reset);
  * 6 window refills, 7 tiles). */
 int l7g_debug_kafka_phase_times(l7g_engine *e, uint64_t *out8, int reset);
 
+/* Kafka correlation-ID rewriting of the in-agent Kafka proxy's forwarding
+ * path (pkg/kafka/correlation_cache.go:97-213; one cache per client
+ * connection, pkg/proxy/kafka.go:335).  Host code.
+ *   l7g_kafka_corr_requests: HandleRequest for a batch of forwarded (allowed)
+ *     request frames, in order: each frame's correlation id (bytes 8..12) is
+ *     replaced in place by the cache's next sequence number (from 1), written
+ *     to new_ids (may be null), and the original remembered.
+ *   l7g_kafka_corr_responses: CorrelateResponse for a batch of broker
+ *     response frames: a known id (bytes 4..8) is replaced in place by the
+ *     original and forgotten; found[i] = 1 then, else 0 (frame untouched).
+ *   l7g_kafka_corr_gc: drop entries at least lifetime_ms old (the reference
+ *     runs this every RequestLifetime = 5 min); returns how many. */
+typedef struct l7g_kafka_corr l7g_kafka_corr;
+l7g_kafka_corr *l7g_kafka_corr_create(void);
+void l7g_kafka_corr_destroy(l7g_kafka_corr *c);
+int l7g_kafka_corr_requests(l7g_kafka_corr *c, uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t n,
+                            uint32_t *new_ids);
+int l7g_kafka_corr_responses(l7g_kafka_corr *c, uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t n,
+                             uint8_t *found);
+uint64_t l7g_kafka_corr_gc(l7g_kafka_corr *c, uint64_t lifetime_ms);
+uint64_t l7g_kafka_corr_size(l7g_kafka_corr *c);
+
 /* Test hook: compile one Go regexp with the product's DFA compiler and run
  * the compiled tables on the host.  Returns 1 match, 0 no match, -1 compile
  * error (err set).  anchored: 1 = full match, 0 = Go regexp.Match. */

@@ -163,3 +163,30 @@ def test_reference_disallowed_topic_case():
     assert (size, corr, nt) == (len(out) - 4, 42, 1)
     assert out[12:14 + 15] == s("disallowedTopic")
     assert struct.unpack(">iihq", out[29:47]) == (1, 0, 29, 0)
+
+
+def test_correlation_cache_round_trip():
+    """correlation_cache.go: forwarded requests get ids 1, 2, ...; responses
+    carrying them get the client's original ids back; unknown ones pass."""
+    cc = _lib.KafkaCorrelationCache()
+    reqs = [gen.k_fetch(0, 1000 + i, "c", TOPICS) for i in range(5)]
+    arena, offs, lens = gen.pack(reqs)
+    arena = np.array(arena, np.uint8)
+    ids = cc.requests(arena, offs, lens)
+    assert ids.tolist() == [1, 2, 3, 4, 5] and len(cc) == 5
+    for i, o in enumerate(offs):
+        assert struct.unpack(">i", bytes(arena[o + 8:o + 12]))[0] == i + 1
+        assert bytes(arena[o + 12:o + lens[i]]) == reqs[i][12:]  # nothing else touched
+    # the broker answers 3, 1 and an id the proxy never issued
+    resp = [expect(1, 0, 3, TOPICS), expect(1, 0, 1, TOPICS), expect(1, 0, 99, TOPICS)]
+    rarena, roffs, rlens = gen.pack(resp)
+    rarena = np.array(rarena, np.uint8)
+    found = cc.responses(rarena, roffs, rlens)
+    assert found.tolist() == [True, True, False]
+    got = [struct.unpack(">i", bytes(rarena[o + 4:o + 8]))[0] for o in roffs]
+    assert got == [1002, 1000, 99]
+    assert len(cc) == 3
+    assert cc.responses(rarena, roffs[:1], rlens[:1]).tolist() == [False]  # 3 is forgotten now
+    assert cc.gc(10 ** 9) == 0 and cc.gc(0) == 3 and len(cc) == 0
+    more = cc.requests(arena, offs[:2], lens[:2])
+    assert more.tolist() == [6, 7]  # the sequence continues
