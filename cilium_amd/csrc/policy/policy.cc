@@ -136,7 +136,8 @@ struct Loader {
         std::string role, key, ver, s;
         str(j, "role", &role);
         str(j, "apiKey", &key);
-        if (!role.empty() && !key.empty()) return fail("kafka: cannot set both Role and APIKey");
+        if (!role.empty() && !key.empty())
+            return fail("Cannot set both Role:\"" + role + "\" and APIKey :\"" + key + "\" together");
         if (!key.empty()) {
             int found = -1;
             for (int i = 0; i < (int)(sizeof kKeys / sizeof kKeys[0]); i++) if (ieq(key, kKeys[i])) found = i;
