@@ -40,7 +40,13 @@ EXPORTS = (
     "l7g_debug_regex", "l7g_debug_phase_times", "l7g_profile_enable", "l7g_profile_last",
     "l7g_debug_kafka_phase_times", "l7g_kafka_deny_response", "l7g_debug_regex_nfa", "l7g_policy_update_proto", "l7g_kafka_corr_create", "l7g_kafka_corr_destroy",
     "l7g_kafka_corr_requests", "l7g_kafka_corr_responses", "l7g_kafka_corr_gc", "l7g_kafka_corr_size",
+    "l7g_flow_stats_enable", "l7g_flow_stats",
 )
+
+
+class FlowStat(C.Structure):
+    _fields_ = [("policy", C.c_int32), ("proto", C.c_uint8), ("ingress", C.c_uint8), ("port", C.c_uint16),
+                ("received", C.c_uint64), ("forwarded", C.c_uint64), ("denied", C.c_uint64), ("error", C.c_uint64)]
 
 _libs = {}
 
@@ -83,6 +89,8 @@ def load(path=None):
     lib.l7g_kafka_corr_size.argtypes = [vp]
     lib.l7g_kafka_deny_response.argtypes = [cp, sz, vp, sz, C.POINTER(C.c_size_t)]
     lib.l7g_profile_enable.argtypes = [vp, C.c_int]
+    lib.l7g_flow_stats_enable.argtypes = [vp, C.c_int]
+    lib.l7g_flow_stats.argtypes = [vp, vp, C.c_uint32, C.POINTER(C.c_uint32), C.c_int]
     lib.l7g_profile_last.argtypes = [vp, vp]
     _libs[path] = lib
     return lib

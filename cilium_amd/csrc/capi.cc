@@ -3,7 +3,9 @@
 #include <hip/hip_runtime_api.h>
 
 #include <cstring>
+#include <map>
 #include <memory>
+#include <tuple>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -29,6 +31,8 @@ hipError_t LaunchMemcacheClassify(const Batch &B, const McTables &T, const uint3
 hipError_t LaunchCounters(const uint8_t *verdict, const int32_t *rule, uint32_t n, uint32_t nrules,
                           uint64_t *counters, uint32_t *scratch, hipStream_t stream);
 size_t CountersScratchBytes();
+hipError_t LaunchFlowStats(const Batch &B, uint32_t nkeys, uint64_t *acc, hipStream_t stream);
+uint32_t FlowStatsMaxKeys();
 hipError_t LaunchHttpNfa(const Batch &B, const HttpTables &T, hipStream_t stream);
 hipError_t LaunchPartition(const Batch &B, uint32_t *sel_kafka, uint32_t *sel_mc, uint32_t *counts, hipStream_t stream);
 hipError_t HttpPhaseTimes(uint64_t *out, bool reset);
@@ -70,6 +74,13 @@ struct l7g_engine {
     size_t nfa_cap = 0;
     // counter histogram scratch (kernels/counters.hip), allocated on first use
     uint32_t *d_hist = nullptr;
+    // proxy statistics: key (policy, proto, port, ingress) per connection, and
+    // the device accumulator u64[keys][4] (l7g_flow_stats_*)
+    std::map<std::tuple<int32_t, uint8_t, uint32_t, uint8_t>, uint16_t> skeys;
+    std::vector<std::tuple<int32_t, uint8_t, uint32_t, uint8_t>> skey_list;
+    bool flow_stats = false;
+    uint64_t *d_flow = nullptr;
+    size_t flow_cap = 0;  // keys the accumulator holds
     // Completion of the last l7g_classify's kernels (recorded on the caller's
     // stream).  The engine waits on it -- never on the caller's stream, which
     // may be gone by then -- before it rewrites or frees anything a launched
@@ -108,8 +119,17 @@ size_t Put(std::vector<uint8_t> &blob, const std::vector<T> &v) {
 bool ResolveOne(l7g_engine *e, size_t i, std::string *err) {
     const l7g_conn_t &a = e->attrs[i];
     DevConn &c = e->conns[i];
-    c = DevConn{-1, PROTO_NONE, 0, {0, 0}};
+    c = DevConn{-1, PROTO_NONE, 0, 0xFFFF};
     c.proto = a.proto;
+    if (a.proto == PROTO_HTTP || a.proto == PROTO_KAFKA || a.proto == PROTO_MEMCACHE) {
+        const auto key = std::make_tuple(a.policy, a.proto, a.port, (uint8_t)(a.ingress != 0));
+        auto it = e->skeys.find(key);
+        if (it == e->skeys.end() && e->skey_list.size() < FlowStatsMaxKeys()) {
+            it = e->skeys.emplace(key, (uint16_t)e->skey_list.size()).first;
+            e->skey_list.push_back(key);
+        }
+        if (it != e->skeys.end()) c.skey = it->second;
+    }
     c.flags = (uint8_t)(a.flags & 3);
     const bool proxylib = (a.flags & L7G_CONN_PROXYLIB) != 0;
     if (a.proto == PROTO_HTTP) {
@@ -157,7 +177,7 @@ size_t TableRulesets(const l7g_engine *e) {
 
 // Resolve every connection (policy update / connection table replaced).
 bool ResolveConns(l7g_engine *e, std::string *err) {
-    e->conns.assign(e->attrs.size(), DevConn{-1, PROTO_NONE, 0, {0, 0}});
+    e->conns.assign(e->attrs.size(), DevConn{-1, PROTO_NONE, 0, 0xFFFF});
     e->has_http = e->has_kafka = e->has_mc = false;
     for (size_t i = 0; i < e->attrs.size(); i++)
         if (!ResolveOne(e, i, err)) return false;
@@ -270,6 +290,7 @@ void l7g_engine_destroy(l7g_engine *e) {
     if (e->d_sel) hipFree(e->d_sel);
     if (e->d_nfa) hipFree(e->d_nfa);
     if (e->d_hist) hipFree(e->d_hist);
+    if (e->d_flow) hipFree(e->d_flow);
     if (e->done_ev) hipEventDestroy(e->done_ev);
     for (hipEvent_t ev : e->prof_ev)
         if (ev) hipEventDestroy(ev);
@@ -346,7 +367,7 @@ int l7g_conn_update(l7g_engine *e, uint32_t index, const l7g_conn_t *conn, char 
         l7g_conn_t none{};
         none.policy = -1;
         e->attrs.resize((size_t)index + 1, none);
-        e->conns.resize((size_t)index + 1, DevConn{-1, PROTO_NONE, 0, {0, 0}});
+        e->conns.resize((size_t)index + 1, DevConn{-1, PROTO_NONE, 0, 0xFFFF});
     }
     const l7g_conn_t prev = e->attrs[index];
     const size_t nrs = TableRulesets(e);
@@ -458,6 +479,23 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
     if (rc == hipSuccess && run[3])
         rc = LaunchMemcacheClassify(B, e->mt, sel_m, cnt ? cnt + L7_KAFKA_CLASSES : nullptr, !partitioned, s);
     mark(4);
+    // proxy statistics (accumulated on the device until read)
+    if (rc == hipSuccess && e->flow_stats && !e->skey_list.empty()) {
+        const size_t nk = e->skey_list.size();
+        if (nk > e->flow_cap) {  // grow, keeping what was accumulated
+            uint64_t *d = nullptr;
+            rc = hipMalloc(&d, nk * 4 * sizeof(uint64_t));
+            if (rc == hipSuccess) rc = hipMemsetAsync(d, 0, nk * 4 * sizeof(uint64_t), s);
+            if (rc == hipSuccess && e->d_flow)
+                rc = hipMemcpyAsync(d, e->d_flow, e->flow_cap * 4 * sizeof(uint64_t), hipMemcpyDeviceToDevice, s);
+            if (rc == hipSuccess) {
+                if (e->d_flow) { hipStreamSynchronize(s); hipFree(e->d_flow); }
+                e->d_flow = d;
+                e->flow_cap = nk;
+            }
+        }
+        if (rc == hipSuccess) rc = LaunchFlowStats(B, (uint32_t)nk, e->d_flow, s);
+    }
     // per-rule allow hits and per-verdict totals, from the outputs
     if (rc == hipSuccess && counters) {
         if (!e->d_hist) {
@@ -544,6 +582,38 @@ int l7g_stats(l7g_engine *e, l7g_stats_t *out) {
     out->mc_nfas = (uint32_t)M.nfas;
     out->nfa_pool_bytes = H.nfa_pool.size() + M.nfa_pool.size();
     return 0;
+}
+
+int l7g_flow_stats_enable(l7g_engine *e, int on) {
+    std::lock_guard<std::mutex> g(e->mu);
+    if (e->device < 0) return (int)hipErrorNoDevice;
+    e->flow_stats = on != 0;
+    return 0;
+}
+
+int l7g_flow_stats(l7g_engine *e, l7g_flow_stat_t *out, uint32_t cap, uint32_t *n, int reset) {
+    std::lock_guard<std::mutex> g(e->mu);
+    if (n) *n = 0;
+    if (e->device < 0) return (int)hipErrorNoDevice;
+    hipError_t rc = hipSetDevice(e->device);
+    if (rc == hipSuccess) rc = WaitLastClassify(e);
+    std::vector<uint64_t> h(e->flow_cap * 4, 0);
+    if (rc == hipSuccess && e->flow_cap)
+        rc = hipMemcpy(h.data(), e->d_flow, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost);
+    if (rc != hipSuccess) return (int)rc;
+    uint32_t k = 0;
+    for (size_t i = 0; i < e->flow_cap && i < e->skey_list.size(); i++) {
+        if (!(h[4 * i] | h[4 * i + 1] | h[4 * i + 2] | h[4 * i + 3])) continue;
+        if (k < cap && out) {
+            const auto &t = e->skey_list[i];
+            out[k] = l7g_flow_stat_t{std::get<0>(t), std::get<1>(t), std::get<3>(t), (uint16_t)std::get<2>(t),
+                                     h[4 * i], h[4 * i + 1], h[4 * i + 2], h[4 * i + 3]};
+        }
+        k++;
+    }
+    if (n) *n = k;
+    if (reset && e->flow_cap) rc = hipMemset(e->d_flow, 0, e->flow_cap * 4 * sizeof(uint64_t));
+    return (int)rc;
 }
 
 int l7g_profile_enable(l7g_engine *e, int on) {

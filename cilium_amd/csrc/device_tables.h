@@ -32,7 +32,7 @@ struct DevConn {
     int32_t ruleset;   // index into HttpTables::rulesets / KafkaTables::rulesets
     uint8_t proto;     // PROTO_*
     uint8_t flags;     // memcached: L7G_CONN_MC_TEXT / _BINARY (0 = by first byte)
-    uint8_t pad[2];
+    uint16_t skey;     // proxy-statistics key (policy, proto, port, direction); 0xFFFF none
 };
 
 // One l7g_classify call as the kernels see it (passed by value): request i is

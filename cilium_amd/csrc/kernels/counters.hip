@@ -72,7 +72,45 @@ __global__ void reduce_kernel(const uint32_t *__restrict__ scratch, uint32_t nbl
     else counters[lo + b] += s;
 }
 
+// Proxy statistics (pkg/endpoint/endpoint.go:2207-2233 UpdateProxyStatistics):
+// per statistics key -- (policy, proto, port, direction), resolved per
+// connection on the host -- received / forwarded / denied / error counts of
+// the call's requests, added into the engine's u64[nkeys][4] accumulator.
+// ALLOW = forwarded, DENY = denied, PARSE_ERROR = error, each also received;
+// INCOMPLETE and UNSUPPORTED requests are no flow yet.
+constexpr uint32_t kFlowBinsMax = 4096 * 4;  // LDS u32 bins (64 KiB)
+
+__global__ __launch_bounds__(kHistBlock) void flowstats_kernel(Batch B, uint32_t nkeys, uint64_t *__restrict__ acc) {
+    __shared__ uint32_t bins[kFlowBinsMax];
+    const uint32_t nb = nkeys * 4;
+    for (uint32_t i = threadIdx.x; i < nb; i += kHistBlock) bins[i] = 0;
+    __syncthreads();
+    const uint32_t per = (B.n + gridDim.x - 1) / gridDim.x;
+    const uint32_t b0 = blockIdx.x * per, b1 = min(B.n, b0 + per);
+    for (uint32_t i = b0 + threadIdx.x; i < b1; i += kHistBlock) {
+        const uint32_t v = B.verdict[i];
+        if (v > V_PARSE_ERROR) continue;
+        const uint32_t ci = B.conn_ids[i];
+        const uint32_t k = ci < B.nconns ? B.conns[ci].skey : 0xFFFFu;
+        if (k >= nkeys) continue;
+        atomicAdd(&bins[4 * k], 1u);
+        atomicAdd(&bins[4 * k + (v == V_ALLOW ? 1 : v == V_DENY ? 2 : 3)], 1u);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nb; i += kHistBlock)
+        if (bins[i]) atomicAdd((unsigned long long *)&acc[i], (unsigned long long)bins[i]);
+}
+
 }  // namespace
+
+uint32_t FlowStatsMaxKeys() { return kFlowBinsMax / 4; }
+
+hipError_t LaunchFlowStats(const Batch &B, uint32_t nkeys, uint64_t *acc, hipStream_t stream) {
+    if (B.n == 0 || nkeys == 0) return hipSuccess;
+    const uint32_t nblocks = std::min<uint32_t>(kHistBlocks, (B.n + kHistBlock - 1) / kHistBlock);
+    hipLaunchKernelGGL(flowstats_kernel, dim3(nblocks), dim3(kHistBlock), 0, stream, B, nkeys, acc);
+    return hipGetLastError();
+}
 
 // Bytes of scratch LaunchCounters needs.
 size_t CountersScratchBytes() { return (size_t)kHistBlocks * (kHistBins + 8) * sizeof(uint32_t); }

@@ -1084,7 +1084,7 @@ __global__ __launch_bounds__(kBlock) void http_classify_kernel(Batch B, HttpTabl
         const uint8_t *img = kHot ? s_img : nullptr;
         if (L.idx < n) {
             const uint32_t ci = B.conn_ids[L.idx];
-            const DevConn conn = ci < nconns ? B.conns[ci] : DevConn{-1, PROTO_NONE, 0, {0, 0}};
+            const DevConn conn = ci < nconns ? B.conns[ci] : DevConn{-1, PROTO_NONE, 0, 0xFFFF};
             // entries of other protocols belong to their own kernels; the HTTP
             // kernel answers entries whose connection is unknown or has no parser
             const bool mine = !(conn.proto == PROTO_KAFKA || conn.proto == PROTO_MEMCACHE);

@@ -347,7 +347,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
             idx = sel[(size_t)c * n + j];
         }
         const uint32_t ci = conn_ids[idx];
-        const DevConn conn = ci < nconns ? conns[ci] : DevConn{-1, PROTO_NONE, 0, {0, 0}};
+        const DevConn conn = ci < nconns ? conns[ci] : DevConn{-1, PROTO_NONE, 0, 0xFFFF};
         const uint64_t off = B.offs[idx];
         const uint32_t len = B.lens[idx];
         const uint8_t *b = arena + off;

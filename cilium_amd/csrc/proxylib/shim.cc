@@ -39,6 +39,11 @@
 #include <memory>
 #include <mutex>
 #include <shared_mutex>
+#include <chrono>
+
+#include <sys/socket.h>
+#include <sys/un.h>
+#include <unistd.h>
 #include <string>
 #include <vector>
 
@@ -49,6 +54,57 @@ namespace {
 
 constexpr int64_t NOP = 256;  // proxylib-internal op (types.go:34)
 
+// ---------------------------------------------------------------- access log
+// proxylib/accesslog/client.go: one "unixpacket" (SOCK_SEQPACKET) connection
+// to the agent's access-log socket per instance, dialled lazily and again
+// after a failed write; each record is one protobuf-encoded cilium.LogEntry
+// (pkg/envoy/cilium/accesslog.pb.go:263-400) per packet.
+struct AccessLog {
+    std::string path;
+    std::mutex mu;
+    int fd = -1;
+    uint64_t sent = 0, failed = 0;
+    ~AccessLog() { if (fd >= 0) close(fd); }
+    void Send(const std::string &msg) {
+        if (path.empty()) return;
+        std::lock_guard<std::mutex> g(mu);
+        if (fd < 0) {
+            sockaddr_un a{};
+            a.sun_family = AF_UNIX;
+            if (path.size() >= sizeof a.sun_path) { failed++; return; }
+            memcpy(a.sun_path, path.data(), path.size());
+            fd = socket(AF_UNIX, SOCK_SEQPACKET | SOCK_CLOEXEC, 0);
+            if (fd >= 0 && connect(fd, (const sockaddr *)&a, sizeof a) != 0) { close(fd); fd = -1; }
+            if (fd < 0) { failed++; return; }
+        }
+        if (send(fd, msg.data(), msg.size(), MSG_NOSIGNAL) != (ssize_t)msg.size()) {
+            close(fd);  // marked broken: redialled on the next record
+            fd = -1;
+            failed++;
+            return;
+        }
+        sent++;
+    }
+};
+
+// proto3 wire encoding of the LogEntry fields (zero / empty values omitted)
+void PbVarint(std::string &o, uint64_t v) {
+    while (v >= 0x80) { o.push_back((char)(v | 0x80)); v >>= 7; }
+    o.push_back((char)v);
+}
+void PbU(std::string &o, uint32_t field, uint64_t v) {
+    if (!v) return;
+    PbVarint(o, (uint64_t)field << 3);
+    PbVarint(o, v);
+}
+void PbS(std::string &o, uint32_t field, const std::string &s, bool keep_empty = false) {
+    if (s.empty() && !keep_empty) return;
+    PbVarint(o, (uint64_t)field << 3 | 2);
+    PbVarint(o, s.size());
+    o += s;
+}
+enum : uint32_t { kEntryRequest = 0, kEntryResponse = 1, kEntryDenied = 2 };  // cilium.EntryType
+
 struct Instance {
     uint64_t id = 0, open = 0;
     std::string node, xds, alog;
@@ -56,6 +112,7 @@ struct Instance {
     std::mutex mu;                 // slot allocation / policy swaps
     std::vector<uint32_t> free_slots;
     uint32_t next_slot = 0;
+    AccessLog log;
 };
 
 std::mutex g_inst_mu;
@@ -212,6 +269,73 @@ struct Connection {
     }
     bool InjectFull(bool r) const { const GoSlice *b = InjectBuf(r); return b->len == b->cap; }
 
+    // Connection.Log (connection.go:211-224): the connection's fields + the
+    // parser's L7 record (already encoded as LogEntry field 100 or 102).
+    void Log(uint32_t type, const std::string &l7) {
+        if (ins->alog.empty()) return;
+        std::string m;
+        PbU(m, 1, (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                      std::chrono::system_clock::now().time_since_epoch()).count());
+        PbU(m, 3, type);
+        PbS(m, 4, policy);
+        PbU(m, 6, src);
+        PbS(m, 7, src_addr);
+        PbS(m, 8, dst_addr);
+        PbU(m, 15, ingress ? 1 : 0);
+        PbU(m, 16, dst);
+        m += l7;
+        ins->log.Send(m);
+    }
+    // cilium.L7LogEntry{proto, fields} as LogEntry.generic_l7 (field 102); fields sorted by key
+    static std::string GenericL7(const std::string &proto, std::map<std::string, std::string> fields) {
+        std::string e;
+        PbS(e, 1, proto);
+        for (auto &kv : fields) {
+            std::string ent;
+            PbS(ent, 1, kv.first, true);
+            PbS(ent, 2, kv.second, true);
+            PbS(e, 2, ent, true);
+        }
+        std::string o;
+        PbS(o, 102, e, true);
+        return o;
+    }
+    // cilium.HttpLogEntry as LogEntry.http (field 100): HTTP/1.1, method, path, host (and status for a denial)
+    static std::string HttpL7(const std::string &d, uint32_t status) {
+        std::string e, method, path, host;
+        const size_t sp1 = d.find(' '), le = d.find("\r\n");
+        if (sp1 != std::string::npos && le != std::string::npos && sp1 < le) {
+            method = d.substr(0, sp1);
+            const size_t sp2 = d.find(' ', sp1 + 1);
+            if (sp2 != std::string::npos && sp2 < le) path = d.substr(sp1 + 1, sp2 - sp1 - 1);
+            const size_t he = d.find("\r\n\r\n");
+            for (size_t ls = le + 2; he != std::string::npos && ls < he;) {
+                const size_t e2 = d.find("\r\n", ls), colon = d.find(':', ls);
+                if (colon != std::string::npos && colon < e2 && colon - ls == 4) {
+                    std::string nm = d.substr(ls, 4);
+                    for (auto &ch : nm) ch = (char)tolower((unsigned char)ch);
+                    if (nm == "host") {
+                        size_t v = colon + 1, ve = e2;
+                        while (v < ve && (d[v] == ' ' || d[v] == '\t')) v++;
+                        while (ve > v && (d[ve - 1] == ' ' || d[ve - 1] == '\t')) ve--;
+                        host = d.substr(v, ve - v);
+                        break;
+                    }
+                }
+                ls = e2 + 2;
+            }
+        }
+        PbU(e, 1, 1);  // HttpProtocol HTTP11
+        PbS(e, 3, host);
+        PbS(e, 4, path);
+        PbS(e, 5, method);
+        PbU(e, 7, status);
+        std::string o;
+        PbS(o, 100, e, true);
+        return o;
+    }
+    std::string src_addr, dst_addr;
+
     l7g_conn_t Attrs() const {
         l7g_conn_t a{};
         a.policy = l7g_policy_index(ins->eng, policy.data(), policy.size());
@@ -285,8 +409,12 @@ struct Connection {
         if (v == L7G_INCOMPLETE) { *n = 1; return FILTEROP_MORE; }
         if (v != L7G_ALLOW && v != L7G_DENY) { *n = FILTEROP_ERROR_INVALID_FRAME_TYPE; return FILTEROP_ERROR; }
         *n = cons;
-        if (v == L7G_ALLOW) return FILTEROP_PASS;
+        if (v == L7G_ALLOW) {
+            Log(kEntryRequest, HttpL7(d.substr(0, cons), 0));
+            return FILTEROP_PASS;
+        }
         Inject(true, kDenied403, sizeof kDenied403 - 1);
+        Log(kEntryDenied, HttpL7(d.substr(0, cons), 403));
         return FILTEROP_DROP;
     }
 
@@ -313,7 +441,16 @@ struct Connection {
         }
         if (v != L7G_ALLOW && v != L7G_DENY) { *n = FILTEROP_ERROR_INVALID_FRAME_TYPE; return FILTEROP_ERROR; }
         *n = cons;
-        if (v == L7G_ALLOW) return FILTEROP_PASS;
+        const uint8_t *kb = (const uint8_t *)d.data();
+        const std::string l7 = GenericL7("kafka", {
+            {"api_key", std::to_string((int16_t)(kb[4] << 8 | kb[5]))},
+            {"api_version", std::to_string((int16_t)(kb[6] << 8 | kb[7]))},
+            {"correlation_id", std::to_string((int32_t)((uint32_t)kb[8] << 24 | (uint32_t)kb[9] << 16 | (uint32_t)kb[10] << 8 | kb[11]))}});
+        if (v == L7G_ALLOW) {
+            Log(kEntryRequest, l7);
+            return FILTEROP_PASS;
+        }
+        Log(kEntryDenied, l7);
         std::string resp;
         if (l7::KafkaDenyResponse((const uint8_t *)d.data(), cons, &resp)) Inject(true, resp.data(), resp.size());
         return FILTEROP_DROP;
@@ -369,14 +506,22 @@ struct Connection {
             else if (cmd == "quit") noreply = true;
             else if (cmd == "watch") watching = true;
             *n = cons;
+            // text/parser.go:163-171: the command and its keys, joined by ", "
+            std::string keys;
+            const size_t k0 = IsRetrieval(cmd) ? (cmd.compare(0, 3, "gat") == 0 ? 2 : 1) : (IsStorage(cmd) || cmd == "delete" || cmd == "incr" || cmd == "decr" || cmd == "touch") ? 1 : nt;
+            const size_t k1 = IsRetrieval(cmd) ? nt : k0 + 1;
+            for (size_t k = k0; k < k1 && k < nt; k++) keys += (keys.empty() ? "" : ", ") + tok[k];
+            const std::string l7 = GenericL7("textmemcached", {{"command", cmd}, {"keys", keys}});
             if (v == L7G_ALLOW) {
                 if (!noreply) reply_queue.push_back({cmd, false});
+                Log(kEntryRequest, l7);
                 return FILTEROP_PASS;
             }
             if (!noreply) {
                 if (reply_queue.empty()) Inject(true, kDeniedText, sizeof kDeniedText - 1);
                 else reply_queue.push_back({cmd, true});
             }
+            Log(kEntryDenied, l7);
             return FILTEROP_DROP;
         }
         if (reply_queue.empty()) throw Panic();  // p.replyQueue[0]
@@ -435,7 +580,15 @@ struct Connection {
             if (v != L7G_ALLOW && v != L7G_DENY) { *n = cons; return FILTEROP_ERROR; }  // ERROR, INVALID_FRAME_TYPE / 0
             requests++;
             *n = cons;
-            if (v == L7G_ALLOW) return FILTEROP_PASS;
+            const uint8_t *hb = (const uint8_t *)d.data();
+            const uint32_t klen = (uint32_t)hb[2] << 8 | hb[3], ext = hb[4];
+            const std::string l7 = GenericL7("binarymemcached", {{"opcode", std::to_string(hb[1])},
+                                                                 {"key", d.size() >= 24 + ext + klen ? d.substr(24 + ext, klen) : std::string()}});
+            if (v == L7G_ALLOW) {
+                Log(kEntryRequest, l7);
+                return FILTEROP_PASS;
+            }
+            Log(kEntryDenied, l7);
             const uint8_t magic = (uint8_t)(0x81 | (uint8_t)d[0]);
             if (requests == replies + 1) BinaryInjectDenied(magic);
             else inject_queue.push_back({magic, requests});
@@ -448,6 +601,8 @@ struct Connection {
         const uint32_t keylen = (uint32_t)b[2] << 8 | b[3], extras = b[4];
         if (keylen > 0 && 24 + keylen + extras > d.size()) { *n = 24 + keylen + extras - (int64_t)d.size(); return FILTEROP_MORE; }
         if ((b[0] & 0x80) != 0x80) { *n = FILTEROP_ERROR_INVALID_FRAME_TYPE; return FILTEROP_ERROR; }
+        Log(kEntryResponse, GenericL7("binarymemcached", {{"opcode", std::to_string(b[1])},
+                                                          {"key", d.size() >= 24 + extras + keylen ? d.substr(24 + extras, keylen) : std::string()}}));
         replies++;
         *n = (int64_t)(uint32_t)(body + 24u);
         return FILTEROP_PASS;
@@ -541,6 +696,7 @@ uint64_t OpenModule(GoSlice params, uint8_t debug) {
     ins->node = node.empty() ? "host~127.0.0.1~libcilium-" + std::to_string(ins->id) + "~localdomain" : node;
     ins->xds = xds;
     ins->alog = alog;
+    ins->log.path = alog;
     ins->eng = e;
     g_instances[ins->id] = ins;
     return ins->id;
@@ -566,7 +722,6 @@ void CloseModule(uint64_t id) {
 FilterResult OnNewConnection(uint64_t instance_id, GoString proto, uint64_t connection_id, uint8_t ingress,
                              uint32_t src_id, uint32_t dst_id, GoString src_addr, GoString dst_addr,
                              GoString policy_name, GoSlice *orig_buf, GoSlice *reply_buf) {
-    (void)src_addr;
     auto ins = FindInstance(instance_id);
     if (!ins) return FILTER_INVALID_INSTANCE;
     std::string p = Str(proto);
@@ -585,6 +740,8 @@ FilterResult OnNewConnection(uint64_t instance_id, GoString proto, uint64_t conn
     c->dst = dst_id;
     c->port = port;
     c->policy = Str(policy_name);
+    c->src_addr = Str(src_addr);
+    c->dst_addr = Str(dst_addr);
     c->proto = p;
     c->kind = kind;
     c->orig = orig_buf;

@@ -130,6 +130,25 @@ class Engine:
             return None
         return out
 
+    def flow_stats_enable(self, on=True):
+        rc = self._lib.l7g_flow_stats_enable(self._h, 1 if on else 0)
+        if rc != 0:
+            raise RuntimeError(f"l7g_flow_stats_enable: {rc}")
+
+    def flow_stats(self, reset=False):
+        """{(policy, proto, port, ingress): (received, forwarded, denied, error)}
+        accumulated since the last reset (pkg/endpoint UpdateProxyStatistics)."""
+        n = C.c_uint32(0)
+        rc = self._lib.l7g_flow_stats(self._h, None, 0, C.byref(n), 0)
+        if rc != 0:
+            raise RuntimeError(f"l7g_flow_stats: {rc}")
+        arr = (_lib.FlowStat * max(1, n.value))()
+        rc = self._lib.l7g_flow_stats(self._h, arr, n.value, C.byref(n), 1 if reset else 0)
+        if rc != 0:
+            raise RuntimeError(f"l7g_flow_stats: {rc}")
+        return {(x.policy, x.proto, x.port, x.ingress): (x.received, x.forwarded, x.denied, x.error)
+                for x in arr[:n.value]}
+
     def stats(self):
         s = _lib.Stats()
         self._lib.l7g_stats(self._h, C.byref(s))

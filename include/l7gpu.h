@@ -46,7 +46,7 @@ enum {
     L7G_ALLOW = 1,       /* policy allows; rule = matched global rule id or -1 */
     L7G_PARSE_ERROR = 2, /* malformed request (connection is closed by the caller) */
     L7G_INCOMPLETE = 3,  /* more bytes are needed (proxylib MORE) */
-    L7G_UNSUPPORTED = 4, /* framing not handled on the device (chunked body, compressed Kafka set) */
+    L7G_UNSUPPORTED = 4, /* no parser for the connection, a request outside the arena, a compressed Kafka set */
 };
 
 /* memcached: proxylib picks the text or binary parser from the first byte a
@@ -144,6 +144,24 @@ int l7g_stats(l7g_engine *e, l7g_stats_t *out);
  * for the last call and returns the device time in ms of its four stages
  * (partition, HTTP, Kafka, memcached; 0 = not launched).  Off by default. */
 int l7g_profile_enable(l7g_engine *e, int on);
+
+/* Proxy statistics (pkg/endpoint/endpoint.go:2207-2233 UpdateProxyStatistics,
+ * the policy_l7_received/forwarded/denied/parse_errors_total counters of
+ * pkg/metrics/metrics.go:269-296): while enabled, every l7g_classify adds, per
+ * (policy, protocol, port, direction) of its connections, the requests that
+ * completed a flow -- ALLOW = forwarded, DENY = denied, PARSE_ERROR = error,
+ * each also received -- into a device accumulator.  l7g_flow_stats copies the
+ * non-zero entries out (at most cap; *n = how many there are) and, with reset,
+ * zeroes the accumulator.  Off by default. */
+typedef struct {
+    int32_t policy;
+    uint8_t proto;     /* L7G_PROTO_* */
+    uint8_t ingress;
+    uint16_t port;
+    uint64_t received, forwarded, denied, error;
+} l7g_flow_stat_t;
+int l7g_flow_stats_enable(l7g_engine *e, int on);
+int l7g_flow_stats(l7g_engine *e, l7g_flow_stat_t *out, uint32_t cap, uint32_t *n, int reset);
 int l7g_profile_last(l7g_engine *e, float out_ms[4]);
 
 /* Profiling hook: per-phase cycle totals of the HTTP kernel (slots: 0 window

@@ -65,6 +65,24 @@ def _pool():
     _msg(fd, "Any", [(1, "type_url", T.TYPE_STRING, OPT), (2, "value", T.TYPE_BYTES, OPT)])
     _msg(fd, "DiscoveryResponse", [(1, "version_info", T.TYPE_STRING, OPT), (2, "resources", T.TYPE_MESSAGE, REP, ".cilium.Any"),
                                    (4, "type_url", T.TYPE_STRING, OPT), (5, "nonce", T.TYPE_STRING, OPT)])
+    # cilium.LogEntry (pkg/envoy/cilium/accesslog.pb.go:79-400): the access-log records
+    _msg(fd, "KeyValue", [(1, "key", T.TYPE_STRING, OPT), (2, "value", T.TYPE_STRING, OPT)])
+    _msg(fd, "HttpLogEntry", [(1, "http_protocol", T.TYPE_INT32, OPT), (2, "scheme", T.TYPE_STRING, OPT),
+                              (3, "host", T.TYPE_STRING, OPT), (4, "path", T.TYPE_STRING, OPT),
+                              (5, "method", T.TYPE_STRING, OPT), (6, "headers", T.TYPE_MESSAGE, REP, ".cilium.KeyValue"),
+                              (7, "status", T.TYPE_UINT32, OPT)])
+    fentry = descriptor_pb2.DescriptorProto(name="FieldsEntry", options=descriptor_pb2.MessageOptions(map_entry=True))
+    fentry.field.add(name="key", number=1, type=T.TYPE_STRING, label=OPT)
+    fentry.field.add(name="value", number=2, type=T.TYPE_STRING, label=OPT)
+    _msg(fd, "L7LogEntry", [(1, "proto", T.TYPE_STRING, OPT), (2, "fields", T.TYPE_MESSAGE, REP, ".cilium.L7LogEntry.FieldsEntry")],
+         nested=[fentry])
+    _msg(fd, "LogEntry", [
+        (1, "timestamp", T.TYPE_UINT64, OPT), (15, "is_ingress", T.TYPE_BOOL, OPT), (3, "entry_type", T.TYPE_INT32, OPT),
+        (4, "policy_name", T.TYPE_STRING, OPT), (5, "cilium_rule_ref", T.TYPE_STRING, OPT),
+        (6, "source_security_id", T.TYPE_UINT32, OPT), (16, "destination_security_id", T.TYPE_UINT32, OPT),
+        (7, "source_address", T.TYPE_STRING, OPT), (8, "destination_address", T.TYPE_STRING, OPT),
+        (100, "http", T.TYPE_MESSAGE, OPT, ".cilium.HttpLogEntry", 0),
+        (102, "generic_l7", T.TYPE_MESSAGE, OPT, ".cilium.L7LogEntry", 0)], oneofs=["l7"])
     pool.Add(fd)
     return pool
 
