@@ -65,18 +65,24 @@ struct AccessLog {
     int fd = -1;
     uint64_t sent = 0, failed = 0;
     ~AccessLog() { if (fd >= 0) close(fd); }
+    bool ConnectLocked() {  // net.DialUnix("unixpacket", ...)
+        if (fd >= 0) return true;
+        sockaddr_un a{};
+        a.sun_family = AF_UNIX;
+        if (path.empty() || path.size() >= sizeof a.sun_path) return false;
+        memcpy(a.sun_path, path.data(), path.size());
+        fd = socket(AF_UNIX, SOCK_SEQPACKET | SOCK_CLOEXEC, 0);
+        if (fd >= 0 && connect(fd, (const sockaddr *)&a, sizeof a) != 0) { close(fd); fd = -1; }
+        return fd >= 0;
+    }
+    void Connect() {  // NewClient dials once up front (client.go:97-104)
+        std::lock_guard<std::mutex> g(mu);
+        ConnectLocked();
+    }
     void Send(const std::string &msg) {
         if (path.empty()) return;
         std::lock_guard<std::mutex> g(mu);
-        if (fd < 0) {
-            sockaddr_un a{};
-            a.sun_family = AF_UNIX;
-            if (path.size() >= sizeof a.sun_path) { failed++; return; }
-            memcpy(a.sun_path, path.data(), path.size());
-            fd = socket(AF_UNIX, SOCK_SEQPACKET | SOCK_CLOEXEC, 0);
-            if (fd >= 0 && connect(fd, (const sockaddr *)&a, sizeof a) != 0) { close(fd); fd = -1; }
-            if (fd < 0) { failed++; return; }
-        }
+        if (!ConnectLocked()) { failed++; return; }
         if (send(fd, msg.data(), msg.size(), MSG_NOSIGNAL) != (ssize_t)msg.size()) {
             close(fd);  // marked broken: redialled on the next record
             fd = -1;
@@ -697,6 +703,7 @@ uint64_t OpenModule(GoSlice params, uint8_t debug) {
     ins->xds = xds;
     ins->alog = alog;
     ins->log.path = alog;
+    ins->log.Connect();
     ins->eng = e;
     g_instances[ins->id] = ins;
     return ins->id;
