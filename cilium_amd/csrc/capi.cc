@@ -22,8 +22,8 @@
 #include "regex/re_dfa.h"
 
 namespace l7 {
-hipError_t LaunchHttpClassify(const Batch &B, const HttpTables &T, bool any_cold, bool answer_other,
-                              hipStream_t stream);
+hipError_t LaunchHttpClassify(const Batch &B, const HttpTables &T, const uint32_t *sel, const uint32_t *sel_count,
+                              bool any_cold, bool answer_other, hipStream_t stream);
 hipError_t LaunchKafkaClassify(const Batch &B, const KafkaTables &T, const uint32_t *sel, const uint32_t *sel_count,
                                bool answer_other, hipStream_t stream);
 hipError_t LaunchMemcacheClassify(const Batch &B, const McTables &T, const uint32_t *sel, const uint32_t *sel_count,
@@ -34,7 +34,8 @@ size_t CountersScratchBytes();
 hipError_t LaunchFlowStats(const Batch &B, uint32_t nkeys, uint64_t *acc, hipStream_t stream);
 uint32_t FlowStatsMaxKeys();
 hipError_t LaunchHttpNfa(const Batch &B, const HttpTables &T, hipStream_t stream);
-hipError_t LaunchPartition(const Batch &B, uint32_t *sel_kafka, uint32_t *sel_mc, uint32_t *counts, hipStream_t stream);
+hipError_t LaunchPartition(const Batch &B, uint32_t *sel_kafka, uint32_t *sel_mc, uint32_t *sel_http, uint32_t *counts,
+                           hipStream_t stream);
 hipError_t HttpPhaseTimes(uint64_t *out, bool reset);
 hipError_t KafkaPhaseTimes(uint64_t *out, bool reset);
 }  // namespace l7
@@ -422,9 +423,9 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
     // (a Kafka-only engine partitions too: the kind / length lists keep the
     // Kafka kernel's waves converged, 1.55 -> 0.99 ms on cfg3)
     const bool partitioned = nproto > 1 || e->has_kafka;
-    uint32_t *sel_k = nullptr, *sel_m = nullptr, *cnt = nullptr;
+    uint32_t *sel_k = nullptr, *sel_m = nullptr, *sel_h = nullptr, *cnt = nullptr;
     if (partitioned) {
-        const size_t need = 16 + (L7_KAFKA_CLASSES + 1) * (size_t)n;
+        const size_t need = 16 + (L7_KAFKA_CLASSES + 2) * (size_t)n;
         // the scratch may still be in use by the previous batch (any stream)
         if (e->launched) rc = hipStreamWaitEvent(s, e->done_ev, 0);
         if (rc == hipSuccess && need > e->sel_cap) {
@@ -438,9 +439,10 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
             if (rc == hipSuccess) e->sel_cap = need;
         }
         if (rc != hipSuccess) return (int)rc;
-        cnt = e->d_sel;  // [0, L7_KAFKA_CLASSES) Kafka length classes, then memcached
+        cnt = e->d_sel;  // [0, L7_KAFKA_CLASSES) Kafka classes, then memcached, then HTTP
         sel_k = e->d_sel + 16;
         sel_m = sel_k + L7_KAFKA_CLASSES * (size_t)n;
+        sel_h = sel_m + (size_t)n;
         rc = hipMemsetAsync(cnt, 0, 16 * sizeof(uint32_t), s);
     }
     // rule sets with NFA-fallback matchers: the pre-pass writes one u64 per request
@@ -469,10 +471,11 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
     const bool run[4] = {partitioned, e->has_http || nproto == 0, e->has_kafka, e->has_mc};
     for (int k = 0; k < 4; k++) e->prof_ran[k] = run[k];
     mark(0);
-    if (rc == hipSuccess && run[0]) rc = LaunchPartition(B, sel_k, sel_m, cnt, s);
+    if (rc == hipSuccess && run[0]) rc = LaunchPartition(B, sel_k, sel_m, sel_h, cnt, s);
     mark(1);
     if (rc == hipSuccess && run[1] && nfa) rc = LaunchHttpNfa(B, ht, s);
-    if (rc == hipSuccess && run[1]) rc = LaunchHttpClassify(B, ht, e->any_cold, !partitioned, s);
+    if (rc == hipSuccess && run[1])
+        rc = LaunchHttpClassify(B, ht, sel_h, cnt ? cnt + L7_KAFKA_CLASSES + 1 : nullptr, e->any_cold, !partitioned, s);
     mark(2);
     if (rc == hipSuccess && run[2]) rc = LaunchKafkaClassify(B, e->kt, sel_k, cnt, !partitioned, s);
     mark(3);

@@ -1046,8 +1046,12 @@ __device__ __forceinline__ void run_tile(Lane &L, const uint8_t *img, uint8_t *w
 //               them when no hot kernel runs (T.hot_ruleset < 0).
 // answer_other: also answer the entries no classifier owns (unknown connection,
 // no parser) UNSUPPORTED; false when partition_kernel has answered them.
+// sel: the HTTP requests of a mixed batch (partition_kernel), tiles of 64
+// list entries; null: the whole batch, tiles of 64 consecutive requests.
 template <bool kHot>
-__global__ __launch_bounds__(kBlock) void http_classify_kernel(Batch B, HttpTables T, uint32_t answer_other) {
+__global__ __launch_bounds__(kBlock) void http_classify_kernel(Batch B, HttpTables T, const uint32_t *__restrict__ sel,
+                                                               const uint32_t *__restrict__ sel_count,
+                                                               uint32_t answer_other) {
     const uint8_t *__restrict__ arena = B.arena;
     const uint32_t n = B.n, nconns = B.nconns;
     __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
@@ -1069,10 +1073,12 @@ __global__ __launch_bounds__(kBlock) void http_classify_kernel(Batch B, HttpTabl
 
     const Out O{B.verdict, B.rule, B.consumed, T.nfa_bits};
     uint8_t *wave_lds = lds + wave * kWaveLds;
-    const uint32_t ntiles = (n + 63) / 64;
+    const uint32_t m = sel ? *sel_count : n;
+    const uint32_t ntiles = (m + 63) / 64;
     for (uint32_t tile = blockIdx.x * kWaves + wave; tile < ntiles; tile += gridDim.x * kWaves) {
         Lane L;
-        L.idx = tile * 64 + lane;
+        const uint32_t slot = tile * 64 + lane;
+        L.idx = sel ? (slot < m ? sel[slot] : n) : slot;
         L.done = true;
         L.owed = false;
         L.verdict = V_UNSUPPORTED;
@@ -1114,8 +1120,8 @@ __global__ __launch_bounds__(kBlock) void http_classify_kernel(Batch B, HttpTabl
 // Host-side launcher (called from the C-ABI): persistent grids of one
 // 512-thread workgroup per CU; the hot-rule-set kernel, then (only if some
 // HTTP connection uses another rule set) the general one.
-hipError_t LaunchHttpClassify(const Batch &B, const HttpTables &T, bool any_cold, bool answer_other,
-                              hipStream_t stream) {
+hipError_t LaunchHttpClassify(const Batch &B, const HttpTables &T, const uint32_t *sel, const uint32_t *sel_count,
+                              bool any_cold, bool answer_other, hipStream_t stream) {
     if (B.n == 0) return hipSuccess;
     static int num_cus = 0;
     if (num_cus == 0) {
@@ -1130,9 +1136,9 @@ hipError_t LaunchHttpClassify(const Batch &B, const HttpTables &T, bool any_cold
     const bool hot = T.hot_ruleset >= 0;
     const uint32_t other = answer_other ? 1u : 0u;
     if (hot)
-        hipLaunchKernelGGL(http_classify_kernel<true>, dim3(blocks), dim3(kBlock), 0, stream, B, T, other);
+        hipLaunchKernelGGL(http_classify_kernel<true>, dim3(blocks), dim3(kBlock), 0, stream, B, T, sel, sel_count, other);
     if (!hot || any_cold)
-        hipLaunchKernelGGL(http_classify_kernel<false>, dim3(blocks), dim3(kBlock), 0, stream, B, T, other);
+        hipLaunchKernelGGL(http_classify_kernel<false>, dim3(blocks), dim3(kBlock), 0, stream, B, T, sel, sel_count, other);
     return hipGetLastError();
 }
 

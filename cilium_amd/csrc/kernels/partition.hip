@@ -22,9 +22,9 @@ namespace {
 constexpr int kBlock = 256;
 constexpr int kPer = 16;
 constexpr int kWaves = kBlock / 64;
-// list classes: 0..kKafkaClasses-1 Kafka by request length, then memcached
+// list classes: 0..kKafkaClasses-1 Kafka by kind / length, then memcached, then HTTP
 constexpr int kKafkaClasses = L7_KAFKA_CLASSES;
-constexpr int kClasses = kKafkaClasses + 1;
+constexpr int kClasses = kKafkaClasses + 2;
 
 static_assert(kKafkaClasses == 1 || kKafkaClasses == 8, "length classes");
 // Kafka list class: the decode path a lane takes is set by the request kind
@@ -39,13 +39,17 @@ __device__ __forceinline__ uint8_t kafka_class(const uint8_t *b, uint32_t len) {
 }
 }  // namespace
 
-// Lists: Kafka class c at sel_kafka + c * n, memcached at sel_mc; counts[c]
-// entries each.  Requests no classifier owns (unknown connection index, a
+// Lists: Kafka class c at sel_kafka + c * n, memcached at sel_mc, HTTP at
+// sel_http; counts[c] entries each (Kafka classes, memcached, HTTP).  Within a
+// block's 4096 requests every list keeps stream order, so an HTTP tile of 64
+// list entries is, but for the tiles that straddle two blocks, a window of
+// the stream (the HTTP kernel's value-stop map streams that window).  Requests no classifier owns (unknown connection index, a
 // connection without a parser) are answered here: UNSUPPORTED, rule -1,
 // consumed 0, so every request of the batch gets a verdict whichever
 // classifiers run (the HTTP kernel is then told not to answer them again).
 __global__ __launch_bounds__(kBlock) void partition_kernel(Batch B, uint32_t *__restrict__ sel_kafka,
                                                            uint32_t *__restrict__ sel_mc,
+                                                           uint32_t *__restrict__ sel_http,
                                                            uint32_t *__restrict__ counts) {
     const uint32_t n = B.n;
     __shared__ uint32_t s_off[kWaves][kClasses];
@@ -67,7 +71,8 @@ __global__ __launch_bounds__(kBlock) void partition_kernel(Batch B, uint32_t *__
                 cls = 1 + kafka_class(B.arena + off, l7_in_arena(off, len, B.arena_len) ? len : 0);
             }
             else if (proto == PROTO_MEMCACHE) cls = 1 + kKafkaClasses;
-            else if (proto != PROTO_HTTP) {
+            else if (proto == PROTO_HTTP) cls = 2 + kKafkaClasses;
+            else {
                 B.verdict[idx] = V_UNSUPPORTED;
                 B.rule[idx] = -1;
                 B.consumed[idx] = 0;
@@ -102,7 +107,7 @@ __global__ __launch_bounds__(kBlock) void partition_kernel(Batch B, uint32_t *__
         for (int c = 0; c < kClasses; c++) {
             const uint64_t mk = __ballot(p[r] == c + 1);
             if (p[r] == c + 1) {
-                uint32_t *dst = c < kKafkaClasses ? sel_kafka + (size_t)c * n : sel_mc;
+                uint32_t *dst = c < kKafkaClasses ? sel_kafka + (size_t)c * n : c == kKafkaClasses ? sel_mc : sel_http;
                 dst[off[c] + __popcll(mk & below)] = idx;
             }
             off[c] += __popcll(mk);
@@ -111,10 +116,11 @@ __global__ __launch_bounds__(kBlock) void partition_kernel(Batch B, uint32_t *__
 }
 
 // counts[0..kClasses) must be zero on entry (the caller clears them on `stream`).
-hipError_t LaunchPartition(const Batch &B, uint32_t *sel_kafka, uint32_t *sel_mc, uint32_t *counts, hipStream_t stream) {
+hipError_t LaunchPartition(const Batch &B, uint32_t *sel_kafka, uint32_t *sel_mc, uint32_t *sel_http, uint32_t *counts,
+                           hipStream_t stream) {
     if (B.n == 0) return hipSuccess;
     const uint32_t blocks = (uint32_t)(((uint64_t)B.n + kBlock * kPer - 1) / (kBlock * kPer));
-    hipLaunchKernelGGL(partition_kernel, dim3(blocks), dim3(kBlock), 0, stream, B, sel_kafka, sel_mc, counts);
+    hipLaunchKernelGGL(partition_kernel, dim3(blocks), dim3(kBlock), 0, stream, B, sel_kafka, sel_mc, sel_http, counts);
     return hipGetLastError();
 }
 
