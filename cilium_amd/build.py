@@ -99,6 +99,28 @@ def build(verbose=False, jobs=8, timing=False, variant=None, defines=()):
     return LIB_OUT
 
 
+def build_test_natives(verbose=False):
+    """tests/native/*.cc -> tests/native/bin/<name>: C++ drivers of the C-ABI
+    headers (e.g. include/l7gpu_envoy.hpp), linked against libl7gpu.so."""
+    lib = build(verbose=verbose)
+    root = os.path.dirname(HERE)
+    out = []
+    for src in sorted(glob.glob(os.path.join(root, "tests", "native", "*.cc"))):
+        name = os.path.splitext(os.path.basename(src))[0]
+        exe = os.path.join(root, "tests", "native", "bin", name)
+        deps = [src, lib] + headers()
+        if not os.path.exists(exe) or os.path.getmtime(exe) < max(os.path.getmtime(d) for d in deps):
+            os.makedirs(os.path.dirname(exe), exist_ok=True)
+            cmd = ["g++", "-O2", "-std=c++17", "-Wall", "-I" + os.path.join(root, "include"), src, "-o", exe + ".tmp",
+                   "-L" + HERE, "-l:libl7gpu.so", "-Wl,-rpath,$ORIGIN/../../../cilium_amd", "-pthread"]
+            r = subprocess.run(cmd, capture_output=True, text=True)
+            if r.returncode != 0:
+                raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+            os.replace(exe + ".tmp", exe)
+        out.append(exe)
+    return out
+
+
 if __name__ == "__main__":
     # python -m cilium_amd.build [--timing] [--variant NAME -DX=Y ...]
     argv = sys.argv[1:]

@@ -47,3 +47,12 @@ def test_engine_without_gpu_fails_loudly():
 def test_debug_regex_error_text():
     with pytest.raises(ValueError, match=r"missing argument to repetition operator: `\*`"):
         cilium_amd.debug_regex("*", b"")
+
+
+def test_envoy_adapter_driver_links():
+    """The C++ adapter header compiles against the C-ABI and its driver links
+    libl7gpu.so (run on the GPU by tests/test_gpu_envoy_adapter.py)."""
+    from cilium_amd import build
+    exe = build.build_test_natives()[0]
+    out = subprocess.run(["ldd", exe], capture_output=True, text=True).stdout
+    assert "libl7gpu.so" in out and "not found" not in out.split("libl7gpu.so")[1].split("\n")[0]
