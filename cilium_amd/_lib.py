@@ -12,7 +12,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("L7G_LIB") or os.path.join(HERE, "libl7gpu.so")
 
 DENY, ALLOW, PARSE_ERROR, INCOMPLETE, UNSUPPORTED = 0, 1, 2, 3, 4
-PROTO_HTTP, PROTO_KAFKA, PROTO_MEMCACHE = 1, 2, 3
+PROTO_HTTP, PROTO_KAFKA, PROTO_MEMCACHE, PROTO_R2D2 = 1, 2, 3, 4
 VERDICT_NAMES = {DENY: "DENY", ALLOW: "ALLOW", PARSE_ERROR: "PARSE_ERROR",
                  INCOMPLETE: "INCOMPLETE", UNSUPPORTED: "UNSUPPORTED"}
 
@@ -31,7 +31,7 @@ class Stats(C.Structure):
         ("table_bytes", C.c_uint64), ("http_image_bytes", C.c_uint64), ("hot_ruleset", C.c_int32),
         ("hot_image_bytes", C.c_uint32)] + [
         (n, C.c_uint32) for n in ("mc_rulesets", "mc_rules", "mc_dfas", "mc_dfa_states", "http_nfas", "mc_nfas")] + [
-        ("nfa_pool_bytes", C.c_uint64)]
+        ("nfa_pool_bytes", C.c_uint64), ("r2d2_rulesets", C.c_uint32), ("r2d2_rules", C.c_uint32)]
 
 
 EXPORTS = (

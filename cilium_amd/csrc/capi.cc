@@ -16,6 +16,7 @@
 #include "engine/kafka_compile.h"
 #include "engine/mc_compile.h"
 #include "engine/nfa_pool.h"
+#include "engine/r2_compile.h"
 #include "policy/npds_proto.h"
 #include "policy/policy.h"
 #include "regex/nfa_walk.h"
@@ -28,6 +29,7 @@ hipError_t LaunchKafkaClassify(const Batch &B, const KafkaTables &T, const uint3
                                bool answer_other, hipStream_t stream);
 hipError_t LaunchMemcacheClassify(const Batch &B, const McTables &T, const uint32_t *sel, const uint32_t *sel_count,
                                   bool answer_other, hipStream_t stream);
+hipError_t LaunchR2d2Classify(const Batch &B, const R2Tables &T, bool answer_other, hipStream_t stream);
 hipError_t LaunchCounters(const uint8_t *verdict, const int32_t *rule, uint32_t n, uint32_t nrules,
                           uint64_t *counters, uint32_t *scratch, hipStream_t stream);
 size_t CountersScratchBytes();
@@ -49,6 +51,7 @@ struct l7g_engine {
     std::unique_ptr<HttpCompiler> hc;
     std::unique_ptr<KafkaCompiler> kc;
     std::unique_ptr<McCompiler> mc;
+    std::unique_ptr<R2Compiler> r2;
     std::vector<l7g_conn_t> attrs;
     std::vector<DevConn> conns;
     uint8_t *d_blob = nullptr;
@@ -58,8 +61,9 @@ struct l7g_engine {
     HttpTables ht{};
     KafkaTables kt{};
     McTables mt{};
+    R2Tables rt{};
     bool tables_dirty = true, conns_dirty = true;
-    bool has_http = false, has_kafka = false, has_mc = false;
+    bool has_http = false, has_kafka = false, has_mc = false, has_r2 = false;
     int32_t hot_ruleset = -1;  // HTTP rule set staged in LDS (most connections)
     // l7g_classify_host scratch (grow-only), guarded by smu
     std::mutex smu;
@@ -122,7 +126,7 @@ bool ResolveOne(l7g_engine *e, size_t i, std::string *err) {
     DevConn &c = e->conns[i];
     c = DevConn{-1, PROTO_NONE, 0, 0xFFFF};
     c.proto = a.proto;
-    if (a.proto == PROTO_HTTP || a.proto == PROTO_KAFKA || a.proto == PROTO_MEMCACHE) {
+    if (a.proto == PROTO_HTTP || a.proto == PROTO_KAFKA || a.proto == PROTO_MEMCACHE || a.proto == PROTO_R2D2) {
         const auto key = std::make_tuple(a.policy, a.proto, a.port, (uint8_t)(a.ingress != 0));
         auto it = e->skeys.find(key);
         if (it == e->skeys.end() && e->skey_list.size() < FlowStatsMaxKeys()) {
@@ -153,6 +157,10 @@ bool ResolveOne(l7g_engine *e, size_t i, std::string *err) {
         c.ruleset = e->mc->RulesetFor(a.policy, a.ingress != 0, a.port, a.src_id, err);
         if (c.ruleset < 0) return false;
         e->has_mc = true;
+    } else if (a.proto == PROTO_R2D2) {  // proxylib r2d2: SrcId in both directions, as memcached
+        c.ruleset = e->r2->RulesetFor(a.policy, a.ingress != 0, a.port, a.src_id, err);
+        if (c.ruleset < 0) return false;
+        e->has_r2 = true;
     }
     return true;
 }
@@ -173,13 +181,14 @@ void PickHot(l7g_engine *e) {
 }
 
 size_t TableRulesets(const l7g_engine *e) {
-    return e->hc->image().rulesets.size() + e->kc->image().rulesets.size() + e->mc->image().rulesets.size();
+    return e->hc->image().rulesets.size() + e->kc->image().rulesets.size() + e->mc->image().rulesets.size() +
+           e->r2->image().rulesets.size();
 }
 
 // Resolve every connection (policy update / connection table replaced).
 bool ResolveConns(l7g_engine *e, std::string *err) {
     e->conns.assign(e->attrs.size(), DevConn{-1, PROTO_NONE, 0, 0xFFFF});
-    e->has_http = e->has_kafka = e->has_mc = false;
+    e->has_http = e->has_kafka = e->has_mc = e->has_r2 = false;
     for (size_t i = 0; i < e->attrs.size(); i++)
         if (!ResolveOne(e, i, err)) return false;
     PickHot(e);
@@ -198,6 +207,8 @@ hipError_t Upload(l7g_engine *e) {
                k_th = Put(blob, K.topic_hash), k_ch = Put(blob, K.client_hash), k_s = Put(blob, K.strings);
         const McImage &M = e->mc->image();
         size_t m_rs = Put(blob, M.rulesets), m_img = Put(blob, M.images), m_nfa = Put(blob, M.nfa_pool);
+        const R2Image &R = e->r2->image();
+        size_t r_rs = Put(blob, R.rulesets), r_img = Put(blob, R.images), r_nfa = Put(blob, R.nfa_pool);
         uint8_t *d = nullptr;
         if ((rc = hipMalloc(&d, blob.size())) != hipSuccess) return rc;
         if ((rc = hipMemcpy(d, blob.data(), blob.size(), hipMemcpyHostToDevice)) != hipSuccess) { hipFree(d); return rc; }
@@ -226,6 +237,11 @@ hipError_t Upload(l7g_engine *e) {
         MT.images = d + m_img;
         MT.nrulesets = (uint32_t)M.rulesets.size();
         MT.nfa_pool = M.nfa_pool.empty() ? nullptr : d + m_nfa;
+        R2Tables &RT = e->rt;
+        RT.rulesets = (const DevRuleset *)(d + r_rs);
+        RT.images = d + r_img;
+        RT.nrulesets = (uint32_t)R.rulesets.size();
+        RT.nfa_pool = R.nfa_pool.empty() ? nullptr : d + r_nfa;
         e->tables_dirty = false;
     }
     if (e->conns_dirty) {
@@ -258,6 +274,7 @@ l7g_engine *l7g_engine_create(int device, char *err, size_t errlen) {
         e->hc = std::make_unique<HttpCompiler>(e->ps.get());
         e->kc = std::make_unique<KafkaCompiler>(e->ps.get());
         e->mc = std::make_unique<McCompiler>(e->ps.get());
+        e->r2 = std::make_unique<R2Compiler>(e->ps.get());
         return e;
     }
     int ndev = 0;
@@ -278,6 +295,7 @@ l7g_engine *l7g_engine_create(int device, char *err, size_t errlen) {
     e->hc = std::make_unique<HttpCompiler>(e->ps.get());
     e->kc = std::make_unique<KafkaCompiler>(e->ps.get());
     e->mc = std::make_unique<McCompiler>(e->ps.get());
+    e->r2 = std::make_unique<R2Compiler>(e->ps.get());
     return e;
 }
 
@@ -326,15 +344,18 @@ static int PolicySwap(l7g_engine *e, std::unique_ptr<PolicySet> ps, char *err, s
     auto hc = std::make_unique<HttpCompiler>(ps.get());
     auto kc = std::make_unique<KafkaCompiler>(ps.get());
     auto mc = std::make_unique<McCompiler>(ps.get());
+    auto r2 = std::make_unique<R2Compiler>(ps.get());
     std::swap(e->ps, ps);
     std::swap(e->hc, hc);
     std::swap(e->kc, kc);
     std::swap(e->mc, mc);
+    std::swap(e->r2, r2);
     if (!ResolveConns(e, &m)) {  // roll back: previous version stays in force
         std::swap(e->ps, ps);
         std::swap(e->hc, hc);
         std::swap(e->kc, kc);
         std::swap(e->mc, mc);
+        std::swap(e->r2, r2);
         std::string m2;
         ResolveConns(e, &m2);
         set_err(err, errlen, m);
@@ -419,7 +440,7 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
     // the requests no classifier owns (unknown connection, no parser) itself.
     // A single-protocol HTTP or memcached engine skips it; its one kernel walks the whole batch
     // and answers those requests.
-    const int nproto = (int)e->has_http + (int)e->has_kafka + (int)e->has_mc;
+    const int nproto = (int)e->has_http + (int)e->has_kafka + (int)e->has_mc + (int)e->has_r2;
     // (a Kafka-only engine partitions too: the kind / length lists keep the
     // Kafka kernel's waves converged, 1.55 -> 0.99 ms on cfg3)
     const bool partitioned = nproto > 1 || e->has_kafka;
@@ -481,6 +502,8 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
     mark(3);
     if (rc == hipSuccess && run[3])
         rc = LaunchMemcacheClassify(B, e->mt, sel_m, cnt ? cnt + L7_KAFKA_CLASSES : nullptr, !partitioned, s);
+    // r2d2 (proxylib's example line protocol): one lane per request over the whole batch
+    if (rc == hipSuccess && e->has_r2) rc = LaunchR2d2Classify(B, e->rt, !partitioned, s);
     mark(4);
     // proxy statistics (accumulated on the device until read)
     if (rc == hipSuccess && e->flow_stats && !e->skey_list.empty()) {
@@ -583,7 +606,9 @@ int l7g_stats(l7g_engine *e, l7g_stats_t *out) {
     out->mc_dfa_states = (uint32_t)M.dfa_states;
     out->http_nfas = (uint32_t)H.nfas;
     out->mc_nfas = (uint32_t)M.nfas;
-    out->nfa_pool_bytes = H.nfa_pool.size() + M.nfa_pool.size();
+    out->nfa_pool_bytes = H.nfa_pool.size() + M.nfa_pool.size() + e->r2->image().nfa_pool.size();
+    out->r2d2_rulesets = (uint32_t)e->r2->image().rulesets.size();
+    out->r2d2_rules = (uint32_t)e->r2->image().rules;
     return 0;
 }
 

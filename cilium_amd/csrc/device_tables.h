@@ -16,7 +16,7 @@ namespace l7 {
 enum : uint8_t {
     V_DENY = 0, V_ALLOW = 1, V_PARSE_ERROR = 2, V_INCOMPLETE = 3, V_UNSUPPORTED = 4,
 };
-enum : uint8_t { PROTO_NONE = 0, PROTO_HTTP = 1, PROTO_KAFKA = 2, PROTO_MEMCACHE = 3 };
+enum : uint8_t { PROTO_NONE = 0, PROTO_HTTP = 1, PROTO_KAFKA = 2, PROTO_MEMCACHE = 3, PROTO_R2D2 = 4 };
 
 // partition_kernel groups Kafka requests into this many length classes
 #define L7_KAFKA_CLASSES 8
@@ -261,6 +261,33 @@ struct McTables {
     uint32_t nrulesets;
     uint32_t pad;
     const uint8_t *nfa_pool;   // DevNfa pool (null: no keyRegex on the NFA fallback)
+};
+
+// ---------------- r2d2 ----------------
+// proxylib's r2d2 parser (proxylib/r2d2/r2d2parser.go): one line per request;
+// fields split on single spaces; rule r holds iff (cmd_r any or equal) and
+// (no file regex or it matches the file field, unanchored).  One image per
+// rule set (DevRuleset directory), rules in chunks of <= 64.
+constexpr int kR2MaxChunks = 4;     // <= 256 rules per rule set
+struct R2ImgHeader {       // 64 B
+    uint8_t nchunks;
+    uint8_t terminal;      // verdict when no rule matches (V_DENY; V_ALLOW when no L7 rules apply)
+    uint8_t ndfa;
+    uint8_t nnfa;
+    uint32_t cmd_off;      // u64[5][nchunks]: rules whose cmd admits READ, WRITE, HALT, RESET, other
+    uint32_t nofile_off;   // u64[nchunks]: rules without a file regex
+    uint32_t rule_off;     // i32[nchunks * 64]: global rule ids
+    uint32_t dfa_off;      // DevDfa[ndfa] (mask rows u64[nstates][nchunks]: rules whose regex accepts)
+    uint32_t nfa_off;      // DevNfaRef[nnfa] (mask_off: u64[nchunks], the rules of that regex)
+    uint32_t pad[10];
+};
+static_assert(sizeof(R2ImgHeader) == 64, "R2ImgHeader layout");
+struct R2Tables {
+    const DevRuleset *rulesets;
+    const uint8_t *images;
+    uint32_t nrulesets;
+    uint32_t pad;
+    const uint8_t *nfa_pool;
 };
 
 // FNV-1a over lower-cased ASCII (header names are tchar, i.e. ASCII)

@@ -1,0 +1,39 @@
+// r2d2 rule-set compiler (product code): proxylib's r2d2 policy semantics
+// (proxylib/r2d2/r2d2parser.go:31-107 + the proxylib policymap,
+// proxylib/proxylib/policymap.go:91-236) lowered to R2ImgHeader images.
+#pragma once
+#include <cstdint>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../device_tables.h"
+#include "../policy/policy.h"
+
+namespace l7 {
+
+struct R2Image {
+    std::vector<DevRuleset> rulesets;
+    std::vector<uint8_t> images;
+    std::vector<uint8_t> nfa_pool;
+    size_t rules = 0, dfas = 0, nfas = 0;
+};
+
+class R2Compiler {
+public:
+    explicit R2Compiler(const PolicySet *ps) : ps_(ps) {}
+    // remote = the connection's source identity (connection.go:176-179)
+    int RulesetFor(int policy, bool ingress, uint32_t port, uint64_t remote, std::string *err);
+    const R2Image &image() const { return img_; }
+    int max_dfa_states = 4096;
+    int max_single_dfa_states = 65535;
+
+private:
+    const PolicySet *ps_;
+    R2Image img_;
+    std::map<std::pair<std::vector<int>, int>, int> cache_;
+    std::map<std::string, uint64_t> nfa_cache_;
+    int Compile(const std::vector<const R2Rule *> &rules, uint8_t terminal, std::string *err);
+};
+
+}  // namespace l7

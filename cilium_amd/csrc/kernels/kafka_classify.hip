@@ -357,7 +357,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
         int32_t rule = -1;
         uint32_t consumed = 0;
         if (conn.proto != PROTO_KAFKA || conn.ruleset < 0 || (uint32_t)conn.ruleset >= T.nrulesets) {
-            if (!answer_other || conn.proto == PROTO_HTTP || conn.proto == PROTO_MEMCACHE) continue;
+            if (!answer_other || conn.proto == PROTO_HTTP || conn.proto == PROTO_MEMCACHE || conn.proto == PROTO_R2D2) continue;
             verdict = V_UNSUPPORTED;  // unknown connection / no parser
         }
         // ---- proto.ReadReq

@@ -72,7 +72,7 @@ __global__ __launch_bounds__(kBlock) void partition_kernel(Batch B, uint32_t *__
             }
             else if (proto == PROTO_MEMCACHE) cls = 1 + kKafkaClasses;
             else if (proto == PROTO_HTTP) cls = 2 + kKafkaClasses;
-            else {
+            else if (proto != PROTO_R2D2) {  // (r2d2: its kernel walks the whole batch)
                 B.verdict[idx] = V_UNSUPPORTED;
                 B.rule[idx] = -1;
                 B.consumed[idx] = 0;

@@ -23,7 +23,7 @@ bool PortRule::RemoteOk(uint64_t id) const {
 }
 
 bool ProxylibParserRegistered(const std::string &name) {
-    return name.empty() || name == "memcache" || name == "PortNetworkPolicyRule_HttpRules" ||
+    return name.empty() || name == "memcache" || name == "r2d2" || name == "PortNetworkPolicyRule_HttpRules" ||
            name == "PortNetworkPolicyRule_KafkaRules";
 }
 
@@ -213,7 +213,8 @@ struct Loader {
                 if (m->isObj())
                     for (auto &kv : m->obj) {
                         if (kv.second.isStr()) x.kv.emplace_back(kv.first, kv.second.str);
-                        else if (r->l7proto == "memcache" && !mc_stop) return fail("NPDS: memcache rule value is not a string");
+                        else if ((r->l7proto == "memcache" || r->l7proto == "r2d2") && !mc_stop)
+                            return fail("NPDS: " + r->l7proto + " rule value is not a string");
                     }
                 r->l7.push_back(std::move(x));
             }
@@ -221,6 +222,11 @@ struct Loader {
                 for (auto &x : r->l7) {
                     r->mc.emplace_back();
                     if (!memcache(x, &r->mc.back())) return false;
+                }
+            if (r->l7proto == "r2d2" && !mc_stop)
+                for (auto &x : r->l7) {
+                    r->r2.emplace_back();
+                    if (!r2d2(x, &r->r2.back())) return false;
                 }
         }
         return true;
@@ -249,6 +255,33 @@ struct Loader {
             m->group = -1;
             m->empty = true;
         }
+        return true;
+    }
+
+    // r2d2.R2d2RuleParser (proxylib/r2d2/r2d2parser.go:69-107); its panics
+    // (ParseError, regexp.MustCompile) NACK the policy
+    bool r2d2(const L7Rule &x, R2Rule *m) {
+        m->id = x.id;
+        std::string cmd;
+        for (auto &kv : x.kv) {
+            const std::string &k = kv.first, &v = kv.second;
+            if (k == "cmd") cmd = v;
+            else if (k == "file") {
+                if (v.empty()) continue;
+                std::string e;
+                auto ast = re::Parse(v, &e);
+                if (!ast) return fail("regexp: Compile(`" + v + "`): " + e);  // regexp.MustCompile's panic
+                m->file_re = std::shared_ptr<re::Node>(std::move(ast));
+                m->file_src = v;
+            } else {
+                return fail("NPDS: Unsupported key: " + k);
+            }
+        }
+        if (!cmd.empty() && cmd != "READ" && cmd != "WRITE" && cmd != "HALT" && cmd != "RESET")
+            return fail("NPDS: Unable to parse L7 r2d2 rule with invalid cmd: '" + cmd + "'");
+        if (m->file_re && !(cmd.empty() || cmd == "READ" || cmd == "WRITE"))
+            return fail("NPDS: Unable to parse L7 r2d2 rule, cmd '" + cmd + "' is not compatible with 'file'");
+        m->cmd = cmd.empty() ? -1 : cmd == "READ" ? R2_READ : cmd == "WRITE" ? R2_WRITE : cmd == "HALT" ? R2_HALT : R2_RESET;
         return true;
     }
 

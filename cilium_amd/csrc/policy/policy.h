@@ -51,6 +51,16 @@ struct McRule {
     int id = -1;
 };
 
+// r2d2.R2d2Rule (proxylib/r2d2/r2d2parser.go:31-67): cmd exact (one of READ
+// WRITE HALT RESET, or any), file regex (unanchored MatchString, or any).
+enum : int { R2_READ = 0, R2_WRITE = 1, R2_HALT = 2, R2_RESET = 3, R2_OTHER = 4, R2_NCMD = 5 };
+struct R2Rule {
+    int cmd = -1;            // R2_* or -1 = any command
+    std::shared_ptr<re::Node> file_re;
+    std::string file_src;
+    int id = -1;
+};
+
 struct PortRule {
     std::vector<uint64_t> remotes;  // empty = any remote
     enum Type { None, Http, Kafka, L7 } type = None;
@@ -59,16 +69,19 @@ struct PortRule {
     std::string l7proto;
     std::vector<L7Rule> l7;
     std::vector<McRule> mc;  // l7proto == "memcache": its parsed L7 rules
+    std::vector<R2Rule> r2;  // l7proto == "r2d2": its parsed L7 rules
     // proxylib parser name: l7_proto, else the oneof type name, "" = no L7
     // (proxylib/proxylib/policymap.go:68-75)
     std::string ParserName() const;
     bool RemoteOk(uint64_t id) const;
     // parsed L7 rules of this group (proxylib's len(L7Rules)): memcache rules,
     // HTTP rules or Kafka rules
-    size_t NumL7() const { return type == Http ? http.size() : type == Kafka ? kafka.size() : mc.size(); }
+    size_t NumL7() const {
+        return type == Http ? http.size() : type == Kafka ? kafka.size() : l7proto == "r2d2" ? r2.size() : mc.size();
+    }
 };
 // L7 rule parsers the proxylib view registers (policymap.go:42-45): "memcache",
-// "PortNetworkPolicyRule_HttpRules", "PortNetworkPolicyRule_KafkaRules".
+// "r2d2", "PortNetworkPolicyRule_HttpRules", "PortNetworkPolicyRule_KafkaRules".
 bool ProxylibParserRegistered(const std::string &name);
 
 struct PortPolicy {

@@ -184,7 +184,7 @@ bool KafkaDenyResponse(const uint8_t *req, size_t len, std::string *out);
 }
 namespace {
 
-enum Kind { K_MEMCACHE, K_HTTP, K_KAFKA };
+enum Kind { K_MEMCACHE, K_HTTP, K_KAFKA, K_R2D2 };
 
 struct Cached {
     uint8_t v;
@@ -222,6 +222,10 @@ size_t NextMcText(const std::string &d, size_t p) {
         next += (size_t)n + 2;
     }
     return next <= d.size() ? next : 0;
+}
+size_t NextLine(const std::string &d, size_t p) {
+    const size_t lf = d.find("\r\n", p);
+    return lf == std::string::npos ? 0 : lf + 2;
 }
 size_t NextHttp(const std::string &d, size_t p) {
     const size_t he = d.find("\r\n\r\n", p);
@@ -347,8 +351,9 @@ struct Connection {
         a.policy = l7g_policy_index(ins->eng, policy.data(), policy.size());
         a.port = port;
         a.ingress = ingress ? 1 : 0;
-        a.proto = kind == K_HTTP ? L7G_PROTO_HTTP : kind == K_KAFKA ? L7G_PROTO_KAFKA : L7G_PROTO_MEMCACHE;
-        a.flags = kind == K_MEMCACHE ? (uint16_t)mode : (uint16_t)L7G_CONN_PROXYLIB;
+        a.proto = kind == K_HTTP ? L7G_PROTO_HTTP : kind == K_KAFKA ? L7G_PROTO_KAFKA
+                : kind == K_R2D2 ? L7G_PROTO_R2D2 : L7G_PROTO_MEMCACHE;
+        a.flags = kind == K_MEMCACHE ? (uint16_t)mode : kind == K_R2D2 ? (uint16_t)0 : (uint16_t)L7G_CONN_PROXYLIB;
         a.src_id = src;
         a.dst_id = dst;
         return a;
@@ -382,6 +387,7 @@ struct Connection {
             cids.push_back(slot);
             const size_t q = kind == K_KAFKA ? NextKafka(d, p)
                            : kind == K_HTTP ? NextHttp(d, p)
+                           : kind == K_R2D2 ? NextLine(d, p)
                            : mode == L7G_CONN_MC_BINARY ? NextMcBinary(d, p) : NextMcText(d, p);
             if (q <= p) break;
             p = q;
@@ -614,9 +620,42 @@ struct Connection {
         return FILTEROP_PASS;
     }
 
+    // ---- "r2d2" (proxylib/r2d2/r2d2parser.go:140-214)
+    int64_t R2d2OnData(bool r, const std::vector<std::string> &in, int64_t *n, bool *err) {
+        std::string d;
+        for (auto &b : in) d += b;
+        const size_t lf = d.find("\r\n");
+        if (lf == std::string::npos) { *n = 1; return FILTEROP_MORE; }
+        const int64_t msg_len = (int64_t)lf + 2;
+        if (r) { *n = msg_len; return FILTEROP_PASS; }  // replies are not processed
+        uint8_t v;
+        int32_t rule;
+        uint32_t cons;
+        if (!Verdict(d, &v, &rule, &cons)) { *err = true; *n = 0; return FILTEROP_ERROR; }
+        if (v != L7G_ALLOW && v != L7G_DENY) { *n = 0; return FILTEROP_ERROR; }
+        const std::string line = d.substr(0, lf);
+        std::vector<std::string> f;  // strings.Split(msgStr, " ")
+        for (size_t a = 0;;) {
+            const size_t sp = line.find(' ', a);
+            f.push_back(line.substr(a, sp == std::string::npos ? std::string::npos : sp - a));
+            if (sp == std::string::npos) break;
+            a = sp + 1;
+        }
+        const std::string l7 = GenericL7("r2d2", {{"cmd", f[0]}, {"file", f.size() == 2 ? f[1] : std::string()}});
+        *n = msg_len;
+        if (v == L7G_ALLOW) {
+            Log(kEntryRequest, l7);
+            return FILTEROP_PASS;
+        }
+        Log(kEntryDenied, l7);
+        Inject(true, "ERROR\r\n", 7);
+        return FILTEROP_DROP;
+    }
+
     // the connection's parser
     int64_t ParserOnData(bool r, const std::vector<std::string> &in, bool first_nonempty, int64_t *n, bool *err) {
         if (kind == K_HTTP) return HttpOnData(r, in, n, err);
+        if (kind == K_R2D2) return R2d2OnData(r, in, n, err);
         if (kind == K_KAFKA) return KafkaOnData(r, in, n, err);
         // memcache.Parser.OnData (memcached/parser.go:186-202)
         if (mode == 0) {
@@ -736,6 +775,7 @@ FilterResult OnNewConnection(uint64_t instance_id, GoString proto, uint64_t conn
     if (p == "memcache") kind = K_MEMCACHE;
     else if (p == "http") kind = K_HTTP;
     else if (p == "kafka") kind = K_KAFKA;
+    else if (p == "r2d2") kind = K_R2D2;
     else return FILTER_UNKNOWN_PARSER;
     uint32_t port;
     if (!DstPort(Str(dst_addr), &port)) return FILTER_INVALID_ADDRESS;

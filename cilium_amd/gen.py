@@ -18,7 +18,7 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from . import api
-from ._lib import PROTO_HTTP, PROTO_KAFKA, PROTO_MEMCACHE
+from ._lib import PROTO_HTTP, PROTO_KAFKA, PROTO_MEMCACHE, PROTO_R2D2
 from .engine import CONN_DTYPE
 
 SEED_BASE = 0x1C1D0000
@@ -844,3 +844,56 @@ def tile_offsets(w, k):
     shift = (np.arange(k, dtype=np.uint64) * np.uint64(len(w.arena)))[:, None]
     offs = (w.offsets[None, :] + shift).reshape(-1)
     return offs, np.tile(w.lengths, k), np.tile(w.conn_ids, k)
+
+
+# ------------------------------------------------------------------ r2d2
+# proxylib's example line protocol (proxylib/r2d2/r2d2parser.go): "CMD [file]\r\n"
+R2D2_PORT = 4040
+
+
+def r2d2_policy():
+    """r2d2 rules (proxylib/r2d2/r2d2parser.go:69-107): cmd only, file only,
+    both, an NFA-fallback file regex, a remote-restricted group, and a port-0
+    entry."""
+    rules = [{"cmd": "READ", "file": "^/pub/"}, {"cmd": "WRITE", "file": "tmp[0-9]+$"}, {"cmd": "HALT"},
+             {"file": "(a|b)*a(a|b){14}"}, {"file": "é"}]
+    groups = [api.port_rule(remote_policies=[7, 8], l7proto="r2d2", l7=[{"cmd": "RESET"}]),
+              api.port_rule(remote_policies=list(range(100, 164)), l7proto="r2d2", l7=rules)]
+    wild = [api.port_rule(l7proto="r2d2", l7=[{"cmd": "READ", "file": "^/wild"}])]
+    return api.policy_set(api.network_policy("r2", 9, ingress=[(R2D2_PORT, groups), (0, wild)]))
+
+
+def r2d2_requests(n, seed):
+    rng = np.random.default_rng(seed)
+    cmds = [b"READ", b"WRITE", b"HALT", b"RESET", b"READX", b"", b"read"]
+    files = [b"/pub/a", b"/priv/b", b"tmp12", b"xtmp7", b"/wild/z", b"\xc3\xa9t\xc3\xa9", b"",
+             b"ab" * 3 + b"a" + b"ab" * 7, b"bbbbbbbbbbbbbbbbbbbb"]
+    out = []
+    for i in range(n):
+        c = cmds[int(rng.integers(0, len(cmds)))]
+        f = files[int(rng.integers(0, len(files)))]
+        k = int(rng.integers(0, 10))
+        if k < 6:
+            line = c + b" " + f
+        elif k == 6:
+            line = c
+        elif k == 7:
+            line = c + b" " + f + b" extra"
+        elif k == 8:
+            line = b" " + c + b" " + f if rng.random() < 0.5 else c + b"  " + f
+        else:
+            line = c + b" " + f + b"\rx"
+        tail = b"\r\n" if rng.random() < 0.95 else (b"\r" if rng.random() < 0.5 else b"")
+        out.append(line + tail)
+    return out
+
+
+def r2d2_workload(n, nconns=64, seed=None):
+    seed = SEED_BASE + 7 if seed is None else seed
+    reqs = r2d2_requests(n, seed)
+    arena, offs, lens = pack(reqs)
+    rng = np.random.default_rng(seed + 1)
+    conn_ids = rng.integers(0, nconns, size=n).astype(np.uint32)
+    remotes = [7, 8, 100, 101, 150, 163, 5] * (nconns // 7 + 1)
+    conns = make_conns(nconns, 0, R2D2_PORT, True, PROTO_R2D2, remotes[:nconns])
+    return Workload("r2d2", arena, offs, lens, conn_ids, conns, r2d2_policy())

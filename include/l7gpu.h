@@ -40,7 +40,7 @@ extern "C" {
 
 typedef struct l7g_engine l7g_engine;
 
-enum { L7G_PROTO_HTTP = 1, L7G_PROTO_KAFKA = 2, L7G_PROTO_MEMCACHE = 3 };
+enum { L7G_PROTO_HTTP = 1, L7G_PROTO_KAFKA = 2, L7G_PROTO_MEMCACHE = 3, L7G_PROTO_R2D2 = 4 };
 enum {
     L7G_DENY = 0,        /* policy denies (HTTP 403 / Kafka ErrTopicAuthorizationFailed) */
     L7G_ALLOW = 1,       /* policy allows; rule = matched global rule id or -1 */
@@ -79,6 +79,7 @@ typedef struct {
     uint32_t http_nfas;         /* distinct patterns on the bit-parallel NFA fallback */
     uint32_t mc_nfas;
     uint64_t nfa_pool_bytes;    /* their device tables */
+    uint32_t r2d2_rulesets, r2d2_rules;
 } l7g_stats_t;
 
 /* Engine bound to one HIP device.  err receives a message on failure.

@@ -186,6 +186,34 @@ static int load_mc_rule(ld *l, const jnode *j, ref_mc_rule *m) {
     return 0;
 }
 
+/* r2d2.R2d2RuleParser (proxylib/r2d2/r2d2parser.go:69-107): keys cmd / file;
+ * an invalid cmd, a file regex with HALT / RESET, an unknown key or a regex
+ * that does not compile (regexp.MustCompile) NACKs the policy. */
+static int load_r2_rule(ld *l, const jnode *j, ref_mc_rule *m) {
+    const jnode *kv = jget(j, "rule");
+    if (!kv) kv = j;
+    if (kv->type != JN_OBJ) return 0;
+    for (int i = 0; i < kv->n; i++) {
+        const char *k = kv->keys[i];
+        const jnode *v = kv->items[i];
+        if (v->type != JN_STR) return lerr(l, "NPDS: r2d2 rule value is not a string%s", NULL);
+        if (!strcmp(k, "cmd")) { free(m->r2_cmd); m->r2_cmd = v->slen ? dupn(v->str, v->slen) : NULL; m->r2_cmd_len = v->slen; }
+        else if (!strcmp(k, "file")) {
+            if (v->slen == 0) continue;
+            char e[256];
+            ref_re_free(m->r2_file);
+            m->r2_file = ref_re_compile(v->str, v->slen, e, sizeof e);
+            if (!m->r2_file) return lerr(l, "regexp: Compile(`%s`)", v->str);
+        } else return lerr(l, "NPDS: Unsupported key: %s", k);
+    }
+    const char *c = m->r2_cmd;
+    if (c && strcmp(c, "READ") && strcmp(c, "WRITE") && strcmp(c, "HALT") && strcmp(c, "RESET"))
+        return lerr(l, "NPDS: Unable to parse L7 r2d2 rule with invalid cmd: '%s'", c);
+    if (m->r2_file && c && strcmp(c, "READ") && strcmp(c, "WRITE"))
+        return lerr(l, "NPDS: Unable to parse L7 r2d2 rule, cmd '%s' is not compatible with 'file'", c);
+    return 0;
+}
+
 static int load_rule(ld *l, const jnode *j, ref_pnp_rule *r) {
     memset(r, 0, sizeof *r);
     const jnode *rp = jget(j, "remote_policies");
@@ -227,9 +255,11 @@ static int load_rule(ld *l, const jnode *j, ref_pnp_rule *r) {
         r->l7type = L7T_L7; r->nl7 = l7->n;
         r->l7 = calloc((size_t)l7->n + 1, sizeof(ref_mc_rule));
         int mc = !l->mc_stop && r->l7proto && !strcmp(r->l7proto, "memcache");
+        int r2 = !l->mc_stop && r->l7proto && !strcmp(r->l7proto, "r2d2");
         for (int i = 0; i < l7->n; i++) {
             r->l7[i].id = l->next_id++;
             if (mc && load_mc_rule(l, l7->items[i], &r->l7[i]) < 0) return -1;
+            if (r2 && load_r2_rule(l, l7->items[i], &r->l7[i]) < 0) return -1;
         }
     }
     return 0;
@@ -264,8 +294,8 @@ static int load_ports(ld *l, const jnode *arr, ref_port **out, int *nout) {
                 if (load_rule(l, rs->items[k], &ps[i].rules[k]) < 0) return -1;
                 if (ps[i].rules[k].l7type == L7T_HTTP) ps[i].has_http = 1;
                 const ref_pnp_rule *pr = &ps[i].rules[k];
-                /* unregistered parser: any l7_proto but "memcache", or generic L7 rules */
-                if ((pr->l7proto && *pr->l7proto && strcmp(pr->l7proto, "memcache")) ||
+                /* unregistered parser: any l7_proto but "memcache" / "r2d2", or generic L7 rules */
+                if ((pr->l7proto && *pr->l7proto && strcmp(pr->l7proto, "memcache") && strcmp(pr->l7proto, "r2d2")) ||
                     ((!pr->l7proto || !*pr->l7proto) && pr->l7type == L7T_L7))
                     l->mc_stop = 1;
             }
@@ -286,7 +316,10 @@ static void free_ports(ref_port *ps, int n) {
                 free(r->http[q].m);
             }
             for (int q = 0; q < r->nkafka; q++) { free(r->kafka[q].topic); free(r->kafka[q].client); }
-            for (int q = 0; q < r->nl7; q++) { free(r->l7[q].key_exact); free(r->l7[q].key_prefix); ref_re_free(r->l7[q].key_re); }
+            for (int q = 0; q < r->nl7; q++) {
+                free(r->l7[q].key_exact); free(r->l7[q].key_prefix); ref_re_free(r->l7[q].key_re);
+                free(r->l7[q].r2_cmd); ref_re_free(r->l7[q].r2_file);
+            }
             free(r->http); free(r->kafka); free(r->l7); free(r->remotes); free(r->l7proto);
         }
         free(ps[i].rules);
@@ -355,7 +388,7 @@ static const char *px_parser(const ref_pnp_rule *r) {  /* policymap.go:68-75 */
 int ref_px_nl7(const ref_pnp_rule *r) {
     if (r->l7type == L7T_HTTP) return r->nhttp;
     if (r->l7type == L7T_KAFKA) return r->nkafka;
-    if (r->l7type == L7T_L7 && r->l7proto && !strcmp(r->l7proto, "memcache")) return r->nl7;
+    if (r->l7type == L7T_L7 && r->l7proto && (!strcmp(r->l7proto, "memcache") || !strcmp(r->l7proto, "r2d2"))) return r->nl7;
     return 0;
 }
 
@@ -364,7 +397,7 @@ int ref_px_installed(const ref_port *pp) {
     for (int r = 0; r < pp->nrules; r++) {
         const char *n = px_parser(&pp->rules[r]);
         if (!*n) continue;
-        if (strcmp(n, "memcache") && strcmp(n, "PortNetworkPolicyRule_HttpRules") &&
+        if (strcmp(n, "memcache") && strcmp(n, "r2d2") && strcmp(n, "PortNetworkPolicyRule_HttpRules") &&
             strcmp(n, "PortNetworkPolicyRule_KafkaRules"))
             return 0;  /* no such parser: port skipped (:128-134, 200-203) */
         if (!first) first = n;
@@ -401,6 +434,7 @@ static void *run(void *arg) {
             if (c->proto == L7_PROTO_HTTP) ref_http_verdict(j->p, c, b, j->len[i], &o);
             else if (c->proto == L7_PROTO_KAFKA) ref_kafka_verdict(j->p, c, b, j->len[i], &o);
             else if (c->proto == L7_PROTO_MEMCACHE) ref_memcache_verdict(j->p, c, b, j->len[i], &o);
+            else if (c->proto == L7_PROTO_R2D2) ref_r2d2_verdict(j->p, c, b, j->len[i], &o);
             else o.verdict = L7_UNSUPPORTED;
         }
         j->verdict[i] = o.verdict; j->rule[i] = o.rule; j->consumed[i] = o.consumed;

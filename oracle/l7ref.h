@@ -55,7 +55,7 @@ typedef struct {
     uint32_t dst_id;    /* destination identity */
 } ref_conn_t;
 
-enum { L7_PROTO_HTTP = 1, L7_PROTO_KAFKA = 2, L7_PROTO_MEMCACHE = 3 };
+enum { L7_PROTO_HTTP = 1, L7_PROTO_KAFKA = 2, L7_PROTO_MEMCACHE = 3, L7_PROTO_R2D2 = 4 };
 
 /* verdict codes (shared meaning with the product, see include/l7gpu.h) */
 enum {

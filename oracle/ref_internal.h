@@ -46,6 +46,9 @@ typedef struct {  /* memcache.Rule (proxylib/memcached/parser.go:35-44) */
     char *key_prefix; size_t key_prefix_len;
     ref_re *key_re;
     int empty; int id;
+    /* r2d2.R2d2Rule (proxylib/r2d2/r2d2parser.go:31-34), for l7_proto "r2d2" */
+    char *r2_cmd; size_t r2_cmd_len;   /* NULL = any */
+    ref_re *r2_file;                   /* NULL = any */
 } ref_mc_rule;
 
 enum { L7T_NONE = 0, L7T_HTTP, L7T_KAFKA, L7T_L7 };
@@ -67,12 +70,13 @@ typedef struct { uint8_t verdict; int32_t rule; uint32_t consumed; } ref_out_t;
 void ref_http_verdict(const ref_policy *pol, const ref_conn_t *c, const uint8_t *buf, uint32_t len, ref_out_t *o);
 void ref_kafka_verdict(const ref_policy *pol, const ref_conn_t *c, const uint8_t *buf, uint32_t len, ref_out_t *o);
 void ref_memcache_verdict(const ref_policy *pol, const ref_conn_t *c, const uint8_t *buf, uint32_t len, ref_out_t *o);
+void ref_r2d2_verdict(const ref_policy *pol, const ref_conn_t *c, const uint8_t *buf, uint32_t len, ref_out_t *o);
 const void *ref_mc_group(const char *name, size_t n);
 
 int ref_port_lookup(const ref_netpolicy *np, int ingress, uint32_t port, const ref_port **exact, const ref_port **wild);
 int ref_remote_ok(const ref_pnp_rule *r, uint64_t id);
 /* proxylib's view of a port entry (proxylib/proxylib/policymap.go:58-206) with
- * the rule parsers "memcache", PortNetworkPolicyRule_HttpRules and
+ * the rule parsers "memcache", "r2d2", PortNetworkPolicyRule_HttpRules and
  * PortNetworkPolicyRule_KafkaRules registered */
 int ref_px_nl7(const ref_pnp_rule *r);          /* len(L7Rules) of a rule */
 int ref_px_installed(const ref_port *pp);       /* entry kept in PortNetworkPolicies */
