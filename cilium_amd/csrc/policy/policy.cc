@@ -23,7 +23,12 @@ bool PortRule::RemoteOk(uint64_t id) const {
 }
 
 bool ProxylibParserRegistered(const std::string &name) {
-    return name.empty() || name == "memcache" || name == "r2d2" || name == "PortNetworkPolicyRule_HttpRules" ||
+    // the reference's libcilium links cassandra, memcached, r2d2 and the test
+    // parsers (proxylib/proxylib.go:24-29), whose init()s register the rule
+    // parsers "cassandra", "memcache", "r2d2" and "test.headerparser"; the
+    // HTTP / Kafka oneof parsers are this library's proxylib "http" / "kafka"
+    return name.empty() || name == "memcache" || name == "r2d2" || name == "cassandra" ||
+           name == "test.headerparser" || name == "PortNetworkPolicyRule_HttpRules" ||
            name == "PortNetworkPolicyRule_KafkaRules";
 }
 
@@ -223,6 +228,7 @@ struct Loader {
                     r->mc.emplace_back();
                     if (!memcache(x, &r->mc.back())) return false;
                 }
+            if (r->l7proto == "cassandra" || r->l7proto == "test.headerparser") r->other_l7 = r->l7.size();
             if (r->l7proto == "r2d2" && !mc_stop)
                 for (auto &x : r->l7) {
                     r->r2.emplace_back();

@@ -70,6 +70,7 @@ struct PortRule {
     std::vector<L7Rule> l7;
     std::vector<McRule> mc;  // l7proto == "memcache": its parsed L7 rules
     std::vector<R2Rule> r2;  // l7proto == "r2d2": its parsed L7 rules
+    size_t other_l7 = 0;     // "cassandra" / "test.headerparser" rules (registered; never match here)
     // proxylib parser name: l7_proto, else the oneof type name, "" = no L7
     // (proxylib/proxylib/policymap.go:68-75)
     std::string ParserName() const;
@@ -77,11 +78,13 @@ struct PortRule {
     // parsed L7 rules of this group (proxylib's len(L7Rules)): memcache rules,
     // HTTP rules or Kafka rules
     size_t NumL7() const {
-        return type == Http ? http.size() : type == Kafka ? kafka.size() : l7proto == "r2d2" ? r2.size() : mc.size();
+        return type == Http ? http.size() : type == Kafka ? kafka.size() : l7proto == "r2d2" ? r2.size()
+             : l7proto == "memcache" ? mc.size() : other_l7;
     }
 };
 // L7 rule parsers the proxylib view registers (policymap.go:42-45): "memcache",
-// "r2d2", "PortNetworkPolicyRule_HttpRules", "PortNetworkPolicyRule_KafkaRules".
+// "r2d2", "cassandra", "test.headerparser", "PortNetworkPolicyRule_HttpRules",
+// "PortNetworkPolicyRule_KafkaRules".
 bool ProxylibParserRegistered(const std::string &name);
 
 struct PortPolicy {

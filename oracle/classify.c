@@ -294,8 +294,10 @@ static int load_ports(ld *l, const jnode *arr, ref_port **out, int *nout) {
                 if (load_rule(l, rs->items[k], &ps[i].rules[k]) < 0) return -1;
                 if (ps[i].rules[k].l7type == L7T_HTTP) ps[i].has_http = 1;
                 const ref_pnp_rule *pr = &ps[i].rules[k];
-                /* unregistered parser: any l7_proto but "memcache" / "r2d2", or generic L7 rules */
-                if ((pr->l7proto && *pr->l7proto && strcmp(pr->l7proto, "memcache") && strcmp(pr->l7proto, "r2d2")) ||
+                /* unregistered parser: an l7_proto no linked parser registers
+                 * (proxylib/proxylib.go:24-29), or generic L7 rules */
+                if ((pr->l7proto && *pr->l7proto && strcmp(pr->l7proto, "memcache") && strcmp(pr->l7proto, "r2d2") &&
+                     strcmp(pr->l7proto, "cassandra") && strcmp(pr->l7proto, "test.headerparser")) ||
                     ((!pr->l7proto || !*pr->l7proto) && pr->l7type == L7T_L7))
                     l->mc_stop = 1;
             }
@@ -388,7 +390,10 @@ static const char *px_parser(const ref_pnp_rule *r) {  /* policymap.go:68-75 */
 int ref_px_nl7(const ref_pnp_rule *r) {
     if (r->l7type == L7T_HTTP) return r->nhttp;
     if (r->l7type == L7T_KAFKA) return r->nkafka;
-    if (r->l7type == L7T_L7 && r->l7proto && (!strcmp(r->l7proto, "memcache") || !strcmp(r->l7proto, "r2d2"))) return r->nl7;
+    if (r->l7type == L7T_L7 && r->l7proto &&
+        (!strcmp(r->l7proto, "memcache") || !strcmp(r->l7proto, "r2d2") || !strcmp(r->l7proto, "cassandra") ||
+         !strcmp(r->l7proto, "test.headerparser")))
+        return r->nl7;
     return 0;
 }
 
@@ -397,7 +402,8 @@ int ref_px_installed(const ref_port *pp) {
     for (int r = 0; r < pp->nrules; r++) {
         const char *n = px_parser(&pp->rules[r]);
         if (!*n) continue;
-        if (strcmp(n, "memcache") && strcmp(n, "r2d2") && strcmp(n, "PortNetworkPolicyRule_HttpRules") &&
+        if (strcmp(n, "memcache") && strcmp(n, "r2d2") && strcmp(n, "cassandra") && strcmp(n, "test.headerparser") &&
+            strcmp(n, "PortNetworkPolicyRule_HttpRules") &&
             strcmp(n, "PortNetworkPolicyRule_KafkaRules"))
             return 0;  /* no such parser: port skipped (:128-134, 200-203) */
         if (!first) first = n;

@@ -109,11 +109,11 @@ def test_memcache_port_entries(engine, oracle):
     remote filtering, unparsed rules after an unknown parser."""
     P = api.port_rule
     pol = api.policy_set(api.network_policy("mc", 1, ingress=[
-        (100, [P(l7proto="memcache", l7=[{"command": "get"}]), P(l7proto="r2d2", l7=[{"file": "x"}])]),
+        (100, [P(l7proto="memcache", l7=[{"command": "get"}]), P(l7proto="no.such.parser", l7=[{"file": "x"}])]),
         (101, [P(remote_policies=[7])]),
         (102, [P(l7proto="memcache", l7=[{"command": "set"}]), P(remote_policies=[8], l7proto="memcache", l7=[])]),
         (103, [P(http=[{}])]),
-        (104, [P(l7proto="r2d2", l7=[{}]), P(l7proto="memcache", l7=[{"keyExact": "no-command"}])]),
+        (104, [P(l7proto="no.such.parser", l7=[{}]), P(l7proto="memcache", l7=[{"keyExact": "no-command"}])]),
         (105, [P(l7proto="memcache", l7=[{"command": "nosuch"}])]),
         (0, [P(remote_policies=[9], l7proto="memcache", l7=[{"command": "delete"}])]),
     ]))

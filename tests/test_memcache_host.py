@@ -32,7 +32,7 @@ def test_rule_errors_match_oracle(host, oracle, kats, rule, msg):
 
 def test_rules_after_unknown_parser_are_not_parsed(host, oracle):
     pol = api.policy_set(api.network_policy("mc", 1, ingress=[(11211, [
-        api.port_rule(l7proto="r2d2", l7=[{"file": "x"}]),
+        api.port_rule(l7proto="no.such.parser", l7=[{"file": "x"}]),
         api.port_rule(l7proto="memcache", l7=[{"keyExact": "k"}])])]))
     oracle.Policy(pol)
     host.update_policy(pol)
