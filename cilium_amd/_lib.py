@@ -59,6 +59,13 @@ def load(path=None):
         return _libs[path]
     if not os.path.exists(path):
         raise RuntimeError(f"{path} is missing: run python -m cilium_amd.build (no CPU fallback exists)")
+    # One HIP runtime per process: torch ships its own libamdhip64 under the same
+    # soname, and whichever loads first serves both.  Loading torch's first keeps
+    # torch.cuda working in processes that use both (batches in torch tensors).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(path)
     vp, sz, cp = C.c_void_p, C.c_size_t, C.c_char_p
     lib.l7g_engine_create.restype = vp

@@ -306,6 +306,71 @@ def k_message(value, key=None, version=0, attributes=0, timestamp=0, bad_crc=Fal
     return struct.pack(">qi", 0, len(msg)) + msg
 
 
+def snappy_block(data, copies=True):
+    """A plain snappy block (varint length + literal / copy tags), greedy over
+    4-byte matches; copies=False emits literals only.  For test streams."""
+    out = bytearray()
+    n = len(data)
+    v = n
+    while True:
+        b = v & 0x7F
+        v >>= 7
+        out.append(b | (0x80 if v else 0))
+        if not v:
+            break
+
+    def literal(lo, hi):
+        while lo < hi:
+            k = min(hi - lo, 1 << 16)
+            if k <= 60:
+                out.append((k - 1) << 2)
+            elif k <= 256:
+                out.extend(bytes([60 << 2, k - 1]))
+            else:
+                out.extend(bytes([61 << 2]) + struct.pack("<H", k - 1))
+            out.extend(data[lo:lo + k])
+            lo += k
+
+    last, i, table = 0, 0, {}
+    while copies and i + 4 <= n:
+        key = bytes(data[i:i + 4])
+        j = table.get(key)
+        table[key] = i
+        if j is not None and 0 < i - j < 65536:
+            m = 4
+            while i + m < n and m < 64 and data[j + m] == data[i + m]:
+                m += 1
+            literal(last, i)
+            out += bytes([((m - 1) << 2) | 2]) + struct.pack("<H", i - j)
+            i += m
+            last = i
+        else:
+            i += 1
+    literal(last, n)
+    return bytes(out)
+
+
+def snappy_xerial(data, chunk=4096, copies=True):
+    """snappy-java (xerial) framing: magic, version 1, compat 1, then
+    (BE32 length, snappy block) per chunk."""
+    out = b"\x82SNAPPY\x00" + struct.pack(">ii", 1, 1)
+    for o in range(0, len(data), chunk):
+        blk = snappy_block(data[o:o + chunk], copies)
+        out += struct.pack(">i", len(blk)) + blk
+    return out
+
+
+def k_compressed(inner, codec, version=0, timestamp=0, xerial=False, gzip_kwargs=None):
+    """A message whose value is the message set `inner` (bytes) compressed:
+    codec 1 = gzip, 2 = snappy (messages.go:460-489)."""
+    if codec == 1:
+        import gzip as _gz
+        value = _gz.compress(inner, **(gzip_kwargs or {}))
+    else:
+        value = snappy_xerial(inner) if xerial else snappy_block(inner)
+    return k_message(value, key=None, version=version, attributes=codec, timestamp=timestamp)
+
+
 def k_request(kind, version, corr, client, body):
     payload = struct.pack(">hhi", kind, version, corr) + k_str(client) + body
     return struct.pack(">i", len(payload)) + payload

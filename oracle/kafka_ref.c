@@ -16,8 +16,10 @@
  *                         ruleMatches :144-195, MatchesRule :200-225
  *   pkg/policy/api/kafka.go CheckAPIKeyRole :248-261, GetAPIVersion :265-271
  *   pkg/proxy/kafka.go canAccess :117-153 (rules.Kafka == nil => deny)
- * Compressed message sets (gzip/snappy) are reported as L7_UNSUPPORTED (the
- * product does the same; decompression on the device is future work).
+ * Compressed messages (gzip / snappy, messages.go:460-489) are decoded by
+ * kafka_inflate.c and their inner message set read recursively; any decode
+ * error fails the request (parity for these is pinned by fixtures built with
+ * Python's zlib/gzip and a test snappy encoder, not by reference vectors).
  */
 #include <stdlib.h>
 #include <string.h>
@@ -68,16 +70,19 @@ static int64_t dec_arraylen(kdec *d, int nullable, int *bad) {
     if (l > MAX_PARSE_BUF) { *bad = 1; return 0; }
     return l;
 }
-/* DecodeBytes: only its error behaviour matters here */
-static void dec_bytes(kdec *d) {
+/* DecodeBytes: the bytes' position (len 0: nil) */
+static void dec_bytes_at(kdec *d, size_t *at, size_t *len) {
+    *at = 0; *len = 0;
     if (d->err) return;
     int32_t sl = (int32_t)dec_int(d, 4);
     if (d->err) return;
     if (sl < 1) return;
     if (sl > MAX_PARSE_BUF) { d->err = KE_OTHER; return; }
-    size_t at; int e = kread(d, (size_t)sl, &at);
+    int e = kread(d, (size_t)sl, at);
     if (e) d->err = e;
+    else *len = (size_t)sl;
 }
+static void dec_bytes(kdec *d) { size_t a, l; dec_bytes_at(d, &a, &l); }
 
 static uint32_t crc_table[256];
 static void crc_init(void) {
@@ -96,7 +101,10 @@ static uint32_t crc32_ieee(const uint8_t *p, size_t n) {
     return c ^ 0xFFFFFFFFu;
 }
 
-/* readMessageSet; returns 0 ok, -1 error, -2 unsupported (compressed) */
+int ref_gunzip(const uint8_t *in, size_t n, uint8_t *out, size_t cap, size_t *outlen);
+int ref_unsnappy(const uint8_t *b, size_t n, uint8_t *out, size_t cap, size_t *outlen);
+
+/* readMessageSet; returns 0 ok, -1 error */
 static int read_message_set(kbuf *r, int32_t size, int16_t version) {
     if (size < 0) return 0;
     if (size > MAX_PARSE_BUF) return -1;
@@ -123,9 +131,20 @@ static int read_message_set(kbuf *r, int32_t size, int16_t version) {
             dec_bytes(&md); dec_bytes(&md);
             if (md.err) return -1;
         } else if (codec == 1 || codec == 2) {
-            dec_bytes(&md); dec_bytes(&md);
+            size_t vat, vlen;
+            dec_bytes(&md); dec_bytes_at(&md, &vat, &vlen);
             if (md.err) return -1;
-            return -2;
+            uint8_t *dec = malloc(MAX_PARSE_BUF + 1);
+            size_t dlen = 0;
+            const uint8_t *val = r->b + at + vat;
+            int bad = codec == 1 ? ref_gunzip(val, vlen, dec, MAX_PARSE_BUF, &dlen)
+                                 : ref_unsnappy(val, vlen, dec, MAX_PARSE_BUF, &dlen);
+            if (!bad) {
+                kbuf inner = {dec, 0, dlen};
+                bad = read_message_set(&inner, (int32_t)dlen, version);
+            }
+            free(dec);
+            if (bad) return -1;
         } else {
             return 0; /* `return nil, err` with err == nil */
         }
@@ -146,7 +165,7 @@ static void add_topic(kreq *q, int32_t off, int32_t len) {
     q->topics[q->ntopics++] = (span_t){off, len};
 }
 
-/* decoders: return 0 ok, -1 error, -2 unsupported */
+/* decoders: return 0 ok, -1 error */
 static int read_body(kreq *q, const uint8_t *raw, size_t rawlen) {
     kbuf buf = {raw, 0, rawlen};
     kdec d = {&buf, -1, 0};
@@ -337,7 +356,6 @@ void ref_kafka_verdict(const ref_policy *pol, const ref_conn_t *c, const uint8_t
     default: q.typed = 0; break;
     }
     if (e == -1) { o->verdict = L7_PARSE_ERROR; free(q.topics); return; }
-    if (e == -2) { o->verdict = L7_UNSUPPORTED; free(q.topics); return; }
     if (q.typed != 1) q.ntopics = 0; /* GetTopics: nil for ConsumerMetadata / unknown */
 
     /* canAccess: GetRelevantRules(source identity) */

@@ -38,6 +38,8 @@ def load():
         lib.ref_policy_load.argtypes = [cp, sz, cp, sz]
         lib.ref_policy_free.argtypes = [vp]
         lib.ref_classify.argtypes = [vp, vp, C.c_uint32, vp, vp, vp, vp, C.c_uint32, vp, vp, vp, C.c_int]
+        for f in (lib.ref_gunzip, lib.ref_unsnappy):
+            f.argtypes = [cp, sz, vp, sz, C.POINTER(sz)]
         _lib = lib
     return _lib
 
@@ -94,6 +96,28 @@ class Policy:
     def __del__(self):
         if getattr(self, "_h", None) and _lib is not None:
             _lib.ref_policy_free(self._h)
+
+
+MAX_PARSE_BUF = 6_553_500
+
+
+def _decode(fn, data, cap):
+    out = C.create_string_buffer(max(cap, 1))
+    n = C.c_size_t(0)
+    if fn(data, len(data), out, cap, C.byref(n)) != 0:
+        return None
+    return out.raw[:n.value]
+
+
+def gunzip(data, cap=MAX_PARSE_BUF):
+    """Go's gzip.NewReader + ReadAll restated (oracle/kafka_inflate.c): the
+    decoded bytes, or None on any error / more than cap bytes."""
+    return _decode(load().ref_gunzip, data, cap)
+
+
+def unsnappy(data, cap=MAX_PARSE_BUF):
+    """proto.snappyDecode restated (plain snappy or xerial framing)."""
+    return _decode(load().ref_unsnappy, data, cap)
 
 
 def classify_workload(w, nthreads=1):

@@ -73,6 +73,12 @@ def main():
         ("cfg2 heads only", variant("d", heads, gen.cfg2_policy())),
         ("no rules heads only", variant("e", heads, allow_all)),
     ]
+    # per-line cost: k unknown 20-byte header lines after a fixed request line
+    for k, letter in ((0, "f"), (4, "g"), (8, "h")):
+        reqs = [b"GET /abcdefghijklmnop HTTP/1.1\r\n" + b"X-Aaaa: 0123456789\r\n" * k + b"\r\n"] * n
+        rows.append((f"no rules, {k} lines", variant(letter, reqs, allow_all)))
+    reqs = [b"GET /abcdefghijklmnop HTTP/1.1\r\n" + b"Host: 0123456789abc\r\n" * 4 + b"\r\n"] * n
+    rows.append(("cfg2 pol, 4 host lines", variant("i", reqs, gen.cfg2_policy())))
     for name, w in rows:
         if only and w.name not in only:
             continue
