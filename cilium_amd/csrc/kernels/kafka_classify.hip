@@ -12,167 +12,13 @@
 #include <hip/hip_runtime.h>
 
 #include "../device_tables.h"
+#include "kafka_dec.h"
 
 namespace l7 {
 
 namespace {
 
 constexpr int kBlock = 256;
-constexpr uint32_t kMaxParseBuf = 6553500;
-constexpr int kCrcSlices = 8;
-constexpr uint32_t kInf = 0xFFFFFFFFu;
-
-// Per-lane byte cursor: the decoders walk their request forward, so each lane
-// keeps the 16-byte aligned chunk it last touched in registers and serves
-// field bytes from it; one dwordx4 load replaces up to 16 byte loads.  A chunk
-// that holds a request byte never leaves that byte's page, so the aligned
-// over-read is safe for any arena alignment.
-struct Cur {
-    uintptr_t line;  // address of the cached chunk (~0 = none)
-    uint32_t w0, w1, w2, w3;  // scalars, not an array: a selected array element would put Cur in scratch
-};
-__device__ __forceinline__ void cur_fill(Cur &c, uintptr_t a) {
-    const uintptr_t ln = a & ~(uintptr_t)15;
-    if (ln != c.line) {
-        const uint4 v = *reinterpret_cast<const uint4 *>(ln);
-        c.w0 = v.x; c.w1 = v.y; c.w2 = v.z; c.w3 = v.w;
-        c.line = ln;
-    }
-}
-// (values are copied out before they are selected: a select between struct
-// members becomes a select between their addresses, i.e. a scratch array)
-__device__ __forceinline__ uint32_t cur_word(const Cur &c, uint32_t k) {
-    const uint32_t a = c.w0, b = c.w1, d = c.w2, e = c.w3;
-    return k < 8 ? (k < 4 ? a : b) : (k < 12 ? d : e);
-}
-__device__ __forceinline__ uint32_t cur_byte(Cur &c, const uint8_t *p) {
-    const uintptr_t a = (uintptr_t)p;
-    cur_fill(c, a);
-    const uint32_t k = (uint32_t)(a & 15);
-    return (cur_word(c, k) >> ((k & 3) * 8)) & 0xFFu;
-}
-
-struct KDec {
-    const uint8_t *b;
-    uint32_t pos, end;
-    int64_t limit;  // LimitReader remaining, -1 = none
-    int err;        // 0 ok, 1 EOF, 2 ErrUnexpectedEOF, 3 other
-    Cur *c;
-};
-
-__device__ __forceinline__ uint32_t kavail(const KDec &d) {
-    uint32_t a = d.end - d.pos;
-    if (d.limit >= 0 && (uint64_t)d.limit < a) a = (uint32_t)d.limit;
-    return a;
-}
-// io.ReadFull(r, buf[:n]); returns start offset, sets d.err on a short read
-__device__ __forceinline__ uint32_t kread(KDec &d, uint32_t n) {
-    uint32_t at = d.pos;
-    if (n == 0) return at;
-    uint32_t a = kavail(d);
-    if (a == 0) { d.err = 1; return at; }
-    uint32_t take = a < n ? a : n;
-    d.pos += take;
-    if (d.limit >= 0) d.limit -= take;
-    if (take < n) d.err = 2;
-    return at;
-}
-// Big-endian n-byte field (n = 1, 2, 4 or 8).  A field inside the cached
-// 16-byte chunk is cut out of two adjacent words (v_alignbyte) and byte-
-// swapped (v_perm); one straddling two chunks is read byte by byte.
-__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_amdgcn_perm(0, x, 0x00010203u); }
-__device__ __forceinline__ uint64_t be_load(Cur &c, const uint8_t *p, int n) {
-    const uintptr_t a = (uintptr_t)p;
-    const uint32_t k = (uint32_t)(a & 15);
-    if (n <= 4 && k + (uint32_t)n <= 16) {
-        cur_fill(c, a);
-        const uint32_t w0 = c.w0, w1 = c.w1, w2 = c.w2, w3 = c.w3;
-        const uint32_t i = k >> 2;
-        const uint32_t lo = i == 0 ? w0 : i == 1 ? w1 : i == 2 ? w2 : w3;
-        const uint32_t hi = i == 0 ? w1 : i == 1 ? w2 : i == 2 ? w3 : 0u;
-        const uint32_t v = bswap32(__builtin_amdgcn_alignbyte(hi, lo, k & 3));  // bytes k..k+3, big-endian
-        return n == 4 ? v : v >> (32 - 8 * n);
-    }
-    if (n == 8) return (be_load(c, p, 4) << 32) | be_load(c, p + 4, 4);
-    uint64_t v = 0;
-    for (int i = 0; i < n; i++) v = (v << 8) | cur_byte(c, p + i);
-    return v;
-}
-__device__ __forceinline__ int64_t dec_int(KDec &d, int n) {
-    if (d.err) return 0;
-    uint32_t at = kread(d, (uint32_t)n);
-    if (d.err) return 0;
-    uint64_t v = be_load(*d.c, d.b + at, n);
-    return n == 1 ? (int64_t)(int8_t)v : n == 2 ? (int64_t)(int16_t)v : n == 4 ? (int64_t)(int32_t)v : (int64_t)v;
-}
-// A field whose value is not needed: only the read (and its errors) matter.
-__device__ __forceinline__ void dec_skip(KDec &d, int n) {
-    if (d.err) return;
-    kread(d, (uint32_t)n);
-}
-// DecodeString -> (off, len); len < 1 => ""
-__device__ __forceinline__ void dec_string(KDec &d, uint32_t &off, uint32_t &len) {
-    off = 0; len = 0;
-    if (d.err) return;
-    int16_t sl = (int16_t)dec_int(d, 2);
-    if (d.err || sl < 1) return;
-    uint32_t at = kread(d, (uint32_t)sl);
-    if (d.err) return;
-    off = at; len = (uint32_t)sl;
-}
-// DecodeArrayLen(nullable): -1 null; sets bad on ErrInvalidArrayLen
-__device__ __forceinline__ int64_t dec_arraylen(KDec &d, bool nullable, bool &bad) {
-    int64_t l = (int32_t)dec_int(d, 4);
-    bad = false;
-    if (l < 0) { if (nullable) return -1; bad = true; return 0; }
-    if (l > kMaxParseBuf) { bad = true; return 0; }
-    return l;
-}
-__device__ __forceinline__ void dec_bytes(KDec &d) {
-    if (d.err) return;
-    int32_t sl = (int32_t)dec_int(d, 4);
-    if (d.err || sl < 1) return;
-    if ((uint32_t)sl > kMaxParseBuf) { d.err = 3; return; }
-    kread(d, (uint32_t)sl);
-}
-
-// CRC32-IEEE (hash/crc32.ChecksumIEEE), slicing-by-8: tab holds 8 LDS tables
-// of 256 entries; the body advances 8 aligned bytes per step with eight
-// independent table reads, so the serial chain is one step per 8 bytes.
-__device__ __forceinline__ uint32_t crc32_ieee(const uint32_t *tab, Cur &cur, const uint8_t *p, uint32_t n) {
-    uint32_t c = 0xFFFFFFFFu;
-    uint32_t i = 0;
-    for (; i < n && (((uintptr_t)(p + i)) & 15); i++) c = tab[(c ^ cur_byte(cur, p + i)) & 0xFF] ^ (c >> 8);
-    // Bulk: 64 aligned bytes per batch, four dwordx4 loads issued together so
-    // one memory latency covers 8 slicing steps (a lane walks its message
-    // alone; back-to-back dependent loads were the kernel's critical path).
-    for (; i + 64 <= n; i += 64) {
-        const uint4 *q = reinterpret_cast<const uint4 *>(p + i);
-        uint4 v[4];
-#pragma unroll
-        for (int j = 0; j < 4; j++) v[j] = q[j];
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            const uint4 &x = v[j >> 1];
-            const uint32_t lo = ((j & 1) ? x.z : x.x) ^ c, hi = (j & 1) ? x.w : x.y;
-            c = tab[7 * 256 + (lo & 0xFF)] ^ tab[6 * 256 + ((lo >> 8) & 0xFF)] ^ tab[5 * 256 + ((lo >> 16) & 0xFF)] ^
-                tab[4 * 256 + (lo >> 24)] ^ tab[3 * 256 + (hi & 0xFF)] ^ tab[2 * 256 + ((hi >> 8) & 0xFF)] ^
-                tab[1 * 256 + ((hi >> 16) & 0xFF)] ^ tab[hi >> 24];
-        }
-    }
-    for (; i + 8 <= n; i += 8) {
-        const uintptr_t a = (uintptr_t)(p + i);
-        cur_fill(cur, a);
-        const uint32_t k = (uint32_t)(a & 15);
-        const uint32_t w0 = cur.w0, w1 = cur.w1, w2 = cur.w2, w3 = cur.w3;
-        const uint32_t lo = (k ? w2 : w0) ^ c, hi = k ? w3 : w1;
-        c = tab[7 * 256 + (lo & 0xFF)] ^ tab[6 * 256 + ((lo >> 8) & 0xFF)] ^ tab[5 * 256 + ((lo >> 16) & 0xFF)] ^
-            tab[4 * 256 + (lo >> 24)] ^ tab[3 * 256 + (hi & 0xFF)] ^ tab[2 * 256 + ((hi >> 8) & 0xFF)] ^
-            tab[1 * 256 + ((hi >> 16) & 0xFF)] ^ tab[hi >> 24];
-    }
-    for (; i < n; i++) c = tab[(c ^ cur_byte(cur, p + i)) & 0xFF] ^ (c >> 8);
-    return ~c;
-}
 
 // readMessageSet on the shared position; 0 ok, -1 error, -2 compressed
 __device__ __forceinline__ int read_message_set(Cur &cur, const uint8_t *b, uint32_t &pos, uint32_t end, int32_t size,
