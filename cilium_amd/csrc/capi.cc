@@ -26,7 +26,11 @@ namespace l7 {
 hipError_t LaunchHttpClassify(const Batch &B, const HttpTables &T, const uint32_t *sel, const uint32_t *sel_count,
                               bool any_cold, bool answer_other, hipStream_t stream);
 hipError_t LaunchKafkaClassify(const Batch &B, const KafkaTables &T, const uint32_t *sel, const uint32_t *sel_count,
-                               bool answer_other, hipStream_t stream);
+                               bool answer_other, uint32_t *zlist, uint32_t *zcount, hipStream_t stream);
+hipError_t LaunchKafkaInflate(const Batch &B, const uint32_t *zlist, const uint32_t *zcount, uint8_t *region,
+                              hipStream_t stream);
+uint32_t KafkaInflateBlocks();
+uint32_t KafkaInflateRegionBytes();
 hipError_t LaunchMemcacheClassify(const Batch &B, const McTables &T, const uint32_t *sel, const uint32_t *sel_count,
                                   bool answer_other, hipStream_t stream);
 hipError_t LaunchR2d2Classify(const Batch &B, const R2Tables &T, bool answer_other, hipStream_t stream);
@@ -71,9 +75,13 @@ struct l7g_engine {
     uint8_t *s_arena = nullptr, *s_req = nullptr;
     size_t s_arena_cap = 0, s_n_cap = 0;
     bool any_cold = false;     // some HTTP connection uses another rule set
-    // protocol split (grow-only, stream-ordered): [counts(16) | L7_KAFKA_CLASSES x n Kafka idx | n memcached idx]
+    // protocol split (grow-only, stream-ordered): [counts(16) | L7_KAFKA_CLASSES x n Kafka idx | n memcached idx |
+    // n HTTP idx | n idx of Kafka requests with compressed messages]
     uint32_t *d_sel = nullptr;
     size_t sel_cap = 0;
+    // decode region of kafka_inflate_kernel (one slice per workgroup), allocated
+    // with the first Kafka batch, stream-ordered as d_sel
+    uint8_t *d_zreg = nullptr;
     // NFA pre-pass results, u64 per request (grow-only, stream-ordered as d_sel)
     uint64_t *d_nfa = nullptr;
     size_t nfa_cap = 0;
@@ -307,6 +315,7 @@ void l7g_engine_destroy(l7g_engine *e) {
     if (e->d_blob) hipFree(e->d_blob);
     if (e->d_conns) hipFree(e->d_conns);
     if (e->d_sel) hipFree(e->d_sel);
+    if (e->d_zreg) hipFree(e->d_zreg);
     if (e->d_nfa) hipFree(e->d_nfa);
     if (e->d_hist) hipFree(e->d_hist);
     if (e->d_flow) hipFree(e->d_flow);
@@ -444,9 +453,9 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
     // (a Kafka-only engine partitions too: the kind / length lists keep the
     // Kafka kernel's waves converged, 1.55 -> 0.99 ms on cfg3)
     const bool partitioned = nproto > 1 || e->has_kafka;
-    uint32_t *sel_k = nullptr, *sel_m = nullptr, *sel_h = nullptr, *cnt = nullptr;
+    uint32_t *sel_k = nullptr, *sel_m = nullptr, *sel_h = nullptr, *sel_z = nullptr, *cnt = nullptr;
     if (partitioned) {
-        const size_t need = 16 + (L7_KAFKA_CLASSES + 2) * (size_t)n;
+        const size_t need = 16 + (L7_KAFKA_CLASSES + 3) * (size_t)n;
         // the scratch may still be in use by the previous batch (any stream)
         if (e->launched) rc = hipStreamWaitEvent(s, e->done_ev, 0);
         if (rc == hipSuccess && need > e->sel_cap) {
@@ -460,11 +469,15 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
             if (rc == hipSuccess) e->sel_cap = need;
         }
         if (rc != hipSuccess) return (int)rc;
-        cnt = e->d_sel;  // [0, L7_KAFKA_CLASSES) Kafka classes, then memcached, then HTTP
+        cnt = e->d_sel;  // [0, L7_KAFKA_CLASSES) Kafka classes, then memcached, HTTP, compressed Kafka
         sel_k = e->d_sel + 16;
         sel_m = sel_k + L7_KAFKA_CLASSES * (size_t)n;
         sel_h = sel_m + (size_t)n;
-        rc = hipMemsetAsync(cnt, 0, 16 * sizeof(uint32_t), s);
+        sel_z = sel_h + (size_t)n;
+        if (rc == hipSuccess) rc = hipMemsetAsync(cnt, 0, 16 * sizeof(uint32_t), s);
+        if (rc == hipSuccess && e->has_kafka && !e->d_zreg)
+            rc = hipMalloc(&e->d_zreg, (size_t)KafkaInflateBlocks() * KafkaInflateRegionBytes());
+        if (rc != hipSuccess) return (int)rc;
     }
     // rule sets with NFA-fallback matchers: the pre-pass writes one u64 per request
     HttpTables ht = e->ht;
@@ -498,7 +511,10 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
     if (rc == hipSuccess && run[1])
         rc = LaunchHttpClassify(B, ht, sel_h, cnt ? cnt + L7_KAFKA_CLASSES + 1 : nullptr, e->any_cold, !partitioned, s);
     mark(2);
-    if (rc == hipSuccess && run[2]) rc = LaunchKafkaClassify(B, e->kt, sel_k, cnt, !partitioned, s);
+    uint32_t *zcount = cnt ? cnt + L7_KAFKA_CLASSES + 2 : nullptr;
+    if (rc == hipSuccess && run[2]) rc = LaunchKafkaClassify(B, e->kt, sel_k, cnt, !partitioned, sel_z, zcount, s);
+    // requests with gzip / snappy messages: decoded, their sets read, failures answered
+    if (rc == hipSuccess && run[2] && sel_z) rc = LaunchKafkaInflate(B, sel_z, zcount, e->d_zreg, s);
     mark(3);
     if (rc == hipSuccess && run[3])
         rc = LaunchMemcacheClassify(B, e->mt, sel_m, cnt ? cnt + L7_KAFKA_CLASSES : nullptr, !partitioned, s);

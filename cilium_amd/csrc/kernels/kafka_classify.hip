@@ -8,7 +8,8 @@
 // (serialization.go:19-203), readMessageSet with CRC32-IEEE per message and
 // stop-without-drain (:363-494), then MatchesRule (pkg/kafka/policy.go:200-225)
 // against the connection's rule set using the precomputed topic / key views
-// (engine/kafka_compile.h).  Compressed message sets => L7_UNSUPPORTED.
+// (engine/kafka_compile.h).  Requests with compressed messages are listed for
+// kafka_inflate_kernel (kafka_inflate.hip), which decodes them.
 #include <hip/hip_runtime.h>
 
 #include "../device_tables.h"
@@ -20,9 +21,10 @@ namespace {
 
 constexpr int kBlock = 256;
 
-// readMessageSet on the shared position; 0 ok, -1 error, -2 compressed
+// readMessageSet on the shared position; 0 ok, -1 error; zflag is set when a
+// compressed message was passed
 __device__ __forceinline__ int read_message_set(Cur &cur, const uint8_t *b, uint32_t &pos, uint32_t end, int32_t size,
-                                int16_t version, const uint32_t *crctab) {
+                                int16_t version, const uint32_t *crctab, bool &zflag) {
     if (size < 0) return 0;
     if ((uint32_t)size > kMaxParseBuf) return -1;
     KDec dec{b, pos, end, size, 0, &cur};
@@ -47,7 +49,9 @@ __device__ __forceinline__ int read_message_set(Cur &cur, const uint8_t *b, uint
         dec_bytes(md);
         dec_bytes(md);
         if (md.err) { rc = -1; break; }
-        if (codec != 0) { rc = -2; break; }
+        // gzip / snappy: decoded (and its set read) by kafka_inflate_kernel;
+        // the walk goes on, since a successful decode changes nothing here
+        if (codec != 0) zflag = true;
     }
     pos = dec.pos;
     return rc;
@@ -157,7 +161,7 @@ __device__ __forceinline__ uint32_t topic_first(const KafkaTables &T, const DevK
 // not Kafka (single-protocol engines, where partition_kernel does not run).
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) void kafka_classify_kernel(
     Batch B, KafkaTables T, const uint32_t *__restrict__ sel, const uint32_t *__restrict__ sel_count,
-    uint32_t answer_other) {
+    uint32_t answer_other, uint32_t *__restrict__ zlist, uint32_t *__restrict__ zcount) {
     const uint32_t n = B.n, nconns = B.nconns;
     const uint8_t *__restrict__ arena = B.arena;
     const uint32_t *__restrict__ conn_ids = B.conn_ids;
@@ -202,6 +206,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
         uint8_t verdict = V_PARSE_ERROR;
         int32_t rule = -1;
         uint32_t consumed = 0;
+        bool zflag = false;  // compressed messages passed: kafka_inflate_kernel decides them
         if (conn.proto != PROTO_KAFKA || conn.ruleset < 0 || (uint32_t)conn.ruleset >= T.nrulesets) {
             if (!answer_other || conn.proto == PROTO_HTTP || conn.proto == PROTO_MEMCACHE || conn.proto == PROTO_R2D2) continue;
             verdict = V_UNSUPPORTED;  // unknown connection / no parser
@@ -264,7 +269,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                             if (d.err) { rc = -1; break; }
                             const int32_t ss = (int32_t)dec_int(d, 4);
                             if (d.err) { rc = -1; break; }
-                            rc = read_message_set(cur, b, d.pos, d.end, ss, ver, crctab);
+                            rc = read_message_set(cur, b, d.pos, d.end, ss, ver, crctab, zflag);
                             if (rc) break;
                         }
                     }
@@ -348,7 +353,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
                 if (rc == 0 && d.err) rc = -1;
             }
             if (rc == -1) { verdict = V_PARSE_ERROR; break; }
-            if (rc == -2) { verdict = V_UNSUPPORTED; break; }
             consumed = rawlen;
             verdict = V_DENY;
             if (!rs.any) break;
@@ -374,18 +378,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
         B.verdict[idx] = verdict;
         B.rule[idx] = rule;
         B.consumed[idx] = consumed;
+        if (zflag && zlist && (verdict == V_ALLOW || verdict == V_DENY)) zlist[atomicAdd(zcount, 1u)] = idx;
     }
 }
 
 hipError_t KafkaPhaseTimes(uint64_t *, bool) { return hipErrorNotSupported; }
 
 hipError_t LaunchKafkaClassify(const Batch &B, const KafkaTables &T, const uint32_t *sel, const uint32_t *sel_count,
-                               bool answer_other, hipStream_t stream) {
+                               bool answer_other, uint32_t *zlist, uint32_t *zcount, hipStream_t stream) {
     if (B.n == 0) return hipSuccess;
     uint32_t blocks = (B.n + kBlock - 1) / kBlock;
     if (blocks > 8192) blocks = 8192;
     hipLaunchKernelGGL(kafka_classify_kernel, dim3(blocks), dim3(kBlock), 0, stream, B, T, sel, sel_count,
-                       answer_other ? 1u : 0u);
+                       answer_other ? 1u : 0u, zlist, zcount);
     return hipGetLastError();
 }
 

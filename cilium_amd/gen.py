@@ -640,6 +640,115 @@ def kafka_adversarial(n, seed):
     return out
 
 
+def _gz_member(data, level=6, strategy=0, flags=0, extra=b"", name=b"", comment=b"", hcrc=False, zdict=None):
+    """One gzip member built field by field (header flags, raw DEFLATE with a
+    chosen strategy / preset history, CRC32 + ISIZE trailer)."""
+    h = bytes([0x1F, 0x8B, 8, flags | (0x02 if hcrc else 0)]) + b"\0\0\0\0\0\xff"
+    if flags & 0x04:
+        h += struct.pack("<H", len(extra)) + extra
+    if flags & 0x08:
+        h += name + b"\0"
+    if flags & 0x10:
+        h += comment + b"\0"
+    if hcrc:
+        h += struct.pack("<H", zlib.crc32(h) & 0xFFFF)
+    kw = {"zdict": zdict} if zdict else {}
+    c = zlib.compressobj(level, zlib.DEFLATED, -15, 9, strategy, **kw)
+    body = c.compress(data) + c.flush()
+    return h + body + struct.pack("<II", zlib.crc32(data) & 0xFFFFFFFF, len(data) & 0xFFFFFFFF)
+
+
+def snappy_far_copy(data, dist):
+    """A snappy block of `data` followed by a copy of its first 64 bytes taken
+    `dist` (> 65535) back with a 4-byte-offset tag."""
+    assert dist >= len(data) and dist >= 65536
+    body = data + bytes(dist - len(data))
+    v, out = len(body) + 64, bytearray()  # literals of body, then one copy-4 tag of 64 bytes
+    while True:
+        b, v = v & 0x7F, v >> 7
+        out.append(b | (0x80 if v else 0))
+        if not v:
+            break
+    for lo in range(0, len(body), 1 << 16):
+        k = min(len(body) - lo, 1 << 16)
+        out.extend(bytes([61 << 2]) + struct.pack("<H", k - 1) + body[lo:lo + k])
+    out.extend(bytes([(63 << 2) | 3]) + struct.pack("<I", dist))
+    return bytes(out)
+
+
+def kafka_compressed_requests(n, seed):
+    """Produce requests whose partitions mix plain and compressed messages:
+    gzip (levels 0-9, fixed / huffman-only / RLE strategies, header fields,
+    several members), snappy (plain and xerial, long offsets), nesting, and
+    corrupted compressed values whose message CRCs are valid, so the decoders
+    see the damage."""
+    rng = np.random.default_rng(seed)
+    topics = ["topic-%04d" % i for i in range(20)]
+    out = []
+
+    def payload(k):
+        a = [b"abcabcabd ", b"kafka-record-%d;", b"\x00\x01\x02\x03"][int(rng.integers(0, 3))]
+        if b"%d" in a:
+            s = b"".join(a % int(rng.integers(0, 50)) for _ in range(k // 12 + 1))
+        else:
+            s = a * (k // len(a) + 1)
+        s = bytearray(s[:k])
+        for _ in range(int(rng.integers(0, 4))):
+            if s:
+                s[int(rng.integers(0, len(s)))] = int(rng.integers(0, 256))
+        return bytes(s)
+
+    def inner(ver, depth=0):
+        msgs = []
+        for _ in range(int(rng.integers(1, 4))):
+            if depth < 2 and rng.random() < 0.15:
+                msgs.append(compressed(inner(ver, depth + 1), ver))
+            else:
+                msgs.append(k_message(payload(int(rng.integers(0, 600))), version=ver))
+        return b"".join(msgs)
+
+    def compressed(data, ver):
+        c = int(rng.integers(0, 8))
+        if c < 4:
+            value = _gz_member(data, level=int(rng.integers(0, 10)),
+                               strategy=int(rng.choice([0, 0, zlib.Z_FIXED, zlib.Z_HUFFMAN_ONLY, zlib.Z_RLE])),
+                               flags=int(rng.choice([0, 0, 0x04, 0x08, 0x1C])), extra=b"xy", name=b"f.bin",
+                               comment=b"c", hcrc=bool(rng.random() < 0.2))
+            if rng.random() < 0.15:  # a second member
+                value += _gz_member(payload(int(rng.integers(0, 50))))
+            codec = 1
+        else:
+            value = snappy_xerial(data, chunk=int(rng.integers(100, 5000))) if c >= 6 else snappy_block(data)
+            codec = 2
+        if rng.random() < 0.25:  # damage the compressed bytes (the message CRC stays valid)
+            value = bytearray(value)
+            op = int(rng.integers(0, 3))
+            if op == 0 and value:
+                i = int(rng.integers(0, len(value)))
+                value[i] ^= 1 << int(rng.integers(0, 8))
+            elif op == 1 and value:
+                del value[int(rng.integers(0, len(value))):]
+            else:
+                value += bytes(int(rng.integers(1, 12)))
+            value = bytes(value)
+        return k_message(value, version=ver, attributes=codec)
+
+    for i in range(n):
+        ver = int(rng.integers(0, 3))
+        tps = []
+        for _ in range(int(rng.integers(1, 3))):
+            parts = []
+            for p in range(int(rng.integers(1, 3))):
+                msgs = []
+                for _ in range(int(rng.integers(1, 4))):
+                    msgs.append(compressed(inner(ver), ver) if rng.random() < 0.6
+                                else k_message(payload(int(rng.integers(0, 200))), version=ver))
+                parts.append((p, msgs))
+            tps.append((topics[int(rng.integers(0, len(topics)))], parts))
+        out.append(k_produce(ver, i, "client-%02d" % int(rng.integers(0, 4)), tps))
+    return out
+
+
 def kafka_workload(n, nconns=256, seed=None, adversarial=False, all_kinds=False):
     seed = SEED_BASE + 3 if seed is None else seed
     if all_kinds:

@@ -28,6 +28,7 @@ typedef struct {
     const uint8_t *in; size_t n, pos;
     uint32_t bitbuf; int bitcnt;
     uint8_t *out; size_t cap, cnt;
+    size_t base;  /* output position where the current member began */
 } inf_t;
 
 /* next bit (LSB first, bytes read as needed); -1 at end of input */
@@ -128,7 +129,10 @@ static int inf_codes(inf_t *s, const huff_t *lit, const huff_t *dist, int fixed_
         if (ds >= 30) return -1;
         if (inf_bits(s, kDExt[ds], &e)) return -1;
         size_t d = (size_t)kDBase[ds] + e;
-        if (d > s->cnt) return -1;  /* before the start of the output */
+        /* before the start of this member's output: each gzip member gets a
+         * fresh flate reader (gunzip.go readHeader: Reset(z.r, nil)), so its
+         * history never reaches into the previous member */
+        if (d > s->cnt - s->base) return -1;
         for (int i = 0; i < len; i++) if (inf_put(s, s->out[s->cnt - d])) return -1;
     }
 }
@@ -226,7 +230,7 @@ static uint32_t crc_upd(uint32_t c, const uint8_t *p, size_t n) {
 
 /* gzip.NewReader + ioutil.ReadAll: 0 ok, -1 error */
 int ref_gunzip(const uint8_t *in, size_t n, uint8_t *out, size_t cap, size_t *outlen) {
-    inf_t s = {in, n, 0, 0, 0, out, cap, 0};
+    inf_t s = {in, n, 0, 0, 0, out, cap, 0, 0};
     for (int member = 0;; member++) {
         /* readHeader */
         if (s.pos == n) { if (member == 0) return -1; break; }  /* io.EOF: end of the members */
@@ -263,6 +267,7 @@ int ref_gunzip(const uint8_t *in, size_t n, uint8_t *out, size_t cap, size_t *ou
             s.pos += 2;
         }
         size_t start = s.cnt;
+        s.base = start;
         if (inflate_stream(&s)) return -1;
         if (n - s.pos < 8) return -1;
         const uint8_t *t = in + s.pos;

@@ -74,6 +74,16 @@ def test_gunzip_header_fields_and_members():
     assert refpy.gunzip(gz_member(d) + gz_member(b"") + gz_member(b"tail")) == d + b"tail"
 
 
+def test_gunzip_member_history_is_reset():
+    """Each member gets a fresh flate reader (gunzip.go readHeader:
+    Reset(z.r, nil)): a back-reference into the previous member's output is
+    corrupt input, even though the bytes are there."""
+    d = b"0123456789abcdef" * 200
+    second = gen._gz_member(d[1600:], zdict=d[:1600])
+    assert refpy.gunzip(gen._gz_member(d[:1600]) + second) is None
+    assert refpy.gunzip(gen._gz_member(d[:1600]) + gen._gz_member(d[1600:])) == d
+
+
 def test_gunzip_errors():
     d = bytes(range(256)) * 40
     m = gz_member(d)
