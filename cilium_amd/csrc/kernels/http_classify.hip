@@ -799,21 +799,47 @@ __device__ __forceinline__ void dma_windows(uint8_t *wave_lds, uint64_t packed, 
 // ---------------------------------------------------------------- value-stop map of a tile
 // A value nobody constrains ends at its first "value stop" byte (< 0x20 other
 // than HT, or DEL: CR normally, anything else is an error).  Before its first
-// window the wave streams the byte span of its tile (packed batches keep the
-// 64 requests side by side) through its window area, 1 KiB pieces with kRing
-// of them in flight, and keeps one bit per 16-byte chunk -- "holds a value
-// stop" -- in registers: lane l holds pieces 4l..4l+3.  A long value is then
-// skipped by finding the first marked chunk at or after L.pa (the owning
-// lane's bits, by ds_bpermute) and reading only that chunk and the next.
-// A tile whose span exceeds kSpanMax has no map; its long values continue
-// window by window.
+// window the wave streams its tile's bytes through its window area, 1 KiB
+// pieces with kRing of them in flight, and keeps one bit per 16-byte chunk --
+// "holds a value stop" -- in registers: lane l holds pieces 4l..4l+3.  A long
+// value is then skipped by finding the first marked chunk at or after L.pa
+// (the owning lane's bits, by ds_bpermute) and reading only that chunk and the
+// next.
+// The chunks are numbered in a tile-wide "map space":
+//   - span mode (packed tiles: the 64 requests lie side by side): chunk v is
+//     the 16 bytes at lo + 16 v, so chunks shared by neighbours load once;
+//   - list mode (the HTTP list of a mixed batch, where other protocols'
+//     requests sit between ours): the requests' own chunks back to back, lane
+//     l's request at [vs_l, vs_l + nch_l), so no foreign byte is streamed.
+// A request's chunk c is map chunk vs + c in both modes.  A tile with more
+// than kMapChunks chunks has no map; its long values continue window by window.
 constexpr int kRing = (int)(kWaveLds / 1024);
-constexpr uint64_t kSpanMax = 256 * 1024;
+constexpr uint32_t kMapChunks = 256 * 64;  // 256 pieces of 64 chunks (4 per lane)
 
 struct TileMap {
-    uint64_t lo, hi;  // span [lo, hi), 16-byte aligned; lo == hi: no map
+    bool on, list;    // a map exists; list mode
+    uint64_t lo;      // span mode: address of map chunk 0
     uint32_t m[8];    // pieces 4*lane .. 4*lane+3, 64 chunk bits each
 };
+
+// a lane's chunk count in the map (lanes without a request or with an empty
+// one: 0)
+__device__ __forceinline__ uint32_t map_nch(const Lane &L) { return L.lena > L.a0 ? (L.lena + 15u) >> 4 : 0u; }
+
+// inclusive prefix sum of v over the wave
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v, uint32_t lane) {
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = (uint32_t)__shfl_up((int)v, o);
+        if (lane >= (uint32_t)o) v += t;
+    }
+    return v;
+}
+
+// this lane's first map chunk (recomputed when needed: no register held for it)
+__device__ __forceinline__ uint32_t map_vs(const TileMap &T, const Lane &L, uint32_t lane) {
+    const uint32_t nch = map_nch(L);
+    return T.list ? wave_incl_sum(nch, lane) - nch : (uint32_t)((L.base - T.lo) >> 4);
+}
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
@@ -833,30 +859,36 @@ __device__ __forceinline__ uint32_t byte_at32(uint4 a, uint4 b, uint32_t i) {
     return (d >> (8 * (i & 3))) & 0xFF;
 }
 
-__device__ __forceinline__ void build_tile_map(TileMap &T, const Lane &L, uint32_t lane, uint8_t *wave_lds) {
+// list mode: the address of map chunk v, by a shuffle search for its owner
+// (the first lane whose inclusive chunk prefix vx exceeds v); stateless, so
+// nothing extra stays live across the ring
+__device__ __forceinline__ uint64_t map_addr(uint32_t v, uint32_t vx, uint32_t nch, uint64_t my_base) {
+    uint32_t r = 0;
 #pragma unroll
-    for (int q = 0; q < 8; q++) T.m[q] = 0;
-    uint64_t lo = L.done ? ~0ull : L.base;
-    uint64_t hi = L.done ? 0ull : L.base + ((L.lena + 15u) & ~15u);
-    for (int o = 32; o > 0; o >>= 1) {
-        const uint64_t l2 = (uint64_t)__shfl_xor((unsigned long long)lo, o);
-        const uint64_t h2 = (uint64_t)__shfl_xor((unsigned long long)hi, o);
-        lo = l2 < lo ? l2 : lo;
-        hi = h2 > hi ? h2 : hi;
+    for (uint32_t step = 32; step; step >>= 1) {
+        const uint32_t t = (uint32_t)__shfl((int)vx, (int)(r + step - 1));
+        if (t <= v) r += step;
     }
-    lo = uniform64(lo);
-    hi = uniform64(hi);
-    T.lo = T.hi = lo;
-    if (lo >= hi || hi - lo > kSpanMax) return;
-    T.hi = hi;
-    const uint32_t npieces = (uint32_t)((hi - lo + 1023) >> 10);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // earlier LDS reads of the window area have landed
-    // piece j -> slot s; an idle slot still issues its load (at the span
-    // start), so a slot is examined with exactly kRing-1 loads behind it
+    r &= 63;
+    const uint32_t vs = (uint32_t)__shfl((int)(vx - nch), (int)r);
+    const uint64_t base = (uint64_t)__shfl((unsigned long long)my_base, (int)r);
+    return base + ((uint64_t)(v - vs) << 4);
+}
+
+// The map's pieces through the window area: piece j -> slot j % kRing; an
+// idle slot still issues its load (at the first chunk), so a slot is examined
+// with exactly kRing-1 loads behind it.  (List mode: every lane runs map_addr,
+// with v clamped into the map, since a lane left out of a ds_bpermute would
+// read as zero to the others.)
+template <bool kList>
+__device__ __forceinline__ void map_ring(TileMap &T, uint32_t lane, uint8_t *wave_lds, uint64_t lo, uint32_t vtot,
+                                         uint32_t vx, uint32_t nch, uint64_t my_base) {
+    const uint32_t npieces = (vtot + 63) >> 6;
 #define MAP_ISSUE(s, j)                                                                                   \
     do {                                                                                                  \
-        const uint64_t a_ = lo + ((uint64_t)(j) << 10) + 16 * lane;                                       \
-        __builtin_amdgcn_global_load_lds((const void *)((j) < npieces && a_ < hi ? a_ : lo),               \
+        const uint32_t v_ = ((uint32_t)(j) << 6) + lane;                                                  \
+        const uint64_t a_ = kList ? map_addr(min(v_, vtot - 1), vx, nch, my_base) : lo + ((uint64_t)v_ << 4); \
+        __builtin_amdgcn_global_load_lds((const void *)((j) < npieces && v_ < vtot ? a_ : lo),             \
                                          (__attribute__((address_space(3))) void *)(wave_lds + (s) * 1024), \
                                          16, 0, 0);                                                       \
     } while (0)
@@ -875,7 +907,7 @@ __device__ __forceinline__ void build_tile_map(TileMap &T, const Lane &L, uint32
                              : "=v"(v)
                              : "v"((uint32_t)(uintptr_t)(wave_lds + s * 1024 + 16 * lane))
                              : "memory");
-                const bool ok = lo + ((uint64_t)j << 10) + 16 * lane < hi;
+                const bool ok = (j << 6) + lane < vtot;
                 const uint64_t M = __ballot(ok && stop_any(v) != 0);  // HT marks too: map_skip sorts it out
                 if (lane == (j >> 2)) {  // j & 3 == s & 3: a constant register index
                     T.m[2 * (s & 3)] = (uint32_t)M;
@@ -889,17 +921,51 @@ __device__ __forceinline__ void build_tile_map(TileMap &T, const Lane &L, uint32
 #undef MAP_ISSUE
 }
 
+__device__ __forceinline__ void build_tile_map(TileMap &T, const Lane &L, uint32_t lane, uint8_t *wave_lds) {
+#pragma unroll
+    for (int q = 0; q < 8; q++) T.m[q] = 0;
+    T.on = false;
+    T.list = false;
+    const uint32_t nch = map_nch(L);
+    uint64_t lo = nch ? L.base : ~0ull;
+    uint64_t hi = nch ? L.base + ((uint64_t)nch << 4) : 0ull;
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t l2 = (uint64_t)__shfl_xor((unsigned long long)lo, o);
+        const uint64_t h2 = (uint64_t)__shfl_xor((unsigned long long)hi, o);
+        lo = l2 < lo ? l2 : lo;
+        hi = h2 > hi ? h2 : hi;
+    }
+    const uint32_t vx = wave_incl_sum(nch, lane);  // inclusive prefix sum of the chunk counts
+    lo = uniform64(lo);
+    hi = uniform64(hi);
+    const uint32_t vtot_list = (uint32_t)__builtin_amdgcn_readlane((int)vx, 63);
+    if (lo >= hi) return;
+    const uint64_t span = (hi - lo) >> 4;
+    // span mode unless the span holds much more than the requests' own chunks
+    const bool list = span > (uint64_t)vtot_list + (vtot_list >> 3);
+    const uint32_t vtot = list ? vtot_list : (uint32_t)min(span, (uint64_t)kMapChunks + 1);
+    if (vtot > kMapChunks) return;
+    T.on = true;
+    T.list = list;
+    T.lo = lo;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // earlier LDS reads of the window area have landed
+    if (list) map_ring<true>(T, lane, wave_lds, lo, vtot, vx, nch, L.base);
+    else map_ring<false>(T, lane, wave_lds, lo, vtot, vx, nch, L.base);
+}
+
 // Lanes with L.scan set: skip the rest of the value with the tile map.
-__device__ __forceinline__ void map_skip(Lane &L, const TileMap &T) {
-    if (T.lo == T.hi) {  // no map: the value continues window by window
+__device__ __forceinline__ void map_skip(Lane &L, const TileMap &T, uint32_t lane) {
+    if (!T.on) {  // no map: the value continues window by window
         L.scan = false;
         return;
     }
+    if (!__any(L.scan)) return;
+    const uint32_t vs = map_vs(T, L, lane);
     while (__any(L.scan)) {
         const bool act = L.scan;
-        // span-relative chunk to search from; the request's chunks end at kend
-        uint32_t k = act ? (uint32_t)((L.base + L.pa - T.lo) >> 4) : 0;
-        const uint32_t kend = act ? (uint32_t)((L.base + L.lena - T.lo + 15) >> 4) : 0;
+        // map chunk to search from; the request's chunks end at kend
+        uint32_t k = act ? vs + (L.pa >> 4) : 0;
+        const uint32_t kend = act ? vs + ((L.lena + 15) >> 4) : 0;
         uint32_t found = 0xFFFFFFFFu;
         bool look = act && k < kend;
         while (__any(look)) {  // every lane takes part in the shuffles
@@ -927,10 +993,10 @@ __device__ __forceinline__ void map_skip(Lane &L, const TileMap &T) {
                 L.pa = L.lena;
                 finish(L, V_INCOMPLETE);
             } else {
-                const uint64_t ca = T.lo + ((uint64_t)found << 4);  // the marked chunk
+                const uint32_t cpos = (found - vs) << 4;  // the marked chunk, request-relative
+                const uint64_t ca = L.base + cpos;
                 const uint4 w0 = *(const uint4 *)ca;
-                const uint4 w1 = ca + 16 < T.hi ? *(const uint4 *)(ca + 16) : make_uint4(0, 0, 0, 0);
-                const uint32_t cpos = (uint32_t)(ca - L.base);  // request-relative
+                const uint4 w1 = cpos + 16 < L.lena ? *(const uint4 *)(ca + 16) : make_uint4(0, 0, 0, 0);
                 const uint32_t lo_b = L.pa > cpos ? L.pa - cpos : 0;
                 const uint32_t hi_b = min(L.lena - cpos, 16u);
                 const uint32_t m = vstop_mask(w0) & (0xFFFFu << lo_b) & ((1u << hi_b) - 1u);
@@ -1020,7 +1086,7 @@ __device__ __forceinline__ void run_tile(Lane &L, const uint8_t *img, uint8_t *w
         }
         PH_MARK(1);
         PH_COUNT(5, __builtin_popcountll(__ballot(L.scan)));
-        map_skip(L, TM);
+        map_skip(L, TM, lane);
         if (L.tail) finish_tail(I, L, O.nfa_bits);
         PH_MARK(2);
         if (L.done && L.owed) {
