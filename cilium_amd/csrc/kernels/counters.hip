@@ -60,15 +60,36 @@ __global__ __launch_bounds__(kHistBlock) void histogram_kernel(const uint8_t *__
     for (uint32_t i = threadIdx.x; i < nb + 8; i += kHistBlock) dst[i] = bins[i];
 }
 
-__global__ void reduce_kernel(const uint32_t *__restrict__ scratch, uint32_t nblocks, uint32_t stride, uint32_t lo,
-                              uint32_t nb, uint32_t nrules, uint64_t *__restrict__ counters) {
-    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool verdict_bin = lo == 0 && b >= nb && b < nb + 8;
-    if (b >= nb && !verdict_bin) return;
+// 64 bins per block; 4 threads per bin each sum a quarter of the rows with 8
+// loads in flight, then LDS combines the quarters (the column sums used to be
+// one thread per bin walking all rows serially: ~80 us of load latency)
+constexpr int kRedBins = 64, kRedParts = 4;
+__global__ __launch_bounds__(kRedBins * kRedParts) void reduce_kernel(const uint32_t *__restrict__ scratch,
+                                                                     uint32_t nblocks, uint32_t stride, uint32_t lo,
+                                                                     uint32_t nb, uint32_t nrules,
+                                                                     uint64_t *__restrict__ counters) {
+    __shared__ uint64_t part[kRedParts][kRedBins];
+    const uint32_t t = threadIdx.x % kRedBins, q = threadIdx.x / kRedBins;
+    const uint32_t b = blockIdx.x * kRedBins + t;
+    const uint32_t nbins = nb + (lo == 0 ? 8 : 0);
     uint64_t s = 0;
-    for (uint32_t k = 0; k < nblocks; k++) s += scratch[(size_t)k * stride + b];
+    if (b < nbins) {
+        uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        uint32_t k = q;
+        for (; k + 7 * kRedParts < nblocks; k += 8 * kRedParts) {
+#pragma unroll
+            for (int u = 0; u < 8; u++) acc[u] += scratch[(size_t)(k + u * kRedParts) * stride + b];
+        }
+        for (; k < nblocks; k += kRedParts) acc[0] += scratch[(size_t)k * stride + b];
+#pragma unroll
+        for (int u = 0; u < 8; u++) s += acc[u];
+    }
+    part[q][t] = s;
+    __syncthreads();
+    if (q != 0 || b >= nbins) return;
+    for (uint32_t p = 1; p < kRedParts; p++) s += part[p][t];
     if (!s) return;
-    if (verdict_bin) counters[nrules + (b - nb)] += s;
+    if (b >= nb) counters[nrules + (b - nb)] += s;  // verdict bins (lo == 0)
     else counters[lo + b] += s;
 }
 
@@ -126,8 +147,8 @@ hipError_t LaunchCounters(const uint8_t *verdict, const int32_t *rule, uint32_t 
         hipLaunchKernelGGL(histogram_kernel, dim3(nblocks), dim3(kHistBlock), 0, stream, verdict, rule, n, lo, nb,
                            scratch, stride);
         const uint32_t nbins = nb + (lo == 0 ? 8 : 0);
-        hipLaunchKernelGGL(reduce_kernel, dim3((nbins + 255) / 256), dim3(256), 0, stream, scratch, nblocks, stride,
-                           lo, nb, nrules, counters);
+        hipLaunchKernelGGL(reduce_kernel, dim3((nbins + kRedBins - 1) / kRedBins), dim3(kRedBins * kRedParts), 0,
+                           stream, scratch, nblocks, stride, lo, nb, nrules, counters);
     }
     return hipGetLastError();
 }
