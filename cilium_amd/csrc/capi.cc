@@ -244,6 +244,7 @@ hipError_t Upload(l7g_engine *e) {
         MT.rulesets = (const DevRuleset *)(d + m_rs);
         MT.images = d + m_img;
         MT.nrulesets = (uint32_t)M.rulesets.size();
+        MT.images_len = (uint32_t)M.images.size();
         MT.nfa_pool = M.nfa_pool.empty() ? nullptr : d + m_nfa;
         R2Tables &RT = e->rt;
         RT.rulesets = (const DevRuleset *)(d + r_rs);

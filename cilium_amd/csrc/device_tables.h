@@ -259,7 +259,7 @@ struct McTables {
     const DevRuleset *rulesets;
     const uint8_t *images;
     uint32_t nrulesets;
-    uint32_t pad;
+    uint32_t images_len;       // bytes of all images (staged in LDS when they fit)
     const uint8_t *nfa_pool;   // DevNfa pool (null: no keyRegex on the NFA fallback)
 };
 

@@ -32,6 +32,7 @@ namespace l7 {
 namespace {
 
 constexpr int kBlock = 256;
+constexpr uint32_t kMcLdsImages = 32 * 1024;  // LDS budget for the staged rule-set images
 
 // 16-byte aligned register window over one request (the arena is readable up
 // to the 16-byte boundary after its last byte; see include/l7gpu.h).
@@ -202,6 +203,18 @@ __global__ __launch_bounds__(kBlock) void memcache_classify_kernel(Batch B, McTa
     const uint32_t n = B.n, nconns = B.nconns;
     const uint32_t *__restrict__ conn_ids = B.conn_ids;
     const DevConn *__restrict__ conns = B.conns;
+    // The rule-set images (command / opcode masks, key DFAs) are read once per
+    // key byte in a dependent chain: when they all fit, every workgroup stages
+    // them in LDS (dynamic shared memory sized by the launcher) and walks them
+    // there instead of through L1/L2.
+    extern __shared__ __attribute__((aligned(16))) uint8_t mc_lds[];
+    const uint8_t *images = T.images;
+    if (T.images_len && T.images_len <= kMcLdsImages) {
+        const uint32_t n16 = (T.images_len + 15) / 16;
+        for (uint32_t i = threadIdx.x; i < n16; i += kBlock) ((uint4 *)mc_lds)[i] = ((const uint4 *)T.images)[i];
+        __syncthreads();
+        images = mc_lds;
+    }
     // sel: this protocol's request indices from partition_kernel (mixed batches), else all n
     const uint32_t m = sel ? *sel_count : n;
     for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < m; i += gridDim.x * kBlock) {
@@ -218,7 +231,7 @@ __global__ __launch_bounds__(kBlock) void memcache_classify_kernel(Batch B, McTa
         }
         const DevRuleset rs = T.rulesets[conn.ruleset];
         Image I;
-        I.p = T.images + rs.image_off;
+        I.p = images + rs.image_off;
         {
             const uint32_t h0 = *(const uint32_t *)I.p;
             I.nch = h0 & 0xFF;
@@ -374,11 +387,12 @@ hipError_t LaunchMemcacheClassify(const Batch &B, const McTables &T, const uint3
     if (B.n == 0) return hipSuccess;
     uint32_t blocks = (B.n + kBlock - 1) / kBlock;
     if (blocks > 8192) blocks = 8192;
+    const size_t lds = T.images_len && T.images_len <= kMcLdsImages ? ((T.images_len + 15) & ~15u) : 0;
     if (T.nfa_pool)
-        hipLaunchKernelGGL(memcache_classify_kernel<true>, dim3(blocks), dim3(kBlock), 0, stream, B, T, sel, sel_count,
+        hipLaunchKernelGGL(memcache_classify_kernel<true>, dim3(blocks), dim3(kBlock), lds, stream, B, T, sel, sel_count,
                            answer_other ? 1u : 0u);
     else
-        hipLaunchKernelGGL(memcache_classify_kernel<false>, dim3(blocks), dim3(kBlock), 0, stream, B, T, sel, sel_count,
+        hipLaunchKernelGGL(memcache_classify_kernel<false>, dim3(blocks), dim3(kBlock), lds, stream, B, T, sel, sel_count,
                            answer_other ? 1u : 0u);
     return hipGetLastError();
 }

@@ -46,7 +46,8 @@ enum {
     L7G_ALLOW = 1,       /* policy allows; rule = matched global rule id or -1 */
     L7G_PARSE_ERROR = 2, /* malformed request (connection is closed by the caller) */
     L7G_INCOMPLETE = 3,  /* more bytes are needed (proxylib MORE) */
-    L7G_UNSUPPORTED = 4, /* no parser for the connection, a request outside the arena, a compressed Kafka set */
+    L7G_UNSUPPORTED = 4, /* no parser for the connection, a request outside the arena, a nested compressed
+                            Kafka set beyond the decode space (kafka_inflate.hip) */
 };
 
 /* memcached: proxylib picks the text or binary parser from the first byte a
