@@ -33,6 +33,11 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr uint32_t kMcLdsImages = 32 * 1024;  // LDS budget for the staged rule-set images
+// waves per SIMD the common kernel is built for (experiments: -DL7G_MC_WAVES=N)
+#ifndef L7G_MC_WAVES
+#define L7G_MC_WAVES 7
+#endif
+#define L7G_MC_OCCUPANCY __attribute__((amdgpu_waves_per_eu(L7G_MC_WAVES, 8)))
 
 // 16-byte aligned register window over one request (the arena is readable up
 // to the 16-byte boundary after its last byte; see include/l7gpu.h).
@@ -196,10 +201,8 @@ __device__ __forceinline__ void classify_cmd(const uint32_t cw[4], uint32_t clen
 // kNfa: the variant that also runs NFA-fallback key matchers (launched only
 // when some memcache rule set has them; the other keeps its registers).
 template <bool kNfa>
-__global__ __launch_bounds__(kBlock) void memcache_classify_kernel(Batch B, McTables T,
-                                                                   const uint32_t *__restrict__ sel,
-                                                                   const uint32_t *__restrict__ sel_count,
-                                                                   uint32_t answer_other) {
+__device__ __forceinline__ void mc_classify(Batch B, McTables T, const uint32_t *__restrict__ sel,
+                                            const uint32_t *__restrict__ sel_count, uint32_t answer_other) {
     const uint32_t n = B.n, nconns = B.nconns;
     const uint32_t *__restrict__ conn_ids = B.conn_ids;
     const DevConn *__restrict__ conns = B.conns;
@@ -382,6 +385,23 @@ __global__ __launch_bounds__(kBlock) void memcache_classify_kernel(Batch B, McTa
     }
 }
 
+// The common kernel is built for L7G_MC_WAVES waves per SIMD (7; 2.4M
+// mixed-stream memcached requests: 4 waves (100 VGPRs, no spill) 0.91 ms,
+// 6 waves 0.79-0.82, 7 waves 0.79, 8 waves 0.84 -- the spills grow);
+// the NFA variant keeps its registers.
+__global__ __launch_bounds__(kBlock) L7G_MC_OCCUPANCY void memcache_classify_kernel(Batch B, McTables T,
+                                                                                  const uint32_t *__restrict__ sel,
+                                                                                  const uint32_t *__restrict__ sel_count,
+                                                                                  uint32_t answer_other) {
+    mc_classify<false>(B, T, sel, sel_count, answer_other);
+}
+__global__ __launch_bounds__(kBlock) void memcache_classify_nfa_kernel(Batch B, McTables T,
+                                                                       const uint32_t *__restrict__ sel,
+                                                                       const uint32_t *__restrict__ sel_count,
+                                                                       uint32_t answer_other) {
+    mc_classify<true>(B, T, sel, sel_count, answer_other);
+}
+
 hipError_t LaunchMemcacheClassify(const Batch &B, const McTables &T, const uint32_t *sel, const uint32_t *sel_count,
                                   bool answer_other, hipStream_t stream) {
     if (B.n == 0) return hipSuccess;
@@ -389,10 +409,10 @@ hipError_t LaunchMemcacheClassify(const Batch &B, const McTables &T, const uint3
     if (blocks > 8192) blocks = 8192;
     const size_t lds = T.images_len && T.images_len <= kMcLdsImages ? ((T.images_len + 15) & ~15u) : 0;
     if (T.nfa_pool)
-        hipLaunchKernelGGL(memcache_classify_kernel<true>, dim3(blocks), dim3(kBlock), lds, stream, B, T, sel, sel_count,
+        hipLaunchKernelGGL(memcache_classify_nfa_kernel, dim3(blocks), dim3(kBlock), lds, stream, B, T, sel, sel_count,
                            answer_other ? 1u : 0u);
     else
-        hipLaunchKernelGGL(memcache_classify_kernel<false>, dim3(blocks), dim3(kBlock), lds, stream, B, T, sel, sel_count,
+        hipLaunchKernelGGL(memcache_classify_kernel, dim3(blocks), dim3(kBlock), lds, stream, B, T, sel, sel_count,
                            answer_other ? 1u : 0u);
     return hipGetLastError();
 }
