@@ -46,6 +46,10 @@ def main():
     arena, offs, lens = gen.pack(reqs)
     h = gen.Workload("http-only", arena, offs, lens, w.conn_ids[keep], w.conns, w.policy, {})
     run(eng, h, 5, "same HTTP requests, packed")
+    # the HTTP requests where they lie in the mixed arena (gaps between them),
+    # classified on their own: memory layout vs the mixed launch itself
+    g = gen.Workload("http-in-place", w.arena, w.offsets[keep], w.lengths[keep], w.conn_ids[keep], w.conns, w.policy, {})
+    run(eng, g, 5, "same HTTP requests, in place")
     # the same packed HTTP requests plus one memcached request: the partition
     # path (HTTP list) with contiguous tiles
     mc = np.nonzero(proto != PROTO_HTTP)[0][:1]
