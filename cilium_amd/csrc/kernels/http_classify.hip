@@ -799,57 +799,47 @@ __device__ __forceinline__ void dma_windows(uint8_t *wave_lds, uint64_t packed, 
 // ---------------------------------------------------------------- value-stop map of a tile
 // A value nobody constrains ends at its first "value stop" byte (< 0x20 other
 // than HT, or DEL: CR normally, anything else is an error).  Before its first
-// window the wave streams its tile's bytes through its window area, 1 KiB
-// pieces with kRing of them in flight, and keeps one bit per 16-byte chunk --
-// "holds a value stop" -- in registers: lane l holds pieces 4l..4l+3.  A long
-// value is then skipped by finding the first marked chunk at or after L.pa
-// (the owning lane's bits, by ds_bpermute) and reading only that chunk and the
-// next.
-// The chunks are numbered in a tile-wide "map space":
-//   - span mode (packed tiles: the 64 requests lie side by side): chunk v is
-//     the 16 bytes at lo + 16 v, so chunks shared by neighbours load once;
-//   - list mode (the HTTP list of a mixed batch, where other protocols'
-//     requests sit between ours): the requests' own chunks back to back, lane
-//     l's request at [vs_l, vs_l + nch_l), so no foreign byte is streamed.
-// A request's chunk c is map chunk vs + c in both modes.  A tile with more
-// than kMapChunks chunks has no map; its long values continue window by window.
-constexpr int kRing = (int)(kWaveLds / 1024);
-constexpr uint32_t kMapChunks = 256 * 64;  // 256 pieces of 64 chunks (4 per lane)
+// window the wave streams its tile's bytes through its window area, and each
+// lane keeps, for its own request, one bit per 16-byte chunk -- "holds a value
+// stop" -- in registers.  Lane l streams request l: a step moves 64 bytes per
+// lane as four 16-byte LDS-DMA loads (the four 1 KiB blocks of a 4 KiB ring
+// slot; lane l's bytes at 16 l of each block), kMapSlots steps in flight.  So
+// every 16-byte chunk of a request is read once, whatever lies between the
+// tile's requests (packed streams, the HTTP list of a mixed batch, scattered
+// offsets), and a lane searches only its own bits.  A long value is then
+// skipped by finding the lane's first marked chunk at or after L.pa and
+// reading only that chunk and the next.  Chunks past the mapped range
+// (kMapChunks, 3 KiB) continue window by window.
+//
+// The bits enter a per-lane shift register four at a time (one step), so
+// after smax steps (the tile's longest request) chunk c sits at bit
+// c + T.off with T.off = kMapChunks - 4 smax, the same for every lane.
+//
+// Packed tiles (the 64 requests side by side, their span at most 9/8 of their
+// own chunks) take the span mode instead: the span streams as coalesced 1 KiB
+// pieces (lane l loads the piece's chunk l), a ballot gives every lane the
+// piece's 64 stop bits, and each lane keeps the (at most four) pieces that
+// overlap its request and finally shifts its own chunks into place (T.off = 0).
+// One 1 KiB piece is 8 full cache lines per load instruction where the
+// per-lane steps touch 64 lines: 0.48 vs 0.64 ms on cfg2's packed 1M stream;
+// on the mixed stream's HTTP list the per-lane steps win (2.35 vs 2.61 ms per
+// 4M requests) since no foreign byte is read.
+constexpr uint32_t kMapWords = 6;
+constexpr uint32_t kMapChunks = kMapWords * 32;             // chunks mapped per request
+constexpr uint32_t kStepBytes = 64 * 64;                    // one step: 64 lanes x 64 bytes
+constexpr int kMapSlots = (int)(kWaveLds / kStepBytes);     // steps in flight
+static_assert(kMapSlots >= 2, "map ring");
+constexpr int kRing = (int)(kWaveLds / 1024);               // span mode: 1 KiB pieces in flight
+constexpr uint64_t kSpanChunksMax = 256 * 64;               // span mode: at most 256 KiB
 
 struct TileMap {
-    bool on, list;    // a map exists; list mode
-    uint64_t lo;      // span mode: address of map chunk 0
-    uint32_t m[8];    // pieces 4*lane .. 4*lane+3, 64 chunk bits each
+    uint32_t off;              // bit position of chunk 0 (uniform)
+    uint32_t m[kMapWords];     // this lane's request: chunk bits (shift register)
 };
-
-// a lane's chunk count in the map (lanes without a request or with an empty
-// one: 0)
-__device__ __forceinline__ uint32_t map_nch(const Lane &L) { return L.lena > L.a0 ? (L.lena + 15u) >> 4 : 0u; }
-
-// inclusive prefix sum of v over the wave
-__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v, uint32_t lane) {
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t t = (uint32_t)__shfl_up((int)v, o);
-        if (lane >= (uint32_t)o) v += t;
-    }
-    return v;
-}
-
-// this lane's first map chunk (recomputed when needed: no register held for it)
-__device__ __forceinline__ uint32_t map_vs(const TileMap &T, const Lane &L, uint32_t lane) {
-    const uint32_t nch = map_nch(L);
-    return T.list ? wave_incl_sum(nch, lane) - nch : (uint32_t)((L.base - T.lo) >> 4);
-}
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
-    return ((uint64_t)hi << 32) | lo;
 }
 
 __device__ __forceinline__ uint32_t byte_at32(uint4 a, uint4 b, uint32_t i) {
@@ -859,45 +849,32 @@ __device__ __forceinline__ uint32_t byte_at32(uint4 a, uint4 b, uint32_t i) {
     return (d >> (8 * (i & 3))) & 0xFF;
 }
 
-// list mode: the address of map chunk v, by a shuffle search for its owner
-// (the first lane whose inclusive chunk prefix vx exceeds v); stateless, so
-// nothing extra stays live across the ring
-__device__ __forceinline__ uint64_t map_addr(uint32_t v, uint32_t vx, uint32_t nch, uint64_t my_base) {
-    uint32_t r = 0;
-#pragma unroll
-    for (uint32_t step = 32; step; step >>= 1) {
-        const uint32_t t = (uint32_t)__shfl((int)vx, (int)(r + step - 1));
-        if (t <= v) r += step;
-    }
-    r &= 63;
-    const uint32_t vs = (uint32_t)__shfl((int)(vx - nch), (int)r);
-    const uint64_t base = (uint64_t)__shfl((unsigned long long)my_base, (int)r);
-    return base + ((uint64_t)(v - vs) << 4);
-}
+// a lane's chunk count (lanes without a request or with an empty one: 0)
+__device__ __forceinline__ uint32_t map_nch(const Lane &L) { return L.lena > L.a0 ? (L.lena + 15u) >> 4 : 0u; }
 
-// The map's pieces through the window area: piece j -> slot j % kRing; an
-// idle slot still issues its load (at the first chunk), so a slot is examined
-// with exactly kRing-1 loads behind it.  (List mode: every lane runs map_addr,
-// with v clamped into the map, since a lane left out of a ds_bpermute would
-// read as zero to the others.)
-template <bool kList>
-__device__ __forceinline__ void map_ring(TileMap &T, uint32_t lane, uint8_t *wave_lds, uint64_t lo, uint32_t vtot,
-                                         uint32_t vx, uint32_t nch, uint64_t my_base) {
+// Span mode (packed tiles): see above.  The lane's request covers span chunks
+// [vs, vs + nch); pieces j0..j0+3 (j0 = vs / 64) hold them.
+__device__ __forceinline__ void map_span(TileMap &T, const Lane &L, uint32_t lane, uint8_t *wave_lds, uint64_t lo,
+                                         uint32_t vtot, uint32_t nch) {
     const uint32_t npieces = (vtot + 63) >> 6;
-#define MAP_ISSUE(s, j)                                                                                   \
+    const uint32_t vs = nch ? (uint32_t)((L.base - lo) >> 4) : 0u;
+    const uint32_t j0 = vs >> 6;
+    uint32_t pc[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // pieces j0..j0+3, 2 words each
+    // piece j -> slot j % kRing; an idle slot still issues its load (at the span
+    // start), so a slot is examined with exactly kRing-1 loads behind it
+#define MAP_PIECE(s, j)                                                                                   \
     do {                                                                                                  \
-        const uint32_t v_ = ((uint32_t)(j) << 6) + lane;                                                  \
-        const uint64_t a_ = kList ? map_addr(min(v_, vtot - 1), vx, nch, my_base) : lo + ((uint64_t)v_ << 4); \
-        __builtin_amdgcn_global_load_lds((const void *)((j) < npieces && v_ < vtot ? a_ : lo),             \
+        const uint64_t a_ = lo + ((uint64_t)(j) << 10) + 16 * lane;                                       \
+        __builtin_amdgcn_global_load_lds((const void *)((j) < npieces && ((j) << 6) + lane < vtot ? a_ : lo), \
                                          (__attribute__((address_space(3))) void *)(wave_lds + (s) * 1024), \
                                          16, 0, 0);                                                       \
     } while (0)
 #pragma unroll
-    for (int s = 0; s < kRing; s++) MAP_ISSUE(s, (uint32_t)s);
-    for (uint32_t j0 = 0; j0 < npieces; j0 += kRing) {
+    for (int s = 0; s < kRing; s++) MAP_PIECE(s, (uint32_t)s);
+    for (uint32_t jb = 0; jb < npieces; jb += kRing) {
 #pragma unroll
         for (int s = 0; s < kRing; s++) {
-            const uint32_t j = j0 + s;
+            const uint32_t j = jb + s;
             wait_vmcnt<kRing - 1>();
             if (j < npieces) {
                 // inline asm: a plain LDS read here would make hipcc drain every
@@ -909,115 +886,166 @@ __device__ __forceinline__ void map_ring(TileMap &T, uint32_t lane, uint8_t *wav
                              : "memory");
                 const bool ok = (j << 6) + lane < vtot;
                 const uint64_t M = __ballot(ok && stop_any(v) != 0);  // HT marks too: map_skip sorts it out
-                if (lane == (j >> 2)) {  // j & 3 == s & 3: a constant register index
-                    T.m[2 * (s & 3)] = (uint32_t)M;
-                    T.m[2 * (s & 3) + 1] = (uint32_t)(M >> 32);
-                }
+                const uint32_t q = j - j0;  // which of the lane's pieces (>= 4 or wrapped: none)
+#pragma unroll
+                for (int t = 0; t < 4; t++)
+                    if (q == (uint32_t)t) {
+                        pc[2 * t] = (uint32_t)M;
+                        pc[2 * t + 1] = (uint32_t)(M >> 32);
+                    }
             }
-            MAP_ISSUE(s, j + kRing);
+            MAP_PIECE(s, j + kRing);
+        }
+    }
+    wait_vmcnt<0>();
+#undef MAP_PIECE
+    // own chunk c = bit (vs & 63) + c of pc[]: shift right by vs & 63
+    const uint32_t sh = vs & 63, wsh = sh >> 5, bsh = sh & 31;
+#pragma unroll
+    for (int w = 0; w < (int)kMapWords; w++) {
+        const uint32_t a0 = wsh ? pc[w + 1] : pc[w];
+        const uint32_t a1 = wsh ? (w + 2 < 8 ? pc[w + 2] : 0u) : pc[w + 1];
+        T.m[w] = __builtin_amdgcn_alignbit(a1, a0, bsh);
+    }
+    T.off = 0;
+}
+
+__device__ __forceinline__ void build_tile_map(TileMap &T, const Lane &L, uint32_t lane, uint8_t *wave_lds) {
+#pragma unroll
+    for (int q = 0; q < (int)kMapWords; q++) T.m[q] = 0;
+    T.off = kMapChunks;
+    const uint32_t nch = min(map_nch(L), kMapChunks);
+    const uint32_t nseg = (nch + 3) >> 2;  // 64-byte steps of this lane
+    uint32_t smax = nseg;
+    for (int o = 32; o > 0; o >>= 1) smax = max(smax, (uint32_t)__shfl_xor((int)smax, o));
+    smax = (uint32_t)__builtin_amdgcn_readfirstlane((int)smax);
+    if (smax == 0) return;
+    const uint64_t act = __ballot(nch > 0);
+    const uint64_t dummy = (uint64_t)__shfl((unsigned long long)L.base, (int)__builtin_ctzll(act));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // earlier LDS reads of the window area have landed
+    {
+        uint64_t lo = nch ? L.base : ~0ull, hi = nch ? L.base + ((uint64_t)nch << 4) : 0ull;
+        uint32_t own = nch;
+        for (int o = 32; o > 0; o >>= 1) {
+            const uint64_t l2 = (uint64_t)__shfl_xor((unsigned long long)lo, o);
+            const uint64_t h2 = (uint64_t)__shfl_xor((unsigned long long)hi, o);
+            lo = l2 < lo ? l2 : lo;
+            hi = h2 > hi ? h2 : hi;
+            own += (uint32_t)__shfl_xor((int)own, o);
+        }
+        lo = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(lo >> 32)) << 32) |
+             (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)lo);
+        hi = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(hi >> 32)) << 32) |
+             (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)hi);
+        own = (uint32_t)__builtin_amdgcn_readfirstlane((int)own);
+        const uint64_t span = (hi - lo) >> 4;
+        if (span <= kSpanChunksMax && span <= (uint64_t)own + (own >> 3)) {
+            map_span(T, L, lane, wave_lds, lo, (uint32_t)span, nch);
+            return;
+        }
+    }
+    T.off = kMapChunks - 4 * smax;
+    // lanes with nothing (more) to load still issue theirs, at a chunk of the
+    // tile, so every step is four loads and vmcnt counts stay exact
+#define MAP_ISSUE(s, j)                                                                                        \
+    do {                                                                                                       \
+        _Pragma("unroll") for (int k_ = 0; k_ < 4; k_++) {                                                     \
+            const uint32_t c_ = 4 * (uint32_t)(j) + (uint32_t)k_;                                              \
+            const uint64_t a_ = c_ < nch ? L.base + ((uint64_t)c_ << 4) : dummy;                               \
+            __builtin_amdgcn_global_load_lds((const void *)a_,                                                \
+                                             (__attribute__((address_space(3))) void *)(wave_lds + (s) * kStepBytes + k_ * 1024), \
+                                             16, 0, 0);                                                        \
+        }                                                                                                      \
+    } while (0)
+#pragma unroll
+    for (int s = 0; s < kMapSlots; s++) MAP_ISSUE(s, (uint32_t)s);
+    for (uint32_t j0 = 0; j0 < smax; j0 += kMapSlots) {
+#pragma unroll
+        for (int s = 0; s < kMapSlots; s++) {
+            const uint32_t j = j0 + s;
+            wait_vmcnt<4 * (kMapSlots - 1)>();
+            if (j < smax) {
+                // inline asm: a plain LDS read here would make hipcc drain every
+                // in-flight LDS-DMA first (vmcnt(0)), serialising the ring
+                uint4 v0, v1, v2, v3;
+                const uint32_t la = (uint32_t)(uintptr_t)(wave_lds + s * kStepBytes + 16 * lane);
+                asm volatile("ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:1024\n\t"
+                             "ds_read_b128 %2, %4 offset:2048\n\tds_read_b128 %3, %4 offset:3072\n\t"
+                             "s_waitcnt lgkmcnt(0)"
+                             : "=v"(v0), "=v"(v1), "=v"(v2), "=v"(v3)
+                             : "v"(la)
+                             : "memory");
+                uint32_t nb = (stop_any(v0) ? 1u : 0u) | (stop_any(v1) ? 2u : 0u) | (stop_any(v2) ? 4u : 0u) |
+                              (stop_any(v3) ? 8u : 0u);
+                if (4 * j >= nch) nb = 0;
+                // shift the register right by 4, the new bits in at the top
+#pragma unroll
+                for (int q = 0; q < (int)kMapWords - 1; q++) T.m[q] = __builtin_amdgcn_alignbit(T.m[q + 1], T.m[q], 4);
+                T.m[kMapWords - 1] = (T.m[kMapWords - 1] >> 4) | (nb << 28);
+            }
+            MAP_ISSUE(s, j + kMapSlots);
         }
     }
     wait_vmcnt<0>();
 #undef MAP_ISSUE
 }
 
-__device__ __forceinline__ void build_tile_map(TileMap &T, const Lane &L, uint32_t lane, uint8_t *wave_lds) {
-#pragma unroll
-    for (int q = 0; q < 8; q++) T.m[q] = 0;
-    T.on = false;
-    T.list = false;
-    const uint32_t nch = map_nch(L);
-    uint64_t lo = nch ? L.base : ~0ull;
-    uint64_t hi = nch ? L.base + ((uint64_t)nch << 4) : 0ull;
-    for (int o = 32; o > 0; o >>= 1) {
-        const uint64_t l2 = (uint64_t)__shfl_xor((unsigned long long)lo, o);
-        const uint64_t h2 = (uint64_t)__shfl_xor((unsigned long long)hi, o);
-        lo = l2 < lo ? l2 : lo;
-        hi = h2 > hi ? h2 : hi;
-    }
-    const uint32_t vx = wave_incl_sum(nch, lane);  // inclusive prefix sum of the chunk counts
-    lo = uniform64(lo);
-    hi = uniform64(hi);
-    const uint32_t vtot_list = (uint32_t)__builtin_amdgcn_readlane((int)vx, 63);
-    if (lo >= hi) return;
-    const uint64_t span = (hi - lo) >> 4;
-    // span mode unless the span holds much more than the requests' own chunks
-    const bool list = span > (uint64_t)vtot_list + (vtot_list >> 3);
-    const uint32_t vtot = list ? vtot_list : (uint32_t)min(span, (uint64_t)kMapChunks + 1);
-    if (vtot > kMapChunks) return;
-    T.on = true;
-    T.list = list;
-    T.lo = lo;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // earlier LDS reads of the window area have landed
-    if (list) map_ring<true>(T, lane, wave_lds, lo, vtot, vx, nch, L.base);
-    else map_ring<false>(T, lane, wave_lds, lo, vtot, vx, nch, L.base);
-}
-
-// Lanes with L.scan set: skip the rest of the value with the tile map.
-__device__ __forceinline__ void map_skip(Lane &L, const TileMap &T, uint32_t lane) {
-    if (!T.on) {  // no map: the value continues window by window
-        L.scan = false;
-        return;
-    }
+// Lanes with L.scan set: skip the rest of the value with the lane's map.
+__device__ __forceinline__ void map_skip(Lane &L, const TileMap &T) {
     if (!__any(L.scan)) return;
-    const uint32_t vs = map_vs(T, L, lane);
-    while (__any(L.scan)) {
-        const bool act = L.scan;
-        // map chunk to search from; the request's chunks end at kend
-        uint32_t k = act ? vs + (L.pa >> 4) : 0;
-        const uint32_t kend = act ? vs + ((L.lena + 15) >> 4) : 0;
+    if (!L.scan) return;
+    const uint32_t nch = map_nch(L);
+    const uint32_t mapped = min(nch, kMapChunks);
+    for (;;) {
+        const uint32_t k = L.pa >> 4;
+        // first marked chunk in [k, mapped): bit positions [k + off, mapped + off)
         uint32_t found = 0xFFFFFFFFu;
-        bool look = act && k < kend;
-        while (__any(look)) {  // every lane takes part in the shuffles
-            const uint32_t j = k >> 6;
-            const int owner = (int)((j >> 2) & 63);
-            uint32_t d[8];
+        if (k < mapped) {
+            const uint32_t p0 = k + T.off, p1 = mapped + T.off;
 #pragma unroll
-            for (int q = 0; q < 8; q++) d[q] = (uint32_t)__shfl((int)T.m[q], owner);
-            const uint32_t w = j & 3;
-            const uint32_t mlo = w == 0 ? d[0] : w == 1 ? d[2] : w == 2 ? d[4] : d[6];
-            const uint32_t mhi = w == 0 ? d[1] : w == 1 ? d[3] : w == 2 ? d[5] : d[7];
-            const uint64_t M = (((uint64_t)mhi << 32) | mlo) & (~0ull << (k & 63));
-            if (look) {
-                if (M) {
-                    found = (j << 6) + (uint32_t)__builtin_ctzll(M);
-                    look = false;
-                } else {
-                    k = (j + 1) << 6;
-                    look = k < kend;
-                }
+            for (int w = (int)kMapWords - 1; w >= 0; w--) {
+                const uint32_t lo = 32u * (uint32_t)w;
+                uint32_t bits = T.m[w];
+                if (p0 > lo) bits = p0 - lo >= 32 ? 0u : bits & (0xFFFFFFFFu << (p0 - lo));
+                if (p1 < lo + 32) bits = p1 <= lo ? 0u : bits & (0xFFFFFFFFu >> (lo + 32 - p1));
+                if (bits) found = lo + (uint32_t)__builtin_ctz(bits) - T.off;
             }
         }
-        if (act) {
-            if (found >= kend) {  // no value stop before the request's end
+        if (found == 0xFFFFFFFFu) {
+            if (mapped < nch) {  // no stop in the mapped chunks: on window by window after them
+                L.pa = max(L.pa, mapped << 4);
+                L.scan = false;
+            } else {             // no value stop before the request's end
                 L.pa = L.lena;
                 finish(L, V_INCOMPLETE);
-            } else {
-                const uint32_t cpos = (found - vs) << 4;  // the marked chunk, request-relative
-                const uint64_t ca = L.base + cpos;
-                const uint4 w0 = *(const uint4 *)ca;
-                const uint4 w1 = cpos + 16 < L.lena ? *(const uint4 *)(ca + 16) : make_uint4(0, 0, 0, 0);
-                const uint32_t lo_b = L.pa > cpos ? L.pa - cpos : 0;
-                const uint32_t hi_b = min(L.lena - cpos, 16u);
-                const uint32_t m = vstop_mask(w0) & (0xFFFFu << lo_b) & ((1u << hi_b) - 1u);
-                if (m) {
-                    const uint32_t b = (uint32_t)__builtin_ctz(m);
-                    L.pa = cpos + b;
-                    L.scan = false;
-                    // "\r\n\r\n" here ends the header block: no window needed for it
-                    if (L.pa + 4 <= L.lena) {
-                        const uint32_t t4 = byte_at32(w0, w1, b) | byte_at32(w0, w1, b + 1) << 8 |
-                                            byte_at32(w0, w1, b + 2) << 16 | byte_at32(w0, w1, b + 3) << 24;
-                        L.tail = t4 == 0x0A0D0A0Du;
-                    }
-                } else {  // the chunk's stops lie before pa: search on
-                    L.pa = cpos + 16;
-                    if (L.pa >= L.lena) {
-                        L.pa = L.lena;
-                        finish(L, V_INCOMPLETE);
-                    }
-                }
             }
+            return;
+        }
+        const uint32_t cpos = found << 4;  // the marked chunk, request-relative
+        const uint64_t ca = L.base + cpos;
+        const uint4 w0 = *(const uint4 *)ca;
+        const uint4 w1 = cpos + 16 < L.lena ? *(const uint4 *)(ca + 16) : make_uint4(0, 0, 0, 0);
+        const uint32_t lo_b = L.pa > cpos ? L.pa - cpos : 0;
+        const uint32_t hi_b = min(L.lena - cpos, 16u);
+        const uint32_t m = vstop_mask(w0) & (0xFFFFu << lo_b) & ((1u << hi_b) - 1u);
+        if (m) {
+            const uint32_t b = (uint32_t)__builtin_ctz(m);
+            L.pa = cpos + b;
+            L.scan = false;
+            // "\r\n\r\n" here ends the header block: no window needed for it
+            if (L.pa + 4 <= L.lena) {
+                const uint32_t t4 = byte_at32(w0, w1, b) | byte_at32(w0, w1, b + 1) << 8 |
+                                    byte_at32(w0, w1, b + 2) << 16 | byte_at32(w0, w1, b + 3) << 24;
+                L.tail = t4 == 0x0A0D0A0Du;
+            }
+            return;
+        }
+        // the chunk's stops lie before pa (or are HT): search on
+        L.pa = cpos + 16;
+        if (L.pa >= L.lena) {
+            L.pa = L.lena;
+            finish(L, V_INCOMPLETE);
+            return;
         }
     }
 }
@@ -1086,7 +1114,7 @@ __device__ __forceinline__ void run_tile(Lane &L, const uint8_t *img, uint8_t *w
         }
         PH_MARK(1);
         PH_COUNT(5, __builtin_popcountll(__ballot(L.scan)));
-        map_skip(L, TM, lane);
+        map_skip(L, TM);
         if (L.tail) finish_tail(I, L, O.nfa_bits);
         PH_MARK(2);
         if (L.done && L.owed) {
