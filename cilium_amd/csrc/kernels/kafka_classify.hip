@@ -159,7 +159,10 @@ __device__ __forceinline__ uint32_t topic_first(const KafkaTables &T, const DevK
 // sel: this protocol's request indices from partition_kernel (mixed batches),
 // else requests 0..n-1.  answer_other: answer entries on connections that are
 // not Kafka (single-protocol engines, where partition_kernel does not run).
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) void kafka_classify_kernel(
+#ifndef L7G_KAFKA_WAVES
+#define L7G_KAFKA_WAVES 6
+#endif
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(L7G_KAFKA_WAVES, 8))) void kafka_classify_kernel(
     Batch B, KafkaTables T, const uint32_t *__restrict__ sel, const uint32_t *__restrict__ sel_count,
     uint32_t answer_other, uint32_t *__restrict__ zlist, uint32_t *__restrict__ zcount) {
     const uint32_t n = B.n, nconns = B.nconns;
