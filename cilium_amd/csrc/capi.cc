@@ -4,6 +4,7 @@
 
 #include <cstring>
 #include <map>
+#include <thread>
 #include <memory>
 #include <tuple>
 #include <mutex>
@@ -48,6 +49,53 @@ hipError_t KafkaPhaseTimes(uint64_t *out, bool reset);
 
 using namespace l7;
 
+// Scratch of the l7g_classify calls on one caller stream: the partition lists,
+// the NFA pre-pass bits, the counter histograms, the compressed-Kafka decode
+// region, and the completion event of the last call on that stream.  Calls on
+// different streams use different scratch and run concurrently; calls on one
+// stream are ordered by the stream itself.
+struct StreamScratch {
+    // protocol split (grow-only): [counts(16) | L7_KAFKA_CLASSES x n Kafka idx | n memcached idx |
+    // n HTTP idx | n idx of Kafka requests with compressed messages]
+    uint32_t *d_sel = nullptr;
+    size_t sel_cap = 0;
+    // decode region of kafka_inflate_kernel (one slice per workgroup), allocated
+    // with the first Kafka batch on this stream
+    uint8_t *d_zreg = nullptr;
+    // NFA pre-pass results, u64 per request (grow-only)
+    uint64_t *d_nfa = nullptr;
+    size_t nfa_cap = 0;
+    // counter histogram scratch (kernels/counters.hip), allocated on first use
+    uint32_t *d_hist = nullptr;
+    // completion of the last call's kernels on this stream
+    hipEvent_t done_ev = nullptr;
+    bool launched = false;
+    uint64_t last_use = 0;
+    ~StreamScratch() {
+        if (d_sel) hipFree(d_sel);
+        if (d_zreg) hipFree(d_zreg);
+        if (d_nfa) hipFree(d_nfa);
+        if (d_hist) hipFree(d_hist);
+        if (done_ev) hipEventDestroy(done_ev);
+    }
+};
+constexpr size_t kMaxStreamScratch = 16;  // beyond: the least recently used one is handed over
+
+// l7g_classify_host's per-thread staging: its own stream, device arena and
+// request arrays (grow-only), so host-buffer calls from different threads
+// overlap instead of queueing on one stream.
+struct HostCtx {
+    hipStream_t s = nullptr;
+    uint8_t *arena = nullptr, *req = nullptr;
+    size_t arena_cap = 0, n_cap = 0;
+    ~HostCtx() {
+        if (s) hipStreamSynchronize(s);
+        if (arena) hipFree(arena);
+        if (req) hipFree(req);
+        if (s) hipStreamDestroy(s);
+    }
+};
+
 struct l7g_engine {
     int device = 0;
     std::mutex mu;
@@ -69,24 +117,13 @@ struct l7g_engine {
     bool tables_dirty = true, conns_dirty = true;
     bool has_http = false, has_kafka = false, has_mc = false, has_r2 = false;
     int32_t hot_ruleset = -1;  // HTTP rule set staged in LDS (most connections)
-    // l7g_classify_host scratch (grow-only), guarded by smu
-    std::mutex smu;
-    hipStream_t sstream = nullptr;
-    uint8_t *s_arena = nullptr, *s_req = nullptr;
-    size_t s_arena_cap = 0, s_n_cap = 0;
+    // l7g_classify_host contexts, one per calling thread (guarded by hmu)
+    std::mutex hmu;
+    std::map<std::thread::id, std::unique_ptr<HostCtx>> hctx;
     bool any_cold = false;     // some HTTP connection uses another rule set
-    // protocol split (grow-only, stream-ordered): [counts(16) | L7_KAFKA_CLASSES x n Kafka idx | n memcached idx |
-    // n HTTP idx | n idx of Kafka requests with compressed messages]
-    uint32_t *d_sel = nullptr;
-    size_t sel_cap = 0;
-    // decode region of kafka_inflate_kernel (one slice per workgroup), allocated
-    // with the first Kafka batch, stream-ordered as d_sel
-    uint8_t *d_zreg = nullptr;
-    // NFA pre-pass results, u64 per request (grow-only, stream-ordered as d_sel)
-    uint64_t *d_nfa = nullptr;
-    size_t nfa_cap = 0;
-    // counter histogram scratch (kernels/counters.hip), allocated on first use
-    uint32_t *d_hist = nullptr;
+    // per-stream scratch of l7g_classify (guarded by mu)
+    std::map<hipStream_t, std::unique_ptr<StreamScratch>> scr;
+    uint64_t calls = 0;
     // proxy statistics: key (policy, proto, port, ingress) per connection, and
     // the device accumulator u64[keys][4] (l7g_flow_stats_*)
     std::map<std::tuple<int32_t, uint8_t, uint32_t, uint8_t>, uint16_t> skeys;
@@ -94,21 +131,60 @@ struct l7g_engine {
     bool flow_stats = false;
     uint64_t *d_flow = nullptr;
     size_t flow_cap = 0;  // keys the accumulator holds
-    // Completion of the last l7g_classify's kernels (recorded on the caller's
-    // stream).  The engine waits on it -- never on the caller's stream, which
-    // may be gone by then -- before it rewrites or frees anything a launched
-    // kernel reads: the connection table, the table blob, the partition scratch.
-    hipEvent_t done_ev = nullptr;
-    bool launched = false;
+    // Every stream's last completion event (StreamScratch::done_ev) is waited
+    // on -- never a caller's stream, which may be gone by then -- before the
+    // engine rewrites or frees anything a launched kernel reads: the
+    // connection table, the table blob, the proxy-statistics accumulator.
     // l7g_profile_*: timing events around each launch of the last call
     bool profile = false;
     hipEvent_t prof_ev[5] = {};
     bool prof_ran[4] = {};
 };
 
+// Waits for the kernels of every stream's last call.  Caller holds e->mu.
 static hipError_t WaitLastClassify(l7g_engine *e) {
-    if (!e->launched) return hipSuccess;
-    return hipEventSynchronize(e->done_ev);
+    hipError_t rc = hipSuccess;
+    for (auto &kv : e->scr)
+        if (kv.second->launched) {
+            hipError_t r = hipEventSynchronize(kv.second->done_ev);
+            if (r != hipSuccess) rc = r;
+        }
+    return rc;
+}
+
+// The scratch of stream s (created on first use; past kMaxStreamScratch the
+// least recently used stream's scratch is handed over once s has been made
+// to wait for that stream's last call).  Caller holds e->mu.
+static hipError_t GetScratch(l7g_engine *e, hipStream_t s, StreamScratch **out) {
+    auto it = e->scr.find(s);
+    if (it == e->scr.end()) {
+        if (e->scr.size() >= kMaxStreamScratch) {
+            auto lru = e->scr.begin();
+            for (auto j = e->scr.begin(); j != e->scr.end(); ++j)
+                if (j->second->last_use < lru->second->last_use) lru = j;
+            std::unique_ptr<StreamScratch> sc = std::move(lru->second);
+            e->scr.erase(lru);
+            if (sc->launched) {
+                hipError_t rc = hipStreamWaitEvent(s, sc->done_ev, 0);
+                if (rc != hipSuccess) return rc;
+            }
+            it = e->scr.emplace(s, std::move(sc)).first;
+        } else {
+            auto sc = std::make_unique<StreamScratch>();
+            hipError_t rc = hipEventCreateWithFlags(&sc->done_ev, hipEventDisableTiming);
+            if (rc != hipSuccess) return rc;
+            it = e->scr.emplace(s, std::move(sc)).first;
+        }
+    }
+    // (a handle can be reused by a new stream while the old one's work is
+    // still pending: order the call after that work whatever the stream)
+    if (it->second->launched) {
+        hipError_t rc = hipStreamWaitEvent(s, it->second->done_ev, 0);
+        if (rc != hipSuccess) return rc;
+    }
+    it->second->last_use = ++e->calls;
+    *out = it->second.get();
+    return hipSuccess;
 }
 
 static void set_err(char *err, size_t errlen, const std::string &m) {
@@ -295,11 +371,6 @@ l7g_engine *l7g_engine_create(int device, char *err, size_t errlen) {
     if ((rc = hipSetDevice(device)) != hipSuccess) { set_err(err, errlen, hipGetErrorString(rc)); return nullptr; }
     auto *e = new l7g_engine();
     e->device = device;
-    if ((rc = hipEventCreateWithFlags(&e->done_ev, hipEventDisableTiming)) != hipSuccess) {
-        set_err(err, errlen, hipGetErrorString(rc));
-        delete e;
-        return nullptr;
-    }
     e->ps = std::make_unique<PolicySet>();
     e->hc = std::make_unique<HttpCompiler>(e->ps.get());
     e->kc = std::make_unique<KafkaCompiler>(e->ps.get());
@@ -315,17 +386,11 @@ void l7g_engine_destroy(l7g_engine *e) {
     hipDeviceSynchronize();
     if (e->d_blob) hipFree(e->d_blob);
     if (e->d_conns) hipFree(e->d_conns);
-    if (e->d_sel) hipFree(e->d_sel);
-    if (e->d_zreg) hipFree(e->d_zreg);
-    if (e->d_nfa) hipFree(e->d_nfa);
-    if (e->d_hist) hipFree(e->d_hist);
+    e->hctx.clear();
+    e->scr.clear();
     if (e->d_flow) hipFree(e->d_flow);
-    if (e->done_ev) hipEventDestroy(e->done_ev);
     for (hipEvent_t ev : e->prof_ev)
         if (ev) hipEventDestroy(ev);
-    if (e->s_arena) hipFree(e->s_arena);
-    if (e->s_req) hipFree(e->s_req);
-    if (e->sstream) hipStreamDestroy(e->sstream);
     delete e;
 }
 
@@ -454,49 +519,48 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
     // (a Kafka-only engine partitions too: the kind / length lists keep the
     // Kafka kernel's waves converged, 1.55 -> 0.99 ms on cfg3)
     const bool partitioned = nproto > 1 || e->has_kafka;
+    StreamScratch *S = nullptr;
+    if ((rc = GetScratch(e, s, &S)) != hipSuccess) return (int)rc;
     uint32_t *sel_k = nullptr, *sel_m = nullptr, *sel_h = nullptr, *sel_z = nullptr, *cnt = nullptr;
     if (partitioned) {
         const size_t need = 16 + (L7_KAFKA_CLASSES + 3) * (size_t)n;
-        // the scratch may still be in use by the previous batch (any stream)
-        if (e->launched) rc = hipStreamWaitEvent(s, e->done_ev, 0);
-        if (rc == hipSuccess && need > e->sel_cap) {
-            if (e->d_sel) {
-                rc = WaitLastClassify(e);
-                hipFree(e->d_sel);
-                e->d_sel = nullptr;
-                e->sel_cap = 0;
+        if (need > S->sel_cap) {
+            if (S->d_sel) {  // the previous call on this stream may still use it
+                if (S->launched) rc = hipEventSynchronize(S->done_ev);
+                hipFree(S->d_sel);
+                S->d_sel = nullptr;
+                S->sel_cap = 0;
             }
-            if (rc == hipSuccess) rc = hipMalloc(&e->d_sel, need * sizeof(uint32_t));
-            if (rc == hipSuccess) e->sel_cap = need;
+            if (rc == hipSuccess) rc = hipMalloc(&S->d_sel, need * sizeof(uint32_t));
+            if (rc == hipSuccess) S->sel_cap = need;
         }
         if (rc != hipSuccess) return (int)rc;
-        cnt = e->d_sel;  // [0, L7_KAFKA_CLASSES) Kafka classes, then memcached, HTTP, compressed Kafka
-        sel_k = e->d_sel + 16;
+        cnt = S->d_sel;  // [0, L7_KAFKA_CLASSES) Kafka classes, then memcached, HTTP, compressed Kafka
+        sel_k = S->d_sel + 16;
         sel_m = sel_k + L7_KAFKA_CLASSES * (size_t)n;
         sel_h = sel_m + (size_t)n;
         sel_z = sel_h + (size_t)n;
         if (rc == hipSuccess) rc = hipMemsetAsync(cnt, 0, 16 * sizeof(uint32_t), s);
-        if (rc == hipSuccess && e->has_kafka && !e->d_zreg)
-            rc = hipMalloc(&e->d_zreg, (size_t)KafkaInflateBlocks() * KafkaInflateRegionBytes());
+        if (rc == hipSuccess && e->has_kafka && !S->d_zreg)
+            rc = hipMalloc(&S->d_zreg, (size_t)KafkaInflateBlocks() * KafkaInflateRegionBytes());
         if (rc != hipSuccess) return (int)rc;
     }
     // rule sets with NFA-fallback matchers: the pre-pass writes one u64 per request
     HttpTables ht = e->ht;
     const bool nfa = e->ht.nfa_pool != nullptr && (e->has_http || nproto == 0);
     if (nfa && rc == hipSuccess) {
-        if (!partitioned && e->launched) rc = hipStreamWaitEvent(s, e->done_ev, 0);
-        if (rc == hipSuccess && n > e->nfa_cap) {
-            if (e->d_nfa) {
-                rc = WaitLastClassify(e);
-                hipFree(e->d_nfa);
-                e->d_nfa = nullptr;
-                e->nfa_cap = 0;
+        if (n > S->nfa_cap) {
+            if (S->d_nfa) {
+                if (S->launched) rc = hipEventSynchronize(S->done_ev);
+                hipFree(S->d_nfa);
+                S->d_nfa = nullptr;
+                S->nfa_cap = 0;
             }
-            if (rc == hipSuccess) rc = hipMalloc(&e->d_nfa, (size_t)n * sizeof(uint64_t));
-            if (rc == hipSuccess) e->nfa_cap = n;
+            if (rc == hipSuccess) rc = hipMalloc(&S->d_nfa, (size_t)n * sizeof(uint64_t));
+            if (rc == hipSuccess) S->nfa_cap = n;
         }
         if (rc != hipSuccess) return (int)rc;
-        ht.nfa_bits = e->d_nfa;
+        ht.nfa_bits = S->d_nfa;
     }
     // profiling: event k is recorded before stage k (partition, http, kafka, memcache), event 4 after the last
     const bool prof = e->profile;
@@ -515,7 +579,7 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
     uint32_t *zcount = cnt ? cnt + L7_KAFKA_CLASSES + 2 : nullptr;
     if (rc == hipSuccess && run[2]) rc = LaunchKafkaClassify(B, e->kt, sel_k, cnt, !partitioned, sel_z, zcount, s);
     // requests with gzip / snappy messages: decoded, their sets read, failures answered
-    if (rc == hipSuccess && run[2] && sel_z) rc = LaunchKafkaInflate(B, sel_z, zcount, e->d_zreg, s);
+    if (rc == hipSuccess && run[2] && sel_z) rc = LaunchKafkaInflate(B, sel_z, zcount, S->d_zreg, s);
     mark(3);
     if (rc == hipSuccess && run[3])
         rc = LaunchMemcacheClassify(B, e->mt, sel_m, cnt ? cnt + L7_KAFKA_CLASSES : nullptr, !partitioned, s);
@@ -532,7 +596,11 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
             if (rc == hipSuccess && e->d_flow)
                 rc = hipMemcpyAsync(d, e->d_flow, e->flow_cap * 4 * sizeof(uint64_t), hipMemcpyDeviceToDevice, s);
             if (rc == hipSuccess) {
-                if (e->d_flow) { hipStreamSynchronize(s); hipFree(e->d_flow); }
+                if (e->d_flow) {  // every stream's kernels may add into the old one
+                    hipStreamSynchronize(s);
+                    WaitLastClassify(e);
+                    hipFree(e->d_flow);
+                }
                 e->d_flow = d;
                 e->flow_cap = nk;
             }
@@ -541,56 +609,63 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
     }
     // per-rule allow hits and per-verdict totals, from the outputs
     if (rc == hipSuccess && counters) {
-        if (!e->d_hist) {
-            if (e->launched) rc = hipStreamWaitEvent(s, e->done_ev, 0);
-            if (rc == hipSuccess) rc = hipMalloc(&e->d_hist, CountersScratchBytes());
-        } else if (e->launched && !partitioned && !nfa) {
-            rc = hipStreamWaitEvent(s, e->done_ev, 0);  // the scratch may still be read by the previous call
-        }
-        if (rc == hipSuccess) rc = LaunchCounters(verdict, rule, n, (uint32_t)e->ps->nrules, counters, e->d_hist, s);
+        if (!S->d_hist) rc = hipMalloc(&S->d_hist, CountersScratchBytes());
+        if (rc == hipSuccess) rc = LaunchCounters(verdict, rule, n, (uint32_t)e->ps->nrules, counters, S->d_hist, s);
     }
-    if (rc == hipSuccess) rc = hipEventRecord(e->done_ev, s);
-    if (rc == hipSuccess) e->launched = true;
+    if (rc == hipSuccess) rc = hipEventRecord(S->done_ev, s);
+    if (rc == hipSuccess) S->launched = true;
     return (int)rc;
 }
 
 int l7g_classify_host(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const uint64_t *off, const uint32_t *len,
                       const uint32_t *conn, uint32_t n, uint8_t *verdict, int32_t *rule, uint32_t *consumed) {
     if (e->device < 0) return (int)hipErrorNoDevice;
-    std::lock_guard<std::mutex> g(e->smu);
     hipError_t rc = hipSetDevice(e->device);
     if (rc != hipSuccess) return (int)rc;
-    if (!e->sstream && (rc = hipStreamCreateWithFlags(&e->sstream, hipStreamNonBlocking)) != hipSuccess) return (int)rc;
-    // grow-only device scratch: arena (+64 B so aligned 16-byte reads stay inside) and per-request arrays
+    // this thread's stream and staging (the engine lock is held only while
+    // l7g_classify enqueues, so threads' copies and kernels overlap)
+    HostCtx *H = nullptr;
+    {
+        std::lock_guard<std::mutex> g(e->hmu);
+        auto &slot = e->hctx[std::this_thread::get_id()];
+        if (!slot) {
+            auto h = std::make_unique<HostCtx>();
+            if ((rc = hipStreamCreateWithFlags(&h->s, hipStreamNonBlocking)) != hipSuccess) return (int)rc;
+            slot = std::move(h);
+        }
+        H = slot.get();
+    }
+    // grow-only device staging: arena (+64 B so aligned 16-byte reads stay inside) and per-request arrays
+    // (the previous call of this thread has synchronised its stream, so nothing still reads them)
     const size_t need_a = arena_len + 64, need_n = std::max<uint32_t>(n, 1);
-    if (need_a > e->s_arena_cap) {
-        if (e->s_arena) hipFree(e->s_arena);
-        e->s_arena = nullptr;
-        e->s_arena_cap = 0;
+    if (need_a > H->arena_cap) {
+        if (H->arena) hipFree(H->arena);
+        H->arena = nullptr;
+        H->arena_cap = 0;
         size_t cap = std::max<size_t>(need_a, 1 << 16);
-        if ((rc = hipMalloc(&e->s_arena, cap)) != hipSuccess) return (int)rc;
-        e->s_arena_cap = cap;
+        if ((rc = hipMalloc(&H->arena, cap)) != hipSuccess) return (int)rc;
+        H->arena_cap = cap;
     }
-    if (need_n > e->s_n_cap) {
-        if (e->s_req) hipFree(e->s_req);
-        e->s_req = nullptr;
-        e->s_n_cap = 0;
+    if (need_n > H->n_cap) {
+        if (H->req) hipFree(H->req);
+        H->req = nullptr;
+        H->n_cap = 0;
         size_t cap = std::max<size_t>(need_n, 1024);
-        if ((rc = hipMalloc(&e->s_req, cap * 25)) != hipSuccess) return (int)rc;
-        e->s_n_cap = cap;
+        if ((rc = hipMalloc(&H->req, cap * 25)) != hipSuccess) return (int)rc;
+        H->n_cap = cap;
     }
-    uint8_t *base = e->s_req;
-    const size_t cap = e->s_n_cap;
+    uint8_t *base = H->req;
+    const size_t cap = H->n_cap;
     uint64_t *d_o = (uint64_t *)base;
     uint32_t *d_l = (uint32_t *)(base + cap * 8), *d_c = (uint32_t *)(base + cap * 12), *d_cons = (uint32_t *)(base + cap * 16);
     int32_t *d_r = (int32_t *)(base + cap * 20);
     uint8_t *d_v = base + cap * 24;
-    hipStream_t s = e->sstream;
-    if (arena_len) rc = hipMemcpyAsync(e->s_arena, arena, arena_len, hipMemcpyHostToDevice, s);
+    hipStream_t s = H->s;
+    if (arena_len) rc = hipMemcpyAsync(H->arena, arena, arena_len, hipMemcpyHostToDevice, s);
     if (rc == hipSuccess && n) rc = hipMemcpyAsync(d_o, off, n * 8, hipMemcpyHostToDevice, s);
     if (rc == hipSuccess && n) rc = hipMemcpyAsync(d_l, len, n * 4, hipMemcpyHostToDevice, s);
     if (rc == hipSuccess && n) rc = hipMemcpyAsync(d_c, conn, n * 4, hipMemcpyHostToDevice, s);
-    if (rc == hipSuccess) rc = (hipError_t)l7g_classify(e, e->s_arena, arena_len, d_o, d_l, d_c, n, d_v, d_r, d_cons, nullptr, s);
+    if (rc == hipSuccess) rc = (hipError_t)l7g_classify(e, H->arena, arena_len, d_o, d_l, d_c, n, d_v, d_r, d_cons, nullptr, s);
     if (rc == hipSuccess && n) rc = hipMemcpyAsync(verdict, d_v, n, hipMemcpyDeviceToHost, s);
     if (rc == hipSuccess && n) rc = hipMemcpyAsync(rule, d_r, n * 4, hipMemcpyDeviceToHost, s);
     if (rc == hipSuccess && n) rc = hipMemcpyAsync(consumed, d_cons, n * 4, hipMemcpyDeviceToHost, s);
@@ -674,7 +749,9 @@ int l7g_profile_enable(l7g_engine *e, int on) {
 int l7g_profile_last(l7g_engine *e, float out_ms[4]) {
     std::lock_guard<std::mutex> g(e->mu);
     for (int k = 0; k < 4; k++) out_ms[k] = 0.f;
-    if (!e->profile || !e->launched) return (int)hipErrorNotReady;
+    bool any = false;
+    for (auto &kv : e->scr) any = any || kv.second->launched;
+    if (!e->profile || !any) return (int)hipErrorNotReady;
     hipError_t rc = hipEventSynchronize(e->prof_ev[4]);
     for (int k = 0; k < 4 && rc == hipSuccess; k++)
         if (e->prof_ran[k]) rc = hipEventElapsedTime(&out_ms[k], e->prof_ev[k], e->prof_ev[k + 1]);

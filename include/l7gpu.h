@@ -126,15 +126,18 @@ int l7g_conn_update(l7g_engine *e, uint32_t index, const l7g_conn_t *conn, char 
  * (a hipStream_t, NULL = default stream).  counters may be NULL, else a
  * device array of (rules + 8) uint64 that accumulates per-rule allow hits
  * followed by per-verdict totals.  Batches with Kafka requests or with more
- * than one protocol use an engine-owned scratch of (9 n + 16) uint32 (the
- * partition lists); it grows on demand, and a call on a different stream than
- * the previous one first waits for that stream.  Returns 0 or a HIP error code. */
+ * than one protocol use a scratch of (11 n + 16) uint32 (the partition lists)
+ * and, with Kafka rules, a 1 GiB decode region for compressed message sets;
+ * scratch is kept per stream (up to 16 streams, then handed over least recently
+ * used first), so calls on different streams run concurrently and calls on one
+ * stream are ordered by it.  Returns 0 or a HIP error code. */
 int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const uint64_t *off, const uint32_t *len,
                  const uint32_t *conn, uint32_t n, uint8_t *verdict, int32_t *rule, uint32_t *consumed,
                  uint64_t *counters, void *stream);
 
-/* Same with host buffers: copies in, classifies, copies out, synchronises
- * (engine-owned device scratch and stream; safe to call from any thread). */
+/* Same with host buffers: copies in, classifies, copies out, synchronises.
+ * Each calling thread gets its own stream and device staging, so calls from
+ * several threads overlap (the engine lock covers only the enqueue). */
 int l7g_classify_host(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const uint64_t *off,
                       const uint32_t *len, const uint32_t *conn, uint32_t n, uint8_t *verdict, int32_t *rule,
                       uint32_t *consumed);
