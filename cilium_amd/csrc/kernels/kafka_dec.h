@@ -140,29 +140,6 @@ __device__ __forceinline__ uint32_t crc32_ieee(const uint32_t *tab, Cur &cur, co
     // Bulk: 64 aligned bytes per batch, four dwordx4 loads issued together so
     // one memory latency covers 8 slicing steps (a lane walks its message
     // alone; back-to-back dependent loads were the kernel's critical path).
-#ifdef L7G_KAFKA_CRC_PIPELINE  // experiment: the next batch's loads in flight while this one is hashed
-    if (i + 64 <= n) {
-        uint4 v[4];
-#pragma unroll
-        for (int j = 0; j < 4; j++) v[j] = reinterpret_cast<const uint4 *>(p + i)[j];
-        for (; i + 64 <= n; i += 64) {
-            uint4 nx[4];
-            const bool more = i + 128 <= n;
-#pragma unroll
-            for (int j = 0; j < 4; j++) nx[j] = more ? reinterpret_cast<const uint4 *>(p + i + 64)[j] : v[j];
-#pragma unroll
-            for (int j = 0; j < 8; j++) {
-                const uint4 &x = v[j >> 1];
-                const uint32_t lo = ((j & 1) ? x.z : x.x) ^ c, hi = (j & 1) ? x.w : x.y;
-                c = tab[7 * 256 + (lo & 0xFF)] ^ tab[6 * 256 + ((lo >> 8) & 0xFF)] ^ tab[5 * 256 + ((lo >> 16) & 0xFF)] ^
-                    tab[4 * 256 + (lo >> 24)] ^ tab[3 * 256 + (hi & 0xFF)] ^ tab[2 * 256 + ((hi >> 8) & 0xFF)] ^
-                    tab[1 * 256 + ((hi >> 16) & 0xFF)] ^ tab[hi >> 24];
-            }
-#pragma unroll
-            for (int j = 0; j < 4; j++) v[j] = nx[j];
-        }
-    }
-#else
     for (; i + 64 <= n; i += 64) {
         const uint4 *q = reinterpret_cast<const uint4 *>(p + i);
         uint4 v[4];
@@ -177,7 +154,6 @@ __device__ __forceinline__ uint32_t crc32_ieee(const uint32_t *tab, Cur &cur, co
                 tab[1 * 256 + ((hi >> 16) & 0xFF)] ^ tab[hi >> 24];
         }
     }
-#endif
     for (; i + 8 <= n; i += 8) {
         const uintptr_t a = (uintptr_t)(p + i);
         cur_fill(cur, a);
