@@ -37,7 +37,8 @@ def run(eng, w, steps, tag):
 
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 4_000_000
-    eng = Engine(0)
+    lib = os.environ.get("EXP_LIB")
+    eng = Engine(0, lib_path=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "cilium_amd", lib)) if lib else Engine(0)
     w = gen.mixed_workload(n)
     run(eng, w, 5, "mixed")
     proto = w.conns["proto"][w.conn_ids]
