@@ -806,7 +806,10 @@ __device__ __forceinline__ void dma_windows(uint8_t *wave_lds, uint64_t packed, 
 // slot; lane l's bytes at 16 l of each block), kMapSlots steps in flight.  So
 // every 16-byte chunk of a request is read once, whatever lies between the
 // tile's requests (packed streams, the HTTP list of a mixed batch, scattered
-// offsets), and a lane searches only its own bits.  A long value is then
+// offsets), and a lane searches only its own bits.  (The loads are issued four
+// lanes per request -- a load instruction covers 16 requests' 64-byte runs, not
+// 64 single lines: 2.42 -> 2.18 ms on 4M mixed-stream HTTP requests -- and a
+// ballot hands each lane its request's four bits.)  A long value is then
 // skipped by finding the lane's first marked chunk at or after L.pa and
 // reading only that chunk and the next.  Chunks past the mapped range
 // (kMapChunks, 3 KiB) continue window by window.
@@ -947,13 +950,20 @@ __device__ __forceinline__ void build_tile_map(TileMap &T, const Lane &L, uint32
     T.off = kMapChunks - 4 * smax;
     // lanes with nothing (more) to load still issue theirs, at a chunk of the
     // tile, so every step is four loads and vmcnt counts stay exact
+    // four lanes per request: load q of step j covers requests 16q..16q+15,
+    // lane l reading chunk 4j + (l & 3) of request 16q + (l >> 2), so one load
+    // instruction touches 16 requests' 64-byte runs instead of 64 lines
+    const uint32_t sub = lane & 3, grp = lane >> 2;
 #define MAP_ISSUE(s, j)                                                                                        \
     do {                                                                                                       \
-        _Pragma("unroll") for (int k_ = 0; k_ < 4; k_++) {                                                     \
-            const uint32_t c_ = 4 * (uint32_t)(j) + (uint32_t)k_;                                              \
-            const uint64_t a_ = c_ < nch ? L.base + ((uint64_t)c_ << 4) : dummy;                               \
+        _Pragma("unroll") for (int q_ = 0; q_ < 4; q_++) {                                                     \
+            const int src_ = 16 * q_ + (int)grp;                                                               \
+            const uint64_t b_ = (uint64_t)__shfl((unsigned long long)L.base, src_);                            \
+            const uint32_t n_ = (uint32_t)__shfl((int)nch, src_);                                              \
+            const uint32_t c_ = 4 * (uint32_t)(j) + sub;                                                       \
+            const uint64_t a_ = c_ < n_ ? b_ + ((uint64_t)c_ << 4) : dummy;                                    \
             __builtin_amdgcn_global_load_lds((const void *)a_,                                                \
-                                             (__attribute__((address_space(3))) void *)(wave_lds + (s) * kStepBytes + k_ * 1024), \
+                                             (__attribute__((address_space(3))) void *)(wave_lds + (s) * kStepBytes + q_ * 1024), \
                                              16, 0, 0);                                                        \
         }                                                                                                      \
     } while (0)
@@ -975,8 +985,12 @@ __device__ __forceinline__ void build_tile_map(TileMap &T, const Lane &L, uint32
                              : "=v"(v0), "=v"(v1), "=v"(v2), "=v"(v3)
                              : "v"(la)
                              : "memory");
-                uint32_t nb = (stop_any(v0) ? 1u : 0u) | (stop_any(v1) ? 2u : 0u) | (stop_any(v2) ? 4u : 0u) |
-                              (stop_any(v3) ? 8u : 0u);
+                // block q, bit l: request 16q + (l >> 2), chunk 4j + (l & 3)
+                const uint64_t M0 = __ballot(stop_any(v0) != 0), M1 = __ballot(stop_any(v1) != 0);
+                const uint64_t M2 = __ballot(stop_any(v2) != 0), M3 = __ballot(stop_any(v3) != 0);
+                const uint32_t qo = lane >> 4;
+                const uint64_t Mq = qo == 0 ? M0 : qo == 1 ? M1 : qo == 2 ? M2 : M3;
+                uint32_t nb = (uint32_t)(Mq >> (4 * (lane & 15))) & 0xFu;
                 if (4 * j >= nch) nb = 0;
                 // shift the register right by 4, the new bits in at the top
 #pragma unroll
