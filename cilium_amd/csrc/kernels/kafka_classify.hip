@@ -24,7 +24,7 @@ constexpr int kBlock = 256;
 // readMessageSet on the shared position; 0 ok, -1 error; zflag is set when a
 // compressed message was passed
 __device__ __forceinline__ int read_message_set(Cur &cur, const uint8_t *b, uint32_t &pos, uint32_t end, int32_t size,
-                                int16_t version, const uint32_t *crctab, bool &zflag) {
+                                int16_t version, const uint32_t *crctab, bool &zflag, uint8_t *stage) {
     if (size < 0) return 0;
     if ((uint32_t)size > kMaxParseBuf) return -1;
     KDec dec{b, pos, end, size, 0, &cur};
@@ -40,7 +40,7 @@ __device__ __forceinline__ int read_message_set(Cur &cur, const uint8_t *b, uint
         KDec md{b, at, at + (uint32_t)msize, -1, 0, &cur};
         uint32_t crc = (uint32_t)dec_int(md, 4);
         if (msize <= 4) break;
-        if (crc != crc32_ieee(crctab, cur, b + at + 4, (uint32_t)msize - 4)) break;  // stop, no drain
+        if (crc != crc32_ieee_staged(crctab, cur, b + at + 4, (uint32_t)msize - 4, stage)) break;  // stop, no drain
         dec_skip(md, 1);
         int8_t attr = (int8_t)dec_int(md, 1);
         if (version >= 1) dec_skip(md, 8);
@@ -171,6 +171,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(L7G_KAFK
     const DevConn *__restrict__ conns = B.conns;
     static_assert(kBlock == 256, "one CRC table entry per thread");
     __shared__ uint32_t crctab[kCrcSlices * 256];
+    // per wave: the CRC's 64-byte-per-lane staging area (crc32_ieee_staged)
+    __shared__ __attribute__((aligned(16))) uint8_t crcstage[kBlock / 64][4096];
+    uint8_t *stage = crcstage[threadIdx.x >> 6];
     {
         const uint32_t t = threadIdx.x;
         uint32_t c = t;
@@ -272,7 +275,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(L7G_KAFK
                             if (d.err) { rc = -1; break; }
                             const int32_t ss = (int32_t)dec_int(d, 4);
                             if (d.err) { rc = -1; break; }
-                            rc = read_message_set(cur, b, d.pos, d.end, ss, ver, crctab, zflag);
+                            rc = read_message_set(cur, b, d.pos, d.end, ss, ver, crctab, zflag, stage);
                             if (rc) break;
                         }
                     }
