@@ -516,9 +516,10 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
     // A single-protocol HTTP or memcached engine skips it; its one kernel walks the whole batch
     // and answers those requests.
     const int nproto = (int)e->has_http + (int)e->has_kafka + (int)e->has_mc + (int)e->has_r2;
-    // (a Kafka-only engine partitions too: the kind / length lists keep the
-    // Kafka kernel's waves converged, 1.55 -> 0.99 ms on cfg3)
-    const bool partitioned = nproto > 1 || e->has_kafka;
+    // (a Kafka-only or memcached-only engine partitions too: the kind / length
+    // lists keep the Kafka kernel's waves converged, 1.55 -> 0.99 ms on cfg3,
+    // and the text / binary lists the memcached kernel's)
+    const bool partitioned = nproto > 1 || e->has_kafka || e->has_mc;
     StreamScratch *S = nullptr;
     if ((rc = GetScratch(e, s, &S)) != hipSuccess) return (int)rc;
     uint32_t *sel_k = nullptr, *sel_m = nullptr, *sel_h = nullptr, *sel_z = nullptr, *cnt = nullptr;
@@ -535,7 +536,7 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
             if (rc == hipSuccess) S->sel_cap = need;
         }
         if (rc != hipSuccess) return (int)rc;
-        cnt = S->d_sel;  // [0, L7_KAFKA_CLASSES) Kafka classes, then memcached, HTTP, compressed Kafka
+        cnt = S->d_sel;  // [0, L7_KAFKA_CLASSES) Kafka classes, memcached text, binary, HTTP; [15] compressed Kafka
         sel_k = S->d_sel + 16;
         sel_m = sel_k + L7_KAFKA_CLASSES * (size_t)n;
         sel_h = sel_m + (size_t)n;
@@ -574,9 +575,9 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
     mark(1);
     if (rc == hipSuccess && run[1] && nfa) rc = LaunchHttpNfa(B, ht, s);
     if (rc == hipSuccess && run[1])
-        rc = LaunchHttpClassify(B, ht, sel_h, cnt ? cnt + L7_KAFKA_CLASSES + 1 : nullptr, e->any_cold, !partitioned, s);
+        rc = LaunchHttpClassify(B, ht, sel_h, cnt ? cnt + L7_KAFKA_CLASSES + 2 : nullptr, e->any_cold, !partitioned, s);
     mark(2);
-    uint32_t *zcount = cnt ? cnt + L7_KAFKA_CLASSES + 2 : nullptr;
+    uint32_t *zcount = cnt ? cnt + 15 : nullptr;
     if (rc == hipSuccess && run[2]) rc = LaunchKafkaClassify(B, e->kt, sel_k, cnt, !partitioned, sel_z, zcount, s);
     // requests with gzip / snappy messages: decoded, their sets read, failures answered
     if (rc == hipSuccess && run[2] && sel_z) rc = LaunchKafkaInflate(B, sel_z, zcount, S->d_zreg, s);

@@ -218,10 +218,13 @@ __device__ __forceinline__ void mc_classify(Batch B, McTables T, const uint32_t 
         __syncthreads();
         images = mc_lds;
     }
-    // sel: this protocol's request indices from partition_kernel (mixed batches), else all n
-    const uint32_t m = sel ? *sel_count : n;
+    // sel: this protocol's request indices from partition_kernel: sel_count[0]
+    // text requests from sel's start, sel_count[1] binary ones from its end
+    // (n slots); null: all n
+    const uint32_t mt = sel ? sel_count[0] : n;
+    const uint32_t m = sel ? mt + sel_count[1] : n;
     for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < m; i += gridDim.x * kBlock) {
-        const uint32_t idx = sel ? sel[i] : i;
+        const uint32_t idx = sel ? (i < mt ? sel[i] : sel[n - 1 - (i - mt)]) : i;
         const uint32_t ci = conn_ids[idx];
         const DevConn conn = ci < nconns ? conns[ci] : DevConn{-1, PROTO_NONE, 0, 0xFFFF};
         if (conn.proto != PROTO_MEMCACHE || conn.ruleset < 0 || (uint32_t)conn.ruleset >= T.nrulesets) {

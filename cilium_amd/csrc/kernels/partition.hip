@@ -22,9 +22,11 @@ namespace {
 constexpr int kBlock = 256;
 constexpr int kPer = 16;
 constexpr int kWaves = kBlock / 64;
-// list classes: 0..kKafkaClasses-1 Kafka by kind / length, then memcached, then HTTP
+// list classes: 0..kKafkaClasses-1 Kafka by kind / length, then memcached
+// text, memcached binary, then HTTP
 constexpr int kKafkaClasses = L7_KAFKA_CLASSES;
-constexpr int kClasses = kKafkaClasses + 2;
+constexpr int kMcText = kKafkaClasses, kMcBinary = kKafkaClasses + 1, kHttp = kKafkaClasses + 2;
+constexpr int kClasses = kKafkaClasses + 3;
 
 static_assert(kKafkaClasses == 1 || kKafkaClasses == 8, "length classes");
 // Kafka list class: the decode path a lane takes is set by the request kind
@@ -39,8 +41,10 @@ __device__ __forceinline__ uint8_t kafka_class(const uint8_t *b, uint32_t len) {
 }
 }  // namespace
 
-// Lists: Kafka class c at sel_kafka + c * n, memcached at sel_mc, HTTP at
-// sel_http; counts[c] entries each (Kafka classes, memcached, HTTP).  Within a
+// Lists: Kafka class c at sel_kafka + c * n; memcached text requests from the
+// start of sel_mc, binary ones from its end (n slots hold both); HTTP at
+// sel_http; counts[c] entries each (Kafka classes, memcached text, memcached
+// binary, HTTP).  Within a
 // block's 4096 requests every list keeps stream order, so an HTTP tile of 64
 // list entries is, but for the tiles that straddle two blocks, a window of
 // the stream (the HTTP kernel's value-stop map streams that window).  Requests no classifier owns (unknown connection index, a
@@ -70,8 +74,17 @@ __global__ __launch_bounds__(kBlock) void partition_kernel(Batch B, uint32_t *__
                 const uint64_t off = B.offs[idx];
                 cls = 1 + kafka_class(B.arena + off, l7_in_arena(off, len, B.arena_len) ? len : 0);
             }
-            else if (proto == PROTO_MEMCACHE) cls = 1 + kKafkaClasses;
-            else if (proto == PROTO_HTTP) cls = 2 + kKafkaClasses;
+            else if (proto == PROTO_MEMCACHE) {
+                // the parser the connection chose, else the one this buffer's
+                // first byte picks (memcached/parser.go:186-202): text and
+                // binary requests take different paths, so they get lists of
+                // their own and a wave runs only one of them
+                uint32_t mode = B.conns[ci].flags & 3;
+                const uint64_t off = B.offs[idx];
+                if (mode == 0) mode = B.lens[idx] > 0 && l7_in_arena(off, 1, B.arena_len) && B.arena[off] >= 0x80 ? 2 : 1;
+                cls = 1 + (mode == 2 ? kMcBinary : kMcText);
+            }
+            else if (proto == PROTO_HTTP) cls = 1 + kHttp;
             else if (proto != PROTO_R2D2) {  // (r2d2: its kernel walks the whole batch)
                 B.verdict[idx] = V_UNSUPPORTED;
                 B.rule[idx] = -1;
@@ -107,8 +120,11 @@ __global__ __launch_bounds__(kBlock) void partition_kernel(Batch B, uint32_t *__
         for (int c = 0; c < kClasses; c++) {
             const uint64_t mk = __ballot(p[r] == c + 1);
             if (p[r] == c + 1) {
-                uint32_t *dst = c < kKafkaClasses ? sel_kafka + (size_t)c * n : c == kKafkaClasses ? sel_mc : sel_http;
-                dst[off[c] + __popcll(mk & below)] = idx;
+                const uint32_t pos = off[c] + __popcll(mk & below);
+                if (c < kKafkaClasses) sel_kafka[(size_t)c * n + pos] = idx;
+                else if (c == kMcText) sel_mc[pos] = idx;
+                else if (c == kMcBinary) sel_mc[n - 1 - pos] = idx;  // binary from the list's end
+                else sel_http[pos] = idx;
             }
             off[c] += __popcll(mk);
         }
