@@ -32,8 +32,8 @@ hipError_t LaunchKafkaInflate(const Batch &B, const uint32_t *zlist, const uint3
                               hipStream_t stream);
 uint32_t KafkaInflateBlocks();
 uint32_t KafkaInflateRegionBytes();
-hipError_t LaunchMemcacheClassify(const Batch &B, const McTables &T, const uint32_t *sel, const uint32_t *sel_count,
-                                  bool answer_other, hipStream_t stream);
+hipError_t LaunchMemcacheClassify(const Batch &B, const McTables &T, const uint32_t *sel, const uint32_t *sel2,
+                                  const uint32_t *sel_count, bool answer_other, hipStream_t stream);
 hipError_t LaunchR2d2Classify(const Batch &B, const R2Tables &T, bool answer_other, hipStream_t stream);
 hipError_t LaunchCounters(const uint8_t *verdict, const int32_t *rule, uint32_t n, uint32_t nrules,
                           uint64_t *counters, uint32_t *scratch, hipStream_t stream);
@@ -536,7 +536,7 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
             if (rc == hipSuccess) S->sel_cap = need;
         }
         if (rc != hipSuccess) return (int)rc;
-        cnt = S->d_sel;  // [0, L7_KAFKA_CLASSES) Kafka classes, memcached text, binary, HTTP; [15] compressed Kafka
+        cnt = S->d_sel;  // [0, L7_KAFKA_CLASSES) Kafka classes, memcached retrievals, binary, HTTP, other text; [15] compressed Kafka
         sel_k = S->d_sel + 16;
         sel_m = sel_k + L7_KAFKA_CLASSES * (size_t)n;
         sel_h = sel_m + (size_t)n;
@@ -583,7 +583,7 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
     if (rc == hipSuccess && run[2] && sel_z) rc = LaunchKafkaInflate(B, sel_z, zcount, S->d_zreg, s);
     mark(3);
     if (rc == hipSuccess && run[3])
-        rc = LaunchMemcacheClassify(B, e->mt, sel_m, cnt ? cnt + L7_KAFKA_CLASSES : nullptr, !partitioned, s);
+        rc = LaunchMemcacheClassify(B, e->mt, sel_m, sel_h, cnt ? cnt + L7_KAFKA_CLASSES : nullptr, !partitioned, s);
     // r2d2 (proxylib's example line protocol): one lane per request over the whole batch
     if (rc == hipSuccess && e->has_r2) rc = LaunchR2d2Classify(B, e->rt, !partitioned, s);
     mark(4);

@@ -202,7 +202,8 @@ __device__ __forceinline__ void classify_cmd(const uint32_t cw[4], uint32_t clen
 // when some memcache rule set has them; the other keeps its registers).
 template <bool kNfa>
 __device__ __forceinline__ void mc_classify(Batch B, McTables T, const uint32_t *__restrict__ sel,
-                                            const uint32_t *__restrict__ sel_count, uint32_t answer_other) {
+                                            const uint32_t *__restrict__ sel2, const uint32_t *__restrict__ sel_count,
+                                            uint32_t answer_other) {
     const uint32_t n = B.n, nconns = B.nconns;
     const uint32_t *__restrict__ conn_ids = B.conn_ids;
     const DevConn *__restrict__ conns = B.conns;
@@ -219,12 +220,14 @@ __device__ __forceinline__ void mc_classify(Batch B, McTables T, const uint32_t 
         images = mc_lds;
     }
     // sel: this protocol's request indices from partition_kernel: sel_count[0]
-    // text requests from sel's start, sel_count[1] binary ones from its end
-    // (n slots); null: all n
-    const uint32_t mt = sel ? sel_count[0] : n;
-    const uint32_t m = sel ? mt + sel_count[1] : n;
+    // text retrievals from sel's start, sel_count[1] binary requests from its
+    // end, sel_count[3] other text commands from sel2's end (n slots each);
+    // null: all n
+    const uint32_t ma = sel ? sel_count[0] : n;
+    const uint32_t mb = sel ? ma + sel_count[3] : n;
+    const uint32_t m = sel ? mb + sel_count[1] : n;
     for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < m; i += gridDim.x * kBlock) {
-        const uint32_t idx = sel ? (i < mt ? sel[i] : sel[n - 1 - (i - mt)]) : i;
+        const uint32_t idx = !sel ? i : i < ma ? sel[i] : i < mb ? sel2[n - 1 - (i - ma)] : sel[n - 1 - (i - mb)];
         const uint32_t ci = conn_ids[idx];
         const DevConn conn = ci < nconns ? conns[ci] : DevConn{-1, PROTO_NONE, 0, 0xFFFF};
         if (conn.proto != PROTO_MEMCACHE || conn.ruleset < 0 || (uint32_t)conn.ruleset >= T.nrulesets) {
@@ -394,28 +397,30 @@ __device__ __forceinline__ void mc_classify(Batch B, McTables T, const uint32_t 
 // the NFA variant keeps its registers.
 __global__ __launch_bounds__(kBlock) L7G_MC_OCCUPANCY void memcache_classify_kernel(Batch B, McTables T,
                                                                                   const uint32_t *__restrict__ sel,
+                                                                                  const uint32_t *__restrict__ sel2,
                                                                                   const uint32_t *__restrict__ sel_count,
                                                                                   uint32_t answer_other) {
-    mc_classify<false>(B, T, sel, sel_count, answer_other);
+    mc_classify<false>(B, T, sel, sel2, sel_count, answer_other);
 }
 __global__ __launch_bounds__(kBlock) void memcache_classify_nfa_kernel(Batch B, McTables T,
                                                                        const uint32_t *__restrict__ sel,
+                                                                       const uint32_t *__restrict__ sel2,
                                                                        const uint32_t *__restrict__ sel_count,
                                                                        uint32_t answer_other) {
-    mc_classify<true>(B, T, sel, sel_count, answer_other);
+    mc_classify<true>(B, T, sel, sel2, sel_count, answer_other);
 }
 
-hipError_t LaunchMemcacheClassify(const Batch &B, const McTables &T, const uint32_t *sel, const uint32_t *sel_count,
-                                  bool answer_other, hipStream_t stream) {
+hipError_t LaunchMemcacheClassify(const Batch &B, const McTables &T, const uint32_t *sel, const uint32_t *sel2,
+                                  const uint32_t *sel_count, bool answer_other, hipStream_t stream) {
     if (B.n == 0) return hipSuccess;
     uint32_t blocks = (B.n + kBlock - 1) / kBlock;
     if (blocks > 8192) blocks = 8192;
     const size_t lds = T.images_len && T.images_len <= kMcLdsImages ? ((T.images_len + 15) & ~15u) : 0;
     if (T.nfa_pool)
-        hipLaunchKernelGGL(memcache_classify_nfa_kernel, dim3(blocks), dim3(kBlock), lds, stream, B, T, sel, sel_count,
+        hipLaunchKernelGGL(memcache_classify_nfa_kernel, dim3(blocks), dim3(kBlock), lds, stream, B, T, sel, sel2, sel_count,
                            answer_other ? 1u : 0u);
     else
-        hipLaunchKernelGGL(memcache_classify_kernel, dim3(blocks), dim3(kBlock), lds, stream, B, T, sel, sel_count,
+        hipLaunchKernelGGL(memcache_classify_kernel, dim3(blocks), dim3(kBlock), lds, stream, B, T, sel, sel2, sel_count,
                            answer_other ? 1u : 0u);
     return hipGetLastError();
 }

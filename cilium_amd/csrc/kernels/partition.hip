@@ -26,7 +26,8 @@ constexpr int kWaves = kBlock / 64;
 // text, memcached binary, then HTTP
 constexpr int kKafkaClasses = L7_KAFKA_CLASSES;
 constexpr int kMcText = kKafkaClasses, kMcBinary = kKafkaClasses + 1, kHttp = kKafkaClasses + 2;
-constexpr int kClasses = kKafkaClasses + 3;
+constexpr int kMcText2 = kKafkaClasses + 3;  // text commands not starting with 'g' (storage, delete, ...)
+constexpr int kClasses = kKafkaClasses + 4;
 
 static_assert(kKafkaClasses == 1 || kKafkaClasses == 8, "length classes");
 // Kafka list class: the decode path a lane takes is set by the request kind
@@ -41,10 +42,11 @@ __device__ __forceinline__ uint8_t kafka_class(const uint8_t *b, uint32_t len) {
 }
 }  // namespace
 
-// Lists: Kafka class c at sel_kafka + c * n; memcached text requests from the
-// start of sel_mc, binary ones from its end (n slots hold both); HTTP at
-// sel_http; counts[c] entries each (Kafka classes, memcached text, memcached
-// binary, HTTP).  Within a
+// Lists: Kafka class c at sel_kafka + c * n; memcached text retrievals from
+// the start of sel_mc, binary requests from its end (n slots hold both); HTTP
+// from the start of sel_http, the other memcached text commands from its end;
+// counts[c] entries each (Kafka classes, memcached retrievals, memcached
+// binary, HTTP, other memcached text).  Within a
 // block's 4096 requests every list keeps stream order, so an HTTP tile of 64
 // list entries is, but for the tiles that straddle two blocks, a window of
 // the stream (the HTTP kernel's value-stop map streams that window).  Requests no classifier owns (unknown connection index, a
@@ -79,10 +81,13 @@ __global__ __launch_bounds__(kBlock) void partition_kernel(Batch B, uint32_t *__
                 // first byte picks (memcached/parser.go:186-202): text and
                 // binary requests take different paths, so they get lists of
                 // their own and a wave runs only one of them
+                // (text: retrievals -- get / gets / gat / gats -- apart from the
+                // rest, whose lines are longer and parse more tokens)
                 uint32_t mode = B.conns[ci].flags & 3;
                 const uint64_t off = B.offs[idx];
-                if (mode == 0) mode = B.lens[idx] > 0 && l7_in_arena(off, 1, B.arena_len) && B.arena[off] >= 0x80 ? 2 : 1;
-                cls = 1 + (mode == 2 ? kMcBinary : kMcText);
+                const uint32_t c0 = B.lens[idx] > 0 && l7_in_arena(off, 1, B.arena_len) ? B.arena[off] : 0u;
+                if (mode == 0) mode = c0 >= 0x80 ? 2 : 1;
+                cls = 1 + (mode == 2 ? kMcBinary : c0 == 'g' ? kMcText : kMcText2);
             }
             else if (proto == PROTO_HTTP) cls = 1 + kHttp;
             else if (proto != PROTO_R2D2) {  // (r2d2: its kernel walks the whole batch)
@@ -124,7 +129,8 @@ __global__ __launch_bounds__(kBlock) void partition_kernel(Batch B, uint32_t *__
                 if (c < kKafkaClasses) sel_kafka[(size_t)c * n + pos] = idx;
                 else if (c == kMcText) sel_mc[pos] = idx;
                 else if (c == kMcBinary) sel_mc[n - 1 - pos] = idx;  // binary from the list's end
-                else sel_http[pos] = idx;
+                else if (c == kHttp) sel_http[pos] = idx;
+                else sel_http[n - 1 - pos] = idx;  // other text commands from the HTTP list's end
             }
             off[c] += __popcll(mk);
         }
