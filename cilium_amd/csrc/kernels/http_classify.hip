@@ -835,8 +835,14 @@ static_assert(kMapSlots >= 2, "map ring");
 constexpr int kRing = (int)(kWaveLds / 1024);               // span mode: 1 KiB pieces in flight
 constexpr uint64_t kSpanChunksMax = 256 * 64;               // span mode: at most 256 KiB
 
+// Lane mode leaves out each request's first kWin bytes: map_skip only ever
+// searches from the end of a window (a value still open there), so the first
+// window's chunks are never looked up, and the head window reads them anyway.
+constexpr uint32_t kSkipSteps = kWin / 64;
+
 struct TileMap {
     uint32_t off;              // bit position of chunk 0 (uniform)
+    uint32_t from;             // first chunk the map holds (uniform)
     uint32_t m[kMapWords];     // this lane's request: chunk bits (shift register)
 };
 
@@ -917,6 +923,7 @@ __device__ __forceinline__ void build_tile_map(TileMap &T, const Lane &L, uint32
 #pragma unroll
     for (int q = 0; q < (int)kMapWords; q++) T.m[q] = 0;
     T.off = kMapChunks;
+    T.from = 0;
     const uint32_t nch = min(map_nch(L), kMapChunks);
     const uint32_t nseg = (nch + 3) >> 2;  // 64-byte steps of this lane
     uint32_t smax = nseg;
@@ -948,6 +955,8 @@ __device__ __forceinline__ void build_tile_map(TileMap &T, const Lane &L, uint32
         }
     }
     T.off = kMapChunks - 4 * smax;
+    T.from = 4 * kSkipSteps;
+    if (smax <= kSkipSteps) return;  // every request fits its head window
     // lanes with nothing (more) to load still issue theirs, at a chunk of the
     // tile, so every step is four loads and vmcnt counts stay exact
     // four lanes per request: load q of step j covers requests 16q..16q+15,
@@ -968,8 +977,8 @@ __device__ __forceinline__ void build_tile_map(TileMap &T, const Lane &L, uint32
         }                                                                                                      \
     } while (0)
 #pragma unroll
-    for (int s = 0; s < kMapSlots; s++) MAP_ISSUE(s, (uint32_t)s);
-    for (uint32_t j0 = 0; j0 < smax; j0 += kMapSlots) {
+    for (int s = 0; s < kMapSlots; s++) MAP_ISSUE(s, kSkipSteps + (uint32_t)s);
+    for (uint32_t j0 = kSkipSteps; j0 < smax; j0 += kMapSlots) {
 #pragma unroll
         for (int s = 0; s < kMapSlots; s++) {
             const uint32_t j = j0 + s;
@@ -1012,6 +1021,10 @@ __device__ __forceinline__ void map_skip(Lane &L, const TileMap &T) {
     const uint32_t mapped = min(nch, kMapChunks);
     for (;;) {
         const uint32_t k = L.pa >> 4;
+        if (k < T.from) {  // (not reached: a scan starts at a window's end) window by window
+            L.scan = false;
+            return;
+        }
         // first marked chunk in [k, mapped): bit positions [k + off, mapped + off)
         uint32_t found = 0xFFFFFFFFu;
         if (k < mapped) {
