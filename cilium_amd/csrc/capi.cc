@@ -55,7 +55,7 @@ using namespace l7;
 // different streams use different scratch and run concurrently; calls on one
 // stream are ordered by the stream itself.
 struct StreamScratch {
-    // protocol split (grow-only): [counts(16) | L7_KAFKA_CLASSES x n Kafka idx | n memcached idx |
+    // protocol split (grow-only): [counts(32) | L7_KAFKA_CLASSES x n Kafka idx | n memcached idx |
     // n HTTP idx | n idx of Kafka requests with compressed messages]
     uint32_t *d_sel = nullptr;
     size_t sel_cap = 0;
@@ -524,7 +524,7 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
     if ((rc = GetScratch(e, s, &S)) != hipSuccess) return (int)rc;
     uint32_t *sel_k = nullptr, *sel_m = nullptr, *sel_h = nullptr, *sel_z = nullptr, *cnt = nullptr;
     if (partitioned) {
-        const size_t need = 16 + (L7_KAFKA_CLASSES + 3) * (size_t)n;
+        const size_t need = 32 + (L7_KAFKA_CLASSES + 3) * (size_t)n;
         if (need > S->sel_cap) {
             if (S->d_sel) {  // the previous call on this stream may still use it
                 if (S->launched) rc = hipEventSynchronize(S->done_ev);
@@ -536,12 +536,12 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
             if (rc == hipSuccess) S->sel_cap = need;
         }
         if (rc != hipSuccess) return (int)rc;
-        cnt = S->d_sel;  // [0, L7_KAFKA_CLASSES) Kafka classes, memcached retrievals, binary, HTTP, other text; [15] compressed Kafka
-        sel_k = S->d_sel + 16;
+        cnt = S->d_sel;  // [0, L7_KAFKA_CLASSES) Kafka classes, memcached retrievals, binary, HTTP, other text; [31] compressed Kafka
+        sel_k = S->d_sel + 32;
         sel_m = sel_k + L7_KAFKA_CLASSES * (size_t)n;
         sel_h = sel_m + (size_t)n;
         sel_z = sel_h + (size_t)n;
-        if (rc == hipSuccess) rc = hipMemsetAsync(cnt, 0, 16 * sizeof(uint32_t), s);
+        if (rc == hipSuccess) rc = hipMemsetAsync(cnt, 0, 32 * sizeof(uint32_t), s);
         if (rc == hipSuccess && e->has_kafka && !S->d_zreg)
             rc = hipMalloc(&S->d_zreg, (size_t)KafkaInflateBlocks() * KafkaInflateRegionBytes());
         if (rc != hipSuccess) return (int)rc;
@@ -577,7 +577,7 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
     if (rc == hipSuccess && run[1])
         rc = LaunchHttpClassify(B, ht, sel_h, cnt ? cnt + L7_KAFKA_CLASSES + 2 : nullptr, e->any_cold, !partitioned, s);
     mark(2);
-    uint32_t *zcount = cnt ? cnt + 15 : nullptr;
+    uint32_t *zcount = cnt ? cnt + 31 : nullptr;
     if (rc == hipSuccess && run[2]) rc = LaunchKafkaClassify(B, e->kt, sel_k, cnt, !partitioned, sel_z, zcount, s);
     // requests with gzip / snappy messages: decoded, their sets read, failures answered
     if (rc == hipSuccess && run[2] && sel_z) rc = LaunchKafkaInflate(B, sel_z, zcount, S->d_zreg, s);

@@ -18,8 +18,10 @@ enum : uint8_t {
 };
 enum : uint8_t { PROTO_NONE = 0, PROTO_HTTP = 1, PROTO_KAFKA = 2, PROTO_MEMCACHE = 3, PROTO_R2D2 = 4 };
 
-// partition_kernel groups Kafka requests into this many length classes
+// partition_kernel groups Kafka requests into this many kind / length classes
+#ifndef L7_KAFKA_CLASSES
 #define L7_KAFKA_CLASSES 8
+#endif
 
 // Header slots recorded by the HTTP framer.
 enum : int { SLOT_METHOD = 0, SLOT_PATH = 1, SLOT_AUTHORITY = 2, SLOT_CUSTOM0 = 3 };

@@ -29,13 +29,20 @@ constexpr int kMcText = kKafkaClasses, kMcBinary = kKafkaClasses + 1, kHttp = kK
 constexpr int kMcText2 = kKafkaClasses + 3;  // text commands not starting with 'g' (storage, delete, ...)
 constexpr int kClasses = kKafkaClasses + 4;
 
-static_assert(kKafkaClasses == 1 || kKafkaClasses == 8, "length classes");
+static_assert(kKafkaClasses == 1 || kKafkaClasses == 8 || kKafkaClasses == 12, "length classes");
+static_assert(kKafkaClasses + 4 <= 31, "counts[31] holds the compressed-Kafka count");
 // Kafka list class: the decode path a lane takes is set by the request kind
 // and, for produce, by how many message bytes it hashes, so fetch requests,
 // the other kinds, and produce requests by length each get lists of their own.
 __device__ __forceinline__ uint8_t kafka_class(const uint8_t *b, uint32_t len) {
     if (kKafkaClasses == 1) return 0;
     const uint32_t kind = len >= 6 ? (uint32_t)b[4] << 8 | b[5] : 0xFFFF;
+    if (kKafkaClasses == 12) {  // fetch by length (topic / partition count), other kinds, produce in 9 bins
+        if (kind == 1) return len < 128 ? 0 : 1;
+        if (kind != 0) return 2;
+        return len < 512 ? 3 : len < 896 ? 4 : len < 1280 ? 5 : len < 1664 ? 6 : len < 2048 ? 7
+             : len < 2560 ? 8 : len < 3072 ? 9 : len < 3712 ? 10 : 11;
+    }
     if (kind == 1) return 0;
     if (kind != 0) return 1;
     return len < 384 ? 2 : len < 640 ? 3 : len < 896 ? 4 : len < 1280 ? 5 : len < 2048 ? 6 : 7;
