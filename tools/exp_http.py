@@ -62,7 +62,8 @@ def variant(name, reqs, policy, nconns=1024):
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
     only = sys.argv[2].split(",") if len(sys.argv) > 2 else None  # variant letters a..e
-    eng = Engine(0)
+    lib = os.environ.get("EXP_LIB")
+    eng = Engine(0, lib_path=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "cilium_amd", lib)) if lib else Engine(0)
     base = gen.http_requests(n, gen.SEED_BASE + 2)
     heads = [r[: r.index(b"X-Pad: ")] + b"\r\n" for r in base]
     allow_all = api.policy_set(api.network_policy("10.0.0.1", 3, ingress=[(80, [api.port_rule()])]))
