@@ -235,7 +235,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(L7G_KAFK
             q.typed = (q.kind == 0 || q.kind == 1 || q.kind == 2 || q.kind == 3 || q.kind == 8 || q.kind == 9) ? 1
                     : (q.kind == 10 ? 2 : 0);
             q.client = -2;
-            const DevKafkaRuleset rs = T.rulesets[conn.ruleset];
+            // fields are read where they are used: a copy would hold 9 VGPRs across the decode
+            const DevKafkaRuleset &rs = T.rulesets[conn.ruleset];
             uint32_t ntopics = 0, cmax = 0;  // raw topic count; max over topics of first matching rule
             int rc = 0;
             if (q.typed) {
@@ -256,7 +257,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(L7G_KAFK
                     uint32_t e = topic_first(T, rs, q, tid);
                     cmax = cmax > e ? cmax : e;
                 };
-                int64_t nt, np;
+                int32_t nt, np;
                 uint32_t o, l;
                 switch (q.kind) {
                 case 0:  // Produce
@@ -264,13 +265,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(L7G_KAFK
                     dec_skip(d, 2); dec_skip(d, 4);
                     nt = dec_arraylen(d, false, bad);
                     if (bad) { rc = -1; break; }
-                    for (int64_t t = 0; t < nt && rc == 0; t++) {
+                    for (int32_t t = 0; t < nt && rc == 0; t++) {
                         dec_string(d, o, l);
                         if (d.err) break;
                         on_topic(o, l);
                         np = dec_arraylen(d, false, bad);
                         if (bad) { rc = -1; break; }
-                        for (int64_t p = 0; p < np; p++) {
+                        for (int32_t p = 0; p < np; p++) {
                             dec_skip(d, 4);
                             if (d.err) { rc = -1; break; }
                             const int32_t ss = (int32_t)dec_int(d, 4);
@@ -286,12 +287,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(L7G_KAFK
                     if (ver >= 4) dec_skip(d, 1);
                     nt = dec_arraylen(d, false, bad);
                     if (bad) { rc = -1; break; }
-                    for (int64_t t = 0; t < nt && !d.err; t++) {
+                    for (int32_t t = 0; t < nt && !d.err; t++) {
                         dec_string(d, o, l);
                         on_topic(o, l);
                         np = dec_arraylen(d, false, bad);
                         if (bad) { rc = -1; break; }
-                        for (int64_t p = 0; p < np && !d.err; p++) {
+                        for (int32_t p = 0; p < np && !d.err; p++) {
                             dec_skip(d, 4); dec_skip(d, 8);
                             if (ver >= 5) dec_skip(d, 8);
                             dec_skip(d, 4);
@@ -303,12 +304,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(L7G_KAFK
                     if (ver >= 2) dec_skip(d, 1);
                     nt = dec_arraylen(d, false, bad);
                     if (bad) { rc = -1; break; }
-                    for (int64_t t = 0; t < nt && !d.err; t++) {
+                    for (int32_t t = 0; t < nt && !d.err; t++) {
                         dec_string(d, o, l);
                         on_topic(o, l);
                         np = dec_arraylen(d, false, bad);
                         if (bad) { rc = -1; break; }
-                        for (int64_t p = 0; p < np && !d.err; p++) {
+                        for (int32_t p = 0; p < np && !d.err; p++) {
                             dec_skip(d, 4); dec_skip(d, 8);
                             if (ver == 0) dec_skip(d, 4);
                         }
@@ -317,7 +318,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(L7G_KAFK
                 case 3:  // Metadata
                     nt = dec_arraylen(d, true, bad);
                     if (bad) { rc = -1; break; }
-                    for (int64_t t = 0; t < nt && !d.err; t++) { dec_string(d, o, l); if (!d.err) on_topic(o, l); }
+                    for (int32_t t = 0; t < nt && !d.err; t++) { dec_string(d, o, l); if (!d.err) on_topic(o, l); }
                     if (ver >= 4) dec_skip(d, 1);
                     break;
                 case 8:  // OffsetCommit
@@ -326,12 +327,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(L7G_KAFK
                     if (ver >= 2) dec_skip(d, 8);
                     nt = dec_arraylen(d, false, bad);
                     if (bad) { rc = -1; break; }
-                    for (int64_t t = 0; t < nt && !d.err; t++) {
+                    for (int32_t t = 0; t < nt && !d.err; t++) {
                         dec_string(d, o, l);
                         on_topic(o, l);
                         np = dec_arraylen(d, false, bad);
                         if (bad) { rc = -1; break; }
-                        for (int64_t p = 0; p < np && !d.err; p++) {
+                        for (int32_t p = 0; p < np && !d.err; p++) {
                             dec_skip(d, 4); dec_skip(d, 8);
                             if (ver == 1) dec_skip(d, 8);
                             uint32_t o2, l2;
@@ -343,12 +344,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(L7G_KAFK
                     dec_string(d, o, l);
                     nt = dec_arraylen(d, true, bad);
                     if (bad) { rc = -1; break; }
-                    for (int64_t t = 0; t < nt && !d.err; t++) {
+                    for (int32_t t = 0; t < nt && !d.err; t++) {
                         dec_string(d, o, l);
                         on_topic(o, l);
                         np = dec_arraylen(d, false, bad);
                         if (bad) { rc = -1; break; }
-                        for (int64_t p = 0; p < np && !d.err; p++) dec_skip(d, 4);
+                        for (int32_t p = 0; p < np && !d.err; p++) dec_skip(d, 4);
                     }
                     break;
                 case 10:  // ConsumerMetadata

@@ -49,14 +49,14 @@ __device__ __forceinline__ uint32_t cur_byte(Cur &c, const uint8_t *p) {
 struct KDec {
     const uint8_t *b;
     uint32_t pos, end;
-    int64_t limit;  // LimitReader remaining, -1 = none
+    int32_t limit;  // LimitReader remaining, -1 = none (a set is at most kMaxParseBuf)
     int err;        // 0 ok, 1 EOF, 2 ErrUnexpectedEOF, 3 other
     Cur *c;
 };
 
 __device__ __forceinline__ uint32_t kavail(const KDec &d) {
     uint32_t a = d.end - d.pos;
-    if (d.limit >= 0 && (uint64_t)d.limit < a) a = (uint32_t)d.limit;
+    if (d.limit >= 0 && (uint32_t)d.limit < a) a = (uint32_t)d.limit;
     return a;
 }
 // io.ReadFull(r, buf[:n]); returns start offset, sets d.err on a short read
@@ -67,7 +67,7 @@ __device__ __forceinline__ uint32_t kread(KDec &d, uint32_t n) {
     if (a == 0) { d.err = 1; return at; }
     uint32_t take = a < n ? a : n;
     d.pos += take;
-    if (d.limit >= 0) d.limit -= take;
+    if (d.limit >= 0) d.limit -= (int32_t)take;
     if (take < n) d.err = 2;
     return at;
 }
@@ -115,11 +115,11 @@ __device__ __forceinline__ void dec_string(KDec &d, uint32_t &off, uint32_t &len
     off = at; len = (uint32_t)sl;
 }
 // DecodeArrayLen(nullable): -1 null; sets bad on ErrInvalidArrayLen
-__device__ __forceinline__ int64_t dec_arraylen(KDec &d, bool nullable, bool &bad) {
-    int64_t l = (int32_t)dec_int(d, 4);
+__device__ __forceinline__ int32_t dec_arraylen(KDec &d, bool nullable, bool &bad) {
+    int32_t l = (int32_t)dec_int(d, 4);
     bad = false;
     if (l < 0) { if (nullable) return -1; bad = true; return 0; }
-    if (l > kMaxParseBuf) { bad = true; return 0; }
+    if ((uint32_t)l > kMaxParseBuf) { bad = true; return 0; }
     return l;
 }
 __device__ __forceinline__ void dec_bytes(KDec &d) {

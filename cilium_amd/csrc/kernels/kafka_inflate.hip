@@ -438,7 +438,7 @@ __device__ int zset(ZCtx &z, const uint8_t *b, uint32_t &pos, uint32_t end, int3
     if ((uint32_t)size > kMaxParseBuf) return -1;
     const uint8_t *fb[kDepth];
     uint32_t fpos[kDepth], fend[kDepth], fbuf[kDepth];
-    int64_t flim[kDepth];
+    int32_t flim[kDepth];  // LimitReader counts: at most the 16 MiB region slice
     int depth = 0;
     fb[0] = b; fpos[0] = pos; fend[0] = end; flim[0] = size; fbuf[0] = 0;
     uint32_t top = 0;  // first free byte of the region slice
@@ -537,14 +537,14 @@ __device__ int zrequest(ZCtx &z, const uint8_t *b) {
     dec_string(d, o, l);
     if (ver >= 3) dec_string(d, o, l);
     dec_skip(d, 2); dec_skip(d, 4);
-    const int64_t nt = dec_arraylen(d, false, bad);
+    const int32_t nt = dec_arraylen(d, false, bad);
     if (bad || d.err) return 0;
-    for (int64_t t = 0; t < nt; t++) {
+    for (int32_t t = 0; t < nt; t++) {
         dec_string(d, o, l);
         if (d.err) return 0;
-        const int64_t np = dec_arraylen(d, false, bad);
+        const int32_t np = dec_arraylen(d, false, bad);
         if (bad) return 0;
-        for (int64_t p = 0; p < np; p++) {
+        for (int32_t p = 0; p < np; p++) {
             dec_skip(d, 4);
             if (d.err) return 0;
             const int32_t ss = (int32_t)dec_int(d, 4);
