@@ -200,25 +200,16 @@ __device__ __forceinline__ void classify_cmd(const uint32_t cw[4], uint32_t clen
 // memcached (single-protocol engines, where partition_kernel does not run).
 // kNfa: the variant that also runs NFA-fallback key matchers (launched only
 // when some memcache rule set has them; the other keeps its registers).
-template <bool kNfa>
-__device__ __forceinline__ void mc_classify(Batch B, McTables T, const uint32_t *__restrict__ sel,
-                                            const uint32_t *__restrict__ sel2, const uint32_t *__restrict__ sel_count,
-                                            uint32_t answer_other) {
+// kLds: `images` is the workgroup's LDS copy.  The two cases are separate
+// instantiations so that every image read compiles to a ds_read (LDS) or a
+// global_load: one pointer that may be either makes them all flat loads.
+template <bool kNfa, bool kLds>
+__device__ __forceinline__ void mc_loop(Batch B, McTables T, const uint8_t *images, const uint32_t *__restrict__ sel,
+                                        const uint32_t *__restrict__ sel2, const uint32_t *__restrict__ sel_count,
+                                        uint32_t answer_other) {
     const uint32_t n = B.n, nconns = B.nconns;
     const uint32_t *__restrict__ conn_ids = B.conn_ids;
     const DevConn *__restrict__ conns = B.conns;
-    // The rule-set images (command / opcode masks, key DFAs) are read once per
-    // key byte in a dependent chain: when they all fit, every workgroup stages
-    // them in LDS (dynamic shared memory sized by the launcher) and walks them
-    // there instead of through L1/L2.
-    extern __shared__ __attribute__((aligned(16))) uint8_t mc_lds[];
-    const uint8_t *images = T.images;
-    if (T.images_len && T.images_len <= kMcLdsImages) {
-        const uint32_t n16 = (T.images_len + 15) / 16;
-        for (uint32_t i = threadIdx.x; i < n16; i += kBlock) ((uint4 *)mc_lds)[i] = ((const uint4 *)T.images)[i];
-        __syncthreads();
-        images = mc_lds;
-    }
     // sel: this protocol's request indices from partition_kernel: sel_count[0]
     // text retrievals from sel's start, sel_count[1] binary requests from its
     // end, sel_count[3] other text commands from sel2's end (n slots each);
@@ -294,7 +285,7 @@ __device__ __forceinline__ void mc_classify(Batch B, McTables T, const uint32_t 
                 // ---- text command line
                 Reader R{b, ~0ull, 0, 0, 0, 0};
                 uint32_t i = 0, lf = 0;
-                bool found = false, in_tok = false;
+                bool found = false;
                 uint32_t nt = 0;              // tokens started
                 uint32_t cw[4] = {0, 0, 0, 0}, clen = 0;
                 int fr = F_NONE;
@@ -304,54 +295,57 @@ __device__ __forceinline__ void mc_classify(Batch B, McTables T, const uint32_t 
                 bool a_ok = false, a_bad = false, a_neg = false;  // strconv.Atoi(tokens[4])
                 uint32_t a_n = 0;
                 uint64_t a_v = 0;
-                while (i < len) {
-                    const uint32_t c = rd(R, i);
-                    if (c == '\r' && i + 1 < len && b[i + 1] == '\n') { lf = i; found = true; break; }
-                    const uint32_t sp = space_len(b, i, len, c);
-                    if (sp) {
-                        if (in_tok) {  // token nt-1 ended
-                            if (nt == 1) classify_cmd(cw, clen, fr, cmd_id);
-                            if (key_tok) keys_end<kNfa>(I, K, b, kstart, i);
-                            in_tok = false;
-                        }
+                // One token per round: its bytes in a tight loop, then the
+                // token-end work (command id, key DFA accept masks) once.  A
+                // wave runs its lanes' divergent paths one after the other, so
+                // token-end work inside the byte loop was paid in nearly every
+                // byte step (some lane is always at a token end).
+                for (;;) {
+                    bool tok = false;  // spaces up to the next token or the line end
+                    while (i < len) {
+                        const uint32_t c = rd(R, i);
+                        if (c == '\r' && i + 1 < len && b[i + 1] == '\n') { lf = i; found = true; break; }
+                        const uint32_t sp = space_len(b, i, len, c);
+                        if (!sp) { tok = true; break; }
                         i += sp;
-                        continue;
                     }
-                    if (!in_tok) {
-                        in_tok = true;
-                        nt++;
-                        key_tok = (fr == F_GET && nt >= 2) || (fr == F_GAT && nt >= 3) ||
-                                  ((fr == F_STORAGE || fr == F_KEY1) && nt == 2);
-                        kstart = i;
-                    }
-                    if (nt == 1) {
-                        if (clen < 16) cw[clen >> 2] |= c << ((clen & 3) * 8);
-                        clen++;
-                    } else if (key_tok) {
-                        keys_step(I, K, c);
-                    }
-                    if (fr == F_STORAGE && nt == 5) {
-                        if (a_n == 0 && (c == '+' || c == '-')) { a_neg = c == '-'; a_ok = false; /* until a digit */ }
-                        else if (c < '0' || c > '9') { a_ok = false; a_bad = true; }
-                        else {
-                            const uint64_t d = c - '0';
-                            if (a_v > (~0ull - d) / 10) a_bad = true;
-                            else a_v = a_v * 10 + d;
-                            if (a_v > 0x7FFFFFFFFFFFFFFFull + (a_neg ? 1u : 0u)) a_bad = true;
-                            a_ok = !a_bad;
+                    if (!tok) break;  // line end, or the data ends: incomplete
+                    nt++;
+                    key_tok = (fr == F_GET && nt >= 2) || (fr == F_GAT && nt >= 3) ||
+                              ((fr == F_STORAGE || fr == F_KEY1) && nt == 2);
+                    kstart = i;
+                    bool ended = false;  // by a space or the line end (not consumed here)
+                    while (i < len) {
+                        const uint32_t c = rd(R, i);
+                        if ((c == '\r' && i + 1 < len && b[i + 1] == '\n') || space_len(b, i, len, c)) { ended = true; break; }
+                        if (nt == 1) {
+                            if (clen < 16) cw[clen >> 2] |= c << ((clen & 3) * 8);
+                            clen++;
+                        } else if (key_tok) {
+                            keys_step(I, K, c);
                         }
-                        a_n++;
+                        if (fr == F_STORAGE && nt == 5) {
+                            if (a_n == 0 && (c == '+' || c == '-')) { a_neg = c == '-'; a_ok = false; /* until a digit */ }
+                            else if (c < '0' || c > '9') { a_ok = false; a_bad = true; }
+                            else {
+                                const uint64_t d = c - '0';
+                                if (a_v > (~0ull - d) / 10) a_bad = true;
+                                else a_v = a_v * 10 + d;
+                                if (a_v > 0x7FFFFFFFFFFFFFFFull + (a_neg ? 1u : 0u)) a_bad = true;
+                                a_ok = !a_bad;
+                            }
+                            a_n++;
+                        }
+                        i++;
                     }
-                    i++;
+                    if (!ended) break;  // the data ends inside the token: incomplete
+                    if (nt == 1) classify_cmd(cw, clen, fr, cmd_id);
+                    if (key_tok) keys_end<kNfa>(I, K, b, kstart, i);
                 }
                 if (!found) {  // MORE 1 if the data ends in '\r', else MORE 2
                     verdict = V_INCOMPLETE;
                     consumed = (len > 0 && b[len - 1] == '\r') ? 1 : 2;
                     break;
-                }
-                if (in_tok) {
-                    if (nt == 1) classify_cmd(cw, clen, fr, cmd_id);
-                    if (key_tok) keys_end<kNfa>(I, K, b, kstart, lf);
                 }
                 if (nt == 0) break;  // tokens[0] panics
                 if (fr == F_BAD) break;  // ERROR, 0
@@ -388,6 +382,25 @@ __device__ __forceinline__ void mc_classify(Batch B, McTables T, const uint32_t 
         B.verdict[idx] = verdict;
         B.rule[idx] = rule;
         B.consumed[idx] = consumed;
+    }
+}
+
+template <bool kNfa>
+__device__ __forceinline__ void mc_classify(Batch B, McTables T, const uint32_t *__restrict__ sel,
+                                            const uint32_t *__restrict__ sel2, const uint32_t *__restrict__ sel_count,
+                                            uint32_t answer_other) {
+    // The rule-set images (command / opcode masks, key DFAs) are read once per
+    // key byte in a dependent chain: when they all fit, every workgroup stages
+    // them in LDS (dynamic shared memory sized by the launcher) and walks them
+    // there instead of through L1/L2.
+    extern __shared__ __attribute__((aligned(16))) uint8_t mc_lds[];
+    if (T.images_len && T.images_len <= kMcLdsImages) {
+        const uint32_t n16 = (T.images_len + 15) / 16;
+        for (uint32_t i = threadIdx.x; i < n16; i += kBlock) ((uint4 *)mc_lds)[i] = ((const uint4 *)T.images)[i];
+        __syncthreads();
+        mc_loop<kNfa, true>(B, T, mc_lds, sel, sel2, sel_count, answer_other);
+    } else {
+        mc_loop<kNfa, false>(B, T, T.images, sel, sel2, sel_count, answer_other);
     }
 }
 
