@@ -45,6 +45,7 @@
 #include <cstddef>
 
 #include "../device_tables.h"
+#include "gmem.h"
 
 namespace l7 {
 
@@ -1050,8 +1051,8 @@ __device__ __forceinline__ void map_skip(Lane &L, const TileMap &T) {
         }
         const uint32_t cpos = found << 4;  // the marked chunk, request-relative
         const uint64_t ca = L.base + cpos;
-        const uint4 w0 = *(const uint4 *)ca;
-        const uint4 w1 = cpos + 16 < L.lena ? *(const uint4 *)(ca + 16) : make_uint4(0, 0, 0, 0);
+        const uint4 w0 = gload16(ca);  // global, not flat (gmem.h)
+        const uint4 w1 = cpos + 16 < L.lena ? gload16(ca + 16) : make_uint4(0, 0, 0, 0);
         const uint32_t lo_b = L.pa > cpos ? L.pa - cpos : 0;
         const uint32_t hi_b = min(L.lena - cpos, 16u);
         const uint32_t m = vstop_mask(w0) & (0xFFFFu << lo_b) & ((1u << hi_b) - 1u);

@@ -9,6 +9,8 @@
 
 #include <stdint.h>
 
+#include "gmem.h"
+
 namespace l7 {
 namespace {
 
@@ -28,7 +30,7 @@ struct Cur {
 __device__ __forceinline__ void cur_fill(Cur &c, uintptr_t a) {
     const uintptr_t ln = a & ~(uintptr_t)15;
     if (ln != c.line) {
-        const uint4 v = *reinterpret_cast<const uint4 *>(ln);
+        const uint4 v = gload16(ln);
         c.w0 = v.x; c.w1 = v.y; c.w2 = v.z; c.w3 = v.w;
         c.line = ln;
     }

@@ -26,6 +26,7 @@
 #include "../device_tables.h"
 #include "../engine/mc_groups.h"
 #include "../regex/nfa_walk.h"
+#include "gmem.h"
 
 namespace l7 {
 
@@ -51,7 +52,7 @@ __device__ __forceinline__ uint32_t rd(Reader &r, uint32_t i) {
     const uint64_t a = (uint64_t)(r.b + i);
     const uint64_t base = a & ~(uint64_t)15;
     if (base != r.base) {
-        const uint4 v = *(const uint4 *)base;
+        const uint4 v = gload16(base);  // global, not flat (gmem.h)
         r.w0 = v.x; r.w1 = v.y; r.w2 = v.z; r.w3 = v.w;
         r.base = base;
     }
