@@ -171,6 +171,66 @@ __device__ __forceinline__ uint32_t crc32_ieee(const uint32_t *tab, Cur &cur, co
 }
 
 
+// One slicing-by-8 step over (lo ^ c, hi), and one slicing-by-4 step over a
+// word x = w ^ c, with every table lookup in flight before the single wait.
+// (Written out because the compiler, short of registers at 6 waves per SIMD,
+// issued the tail loop's eight lookups one or two at a time, each behind its
+// own LDS wait.)  tabaddr: the LDS address of table 0; table k is k KiB on.
+__device__ __forceinline__ uint32_t crc_step8(uint32_t tabaddr, uint32_t lo, uint32_t hi) {
+    const uint32_t a0 = tabaddr + ((lo & 0xFF) << 2), a1 = tabaddr + (((lo >> 8) & 0xFF) << 2),
+                   a2 = tabaddr + (((lo >> 16) & 0xFF) << 2), a3 = tabaddr + ((lo >> 24) << 2),
+                   a4 = tabaddr + ((hi & 0xFF) << 2), a5 = tabaddr + (((hi >> 8) & 0xFF) << 2),
+                   a6 = tabaddr + (((hi >> 16) & 0xFF) << 2), a7 = tabaddr + ((hi >> 24) << 2);
+    uint32_t r0, r1, r2, r3, r4, r5, r6, r7;
+    asm volatile(
+        "ds_read_b32 %0, %8 offset:7168\n\tds_read_b32 %1, %9 offset:6144\n\t"
+        "ds_read_b32 %2, %10 offset:5120\n\tds_read_b32 %3, %11 offset:4096\n\t"
+        "ds_read_b32 %4, %12 offset:3072\n\tds_read_b32 %5, %13 offset:2048\n\t"
+        "ds_read_b32 %6, %14 offset:1024\n\tds_read_b32 %7, %15\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(r0), "=&v"(r1), "=&v"(r2), "=&v"(r3), "=&v"(r4), "=&v"(r5), "=&v"(r6), "=&v"(r7)
+        : "v"(a0), "v"(a1), "v"(a2), "v"(a3), "v"(a4), "v"(a5), "v"(a6), "v"(a7)
+        : "memory");
+    return (r0 ^ r1) ^ (r2 ^ r3) ^ (r4 ^ r5) ^ (r6 ^ r7);
+}
+__device__ __forceinline__ uint32_t crc_step4(uint32_t tabaddr, uint32_t x) {
+    const uint32_t a0 = tabaddr + ((x & 0xFF) << 2), a1 = tabaddr + (((x >> 8) & 0xFF) << 2),
+                   a2 = tabaddr + (((x >> 16) & 0xFF) << 2), a3 = tabaddr + ((x >> 24) << 2);
+    uint32_t r0, r1, r2, r3;
+    asm volatile(
+        "ds_read_b32 %0, %4 offset:3072\n\tds_read_b32 %1, %5 offset:2048\n\t"
+        "ds_read_b32 %2, %6 offset:1024\n\tds_read_b32 %3, %7\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(r0), "=&v"(r1), "=&v"(r2), "=&v"(r3)
+        : "v"(a0), "v"(a1), "v"(a2), "v"(a3)
+        : "memory");
+    return (r0 ^ r1) ^ (r2 ^ r3);
+}
+// The CRC over r <= 3 bytes (x: those bytes little-endian, upper bytes ignored):
+// c' = (c >> 8r) ^ sum_j T[r-1-j][(c >> 8j ^ b_j) & 0xFF], the lookups in flight
+// together (1 <= r <= 3).
+__device__ __forceinline__ uint32_t crc_bytes3(uint32_t tabaddr, uint32_t c, uint32_t x, uint32_t r) {
+    const uint32_t y = c ^ x;
+    const uint32_t a0 = tabaddr + ((r - 1) << 10) + ((y & 0xFF) << 2);
+    const uint32_t a1 = tabaddr + ((r - 2) << 10) + (((y >> 8) & 0xFF) << 2);
+    const uint32_t a2 = tabaddr + (((y >> 16) & 0xFF) << 2);
+    const uint32_t b0 = r >= 1 ? a0 : tabaddr, b1 = r >= 2 ? a1 : tabaddr, b2 = r >= 3 ? a2 : tabaddr;
+    uint32_t r0, r1, r2;
+    asm volatile("ds_read_b32 %0, %3\n\tds_read_b32 %1, %4\n\tds_read_b32 %2, %5\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&v"(r0), "=&v"(r1), "=&v"(r2)
+                 : "v"(b0), "v"(b1), "v"(b2)
+                 : "memory");
+    return (c >> (8 * r)) ^ r0 ^ (r >= 2 ? r1 : 0u) ^ (r >= 3 ? r2 : 0u);
+}
+// little-endian bytes k .. k+3 of the cursor's chunk (k <= 12)
+__device__ __forceinline__ uint32_t cur_word_at(const Cur &c, uint32_t k) {
+    const uint32_t w0 = c.w0, w1 = c.w1, w2 = c.w2, w3 = c.w3;
+    const uint32_t i = k >> 2;
+    const uint32_t lo = i == 0 ? w0 : i == 1 ? w1 : i == 2 ? w2 : w3;
+    const uint32_t hi = i == 0 ? w1 : i == 1 ? w2 : i == 2 ? w3 : 0u;
+    return __builtin_amdgcn_alignbyte(hi, lo, k & 3);
+}
+
 // The same CRC with the bulk loads staged through LDS (kafka_classify): the
 // next 64-byte batch is in flight into the wave's 4 KiB staging area (lane l's
 // 16-byte pieces at 16 l of each 1 KiB block) while the current one is hashed
@@ -181,9 +241,31 @@ __device__ __forceinline__ uint32_t crc32_ieee(const uint32_t *tab, Cur &cur, co
 // bytes, and every batch is exactly four loads, so vmcnt counts are exact.
 __device__ __forceinline__ uint32_t crc32_ieee_staged(const uint32_t *tab, Cur &cur, const uint8_t *p, uint32_t n,
                                                       uint8_t *stage) {
+    const uint32_t tabaddr = (uint32_t)(uintptr_t)tab;
     uint32_t c = 0xFFFFFFFFu;
     uint32_t i = 0;
-    for (; i < n && (((uintptr_t)(p + i)) & 15); i++) c = tab[(c ^ cur_byte(cur, p + i)) & 0xFF] ^ (c >> 8);
+    {
+        // up to the first 16-byte boundary: one chunk, in 8-, 4- and 1-byte steps
+        const uint32_t k0 = (uint32_t)((uintptr_t)p & 15);
+        uint32_t h = (16 - k0) & 15;
+        if (h > n) h = n;
+        if (h >= 4) {
+            cur_fill(cur, (uintptr_t)p);
+            if (h >= 8) {
+                c = crc_step8(tabaddr, cur_word_at(cur, k0) ^ c, cur_word_at(cur, k0 + 4));
+                i = 8;
+            }
+            if (h - i >= 4) {
+                c = crc_step4(tabaddr, cur_word_at(cur, k0 + i) ^ c);
+                i += 4;
+            }
+        }
+        if (i < h) {
+            cur_fill(cur, (uintptr_t)p);
+            c = crc_bytes3(tabaddr, c, cur_word_at(cur, k0 + i), h - i);
+            i = h;
+        }
+    }
     if (i + 64 <= n) {
         const uint32_t la = (uint32_t)(uintptr_t)(stage + 16 * (threadIdx.x & 63));
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -218,17 +300,25 @@ __device__ __forceinline__ uint32_t crc32_ieee_staged(const uint32_t *tab, Cur &
         }
 #undef CRC_STAGE
     }
+    // the rest from 16-byte aligned chunks: 8-byte steps, then one 4-byte step, then bytes
     for (; i + 8 <= n; i += 8) {
         const uintptr_t a = (uintptr_t)(p + i);
         cur_fill(cur, a);
         const uint32_t k = (uint32_t)(a & 15);
         const uint32_t w0 = cur.w0, w1 = cur.w1, w2 = cur.w2, w3 = cur.w3;
-        const uint32_t lo = (k ? w2 : w0) ^ c, hi = k ? w3 : w1;
-        c = tab[7 * 256 + (lo & 0xFF)] ^ tab[6 * 256 + ((lo >> 8) & 0xFF)] ^ tab[5 * 256 + ((lo >> 16) & 0xFF)] ^
-            tab[4 * 256 + (lo >> 24)] ^ tab[3 * 256 + (hi & 0xFF)] ^ tab[2 * 256 + ((hi >> 8) & 0xFF)] ^
-            tab[1 * 256 + ((hi >> 16) & 0xFF)] ^ tab[hi >> 24];
+        c = crc_step8(tabaddr, (k ? w2 : w0) ^ c, k ? w3 : w1);
     }
-    for (; i < n; i++) c = tab[(c ^ cur_byte(cur, p + i)) & 0xFF] ^ (c >> 8);
+    if (i + 4 <= n) {
+        const uintptr_t a = (uintptr_t)(p + i);
+        cur_fill(cur, a);
+        c = crc_step4(tabaddr, cur_word_at(cur, (uint32_t)(a & 15)) ^ c);
+        i += 4;
+    }
+    if (i < n) {
+        const uintptr_t a = (uintptr_t)(p + i);
+        cur_fill(cur, a);
+        c = crc_bytes3(tabaddr, c, cur_word_at(cur, (uint32_t)(a & 15)), n - i);
+    }
     return ~c;
 }
 
