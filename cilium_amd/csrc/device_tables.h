@@ -256,6 +256,7 @@ struct McImgHeader {       // 64 B, at offset 0 of every memcache image
     uint32_t pad1[6];
 };
 static_assert(sizeof(McImgHeader) == 64, "McImgHeader layout");
+constexpr uint32_t kMcDfaOff = sizeof(McImgHeader);  // DevDfa[ndfa] follow the header
 
 struct McTables {
     const DevRuleset *rulesets;

@@ -158,6 +158,11 @@ int McCompiler::Compile(const std::vector<const McRule *> &rules, uint8_t termin
     H.ndfa = (uint8_t)dfas.size();
 
     std::vector<uint8_t> img(sizeof(McImgHeader));
+    // the DFA descriptors first, at kMcDfaOff: the kernel's key-byte step then
+    // reads them at a constant offset instead of through the header
+    std::vector<DevDfa> dd(dfas.size());
+    H.dfa_off = Append(img, dd.data(), dd.size());
+    if (H.dfa_off != kMcDfaOff) { *err = "memcache image layout"; return -1; }
     H.text_off = Append(img, text.data(), text.size());
     H.op_off = Append(img, ops.data(), ops.size());
     H.empty_off = Append(img, empty.data(), empty.size());
@@ -165,8 +170,6 @@ int McCompiler::Compile(const std::vector<const McRule *> &rules, uint8_t termin
     std::vector<int32_t> ids(nch * 64, -1);
     for (size_t r = 0; r < nr; r++) ids[r] = rules[r]->id;
     H.rule_off = Append(img, ids.data(), ids.size());
-    std::vector<DevDfa> dd(dfas.size());
-    H.dfa_off = Append(img, dd.data(), dd.size());
     std::vector<uint64_t> owned(dfas.size() * nch, 0);
     for (size_t k = 0; k < dfas.size(); k++)
         for (auto &rp : rule_pat)

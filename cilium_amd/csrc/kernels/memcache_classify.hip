@@ -130,7 +130,7 @@ __device__ __forceinline__ void keys_reset(const Image &I, Keys &K) {
 #pragma unroll
     for (int d = 0; d < kMcMaxDfas; d++)
         if ((uint32_t)d < I.dn) {
-            const DevDfa *dd = (const DevDfa *)(I.p + hdr32(I, MC_OFF(dfa_off))) + I.d0 + d;
+            const DevDfa *dd = (const DevDfa *)(I.p + kMcDfaOff) + I.d0 + d;
             K.st[d] = dd->start;
         }
 }
@@ -139,7 +139,7 @@ __device__ __forceinline__ void keys_step(const Image &I, Keys &K, uint32_t c) {
 #pragma unroll
     for (int d = 0; d < kMcMaxDfas; d++)
         if ((uint32_t)d < I.dn && K.st[d] != 0) {
-            const DevDfa *dd = (const DevDfa *)(I.p + hdr32(I, MC_OFF(dfa_off))) + I.d0 + d;
+            const DevDfa *dd = (const DevDfa *)(I.p + kMcDfaOff) + I.d0 + d;
             const uint32_t cls = I.p[dd->cls_off + c];
             K.st[d] = ((const uint16_t *)(I.p + dd->trans_off))[K.st[d] * dd->ncls + cls];
         }
@@ -173,7 +173,7 @@ __device__ __forceinline__ void keys_end(const Image &I, Keys &K, const uint8_t 
 #pragma unroll
         for (int d = 0; d < kMcMaxDfas; d++)
             if ((uint32_t)d < I.dn) {
-                const DevDfa *dd = (const DevDfa *)(I.p + hdr32(I, MC_OFF(dfa_off))) + I.d0 + d;
+                const DevDfa *dd = (const DevDfa *)(I.p + kMcDfaOff) + I.d0 + d;
                 own |= owned[(I.d0 + d) * I.nch + c];
                 acc |= ((const uint64_t *)(I.p + dd->mask_off))[K.st[d] * I.nch + c];
             }
