@@ -162,6 +162,9 @@ __device__ __forceinline__ uint32_t topic_first(const KafkaTables &T, const DevK
 #ifndef L7G_KAFKA_WAVES
 #define L7G_KAFKA_WAVES 6
 #endif
+#ifndef L7G_KAFKA_MAX_BLOCKS
+#define L7G_KAFKA_MAX_BLOCKS 8192  // grid-stride beyond this
+#endif
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(L7G_KAFKA_WAVES, 8))) void kafka_classify_kernel(
     Batch B, KafkaTables T, const uint32_t *__restrict__ sel, const uint32_t *__restrict__ sel_count,
     uint32_t answer_other, uint32_t *__restrict__ zlist, uint32_t *__restrict__ zcount) {
@@ -395,7 +398,7 @@ hipError_t LaunchKafkaClassify(const Batch &B, const KafkaTables &T, const uint3
                                bool answer_other, uint32_t *zlist, uint32_t *zcount, hipStream_t stream) {
     if (B.n == 0) return hipSuccess;
     uint32_t blocks = (B.n + kBlock - 1) / kBlock;
-    if (blocks > 8192) blocks = 8192;
+    if (blocks > L7G_KAFKA_MAX_BLOCKS) blocks = L7G_KAFKA_MAX_BLOCKS;
     hipLaunchKernelGGL(kafka_classify_kernel, dim3(blocks), dim3(kBlock), 0, stream, B, T, sel, sel_count,
                        answer_other ? 1u : 0u, zlist, zcount);
     return hipGetLastError();
