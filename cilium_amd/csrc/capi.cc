@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "../../include/l7gpu.h"
+#include "capi_internal.h"
 #include "device_tables.h"
 #include "engine/http_compile.h"
 #include "engine/kafka_compile.h"
@@ -59,9 +60,6 @@ struct StreamScratch {
     // n HTTP idx | n idx of Kafka requests with compressed messages]
     uint32_t *d_sel = nullptr;
     size_t sel_cap = 0;
-    // decode region of kafka_inflate_kernel (one slice per workgroup), allocated
-    // with the first Kafka batch on this stream
-    uint8_t *d_zreg = nullptr;
     // NFA pre-pass results, u64 per request (grow-only)
     uint64_t *d_nfa = nullptr;
     size_t nfa_cap = 0;
@@ -73,7 +71,6 @@ struct StreamScratch {
     uint64_t last_use = 0;
     ~StreamScratch() {
         if (d_sel) hipFree(d_sel);
-        if (d_zreg) hipFree(d_zreg);
         if (d_nfa) hipFree(d_nfa);
         if (d_hist) hipFree(d_hist);
         if (done_ev) hipEventDestroy(done_ev);
@@ -121,6 +118,12 @@ struct l7g_engine {
     std::mutex hmu;
     std::map<std::thread::id, std::unique_ptr<HostCtx>> hctx;
     bool any_cold = false;     // some HTTP connection uses another rule set
+    // decode region of kafka_inflate_kernel (one slice per workgroup, 1 GiB),
+    // allocated with the first Kafka batch and shared by every stream: each
+    // call's inflate launch waits for zreg_ev, the previous one's completion
+    uint8_t *d_zreg = nullptr;
+    hipEvent_t zreg_ev = nullptr;
+    bool zreg_used = false;
     // per-stream scratch of l7g_classify (guarded by mu)
     std::map<hipStream_t, std::unique_ptr<StreamScratch>> scr;
     uint64_t calls = 0;
@@ -389,6 +392,8 @@ void l7g_engine_destroy(l7g_engine *e) {
     e->hctx.clear();
     e->scr.clear();
     if (e->d_flow) hipFree(e->d_flow);
+    if (e->d_zreg) hipFree(e->d_zreg);
+    if (e->zreg_ev) hipEventDestroy(e->zreg_ev);
     for (hipEvent_t ev : e->prof_ev)
         if (ev) hipEventDestroy(ev);
     delete e;
@@ -397,20 +402,31 @@ void l7g_engine_destroy(l7g_engine *e) {
 static int PolicySwap(l7g_engine *e, std::unique_ptr<PolicySet> ps, char *err, size_t errlen);
 
 int l7g_policy_update(l7g_engine *e, const char *json, size_t len, char *err, size_t errlen) {
-    std::lock_guard<std::mutex> g(e->mu);
-    auto ps = std::make_unique<PolicySet>();
-    std::string m;
-    if (!LoadPolicySet(json, len, ps.get(), &m)) { set_err(err, errlen, m); return -1; }
-    return PolicySwap(e, std::move(ps), err, errlen);
+    return l7g_policy_update_view(e, (const uint8_t *)json, len, 0, 0, err, errlen);
 }
 
 int l7g_policy_update_proto(l7g_engine *e, const uint8_t *buf, size_t len, char *err, size_t errlen) {
+    return l7g_policy_update_view(e, buf, len, 1, 0, err, errlen);
+}
+
+}  // extern "C"
+
+// capi_internal.h: proto_form 0 = JSON, 1 = NPDS DiscoveryResponse; proxylib
+// != 0 = the proxylib instance's update (instance.go:168-219), which also
+// NACKs what only proxylib's policymap rejects (PolicySet::px_nack).
+int l7g_policy_update_view(l7g_engine *e, const uint8_t *buf, size_t len, int proto_form, int proxylib, char *err,
+                           size_t errlen) {
     std::lock_guard<std::mutex> g(e->mu);
     auto ps = std::make_unique<PolicySet>();
     std::string m;
-    if (!LoadPolicySetProto(buf, len, ps.get(), &m)) { set_err(err, errlen, m); return -1; }
+    const bool ok = proto_form ? LoadPolicySetProto(buf, len, ps.get(), &m)
+                               : LoadPolicySet((const char *)buf, len, ps.get(), &m);
+    if (!ok) { set_err(err, errlen, m); return -1; }
+    if (proxylib && !ps->px_nack.empty()) { set_err(err, errlen, ps->px_nack); return -1; }
     return PolicySwap(e, std::move(ps), err, errlen);
 }
+
+extern "C" {
 
 // Swap in a loaded policy version; on a compile failure the previous version
 // stays in force (an NPDS NACK).  Caller holds e->mu.
@@ -542,8 +558,10 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
         sel_h = sel_m + (size_t)n;
         sel_z = sel_h + (size_t)n;
         if (rc == hipSuccess) rc = hipMemsetAsync(cnt, 0, 32 * sizeof(uint32_t), s);
-        if (rc == hipSuccess && e->has_kafka && !S->d_zreg)
-            rc = hipMalloc(&S->d_zreg, (size_t)KafkaInflateBlocks() * KafkaInflateRegionBytes());
+        if (rc == hipSuccess && e->has_kafka && !e->d_zreg) {
+            rc = hipEventCreateWithFlags(&e->zreg_ev, hipEventDisableTiming);
+            if (rc == hipSuccess) rc = hipMalloc(&e->d_zreg, (size_t)KafkaInflateBlocks() * KafkaInflateRegionBytes());
+        }
         if (rc != hipSuccess) return (int)rc;
     }
     // rule sets with NFA-fallback matchers: the pre-pass writes one u64 per request
@@ -580,7 +598,13 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
     uint32_t *zcount = cnt ? cnt + 31 : nullptr;
     if (rc == hipSuccess && run[2]) rc = LaunchKafkaClassify(B, e->kt, sel_k, cnt, !partitioned, sel_z, zcount, s);
     // requests with gzip / snappy messages: decoded, their sets read, failures answered
-    if (rc == hipSuccess && run[2] && sel_z) rc = LaunchKafkaInflate(B, sel_z, zcount, S->d_zreg, s);
+    if (rc == hipSuccess && run[2] && sel_z) {
+        // the engine's one decode region: after the previous inflate launch on any stream
+        if (e->zreg_used) rc = hipStreamWaitEvent(s, e->zreg_ev, 0);
+        if (rc == hipSuccess) rc = LaunchKafkaInflate(B, sel_z, zcount, e->d_zreg, s);
+        if (rc == hipSuccess) rc = hipEventRecord(e->zreg_ev, s);
+        if (rc == hipSuccess) e->zreg_used = true;
+    }
     mark(3);
     if (rc == hipSuccess && run[3])
         rc = LaunchMemcacheClassify(B, e->mt, sel_m, sel_h, cnt ? cnt + L7_KAFKA_CLASSES : nullptr, !partitioned, s);
@@ -592,14 +616,17 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
         const size_t nk = e->skey_list.size();
         if (nk > e->flow_cap) {  // grow, keeping what was accumulated
             uint64_t *d = nullptr;
-            rc = hipMalloc(&d, nk * 4 * sizeof(uint64_t));
+            // every stream's earlier flowstats kernels may still add into the old
+            // accumulator: they finish before it is copied (e->mu is held, so no
+            // new launch can race with the copy)
+            if (e->d_flow) rc = WaitLastClassify(e);
+            if (rc == hipSuccess) rc = hipMalloc(&d, nk * 4 * sizeof(uint64_t));
             if (rc == hipSuccess) rc = hipMemsetAsync(d, 0, nk * 4 * sizeof(uint64_t), s);
             if (rc == hipSuccess && e->d_flow)
                 rc = hipMemcpyAsync(d, e->d_flow, e->flow_cap * 4 * sizeof(uint64_t), hipMemcpyDeviceToDevice, s);
             if (rc == hipSuccess) {
-                if (e->d_flow) {  // every stream's kernels may add into the old one
+                if (e->d_flow) {
                     hipStreamSynchronize(s);
-                    WaitLastClassify(e);
                     hipFree(e->d_flow);
                 }
                 e->d_flow = d;
@@ -733,7 +760,12 @@ int l7g_flow_stats(l7g_engine *e, l7g_flow_stat_t *out, uint32_t cap, uint32_t *
         k++;
     }
     if (n) *n = k;
-    if (reset && e->flow_cap) rc = hipMemset(e->d_flow, 0, e->flow_cap * 4 * sizeof(uint64_t));
+    // the reset completes before e->mu is released: the next call's flowstats
+    // kernel (on a non-blocking stream) cannot overlap it
+    if (reset && e->flow_cap) {
+        rc = hipMemsetAsync(e->d_flow, 0, e->flow_cap * 4 * sizeof(uint64_t), nullptr);
+        if (rc == hipSuccess) rc = hipStreamSynchronize(nullptr);
+    }
     return (int)rc;
 }
 

@@ -89,8 +89,10 @@ __global__ __launch_bounds__(kRedBins * kRedParts) void reduce_kernel(const uint
     if (q != 0 || b >= nbins) return;
     for (uint32_t p = 1; p < kRedParts; p++) s += part[p][t];
     if (!s) return;
-    if (b >= nb) counters[nrules + (b - nb)] += s;  // verdict bins (lo == 0)
-    else counters[lo + b] += s;
+    // atomic: calls on different streams may share one counters array
+    unsigned long long *dst = (unsigned long long *)(b >= nb ? &counters[nrules + (b - nb)]  // verdict bins (lo == 0)
+                                                             : &counters[lo + b]);
+    atomicAdd(dst, (unsigned long long)s);
 }
 
 // Proxy statistics (pkg/endpoint/endpoint.go:2207-2233 UpdateProxyStatistics):

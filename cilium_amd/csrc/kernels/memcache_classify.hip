@@ -36,7 +36,7 @@ constexpr int kBlock = 256;
 constexpr uint32_t kMcLdsImages = 32 * 1024;  // LDS budget for the staged rule-set images
 // waves per SIMD the common kernel is built for (experiments: -DL7G_MC_WAVES=N)
 #ifndef L7G_MC_WAVES
-#define L7G_MC_WAVES 7
+#define L7G_MC_WAVES 5
 #endif
 #define L7G_MC_OCCUPANCY __attribute__((amdgpu_waves_per_eu(L7G_MC_WAVES, 8)))
 

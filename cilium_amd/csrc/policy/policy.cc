@@ -60,6 +60,7 @@ struct Loader {
     std::string err;
     int next_id = 0;
     bool mc_stop = false;  // an earlier rule of this port has an unregistered parser
+    std::string px_nack;   // first proxylib ParseError of this version (PolicySet::px_nack)
     bool fail(const std::string &m) { if (err.empty()) err = m; return false; }
 
     static const Value *list(const Value *v, const char *inner) {
@@ -312,12 +313,21 @@ struct Loader {
                     if (!rule(rj, &r)) return false;
                     if (r.type == PortRule::Http) p.has_http = true;
                     std::string pn = r.ParserName();
-                    // proxylib stops parsing a port at the first unregistered parser
-                    // (policymap.go:118-131): later memcache rules are never parsed
-                    if (!ProxylibParserRegistered(pn)) { mc_stop = true; p.px_installed = false; }
-                    if (!pn.empty()) {
-                        if (first_parser.empty()) first_parser = pn;
-                        else if (pn != first_parser) p.px_installed = false;  // mismatching L7 types
+                    // newPortNetworkPolicyRules (policymap.go:113-148), rule by rule:
+                    // an unregistered parser returns the port as drop-all at once
+                    // (later rules are never parsed, :128-134); a registered one whose
+                    // name differs from the port's first is a ParseError panic that
+                    // NACKs the whole proxylib update (:135-143).  UDP ports are never
+                    // parsed by proxylib (:206-209).
+                    if (!mc_stop) {
+                        if (!ProxylibParserRegistered(pn)) {
+                            mc_stop = true;
+                            p.px_installed = false;
+                        } else if (!pn.empty()) {
+                            if (first_parser.empty()) first_parser = pn;
+                            else if (pn != first_parser && p.tcp && px_nack.empty())
+                                px_nack = "NPDS: Mismatching L7 types on the same port";
+                        }
                     }
                     if (!mc_stop && r.NumL7() > 0) p.px_have_l7 = true;
                 }
@@ -355,6 +365,7 @@ bool LoadPolicySetTree(const json::Value &root, PolicySet *out, std::string *err
         ps.policies.push_back(std::move(np));
     }
     ps.nrules = L.next_id;
+    ps.px_nack = L.px_nack;
     *out = std::move(ps);
     return true;
 }

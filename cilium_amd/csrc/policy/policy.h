@@ -93,9 +93,9 @@ struct PortPolicy {
     std::vector<PortRule> rules;
     bool has_http = false;
     // proxylib view (policymap.go:113-148): the entry is installed only if every
-    // rule's parser is registered and they agree (the reference NACKs the
-    // proxylib update on "Mismatching L7 types on the same port" :135-140; here
-    // the port is left out of the proxylib view, as for an unregistered parser);
+    // rule's parser up to the first unregistered one is registered (an
+    // unregistered parser makes the port drop-all); mismatching parsers before
+    // that NACK the whole proxylib update (PolicySet::px_nack);
     // HaveL7Rules = some rule has parsed L7 rules.
     bool px_installed = true;
     bool px_have_l7 = false;
@@ -113,6 +113,12 @@ struct PolicySet {
     std::vector<NetworkPolicy> policies;
     std::map<std::string, int> by_name;
     int nrules = 0;  // global rule ids are 0..nrules-1 in document order
+    // Non-empty: the proxylib view NACKs this version (its ParseError panic,
+    // recovered in Instance.PolicyUpdate, proxylib/proxylib/instance.go:168-176):
+    // "Mismatching L7 types on the same port" (policymap.go:135-143).  Envoy's
+    // NPDS accepts the same version (cilium_network_policy.h has no such check),
+    // so only the proxylib entry points reject it.
+    std::string px_nack;
 };
 
 bool LoadPolicySet(const char *json, size_t n, PolicySet *out, std::string *err);

@@ -49,6 +49,7 @@
 
 #include "../../../include/l7gpu.h"
 #include "../../../include/proxylib_abi.h"
+#include "../capi_internal.h"
 
 namespace {
 
@@ -912,12 +913,15 @@ extern "C" {
 
 int l7g_proxylib_policy_update(uint64_t instance_id, const char *json, size_t len, char *err, size_t errlen) {
     return InstancePolicyUpdate(
-        instance_id, [&](l7g_engine *e) { return l7g_policy_update(e, json, len, err, errlen); }, err, errlen);
+        instance_id,
+        [&](l7g_engine *e) { return l7g_policy_update_view(e, (const uint8_t *)json, len, 0, 1, err, errlen); }, err,
+        errlen);
 }
 
 int l7g_proxylib_policy_update_proto(uint64_t instance_id, const uint8_t *buf, size_t len, char *err, size_t errlen) {
     return InstancePolicyUpdate(
-        instance_id, [&](l7g_engine *e) { return l7g_policy_update_proto(e, buf, len, err, errlen); }, err, errlen);
+        instance_id, [&](l7g_engine *e) { return l7g_policy_update_view(e, buf, len, 1, 1, err, errlen); }, err,
+        errlen);
 }
 
 uint64_t l7g_proxylib_connections(void) {

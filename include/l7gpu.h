@@ -125,12 +125,17 @@ int l7g_conn_update(l7g_engine *e, uint32_t index, const l7g_conn_t *conn, char 
  * (2 = INVALID_FRAME_TYPE; 0 = parser error); 0 otherwise.  Asynchronous on `stream`
  * (a hipStream_t, NULL = default stream).  counters may be NULL, else a
  * device array of (rules + 8) uint64 that accumulates per-rule allow hits
- * followed by per-verdict totals.  Batches with Kafka requests or with more
- * than one protocol use a scratch of (11 n + 16) uint32 (the partition lists)
- * and, with Kafka rules, a 1 GiB decode region for compressed message sets;
- * scratch is kept per stream (up to 16 streams, then handed over least recently
- * used first), so calls on different streams run concurrently and calls on one
- * stream are ordered by it.  Returns 0 or a HIP error code. */
+ * followed by per-verdict totals (added atomically, so calls on different
+ * streams may share one array).  Batches with Kafka requests or with more
+ * than one protocol use a scratch of 32 + (L7_KAFKA_CLASSES + 3) n uint32 (the
+ * partition lists; 32 + 11 n with 8 classes); scratch is kept per stream (up to
+ * 16 streams, then handed over least recently used first), so calls on
+ * different streams run concurrently and calls on one stream are ordered by
+ * it.  With Kafka rules the engine also holds ONE 1 GiB decode region for
+ * compressed message sets, allocated with the first Kafka batch and shared by
+ * all streams: the decode kernels of calls on different streams run one after
+ * the other (each waits for the previous one's completion event).  Returns 0
+ * or a HIP error code. */
 int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const uint64_t *off, const uint32_t *len,
                  const uint32_t *conn, uint32_t n, uint8_t *verdict, int32_t *rule, uint32_t *consumed,
                  uint64_t *counters, void *stream);

@@ -64,3 +64,26 @@ def test_pipelined_stream_matches_oracle(module, oracle, binary):
     assert ops[:len(reqs)] == want
     assert ops[len(reqs)] == (P.MORE, 24 if binary else 2)
     c.close()
+
+
+def test_mismatched_l7_update_keeps_previous_policy(module):
+    """A NACKed update (mismatching L7 types on one port, policymap.go:135-143)
+    leaves the previous policy in force (instance.go:168-219): the connection
+    still gets the old verdicts, where leaving the port out would drop."""
+    from cilium_amd import api
+    old = api.policy_set(api.network_policy("pm-nack", 3, ingress=[
+        (11211, [api.port_rule(l7proto="memcache", l7=[{"command": "get"}])])]))
+    P.policy_update(module, old)
+    c = P.Connection(module, "memcache", 4242, True, 1, 2, "1.1.1.1:1", "2.2.2.2:11211", "pm-nack", 1024)
+    assert c.result == P.OK
+    req = b"get a\r\n"
+    res, ops = c.on_data(False, [req], 4)
+    assert res == P.OK and ops[0] == (P.PASS, len(req))
+    bad = api.policy_set(api.network_policy("pm-nack", 3, ingress=[
+        (11211, [api.port_rule(l7proto="memcache", l7=[{"command": "set"}]),
+                 api.port_rule(l7proto="r2d2", l7=[{"cmd": "READ"}])])]))
+    with pytest.raises(ValueError, match="Mismatching L7 types"):
+        P.policy_update(module, bad)
+    res, ops = c.on_data(False, [req], 4)
+    assert res == P.OK and ops[0] == (P.PASS, len(req))  # still the old "get" rule
+    c.close()

@@ -1,13 +1,15 @@
 """Concurrent submission (SURVEY.md §8(b) threading row): host-buffer calls
 from several threads (each thread its own stream and staging) and device
 calls on several torch streams (each stream its own partition scratch) on one
-engine give the oracle's verdicts, bit-exact."""
+engine give the oracle's verdicts, bit-exact; calls on different streams that
+share one counters array lose no hit (the reduce adds atomically)."""
 import threading
 
 import numpy as np
 import pytest
 
 from cilium_amd import gen
+from cilium_amd._lib import ALLOW
 
 from test_gpu_http import assert_same
 
@@ -55,6 +57,8 @@ def test_device_calls_on_streams(engine, oracle):
     arena = torch.from_numpy(w.arena).to(dev)
     parts = slices(w, 3)
     streams = [torch.cuda.Stream() for _ in parts]
+    nrules = engine.nrules
+    counters = torch.zeros(nrules + 8, dtype=torch.int64, device=dev)  # shared by every stream
     outs = []
     for p, s in zip(parts, streams):
         d = [torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in
@@ -65,8 +69,14 @@ def test_device_calls_on_streams(engine, oracle):
     for rep in range(3):
         for (d, o), p, s in zip(outs, parts, streams):
             engine.classify_device(arena.data_ptr(), arena.numel(), d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(),
-                                   len(p), o[0].data_ptr(), o[1].data_ptr(), o[2].data_ptr(), stream=s.cuda_stream)
+                                   len(p), o[0].data_ptr(), o[1].data_ptr(), o[2].data_ptr(),
+                                   counters_ptr=counters.data_ptr(), stream=s.cuda_stream)
     torch.cuda.synchronize()
+    v, r = ref[0], ref[1]
+    cnt = counters.cpu().numpy()
+    hits = np.bincount(r[(v == ALLOW) & (r >= 0)], minlength=nrules)[:nrules]
+    np.testing.assert_array_equal(cnt[:nrules], 3 * hits)
+    np.testing.assert_array_equal(cnt[nrules:nrules + 5], 3 * np.bincount(v, minlength=5)[:5])
     for (d, o), p in zip(outs, parts):
         got = (o[0].cpu().numpy(), o[1].cpu().numpy(), o[2].cpu().numpy().view(np.uint32))
         assert_same(got, tuple(r[p] for r in ref))

@@ -84,3 +84,53 @@ def test_request_needs_the_device(host_module):
     assert c2.on_data(False, [b"get a\r"], 4) == (P.OK, [(P.MORE, 1)])
     c.close()
     c2.close()
+
+
+def _mixed_port_policy(rules, protocol="TCP"):
+    from cilium_amd import api
+    return api.policy_set(api.network_policy("bm1", 3, ingress=[{"port": 80, "protocol": protocol, "rules": rules}]))
+
+
+def _mc_rule(cmd="get"):
+    from cilium_amd import api
+    return api.port_rule(l7proto="memcache", l7=[{"command": cmd}])
+
+
+def test_mismatched_l7_types_nack(host_module):
+    """newPortNetworkPolicyRules panics with ParseError on a second, different
+    registered parser on one port (proxylib/proxylib/policymap.go:135-143);
+    Instance.PolicyUpdate recovers it as the update's error and keeps the old
+    map (instance.go:168-219)."""
+    from cilium_amd import api
+    good = _mixed_port_policy([_mc_rule()])
+    P.policy_update(host_module, good)
+    r2 = api.port_rule(l7proto="r2d2", l7=[{"cmd": "READ"}])
+    with pytest.raises(ValueError, match="Mismatching L7 types on the same port"):
+        P.policy_update(host_module, _mixed_port_policy([_mc_rule(), r2]))
+    http = api.port_rule(http=[{"headers": [{"name": ":path", "regex_match": "/a"}]}])
+    with pytest.raises(ValueError, match="Mismatching L7 types"):
+        P.policy_update(host_module, _mixed_port_policy([http, _mc_rule()]))
+
+
+def test_unregistered_parser_before_mismatch_is_drop_all_not_nack(host_module):
+    """An unregistered parser returns the port as drop-all before any later rule
+    is looked at (policymap.go:128-134), so no mismatch is seen after it; a
+    rule without L7 (type name "") never mismatches; UDP ports are never parsed
+    by proxylib (:206-209)."""
+    from cilium_amd import api
+    unknown = api.port_rule(l7proto="no-such-parser", l7=[{"x": "y"}])
+    r2 = api.port_rule(l7proto="r2d2", l7=[{"cmd": "READ"}])
+    P.policy_update(host_module, _mixed_port_policy([_mc_rule(), unknown, r2]))
+    P.policy_update(host_module, _mixed_port_policy([api.port_rule(remote_policies=[7]), _mc_rule()]))
+    P.policy_update(host_module, _mixed_port_policy([_mc_rule(), r2], protocol="UDP"))
+
+
+def test_envoy_view_accepts_mismatched_l7_types():
+    """Envoy's NPDS has no such check (envoy/cilium_network_policy.h:150-165):
+    the batch API installs the same version."""
+    from cilium_amd import api
+    from cilium_amd.engine import Engine
+    r2 = api.port_rule(l7proto="r2d2", l7=[{"cmd": "READ"}])
+    e = Engine(-1)  # L7G_HOST_ONLY: compile-only engine
+    e.update_policy(_mixed_port_policy([_mc_rule(), r2]))
+    e.close()
