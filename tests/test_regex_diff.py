@@ -132,3 +132,34 @@ def test_blowup_patterns_nfa_vs_oracle(oracle, pat):
 def test_nfa_position_limit():
     with pytest.raises(ValueError, match="NFA positions"):
         ca.debug_regex(".{1000}.{100}", b"", True, nfa=True)
+
+
+# Unicode version of Go 1.10 (Unicode 10.0.0): the tables are restricted to the
+# assigned10_0_0 set the reference vendors
+# (vendor/golang.org/x/text/unicode/rangetable/tables10.0.0.go:5739), so code
+# points Unicode 11-13 assigned are unassigned (Cn) and fold with nothing.
+UNICODE10 = [
+    # Georgian Mtavruli (Unicode 11): no category, no (?i) pair with Mkhedruli
+    ("\\p{Lu}", "Ა", False), ("\\PL", "Ა", True), ("\\p{Georgian}", "Ა", False),
+    ("(?i)ა", "Ა", False), ("(?i)ა", "ა", True), ("(?i)Ა", "ა", False),
+    ("[^\\pL\\pM\\pN\\pP\\pS\\pZ\\pC]", "Ჿ", True),
+    # Syriac Supplement (Unicode 10): assigned Lo
+    ("\\p{Lo}", "ࡠ", True), ("\\p{Syriac}", "ࡪ", True), ("\\p{Lo}", "࡫", False),
+    # Unicode 10 additions stay (Masaram Gondi U+11D00), Unicode 11 ones go (Dogra U+11800)
+    ("\\p{Lo}", "\U00011D00", True), ("\\p{Lo}", "\U00011800", False),
+    ("\\p{Masaram_Gondi}", "\U00011D00", True),
+]
+
+
+@pytest.mark.parametrize("nfa", [False, True])
+@pytest.mark.parametrize("pat,text,want", UNICODE10)
+def test_unicode10_tables(oracle, pat, text, want, nfa):
+    data = text.encode()
+    assert oracle.Regex(pat).match(data, True) == want, (pat, text)
+    assert ca.debug_regex(pat, data, True, nfa) == want, (pat, text)
+
+
+def test_unicode10_unknown_script():
+    # scripts Unicode 11+ introduced do not exist in Go 1.10's unicode.Scripts
+    with pytest.raises(ValueError):
+        ca.debug_regex("\\p{Dogra}", b"", True)

@@ -11,12 +11,20 @@ contrib/packaging/docker/Dockerfile.runtime:84, i.e. Unicode 10.0):
   * general categories for \\pL, \\p{Lu}, ...  (unicode.Categories)
   * scripts for \\p{Greek}, ...                (unicode.Scripts)
 
-This container only has Unicode 13.0 data (Python unicodedata, Perl unicore),
-so code points assigned after 10.0 are classified as in 13.0.  Scripts that
-did not exist in Unicode 10.0 are dropped so the *accept set* of \\p{Name}
-matches Go 1.10.  Non-ASCII class/fold behaviour is therefore "parity
-unpinned" (no reference test covers it), see DESIGN.md.
+  * simple lower-case mapping (unicode.ToLower) for proxylib cassandra's
+    strings.ToLower (proxylib/cassandra/cassandraparser.go:373)
+
+This container only has Unicode 13.0 data (Python unicodedata, Perl unicore).
+The reference holds the Unicode 10.0.0 *assigned* set
+(vendor/golang.org/x/text/unicode/rangetable/tables10.0.0.go, assigned10_0_0):
+every table is intersected with it, so code points Unicode 11-13 assigned
+(e.g. the Georgian Mtavruli capitals U+1C90-U+1CBF and their fold pairs) are
+unassigned here, as in Go 1.10.  Properties of code points already assigned in
+10.0 are taken from 13.0 data (changes to those are not pinned).  Scripts that
+did not exist in Unicode 10.0 are dropped.  Generation runs in the build
+container only (it reads /root/reference); the output is committed.
 """
+import re
 import os
 import subprocess
 import sys
@@ -24,6 +32,22 @@ import unicodedata
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 MAXR = 0x10FFFF
+ASSIGNED10 = os.environ.get(
+    "L7G_ASSIGNED10", "/root/reference/vendor/golang.org/x/text/unicode/rangetable/tables10.0.0.go")
+
+
+def load_assigned10(path=ASSIGNED10):
+    """assigned10_0_0 of x/text/unicode/rangetable: R16 + R32 {lo, hi, stride}."""
+    src = open(path).read()
+    body = src[src.index("var assigned10_0_0 = &unicode.RangeTable{"):]
+    body = body[:body.index("LatinOffset")]
+    cps = set()
+    for lo, hi, st in re.findall(r"\{0x([0-9a-fA-F]+), 0x([0-9a-fA-F]+), (\d+)\}", body):
+        cps.update(range(int(lo, 16), int(hi, 16) + 1, int(st)))
+    return cps
+
+
+A10 = None  # set of code points assigned in Unicode 10.0 (main() loads it)
 
 # Scripts added in Unicode 11.0-13.0 (absent from Go 1.10's unicode.Scripts).
 POST10_SCRIPTS = {
@@ -85,10 +109,10 @@ def fold_orbits():
             parent[max(ra, rb)] = min(ra, rb)
 
     for c in range(MAXR + 1):
-        if 0xD800 <= c <= 0xDFFF:
+        if 0xD800 <= c <= 0xDFFF or c not in A10:
             continue
         t = simple_fold_target(c)
-        if t != c:
+        if t != c and t in A10:
             union(c, t)
     groups = {}
     for c in list(parent.keys()):
@@ -110,7 +134,7 @@ def categories():
     cats = {}
     for c in range(MAXR + 1):
         cat = unicodedata.category(chr(c))
-        if cat == "Cn":
+        if cat == "Cn" or c not in A10:
             continue
         cats.setdefault(cat, []).append(c)
     out = {}
@@ -135,27 +159,38 @@ def scripts():
         name = go_script_name(parts[0])
         if name in POST10_SCRIPTS or name in ("Unknown", "Zzzz"):
             continue
-        rs = []
+        codes = set()
         for p in parts[1:]:
             a, b = p.split("-")
-            rs.append((int(a), int(b)))
-        rs.sort()
-        merged = []
-        for a, b in rs:
-            if merged and a <= merged[-1][1] + 1:
-                merged[-1] = (merged[-1][0], max(b, merged[-1][1]))
-            else:
-                merged.append((a, b))
-        out[name] = merged
+            codes.update(range(int(a), int(b) + 1))
+        merged = ranges_of(sorted(codes & A10))
+        if merged:
+            out[name] = merged
     return out
 
 
-def emit(path, pairs, cats, scr):
+def simple_lower():
+    """unicode.ToLower: the UnicodeData simple lower-case mapping (one rune);
+    str.lower() agrees except for U+0130, whose full mapping has two runes."""
+    out = []
+    for c in range(MAXR + 1):
+        if 0xD800 <= c <= 0xDFFF or c not in A10:
+            continue
+        lo = chr(c).lower()
+        t = 0x69 if c == 0x130 else (ord(lo) if len(lo) == 1 else c)
+        if t != c and t in A10:
+            out.append((c, t))
+    return out
+
+
+def emit(path, pairs, cats, scr, lower):
     lines = []
     w = lines.append
     w("/* GENERATED by tools/gen_unicode.py -- do not edit.")
-    w(" * Unicode %s data (Python unicodedata + Perl Unicode::UCD)." % unicodedata.unidata_version)
-    w(" * Tables for Go regexp/syntax semantics: SimpleFold orbits, categories, scripts. */")
+    w(" * Unicode %s properties (Python unicodedata + Perl Unicode::UCD) restricted to the" % unicodedata.unidata_version)
+    w(" * Unicode 10.0.0 assigned set of Go 1.10 (x/text rangetable assigned10_0_0).")
+    w(" * Tables for Go regexp/syntax semantics: SimpleFold orbits, categories, scripts;")
+    w(" * unicode.ToLower pairs. */")
     w("#pragma once")
     w("#include <stdint.h>")
     w("")
@@ -184,17 +219,28 @@ def emit(path, pairs, cats, scr):
         w('  {"%s", %d, %d, %d},' % (name, off, n, isscr))
     w("};")
     w("static const int UNI_NTABLES = %d;" % len(table))
+    w("")
+    w("/* (rune, unicode.ToLower(rune)) for every rune the mapping changes, sorted. */")
+    w("static const uint32_t UNI_LOWER_PAIRS[][2] = {")
+    for i in range(0, len(lower), 6):
+        w("  " + " ".join("{0x%X,0x%X}," % p for p in lower[i:i + 6]))
+    w("};")
+    w("static const int UNI_LOWER_NPAIRS = %d;" % len(lower))
     with open(path, "w") as f:
         f.write("\n".join(lines) + "\n")
 
 
 def main():
+    global A10
+    A10 = load_assigned10()
     pairs = fold_orbits()
     cats = categories()
     scr = scripts()
+    lower = simple_lower()
     for rel in ("cilium_amd/csrc/regex/unicode_tables.h", "oracle/unicode_tables.h"):
-        emit(os.path.join(ROOT, rel), pairs, cats, scr)
-    print("fold pairs", len(pairs), "categories", len(cats), "scripts", len(scr), file=sys.stderr)
+        emit(os.path.join(ROOT, rel), pairs, cats, scr, lower)
+    print("fold pairs", len(pairs), "categories", len(cats), "scripts", len(scr), "lower", len(lower),
+          file=sys.stderr)
 
 
 if __name__ == "__main__":
