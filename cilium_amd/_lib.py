@@ -12,7 +12,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("L7G_LIB") or os.path.join(HERE, "libl7gpu.so")
 
 DENY, ALLOW, PARSE_ERROR, INCOMPLETE, UNSUPPORTED = 0, 1, 2, 3, 4
-PROTO_HTTP, PROTO_KAFKA, PROTO_MEMCACHE, PROTO_R2D2 = 1, 2, 3, 4
+PROTO_HTTP, PROTO_KAFKA, PROTO_MEMCACHE, PROTO_R2D2, PROTO_CASSANDRA = 1, 2, 3, 4, 5
 VERDICT_NAMES = {DENY: "DENY", ALLOW: "ALLOW", PARSE_ERROR: "PARSE_ERROR",
                  INCOMPLETE: "INCOMPLETE", UNSUPPORTED: "UNSUPPORTED"}
 

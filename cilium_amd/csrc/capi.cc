@@ -14,6 +14,7 @@
 #include "../../include/l7gpu.h"
 #include "capi_internal.h"
 #include "device_tables.h"
+#include "engine/cass_compile.h"
 #include "engine/http_compile.h"
 #include "engine/kafka_compile.h"
 #include "engine/mc_compile.h"
@@ -36,6 +37,8 @@ uint32_t KafkaInflateRegionBytes();
 hipError_t LaunchMemcacheClassify(const Batch &B, const McTables &T, const uint32_t *sel, const uint32_t *sel2,
                                   const uint32_t *sel_count, bool answer_other, hipStream_t stream);
 hipError_t LaunchR2d2Classify(const Batch &B, const R2Tables &T, bool answer_other, hipStream_t stream);
+hipError_t LaunchCassandraClassify(const Batch &B, const CassTables &T, uint32_t *use_list, uint32_t *use_count,
+                                   bool answer_other, hipStream_t stream);
 hipError_t LaunchCounters(const uint8_t *verdict, const int32_t *rule, uint32_t n, uint32_t nrules,
                           uint64_t *counters, uint32_t *scratch, hipStream_t stream);
 size_t CountersScratchBytes();
@@ -65,6 +68,9 @@ struct StreamScratch {
     size_t nfa_cap = 0;
     // counter histogram scratch (kernels/counters.hip), allocated on first use
     uint32_t *d_hist = nullptr;
+    // cassandra USE list: [count | n request indices] (grow-only)
+    uint32_t *d_use = nullptr;
+    size_t use_cap = 0;
     // completion of the last call's kernels on this stream
     hipEvent_t done_ev = nullptr;
     bool launched = false;
@@ -73,6 +79,7 @@ struct StreamScratch {
         if (d_sel) hipFree(d_sel);
         if (d_nfa) hipFree(d_nfa);
         if (d_hist) hipFree(d_hist);
+        if (d_use) hipFree(d_use);
         if (done_ev) hipEventDestroy(done_ev);
     }
 };
@@ -101,6 +108,7 @@ struct l7g_engine {
     std::unique_ptr<KafkaCompiler> kc;
     std::unique_ptr<McCompiler> mc;
     std::unique_ptr<R2Compiler> r2;
+    std::unique_ptr<CassCompiler> cs;
     std::vector<l7g_conn_t> attrs;
     std::vector<DevConn> conns;
     uint8_t *d_blob = nullptr;
@@ -111,8 +119,9 @@ struct l7g_engine {
     KafkaTables kt{};
     McTables mt{};
     R2Tables rt{};
+    CassTables ct{};
     bool tables_dirty = true, conns_dirty = true;
-    bool has_http = false, has_kafka = false, has_mc = false, has_r2 = false;
+    bool has_http = false, has_kafka = false, has_mc = false, has_r2 = false, has_cs = false;
     int32_t hot_ruleset = -1;  // HTTP rule set staged in LDS (most connections)
     // l7g_classify_host contexts, one per calling thread (guarded by hmu)
     std::mutex hmu;
@@ -213,7 +222,7 @@ bool ResolveOne(l7g_engine *e, size_t i, std::string *err) {
     DevConn &c = e->conns[i];
     c = DevConn{-1, PROTO_NONE, 0, 0xFFFF};
     c.proto = a.proto;
-    if (a.proto == PROTO_HTTP || a.proto == PROTO_KAFKA || a.proto == PROTO_MEMCACHE || a.proto == PROTO_R2D2) {
+    if (L7_PROTO_OWNED(a.proto)) {
         const auto key = std::make_tuple(a.policy, a.proto, a.port, (uint8_t)(a.ingress != 0));
         auto it = e->skeys.find(key);
         if (it == e->skeys.end() && e->skey_list.size() < FlowStatsMaxKeys()) {
@@ -248,6 +257,10 @@ bool ResolveOne(l7g_engine *e, size_t i, std::string *err) {
         c.ruleset = e->r2->RulesetFor(a.policy, a.ingress != 0, a.port, a.src_id, err);
         if (c.ruleset < 0) return false;
         e->has_r2 = true;
+    } else if (a.proto == PROTO_CASSANDRA) {  // proxylib cassandra: SrcId in both directions
+        c.ruleset = e->cs->RulesetFor(a.policy, a.ingress != 0, a.port, a.src_id, err);
+        if (c.ruleset < 0) return false;
+        e->has_cs = true;
     }
     return true;
 }
@@ -269,13 +282,13 @@ void PickHot(l7g_engine *e) {
 
 size_t TableRulesets(const l7g_engine *e) {
     return e->hc->image().rulesets.size() + e->kc->image().rulesets.size() + e->mc->image().rulesets.size() +
-           e->r2->image().rulesets.size();
+           e->r2->image().rulesets.size() + e->cs->image().rulesets.size();
 }
 
 // Resolve every connection (policy update / connection table replaced).
 bool ResolveConns(l7g_engine *e, std::string *err) {
     e->conns.assign(e->attrs.size(), DevConn{-1, PROTO_NONE, 0, 0xFFFF});
-    e->has_http = e->has_kafka = e->has_mc = e->has_r2 = false;
+    e->has_http = e->has_kafka = e->has_mc = e->has_r2 = e->has_cs = false;
     for (size_t i = 0; i < e->attrs.size(); i++)
         if (!ResolveOne(e, i, err)) return false;
     PickHot(e);
@@ -296,6 +309,9 @@ hipError_t Upload(l7g_engine *e) {
         size_t m_rs = Put(blob, M.rulesets), m_img = Put(blob, M.images), m_nfa = Put(blob, M.nfa_pool);
         const R2Image &R = e->r2->image();
         size_t r_rs = Put(blob, R.rulesets), r_img = Put(blob, R.images), r_nfa = Put(blob, R.nfa_pool);
+        const CassImage &CI = e->cs->image();
+        size_t c_rs = Put(blob, CI.rulesets), c_img = Put(blob, CI.images), c_nfa = Put(blob, CI.nfa_pool),
+               c_low = Put(blob, CI.lower);
         uint8_t *d = nullptr;
         if ((rc = hipMalloc(&d, blob.size())) != hipSuccess) return rc;
         if ((rc = hipMemcpy(d, blob.data(), blob.size(), hipMemcpyHostToDevice)) != hipSuccess) { hipFree(d); return rc; }
@@ -330,6 +346,13 @@ hipError_t Upload(l7g_engine *e) {
         RT.images = d + r_img;
         RT.nrulesets = (uint32_t)R.rulesets.size();
         RT.nfa_pool = R.nfa_pool.empty() ? nullptr : d + r_nfa;
+        CassTables &CT = e->ct;
+        CT.rulesets = (const DevRuleset *)(d + c_rs);
+        CT.images = d + c_img;
+        CT.nrulesets = (uint32_t)CI.rulesets.size();
+        CT.nfa_pool = CI.nfa_pool.empty() ? nullptr : d + c_nfa;
+        CT.lower = (const uint32_t *)(d + c_low);
+        CT.nlower = (uint32_t)(CI.lower.size() / 2);
         e->tables_dirty = false;
     }
     if (e->conns_dirty) {
@@ -363,6 +386,7 @@ l7g_engine *l7g_engine_create(int device, char *err, size_t errlen) {
         e->kc = std::make_unique<KafkaCompiler>(e->ps.get());
         e->mc = std::make_unique<McCompiler>(e->ps.get());
         e->r2 = std::make_unique<R2Compiler>(e->ps.get());
+        e->cs = std::make_unique<CassCompiler>(e->ps.get());
         return e;
     }
     int ndev = 0;
@@ -379,6 +403,7 @@ l7g_engine *l7g_engine_create(int device, char *err, size_t errlen) {
     e->kc = std::make_unique<KafkaCompiler>(e->ps.get());
     e->mc = std::make_unique<McCompiler>(e->ps.get());
     e->r2 = std::make_unique<R2Compiler>(e->ps.get());
+    e->cs = std::make_unique<CassCompiler>(e->ps.get());
     return e;
 }
 
@@ -436,17 +461,20 @@ static int PolicySwap(l7g_engine *e, std::unique_ptr<PolicySet> ps, char *err, s
     auto kc = std::make_unique<KafkaCompiler>(ps.get());
     auto mc = std::make_unique<McCompiler>(ps.get());
     auto r2 = std::make_unique<R2Compiler>(ps.get());
+    auto cs = std::make_unique<CassCompiler>(ps.get());
     std::swap(e->ps, ps);
     std::swap(e->hc, hc);
     std::swap(e->kc, kc);
     std::swap(e->mc, mc);
     std::swap(e->r2, r2);
+    std::swap(e->cs, cs);
     if (!ResolveConns(e, &m)) {  // roll back: previous version stays in force
         std::swap(e->ps, ps);
         std::swap(e->hc, hc);
         std::swap(e->kc, kc);
         std::swap(e->mc, mc);
         std::swap(e->r2, r2);
+        std::swap(e->cs, cs);
         std::string m2;
         ResolveConns(e, &m2);
         set_err(err, errlen, m);
@@ -531,7 +559,7 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
     // the requests no classifier owns (unknown connection, no parser) itself.
     // A single-protocol HTTP or memcached engine skips it; its one kernel walks the whole batch
     // and answers those requests.
-    const int nproto = (int)e->has_http + (int)e->has_kafka + (int)e->has_mc + (int)e->has_r2;
+    const int nproto = (int)e->has_http + (int)e->has_kafka + (int)e->has_mc + (int)e->has_r2 + (int)e->has_cs;
     // (a Kafka-only or memcached-only engine partitions too: the kind / length
     // lists keep the Kafka kernel's waves converged, 1.55 -> 0.99 ms on cfg3,
     // and the text / binary lists the memcached kernel's)
@@ -610,6 +638,20 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
         rc = LaunchMemcacheClassify(B, e->mt, sel_m, sel_h, cnt ? cnt + L7_KAFKA_CLASSES : nullptr, !partitioned, s);
     // r2d2 (proxylib's example line protocol): one lane per request over the whole batch
     if (rc == hipSuccess && e->has_r2) rc = LaunchR2d2Classify(B, e->rt, !partitioned, s);
+    // cassandra (proxylib): the batch's USE requests, then one lane per request
+    if (rc == hipSuccess && e->has_cs) {
+        if ((size_t)n + 1 > S->use_cap) {
+            if (S->d_use) {
+                if (S->launched) rc = hipEventSynchronize(S->done_ev);
+                hipFree(S->d_use);
+                S->d_use = nullptr;
+                S->use_cap = 0;
+            }
+            if (rc == hipSuccess) rc = hipMalloc(&S->d_use, ((size_t)n + 1) * sizeof(uint32_t));
+            if (rc == hipSuccess) S->use_cap = (size_t)n + 1;
+        }
+        if (rc == hipSuccess) rc = LaunchCassandraClassify(B, e->ct, S->d_use + 1, S->d_use, !partitioned, s);
+    }
     mark(4);
     // proxy statistics (accumulated on the device until read)
     if (rc == hipSuccess && e->flow_stats && !e->skey_list.empty()) {

@@ -16,7 +16,9 @@ namespace l7 {
 enum : uint8_t {
     V_DENY = 0, V_ALLOW = 1, V_PARSE_ERROR = 2, V_INCOMPLETE = 3, V_UNSUPPORTED = 4,
 };
-enum : uint8_t { PROTO_NONE = 0, PROTO_HTTP = 1, PROTO_KAFKA = 2, PROTO_MEMCACHE = 3, PROTO_R2D2 = 4 };
+enum : uint8_t { PROTO_NONE = 0, PROTO_HTTP = 1, PROTO_KAFKA = 2, PROTO_MEMCACHE = 3, PROTO_R2D2 = 4, PROTO_CASSANDRA = 5 };
+// a protocol some classifier owns (the others answer its requests UNSUPPORTED)
+#define L7_PROTO_OWNED(p) ((p) >= PROTO_HTTP && (p) <= PROTO_CASSANDRA)
 
 // partition_kernel groups Kafka requests into this many kind / length classes
 #ifndef L7_KAFKA_CLASSES
@@ -291,6 +293,37 @@ struct R2Tables {
     uint32_t nrulesets;
     uint32_t pad;
     const uint8_t *nfa_pool;
+};
+
+// ---------------- cassandra ----------------
+// proxylib's cassandra parser (proxylib/cassandra/cassandraparser.go): rule r
+// holds for a query-like path iff (query_action any or equal to the path's
+// action) and (no query_table regex, an empty table part, or the regex matches
+// it, unanchored); for other opcodes every rule holds.  One image per rule
+// set, rules in chunks of <= 64.
+constexpr int kCassMaxChunks = 4;   // <= 256 rules per rule set
+struct CassImgHeader {     // 64 B
+    uint8_t nchunks;
+    uint8_t terminal;      // verdict when no rule matches (V_DENY; V_ALLOW when no L7 rules apply)
+    uint8_t ndfa;
+    uint8_t nnfa;
+    uint32_t act_off;      // u64[kCassActions + 1][nchunks]: rules admitting action a; row kCassActions:
+                           // an action outside queryActionMap (rules without query_action)
+    uint32_t notab_off;    // u64[nchunks]: rules without a query_table regex
+    uint32_t rule_off;     // i32[nchunks * 64]: global rule ids
+    uint32_t dfa_off;      // DevDfa[ndfa] (mask rows u64[nstates][nchunks]: rules whose regex accepts)
+    uint32_t nfa_off;      // DevNfaRef[nnfa] (mask_off: u64[nchunks], the rules of that regex)
+    uint32_t nrules;
+    uint32_t pad[9];
+};
+static_assert(sizeof(CassImgHeader) == 64, "CassImgHeader layout");
+struct CassTables {
+    const DevRuleset *rulesets;
+    const uint8_t *images;
+    uint32_t nrulesets;
+    uint32_t nlower;           // (rune, lower) pairs of unicode.ToLower
+    const uint8_t *nfa_pool;
+    const uint32_t *lower;
 };
 
 // FNV-1a over lower-cased ASCII (header names are tchar, i.e. ASCII)

@@ -1215,7 +1215,7 @@ __global__ __launch_bounds__(kBlock) void http_classify_kernel(Batch B, HttpTabl
             const DevConn conn = ci < nconns ? B.conns[ci] : DevConn{-1, PROTO_NONE, 0, 0xFFFF};
             // entries of other protocols belong to their own kernels; the HTTP
             // kernel answers entries whose connection is unknown or has no parser
-            const bool mine = !(conn.proto == PROTO_KAFKA || conn.proto == PROTO_MEMCACHE || conn.proto == PROTO_R2D2);
+            const bool mine = !L7_PROTO_OWNED(conn.proto) || conn.proto == PROTO_HTTP;
             const bool http = mine && conn.proto == PROTO_HTTP && conn.ruleset >= 0 && (uint32_t)conn.ruleset < T.nrulesets;
             const bool is_hot = http && hot_ok && conn.ruleset == hot;
             if (mine && !http && answer_other && (kHot || !hot_ok)) L.owed = true;  // unsupported connection: answered as is

@@ -217,7 +217,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(L7G_KAFK
         uint32_t consumed = 0;
         bool zflag = false;  // compressed messages passed: kafka_inflate_kernel decides them
         if (conn.proto != PROTO_KAFKA || conn.ruleset < 0 || (uint32_t)conn.ruleset >= T.nrulesets) {
-            if (!answer_other || conn.proto == PROTO_HTTP || conn.proto == PROTO_MEMCACHE || conn.proto == PROTO_R2D2) continue;
+            if (!answer_other || (L7_PROTO_OWNED(conn.proto) && conn.proto != PROTO_KAFKA)) continue;
             verdict = V_UNSUPPORTED;  // unknown connection / no parser
         }
         // ---- proto.ReadReq

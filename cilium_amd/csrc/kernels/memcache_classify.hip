@@ -223,7 +223,7 @@ __device__ __forceinline__ void mc_loop(Batch B, McTables T, const uint8_t *imag
         const uint32_t ci = conn_ids[idx];
         const DevConn conn = ci < nconns ? conns[ci] : DevConn{-1, PROTO_NONE, 0, 0xFFFF};
         if (conn.proto != PROTO_MEMCACHE || conn.ruleset < 0 || (uint32_t)conn.ruleset >= T.nrulesets) {
-            if (answer_other && conn.proto != PROTO_HTTP && conn.proto != PROTO_KAFKA && conn.proto != PROTO_R2D2) {  // no parser: UNSUPPORTED
+            if (answer_other && (!L7_PROTO_OWNED(conn.proto) || conn.proto == PROTO_MEMCACHE)) {  // no parser: UNSUPPORTED
                 B.verdict[idx] = V_UNSUPPORTED;
                 B.rule[idx] = -1;
                 B.consumed[idx] = 0;

@@ -97,7 +97,7 @@ __global__ __launch_bounds__(kBlock) void partition_kernel(Batch B, uint32_t *__
                 cls = 1 + (mode == 2 ? kMcBinary : c0 == 'g' ? kMcText : kMcText2);
             }
             else if (proto == PROTO_HTTP) cls = 1 + kHttp;
-            else if (proto != PROTO_R2D2) {  // (r2d2: its kernel walks the whole batch)
+            else if (!L7_PROTO_OWNED(proto)) {  // (r2d2, cassandra: their kernels walk the whole batch)
                 B.verdict[idx] = V_UNSUPPORTED;
                 B.rule[idx] = -1;
                 B.consumed[idx] = 0;

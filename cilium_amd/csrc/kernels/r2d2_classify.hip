@@ -47,8 +47,7 @@ __global__ __launch_bounds__(kBlock) void r2d2_classify_kernel(Batch B, R2Tables
     const uint32_t ci = B.conn_ids[i];
     const DevConn conn = ci < B.nconns ? B.conns[ci] : DevConn{-1, PROTO_NONE, 0, 0xFFFF};
     if (conn.proto != PROTO_R2D2 || conn.ruleset < 0 || (uint32_t)conn.ruleset >= T.nrulesets) {
-        if (answer_other && conn.proto != PROTO_HTTP && conn.proto != PROTO_KAFKA && conn.proto != PROTO_MEMCACHE &&
-            conn.proto != PROTO_R2D2) {
+        if (answer_other && !L7_PROTO_OWNED(conn.proto)) {
             B.verdict[i] = V_UNSUPPORTED;
             B.rule[i] = -1;
             B.consumed[i] = 0;

@@ -14,6 +14,7 @@
 #include <cstring>
 
 #include "json.h"
+#include "../kernels/cass_parse.h"
 
 namespace l7 {
 
@@ -219,7 +220,7 @@ struct Loader {
                 if (m->isObj())
                     for (auto &kv : m->obj) {
                         if (kv.second.isStr()) x.kv.emplace_back(kv.first, kv.second.str);
-                        else if ((r->l7proto == "memcache" || r->l7proto == "r2d2") && !mc_stop)
+                        else if ((r->l7proto == "memcache" || r->l7proto == "r2d2" || r->l7proto == "cassandra") && !mc_stop)
                             return fail("NPDS: " + r->l7proto + " rule value is not a string");
                     }
                 r->l7.push_back(std::move(x));
@@ -229,7 +230,12 @@ struct Loader {
                     r->mc.emplace_back();
                     if (!memcache(x, &r->mc.back())) return false;
                 }
-            if (r->l7proto == "cassandra" || r->l7proto == "test.headerparser") r->other_l7 = r->l7.size();
+            if (r->l7proto == "test.headerparser") r->other_l7 = r->l7.size();
+            if (r->l7proto == "cassandra" && !mc_stop)
+                for (auto &x : r->l7) {
+                    r->cass.emplace_back();
+                    if (!cassandra(x, &r->cass.back())) return false;
+                }
             if (r->l7proto == "r2d2" && !mc_stop)
                 for (auto &x : r->l7) {
                     r->r2.emplace_back();
@@ -289,6 +295,40 @@ struct Loader {
         if (m->file_re && !(cmd.empty() || cmd == "READ" || cmd == "WRITE"))
             return fail("NPDS: Unable to parse L7 r2d2 rule, cmd '" + cmd + "' is not compatible with 'file'");
         m->cmd = cmd.empty() ? -1 : cmd == "READ" ? R2_READ : cmd == "WRITE" ? R2_WRITE : cmd == "HALT" ? R2_HALT : R2_RESET;
+        return true;
+    }
+
+    // cassandra.CassandraRuleParser (proxylib/cassandra/cassandraparser.go:99-134);
+    // its ParseError / regexp.MustCompile panics NACK the policy
+    bool cassandra(const L7Rule &x, CassRule *m) {
+        m->id = x.id;
+        std::string action;
+        bool has_action = false;
+        for (auto &kv : x.kv) {
+            const std::string &k = kv.first, &v = kv.second;
+            if (k == "query_action") {
+                action = v;
+                has_action = !v.empty();
+            } else if (k == "query_table") {
+                if (v.empty()) continue;
+                std::string e;
+                auto ast = re::Parse(v, &e);
+                if (!ast) return fail("regexp: Compile(`" + v + "`): " + e);
+                m->table_re = std::shared_ptr<re::Node>(std::move(ast));
+                m->table_src = v;
+            } else {
+                return fail("NPDS: Unsupported key: " + k);
+            }
+        }
+        if (has_action) {
+            m->action = -1;
+            for (int a = 0; a < kCassActions; a++)
+                if (action == CassActionName(a)) m->action = a;
+            if (m->action < 0)
+                return fail("NPDS: Unable to parse L7 cassandra rule with invalid query_action: '" + action + "'");
+            if (m->action >= kCassTableActions && m->table_re)
+                return fail("NPDS: query_action '" + action + "' is not compatible with a query_table match");
+        }
         return true;
     }
 

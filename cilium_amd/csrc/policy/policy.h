@@ -61,6 +61,16 @@ struct R2Rule {
     int id = -1;
 };
 
+// cassandra.CassandraRule (proxylib/cassandra/cassandraparser.go:50-53):
+// query_action exact (an action id of kernels/cass_parse.h, -1 = any) and a
+// query_table regex (unanchored MatchString, or any).
+struct CassRule {
+    int action = -1;
+    std::shared_ptr<re::Node> table_re;
+    std::string table_src;
+    int id = -1;
+};
+
 struct PortRule {
     std::vector<uint64_t> remotes;  // empty = any remote
     enum Type { None, Http, Kafka, L7 } type = None;
@@ -70,7 +80,8 @@ struct PortRule {
     std::vector<L7Rule> l7;
     std::vector<McRule> mc;  // l7proto == "memcache": its parsed L7 rules
     std::vector<R2Rule> r2;  // l7proto == "r2d2": its parsed L7 rules
-    size_t other_l7 = 0;     // "cassandra" / "test.headerparser" rules (registered; never match here)
+    std::vector<CassRule> cass;  // l7proto == "cassandra": its parsed L7 rules
+    size_t other_l7 = 0;     // "test.headerparser" rules (registered; never match here)
     // proxylib parser name: l7_proto, else the oneof type name, "" = no L7
     // (proxylib/proxylib/policymap.go:68-75)
     std::string ParserName() const;
@@ -79,7 +90,7 @@ struct PortRule {
     // HTTP rules or Kafka rules
     size_t NumL7() const {
         return type == Http ? http.size() : type == Kafka ? kafka.size() : l7proto == "r2d2" ? r2.size()
-             : l7proto == "memcache" ? mc.size() : other_l7;
+             : l7proto == "memcache" ? mc.size() : l7proto == "cassandra" ? cass.size() : other_l7;
     }
 };
 // L7 rule parsers the proxylib view registers (policymap.go:42-45): "memcache",

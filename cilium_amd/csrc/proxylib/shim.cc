@@ -13,7 +13,12 @@
 //   "kafka"     Kafka requests with the in-agent proxy's verdict
 //               (pkg/proxy/kafka.go:117-153, 249-261): allowed => PASS, denied
 //               => DROP and the CreateResponse(ErrTopicAuthorizationFailed)
-//               reply injected (kafka_response.cc).
+//               reply injected (kafka_response.cc);
+//   "cassandra" proxylib/cassandra/cassandraparser.go: the device parses each
+//               query and matches the path; the host keeps the parser's
+//               state (the frame that set the keyspace, the PREPARE frames by
+//               stream id and by prepared id) and replays it to the device as
+//               extra requests of the same launch (see CassClassify).
 // HTTP and Kafka connections use proxylib's policymap semantics
 // (L7G_CONN_PROXYLIB: no port entry => drop, SrcId as the remote).
 //
@@ -50,6 +55,8 @@
 #include "../../../include/l7gpu.h"
 #include "../../../include/proxylib_abi.h"
 #include "../capi_internal.h"
+#include "../kernels/cass_parse.h"
+#include "../regex/unicode_tables.h"
 
 namespace {
 
@@ -185,7 +192,109 @@ bool KafkaDenyResponse(const uint8_t *req, size_t len, std::string *out);
 }
 namespace {
 
-enum Kind { K_MEMCACHE, K_HTTP, K_KAFKA, K_R2D2 };
+enum Kind { K_MEMCACHE, K_HTTP, K_KAFKA, K_R2D2, K_CASSANDRA };
+
+// ---------------------------------------------------------------- cassandra helpers
+uint32_t Be32(const std::string &d, size_t o) {
+    return (uint32_t)(uint8_t)d[o] << 24 | (uint32_t)(uint8_t)d[o + 1] << 16 | (uint32_t)(uint8_t)d[o + 2] << 8 |
+           (uint8_t)d[o + 3];
+}
+uint32_t Be16(const std::string &d, size_t o) { return (uint32_t)(uint8_t)d[o] << 8 | (uint8_t)d[o + 1]; }
+
+// unicode.ToLower pairs, flattened (the tables the device gets, engine/cass_compile.cc)
+const std::vector<uint32_t> &CassLower() {
+    static const std::vector<uint32_t> v = [] {
+        std::vector<uint32_t> x;
+        for (int i = 0; i < UNI_LOWER_NPAIRS; i++) { x.push_back(UNI_LOWER_PAIRS[i][0]); x.push_back(UNI_LOWER_PAIRS[i][1]); }
+        return x;
+    }();
+    return v;
+}
+
+struct StrSink {
+    std::string s;
+    void raw(uint32_t c) { s.push_back((char)c); }
+    void rune(uint32_t r) {
+        uint8_t e[4];
+        s.append((const char *)e, l7::cass_encode(r, e));
+    }
+};
+
+// The query of a complete QUERY / PREPARE frame (nullptr: none, or its slice
+// expressions panic) -- the device decided that already; this is for the
+// host's bookkeeping and access-log records only.
+const uint8_t *CassQueryOf(const std::string &f, uint32_t *qn) {
+    if (f.size() < 13 || (f[4] != 0x07 && f[4] != 0x09)) return nullptr;
+    const uint32_t ql = Be32(f, 9);
+    if (13u + ql < 13u || 13u + ql > f.size()) return nullptr;
+    *qn = ql;
+    return (const uint8_t *)f.data() + 13;
+}
+
+// The path cassandraParseRequest builds for a QUERY / PREPARE frame
+// ("/<opcode>/<action>/<table>", cassandraparser.go:496-515) under the
+// keyspace the frame `use` set ("" = none), as the reference's strings: the
+// access log splits it on "/".  Empty if the query does not parse.
+std::string CassPath(const std::string &f, const std::string &use) {
+    uint32_t qn;
+    const uint8_t *q = CassQueryOf(f, &qn);
+    if (!q) return "";
+    const auto &L = CassLower();
+    const l7::CassQuery Q = l7::cass_parse_query(q, qn, L.data(), (uint32_t)(L.size() / 2));
+    if (Q.status != l7::CQ_OK) return "";
+    StrSink a, t;
+    switch (Q.kw) {
+    case l7::CW_SELECT: a.s = "select"; break;
+    case l7::CW_DELETE: a.s = "delete"; break;
+    case l7::CW_INSERT: a.s = "insert"; break;
+    case l7::CW_UPDATE: a.s = "update"; break;
+    case l7::CW_USE: a.s = "use"; break;
+    default: {
+        static const char *const kw[] = {"alter", "create", "drop", "truncate", "list"};
+        a.s = std::string(kw[Q.kw - l7::CW_ALTER]) + "-";
+        l7::cass_emit(q, Q.f1s, Q.f1e, Q.fc, L.data(), (uint32_t)(L.size() / 2), a, false);
+        const uint32_t w1 = l7::cass_word(q, Q.f1s, Q.f1e);
+        if (w1 == l7::CW_MATERIALIZED) a.s += "-view";
+        else if (w1 == l7::CW_CUSTOM) a.s = "create-index";
+    }
+    }
+    if (Q.has_table) {
+        l7::cass_emit(q, Q.ts, Q.te, Q.fc, L.data(), (uint32_t)(L.size() / 2), t, false);
+        if (!Q.is_use && t.s.find('.') == std::string::npos) {
+            StrSink k;
+            uint32_t kn;
+            const uint8_t *kq = use.empty() ? nullptr : CassQueryOf(use, &kn);
+            if (kq) {
+                const l7::CassQuery K = l7::cass_parse_query(kq, kn, L.data(), (uint32_t)(L.size() / 2));
+                l7::cass_emit(kq, K.ts, K.te, K.fc, L.data(), (uint32_t)(L.size() / 2), k, false);
+            }
+            t.s = k.s + "." + t.s;
+        }
+    }
+    return std::string("/") + (f[4] == 0x09 ? "prepare" : "query") + "/" + a.s + "/" + t.s;
+}
+
+bool CassIsUse(const std::string &f) {
+    uint32_t qn;
+    const uint8_t *q = CassQueryOf(f, &qn);
+    if (!q) return false;
+    const auto &L = CassLower();
+    const l7::CassQuery Q = l7::cass_parse_query(q, qn, L.data(), (uint32_t)(L.size() / 2));
+    return Q.status == l7::CQ_OK && Q.is_use;
+}
+
+// A QUERY frame "use ''": the empty keyspace, for replays that must not see
+// a USE the batch holds before them
+std::string CassEmptyUse() {
+    const std::string q = "use ''";
+    std::string f = {4, 0, 0, 0, 7, 0, 0, 0, (char)(4 + q.size()), 0, 0, 0, (char)q.size()};
+    return f + q;
+}
+
+const uint8_t kCassUnauth[35] = {0, 0, 0, 0, 0, 0, 0, 0, 0x1a, 0, 0, 0x21, 0, 0, 0x14, 'R', 'e', 'q',
+                                 'u', 'e', 's', 't', ' ', 'U', 'n', 'a', 'u', 't', 'h', 'o', 'r', 'i', 'z',
+                                 'e', 'd'};  // unauthMsgBase (cassandraparser.go:269-278)
+const uint8_t kCassUnprepared[13] = {0, 0, 0, 0, 0, 0, 0, 0, 0x1a, 0, 0, 0x25, 0};  // unpreparedMsgBase (:284-292)
 
 struct Cached {
     uint8_t v;
@@ -269,6 +378,13 @@ struct Connection {
     struct Queued { uint8_t magic; uint32_t request; };
     std::deque<Queued> inject_queue;
     uint32_t requests = 0, replies = 0;
+    // cassandra parser state (cassandraparser.go:146-160), as raw frames the
+    // device re-reads: the frame whose query set the keyspace (a USE), and per
+    // stream id / prepared id the PREPARE frame with the USE frame then in force
+    std::string cass_use;
+    std::map<uint16_t, std::pair<std::string, std::string>> cass_by_stream;
+    std::map<std::string, std::pair<std::string, std::string>> cass_by_id;
+    std::map<uint64_t, std::pair<std::string, std::string>> cass_exec;  // this call's EXECUTE frames resolved
 
     GoSlice *InjectBuf(bool r) const { return r ? reply : orig; }
     int64_t Inject(bool r, const void *data, size_t n) {  // connection.go:190-203
@@ -353,8 +469,9 @@ struct Connection {
         a.port = port;
         a.ingress = ingress ? 1 : 0;
         a.proto = kind == K_HTTP ? L7G_PROTO_HTTP : kind == K_KAFKA ? L7G_PROTO_KAFKA
-                : kind == K_R2D2 ? L7G_PROTO_R2D2 : L7G_PROTO_MEMCACHE;
-        a.flags = kind == K_MEMCACHE ? (uint16_t)mode : kind == K_R2D2 ? (uint16_t)0 : (uint16_t)L7G_CONN_PROXYLIB;
+                : kind == K_R2D2 ? L7G_PROTO_R2D2 : kind == K_CASSANDRA ? L7G_PROTO_CASSANDRA : L7G_PROTO_MEMCACHE;
+        a.flags = kind == K_MEMCACHE ? (uint16_t)mode : (kind == K_R2D2 || kind == K_CASSANDRA) ? (uint16_t)0
+                : (uint16_t)L7G_CONN_PROXYLIB;
         a.src_id = src;
         a.dst_id = dst;
         return a;
@@ -403,6 +520,139 @@ struct Connection {
             return false;
         for (size_t i = 0; i < n; i++) batch[offs[i]] = Cached{v[i], r[i], c[i]};
         return true;
+    }
+
+    // ---- "cassandra" (proxylib/cassandra/cassandraparser.go)
+    // Classify the frames at offs of d in one launch, as the device sees a
+    // connection's frames: [the frame that set the keyspace] + the frames +
+    // per resolvable EXECUTE [its USE frame (or "use ''"), its PREPARE frame],
+    // the replayed PREPARE's verdict standing for the EXECUTE's.  Results are
+    // kept under key + offset (key = where d starts in this call's input).
+    bool CassClassify(const std::string &d, const std::vector<uint64_t> &offs, uint64_t key) {
+        std::string arena = cass_use;
+        std::vector<uint64_t> o;
+        std::vector<uint32_t> l;
+        if (!cass_use.empty()) { o.push_back(0); l.push_back((uint32_t)cass_use.size()); }
+        const size_t first = o.size();
+        for (uint64_t p : offs) { o.push_back(arena.size() + p); l.push_back((uint32_t)(d.size() - p)); }
+        arena += d;
+        std::vector<std::pair<uint64_t, size_t>> replay;  // (frame offset in d, request index of its PREPARE)
+        for (uint64_t p : offs) {
+            if (d.size() - p < 11 || d[p + 4] != 0x0A || (d[p] & 0x80) || (d[p + 1] & 1)) continue;
+            const uint32_t fl = 9 + Be32(d, p + 5);
+            const uint32_t il = Be16(d, p + 9);
+            if (fl > d.size() - p || 11u + il > fl) continue;
+            auto it = cass_by_id.find(d.substr(p + 11, il));
+            if (it == cass_by_id.end()) continue;
+            const std::string u = it->second.first.empty() ? CassEmptyUse() : it->second.first;
+            o.push_back(arena.size()); l.push_back((uint32_t)u.size()); arena += u;
+            o.push_back(arena.size()); l.push_back((uint32_t)it->second.second.size()); arena += it->second.second;
+            replay.emplace_back(p, o.size() - 1);
+            cass_exec[key + p] = it->second;
+        }
+        const size_t n = o.size();
+        std::vector<uint32_t> cids(n, slot);
+        std::vector<uint8_t> v(n);
+        std::vector<int32_t> r(n);
+        std::vector<uint32_t> c(n);
+        if (l7g_classify_host(ins->eng, (const uint8_t *)arena.data(), arena.size(), o.data(), l.data(), cids.data(),
+                              (uint32_t)n, v.data(), r.data(), c.data()) != 0)
+            return false;
+        for (size_t i = 0; i < offs.size(); i++) batch[key + offs[i]] = Cached{v[first + i], r[first + i], c[first + i]};
+        for (auto &rp : replay) {
+            const std::string &pf = cass_exec[key + rp.first].second;
+            batch[key + rp.first] =
+                Cached{v[rp.second], r[rp.second], 9 + Be32(pf, 5) == c[rp.second] ? 9 + Be32(d, rp.first + 5) : 0};
+        }
+        return true;
+    }
+    bool CassPrefetch(const std::string &d, size_t max) {
+        cass_exec.clear();
+        std::vector<uint64_t> offs;
+        for (size_t p = 0; p + 9 <= d.size() && offs.size() < max;) {
+            offs.push_back(p);
+            const uint64_t fl = 9 + (uint64_t)Be32(d, p + 5);
+            if (fl > d.size() - p) break;
+            p += fl;
+        }
+        if (offs.empty()) return true;
+        return CassClassify(d, offs, 0);
+    }
+    int64_t CassOnData(bool r, const std::vector<std::string> &in, int64_t *n, bool *err) {
+        std::string d;
+        for (auto &b : in) d += b;
+        if (d.size() < 9) { *n = 9 - (int64_t)d.size(); return FILTEROP_MORE; }
+        const uint32_t rl = Be32(d, 5);
+        if (rl > 268435456u) { *n = FILTEROP_ERROR_INVALID_FRAME_LENGTH; return FILTEROP_ERROR; }
+        const int64_t missing = 9 + (int64_t)rl - (int64_t)d.size();
+        if (missing > 0) { *n = missing; return FILTEROP_MORE; }
+        const uint32_t fl = 9 + rl;
+        const std::string f = d.substr(0, fl);
+        if (r) {  // cassandraParseReply (:605-642): RESULT / prepared binds a prepared id
+            if ((f[0] & 0x80) && !(f[1] & 1) && f[4] == 0x08) {
+                if (fl < 13) throw Panic();
+                if (Be32(f, 9) == 4) {
+                    if (fl < 15) throw Panic();
+                    const uint32_t il = Be16(f, 13);
+                    if (15u + il > fl) throw Panic();
+                    auto it = cass_by_stream.find((uint16_t)Be16(f, 2));
+                    if (it != cass_by_stream.end()) cass_by_id[f.substr(15, il)] = it->second;
+                }
+            }
+            *n = fl;
+            return FILTEROP_PASS;
+        }
+        if (batch.find(base) == batch.end() && !CassClassify(d, {0}, base)) { *err = true; *n = 0; return FILTEROP_ERROR; }
+        const Cached res = batch[base];
+        if (res.v == L7G_PARSE_ERROR) {
+            if (res.consumed == 0) throw Panic();  // a Go panic in cassandraParseRequest
+            if (f[4] == 0x0A && res.consumed == FILTEROP_ERROR_INVALID_FRAME_TYPE) {  // no cached path: sendUnpreparedMsg
+                uint8_t m[sizeof kCassUnprepared];
+                memcpy(m, kCassUnprepared, sizeof m);
+                m[0] = (uint8_t)(0x80 | (f[0] & 0x07));
+                m[2] = (uint8_t)f[2];
+                m[3] = (uint8_t)f[3];
+                Inject(true, m, sizeof m);
+                Inject(true, f.data() + 9, 2 + Be16(f, 9));
+            }
+            *n = res.consumed;
+            return FILTEROP_ERROR;
+        }
+        if (res.v != L7G_ALLOW && res.v != L7G_DENY) { *n = res.consumed ? res.consumed : 1; return FILTEROP_MORE; }
+        // the request's path: the parser state's bookkeeping, and the access log
+        std::string path;
+        if (f[4] == 0x0A) {
+            auto it = cass_exec.find(base);
+            if (it != cass_exec.end()) {
+                path = CassPath(it->second.second, it->second.first);
+                const size_t k = path.find("prepare");  // strings.Replace(path, "prepare", "execute", 1)
+                if (k != std::string::npos) path.replace(k, 7, "execute");
+            }
+        } else if (f[4] == 0x07 || f[4] == 0x09) {
+            const std::string use_before = cass_use;
+            path = CassPath(f, use_before);
+            if (CassIsUse(f)) cass_use = f;
+            if (f[4] == 0x09) cass_by_stream[(uint16_t)Be16(f, 2)] = {use_before, f};
+        }
+        std::vector<std::string> parts;
+        for (size_t a = 0;;) {
+            const size_t s = path.find('/', a);
+            parts.push_back(path.substr(a, s == std::string::npos ? std::string::npos : s - a));
+            if (s == std::string::npos) break;
+            a = s + 1;
+        }
+        const bool ok = res.v == L7G_ALLOW;
+        if (parts.size() == 4)
+            Log(ok ? kEntryRequest : kEntryDenied, GenericL7("cassandra", {{"query_action", parts[2]}, {"query_table", parts[3]}}));
+        *n = fl;
+        if (ok) return FILTEROP_PASS;
+        uint8_t m[sizeof kCassUnauth];
+        memcpy(m, kCassUnauth, sizeof m);
+        m[0] = (uint8_t)(0x80 | (f[0] & 0x07));
+        m[2] = (uint8_t)f[2];
+        m[3] = (uint8_t)f[3];
+        Inject(true, m, sizeof m);
+        return FILTEROP_DROP;
     }
 
     // ---- "http": a request's verdict from its headers (cilium_l7policy.cc:127-182)
@@ -658,6 +908,7 @@ struct Connection {
         if (kind == K_HTTP) return HttpOnData(r, in, n, err);
         if (kind == K_R2D2) return R2d2OnData(r, in, n, err);
         if (kind == K_KAFKA) return KafkaOnData(r, in, n, err);
+        if (kind == K_CASSANDRA) return CassOnData(r, in, n, err);
         // memcache.Parser.OnData (memcached/parser.go:186-202)
         if (mode == 0) {
             if (!first_nonempty) { *n = 0; return NOP; }
@@ -777,6 +1028,7 @@ FilterResult OnNewConnection(uint64_t instance_id, GoString proto, uint64_t conn
     else if (p == "http") kind = K_HTTP;
     else if (p == "kafka") kind = K_KAFKA;
     else if (p == "r2d2") kind = K_R2D2;
+    else if (p == "cassandra") kind = K_CASSANDRA;
     else return FILTER_UNKNOWN_PARSER;
     uint32_t port;
     if (!DstPort(Str(dst_addr), &port)) return FILTER_INVALID_ADDRESS;
@@ -837,7 +1089,8 @@ FilterResult OnData(uint64_t connection_id, uint8_t reply, uint8_t end_stream, G
     if (!reply) {  // the request frames of this call: one device launch
         std::string all;
         for (auto &b : in) all += b;
-        if (!c->Prefetch(all, (size_t)(ops->cap - ops->len))) return FILTER_UNKNOWN_ERROR;
+        const size_t room = (size_t)(ops->cap - ops->len);
+        if (!(c->kind == K_CASSANDRA ? c->CassPrefetch(all, room) : c->Prefetch(all, room))) return FILTER_UNKNOWN_ERROR;
     }
     try {
         while (ops->len < ops->cap) {  // connection.go:138-172

@@ -18,7 +18,7 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from . import api
-from ._lib import PROTO_HTTP, PROTO_KAFKA, PROTO_MEMCACHE, PROTO_R2D2
+from ._lib import PROTO_CASSANDRA, PROTO_HTTP, PROTO_KAFKA, PROTO_MEMCACHE, PROTO_R2D2
 from .engine import CONN_DTYPE
 
 SEED_BASE = 0x1C1D0000
@@ -1071,3 +1071,92 @@ def r2d2_workload(n, nconns=64, seed=None):
     remotes = [7, 8, 100, 101, 150, 163, 5] * (nconns // 7 + 1)
     conns = make_conns(nconns, 0, R2D2_PORT, True, PROTO_R2D2, remotes[:nconns])
     return Workload("r2d2", arena, offs, lens, conn_ids, conns, r2d2_policy())
+
+
+# ------------------------------------------------------------------ cassandra
+# proxylib's cassandra parser (proxylib/cassandra/cassandraparser.go): CQL
+# native-protocol v3/v4 frames (9-byte header + body); QUERY / PREPARE carry a
+# [long string] query
+CASS_PORT = 9042
+
+
+def cassandra_policy():
+    """cassandra rules (cassandraparser.go:99-134): action only, table regex
+    only, both, an NFA-fallback table regex, a table-less action, a
+    remote-restricted group and a port-0 entry."""
+    rules = [{"query_action": "select", "query_table": "^ks1\\."}, {"query_action": "insert", "query_table": "users$"},
+             {"query_table": "^system\\.local$"}, {"query_action": "use"}, {"query_action": "create-index"},
+             {"query_table": "(a|b)*a(a|b){14}"}, {"query_action": "update", "query_table": "é"},
+             {"query_action": "drop-table", "query_table": "^\\.tmp"}]
+    groups = [api.port_rule(remote_policies=[7, 8], l7proto="cassandra", l7=[{"query_action": "delete"}]),
+              api.port_rule(remote_policies=list(range(100, 164)), l7proto="cassandra", l7=rules)]
+    wild = [api.port_rule(l7proto="cassandra", l7=[{"query_action": "select", "query_table": "^wild"}])]
+    return api.policy_set(api.network_policy("cs", 11, ingress=[(CASS_PORT, groups), (0, wild)]))
+
+
+def cass_frame(op, body, stream=1, version=4, flags=0):
+    return bytes([version, flags, (stream >> 8) & 0xFF, stream & 0xFF, op]) + len(body).to_bytes(4, "big") + body
+
+
+def cass_query_frame(q, op=0x07, stream=1, trailer=b"\x00\x01\x00"):
+    b = q.encode() if isinstance(q, str) else q
+    return cass_frame(op, len(b).to_bytes(4, "big") + b + trailer, stream)
+
+
+_CASS_QUERIES = [
+    "SELECT * FROM ks1.users WHERE id = 1", "select a, b from users", "select * from system.local",
+    "SELECT * FROM System.Local;", "select x from t from ks1.t2", "select * from", "select * from t -- c",
+    "INSERT INTO users (a) VALUES (1)", "insert into ks2.users (a) values (1)", "insert into",
+    "update ks1.t set a = 1", "UPDATE t SET b = 2", "delete from ks1.old where x = 1", "use ks1", "USE \"KS2\"",
+    "use 'ks/x'", "create table if not exists ks1.t (a int)", "drop table if exists .tmp1", "drop table tmpx",
+    "create index i on t (a)", "create custom index j on t (b)", "drop materialized view v",
+    "truncate table ks1.t", "truncate t", "list roles", "create role r", "create a/bab c",
+    "alter keyspace ks1 with x", "grant select on t to r", "select * from a/b", "select * from wildcat",
+    "select * from ÉTÉ", "update été set a = 1", "SELECT * FROM \u212aS1.t", "\u0130NSERT INTO users x",
+    "select\u00a0*\u00a0from\u2003ks1.a", "select * from t\udcff", "", "select",
+    "select * from " + "ab" * 3 + "a" + "ab" * 7, "select * from bbbbbbbbbbbbbbbbbbbb",
+]
+
+
+def cassandra_requests(n, seed):
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        k = int(rng.integers(0, 20))
+        stream = int(rng.integers(0, 65536))
+        if k < 13:
+            q = _CASS_QUERIES[int(rng.integers(0, len(_CASS_QUERIES)))]
+            b = q.encode("utf-8", "surrogateescape")
+            if rng.random() < 0.05:
+                b = b.replace(b"t", b"\xff", 1)  # an invalid UTF-8 byte
+            out.append(cass_query_frame(b, 0x09 if rng.random() < 0.2 else 0x07, stream))
+        elif k == 13:
+            out.append(cass_frame(int(rng.choice([0x01, 0x05, 0x0B, 0x0F, 0x20])), b"\x00" * int(rng.integers(0, 8)), stream))
+        elif k == 14:
+            out.append(cass_frame(0x0A, b"\x00\x02ab\x00\x00", stream))                  # EXECUTE
+        elif k == 15:
+            out.append(cass_frame(0x0D, b"\x00\x00\x01\x00\x00\x00\x00\x04use x", stream))  # BATCH: panics
+        elif k == 16:
+            f = cass_query_frame("select * from ks1.t", 0x07, stream)
+            out.append(f[:int(rng.integers(0, len(f)))])                                    # short
+        elif k == 17:
+            f = bytearray(cass_query_frame("select * from ks1.t", 0x07, stream))
+            f[int(rng.choice([0, 1]))] |= int(rng.choice([0x80, 0x01]))                     # reply / compressed
+            out.append(bytes(f))
+        elif k == 18:
+            body = (1000).to_bytes(4, "big") + b"use x"                                     # query past the frame
+            out.append(cass_frame(0x07, body, stream))
+        else:
+            out.append(bytes([4, 0, 0, 1, 7]) + (0x10000001).to_bytes(4, "big"))             # > 256 MB
+    return out
+
+
+def cassandra_workload(n, nconns=16, seed=None):
+    seed = SEED_BASE + 9 if seed is None else seed
+    reqs = cassandra_requests(n, seed)
+    arena, offs, lens = pack(reqs)
+    rng = np.random.default_rng(seed + 1)
+    conn_ids = rng.integers(0, nconns, size=n).astype(np.uint32)
+    remotes = [7, 8, 100, 101, 150, 163, 5] * (nconns // 7 + 1)
+    conns = make_conns(nconns, 0, CASS_PORT, True, PROTO_CASSANDRA, remotes[:nconns])
+    return Workload("cassandra", arena, offs, lens, conn_ids, conns, cassandra_policy())

@@ -40,7 +40,7 @@ extern "C" {
 
 typedef struct l7g_engine l7g_engine;
 
-enum { L7G_PROTO_HTTP = 1, L7G_PROTO_KAFKA = 2, L7G_PROTO_MEMCACHE = 3, L7G_PROTO_R2D2 = 4 };
+enum { L7G_PROTO_HTTP = 1, L7G_PROTO_KAFKA = 2, L7G_PROTO_MEMCACHE = 3, L7G_PROTO_R2D2 = 4, L7G_PROTO_CASSANDRA = 5 };
 enum {
     L7G_DENY = 0,        /* policy denies (HTTP 403 / Kafka ErrTopicAuthorizationFailed) */
     L7G_ALLOW = 1,       /* policy allows; rule = matched global rule id or -1 */

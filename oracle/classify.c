@@ -214,6 +214,48 @@ static int load_r2_rule(ld *l, const jnode *j, ref_mc_rule *m) {
     return 0;
 }
 
+/* cassandra.CassandraRuleParser (proxylib/cassandra/cassandraparser.go:99-134):
+ * keys query_action / query_table; an unknown key, a query_action outside
+ * queryActionMap (:319-366), a query_table with a table-less action, or a
+ * regex that does not compile (regexp.MustCompile) NACKs the policy. */
+static const char *kCassActions[] = {
+    "select", "delete", "insert", "update", "create-table", "drop-table", "alter-table", "truncate-table", "use",
+    "create-keyspace", "alter-keyspace", "drop-keyspace", "drop-index", "create-index", "create-materialized-view",
+    "drop-materialized-view", "create-role", "alter-role", "drop-role", "grant-role", "revoke-role", "list-roles",
+    "grant-permission", "revoke-permission", "list-permissions", "create-user", "alter-user", "drop-user",
+    "list-users", "create-function", "drop-function", "create-aggregate", "drop-aggregate", "create-type",
+    "alter-type", "drop-type", "create-trigger", "drop-trigger"};
+static int cass_action_kind(const char *a) {  /* 0 invalid, 1 with table, 2 without */
+    for (size_t i = 0; i < sizeof kCassActions / sizeof kCassActions[0]; i++)
+        if (!strcmp(a, kCassActions[i])) return i < 12 ? 1 : 2;
+    return 0;
+}
+static int load_cass_rule(ld *l, const jnode *j, ref_mc_rule *m) {
+    const jnode *kv = jget(j, "rule");
+    if (!kv) kv = j;
+    if (kv->type != JN_OBJ) return 0;
+    for (int i = 0; i < kv->n; i++) {
+        const char *k = kv->keys[i];
+        const jnode *v = kv->items[i];
+        if (v->type != JN_STR) return lerr(l, "NPDS: cassandra rule value is not a string%s", NULL);
+        if (!strcmp(k, "query_action")) { free(m->cass_action); m->cass_action = v->slen ? dupn(v->str, v->slen) : NULL; }
+        else if (!strcmp(k, "query_table")) {
+            if (v->slen == 0) continue;
+            char e[256];
+            ref_re_free(m->cass_table);
+            m->cass_table = ref_re_compile(v->str, v->slen, e, sizeof e);
+            if (!m->cass_table) return lerr(l, "regexp: Compile(`%s`)", v->str);
+        } else return lerr(l, "NPDS: Unsupported key: %s", k);
+    }
+    if (m->cass_action) {
+        const int kind = cass_action_kind(m->cass_action);
+        if (kind == 0) return lerr(l, "NPDS: Unable to parse L7 cassandra rule with invalid query_action: '%s'", m->cass_action);
+        if (kind == 2 && m->cass_table)
+            return lerr(l, "NPDS: query_action '%s' is not compatible with a query_table match", m->cass_action);
+    }
+    return 0;
+}
+
 static int load_rule(ld *l, const jnode *j, ref_pnp_rule *r) {
     memset(r, 0, sizeof *r);
     const jnode *rp = jget(j, "remote_policies");
@@ -256,10 +298,12 @@ static int load_rule(ld *l, const jnode *j, ref_pnp_rule *r) {
         r->l7 = calloc((size_t)l7->n + 1, sizeof(ref_mc_rule));
         int mc = !l->mc_stop && r->l7proto && !strcmp(r->l7proto, "memcache");
         int r2 = !l->mc_stop && r->l7proto && !strcmp(r->l7proto, "r2d2");
+        int cs = !l->mc_stop && r->l7proto && !strcmp(r->l7proto, "cassandra");
         for (int i = 0; i < l7->n; i++) {
             r->l7[i].id = l->next_id++;
             if (mc && load_mc_rule(l, l7->items[i], &r->l7[i]) < 0) return -1;
             if (r2 && load_r2_rule(l, l7->items[i], &r->l7[i]) < 0) return -1;
+            if (cs && load_cass_rule(l, l7->items[i], &r->l7[i]) < 0) return -1;
         }
     }
     return 0;
@@ -321,6 +365,7 @@ static void free_ports(ref_port *ps, int n) {
             for (int q = 0; q < r->nl7; q++) {
                 free(r->l7[q].key_exact); free(r->l7[q].key_prefix); ref_re_free(r->l7[q].key_re);
                 free(r->l7[q].r2_cmd); ref_re_free(r->l7[q].r2_file);
+                free(r->l7[q].cass_action); ref_re_free(r->l7[q].cass_table);
             }
             free(r->http); free(r->kafka); free(r->l7); free(r->remotes); free(r->l7proto);
         }
@@ -406,8 +451,8 @@ int ref_px_installed(const ref_port *pp) {
             strcmp(n, "PortNetworkPolicyRule_HttpRules") &&
             strcmp(n, "PortNetworkPolicyRule_KafkaRules"))
             return 0;  /* no such parser: port skipped (:128-134, 200-203) */
-        if (!first) first = n;
-        else if (strcmp(first, n)) return 0;  /* mismatching L7 types (:135-140; the reference NACKs) */
+        (void)first;  /* mismatching L7 types NACK the whole proxylib update
+                       * (:135-143): such a version is never installed */
     }
     return 1;
 }
@@ -441,6 +486,7 @@ static void *run(void *arg) {
             else if (c->proto == L7_PROTO_KAFKA) ref_kafka_verdict(j->p, c, b, j->len[i], &o);
             else if (c->proto == L7_PROTO_MEMCACHE) ref_memcache_verdict(j->p, c, b, j->len[i], &o);
             else if (c->proto == L7_PROTO_R2D2) ref_r2d2_verdict(j->p, c, b, j->len[i], &o);
+            else if (c->proto == L7_PROTO_CASSANDRA) continue;  /* answered in order by ref_classify */
             else o.verdict = L7_UNSUPPORTED;
         }
         j->verdict[i] = o.verdict; j->rule[i] = o.rule; j->consumed[i] = o.consumed;
@@ -454,6 +500,22 @@ int ref_classify(const ref_policy *p, const ref_conn_t *conns, uint32_t nconns,
                  uint32_t *consumed, int nthreads) {
     if (nthreads < 1) nthreads = 1;
     if (nthreads > 256) nthreads = 256;
+    /* cassandra: requests in batch order, one parser state (keyspace) per
+     * connection, as proxylib's OnData walks a connection's frames */
+    ref_cass **cs = NULL;
+    for (uint32_t i = 0; i < n; i++) {
+        const uint32_t ci = conn[i];
+        if (ci >= nconns || conns[ci].proto != L7_PROTO_CASSANDRA) continue;
+        if (!cs) cs = calloc(nconns, sizeof *cs);
+        if (!cs[ci]) cs[ci] = ref_cass_new();
+        ref_out_t o = {L7_UNSUPPORTED, -1, 0};
+        ref_cassandra_verdict(cs[ci], p, &conns[ci], arena + off[i], len[i], &o);
+        verdict[i] = o.verdict; rule[i] = o.rule; consumed[i] = o.consumed;
+    }
+    if (cs) {
+        for (uint32_t k = 0; k < nconns; k++) ref_cass_free(cs[k]);
+        free(cs);
+    }
     job_t jobs[256]; pthread_t th[256];
     uint32_t per = (n + (uint32_t)nthreads - 1) / (uint32_t)nthreads;
     int used = 0;

@@ -55,7 +55,7 @@ typedef struct {
     uint32_t dst_id;    /* destination identity */
 } ref_conn_t;
 
-enum { L7_PROTO_HTTP = 1, L7_PROTO_KAFKA = 2, L7_PROTO_MEMCACHE = 3, L7_PROTO_R2D2 = 4 };
+enum { L7_PROTO_HTTP = 1, L7_PROTO_KAFKA = 2, L7_PROTO_MEMCACHE = 3, L7_PROTO_R2D2 = 4, L7_PROTO_CASSANDRA = 5 };
 
 /* verdict codes (shared meaning with the product, see include/l7gpu.h) */
 enum {
@@ -73,6 +73,25 @@ int ref_classify(const ref_policy *p, const ref_conn_t *conns, uint32_t nconns,
                  const uint8_t *arena, const uint64_t *off, const uint32_t *len,
                  const uint32_t *conn, uint32_t n, uint8_t *verdict, int32_t *rule,
                  uint32_t *consumed, int nthreads);
+
+/* proxylib cassandra parser (proxylib/cassandra/cassandraparser.go), one
+ * parser state per connection: keyspace of the last USE, prepared paths by
+ * stream id and by prepared id. */
+typedef struct ref_cass ref_cass;
+ref_cass *ref_cass_new(void);
+void ref_cass_free(ref_cass *st);
+/* Request direction, one CassandraParser.OnData step on the joined input:
+ * returns the op (0 MORE, 1 PASS, 2 DROP, 4 ERROR; -1 = a Go panic, i.e.
+ * PARSER_ERROR) and *n; *rule = matched rule id; *path (malloc'd or NULL) =
+ * the request's path; inject[*inject_len] = the reply-direction injection
+ * (unauthorized / unprepared message).  inject needs 65600 bytes. */
+int ref_cass_request(ref_cass *st, const ref_policy *pol, const ref_conn_t *c, const uint8_t *d, uint32_t n,
+                     int64_t *nout, int32_t *rule, char **path, uint8_t *inject, uint32_t *inject_len);
+/* Reply direction: framing, cassandraParseReply (prepared ids), PASS. */
+int ref_cass_reply(ref_cass *st, const uint8_t *d, uint32_t n, int64_t *nout);
+/* parseQuery test hook: 0 ok (action / table written), 1 invalid, 2 panic. */
+int ref_cass_parse_query(ref_cass *st, const uint8_t *q, size_t n, char *action, size_t alen, char *table, size_t tlen);
+const char *ref_cass_keyspace(const ref_cass *st);
 
 /* HTTP/1 framing restatement (debug/test helper): returns status and fills
  * the spans of :method, :path, :authority (offsets relative to buf, -1 = absent). */

@@ -49,6 +49,9 @@ typedef struct {  /* memcache.Rule (proxylib/memcached/parser.go:35-44) */
     /* r2d2.R2d2Rule (proxylib/r2d2/r2d2parser.go:31-34), for l7_proto "r2d2" */
     char *r2_cmd; size_t r2_cmd_len;   /* NULL = any */
     ref_re *r2_file;                   /* NULL = any */
+    /* cassandra.CassandraRule (proxylib/cassandra/cassandraparser.go:50-53) */
+    char *cass_action;                 /* query_action, NULL = any */
+    ref_re *cass_table;                /* query_table, NULL = any */
 } ref_mc_rule;
 
 enum { L7T_NONE = 0, L7T_HTTP, L7T_KAFKA, L7T_L7 };
@@ -71,6 +74,8 @@ void ref_http_verdict(const ref_policy *pol, const ref_conn_t *c, const uint8_t 
 void ref_kafka_verdict(const ref_policy *pol, const ref_conn_t *c, const uint8_t *buf, uint32_t len, ref_out_t *o);
 void ref_memcache_verdict(const ref_policy *pol, const ref_conn_t *c, const uint8_t *buf, uint32_t len, ref_out_t *o);
 void ref_r2d2_verdict(const ref_policy *pol, const ref_conn_t *c, const uint8_t *buf, uint32_t len, ref_out_t *o);
+void ref_cassandra_verdict(ref_cass *st, const ref_policy *pol, const ref_conn_t *c, const uint8_t *buf, uint32_t len,
+                           ref_out_t *o);
 const void *ref_mc_group(const char *name, size_t n);
 
 int ref_port_lookup(const ref_netpolicy *np, int ingress, uint32_t port, const ref_port **exact, const ref_port **wild);

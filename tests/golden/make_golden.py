@@ -333,6 +333,50 @@ def memcache_ops_section():
             "calls": calls}
 
 
+CASS_SELECT = bytes.fromhex(
+    "0400000407000000760000006f53454c45435420636c75737465725f6e616d652c20646174615f63656e7465722c207261636b2c"
+    "20746f6b656e732c20706172746974696f6e65722c20736368656d615f76657273696f6e2046524f4d2073797374656d2e6c6f63"
+    "616c205748455245206b65793d276c6f63616c27000100")
+CASS_OPTIONS = bytes.fromhex("040000000500000000")
+CASS_UNAUTH = bytes([0x84, 0x0, 0x0, 0x4, 0x0, 0x0, 0x0, 0x0, 0x1a, 0x0, 0x0, 0x21, 0x00, 0x0, 0x14]) + b"Request Unauthorized"
+
+
+def cassandra_section():
+    """The proxylib cassandra parser cases (proxylib/cassandra/cassandraparser_test.go:79-282):
+    policy (one port-80 rule group, remotes 1/3/4, l7_proto cassandra, one L7
+    rule), connection (ingress, src 1, dst 2, 2.2.2.2:80), OnData calls with
+    the expected ops (MORE 0 / PASS 1 / DROP 2), the reply inject buffer and
+    the access-log (passes, drops) counts where the test checks them."""
+    MORE, PASS, DROP = 0, 1, 2
+    sel = CASS_SELECT
+
+    def case(name, rule, bufs, ops, inject=b"", logs=None, ref=""):
+        return {"name": name, "policy_name": name and rule and rule[0] or "no-policy",
+                "l7_rule": rule and rule[1], "data": [b.hex() for b in bufs], "ops": ops, "inject": inject.hex(),
+                "logs": logs, "ref": "proxylib/cassandra/cassandraparser_test.go:" + ref}
+    cases = [
+        case("TestCassandraOnDataNoHeader", None, [bytes.fromhex("0400")], [[MORE, 7]], ref="79-84"),
+        case("TestCassandraOnDataOptionsReq", ("cp6", {"query_action": "select"}), [CASS_OPTIONS],
+             [[PASS, 9], [MORE, 9]], ref="86-114"),
+        case("TestCassandraOnDataPartialReq", ("cp5", {"query_table": ".*"}), [sel[:-1]], [[MORE, 1]], ref="116-143"),
+        case("TestCassandraOnDataQueryReq", ("cp4", {"query_table": ".*"}), [sel], [[PASS, len(sel)], [MORE, 9]],
+             ref="145-172"),
+        case("TestCassandraOnDataSplitQueryReq", ("cp3", {"query_table": ".*"}), [sel[:10], sel[10:]],
+             [[PASS, len(sel)], [MORE, 9]], ref="174-201"),
+        case("TestCassandraOnDataMultiReq", ("cp2", {"query_table": ".*"}), [CASS_OPTIONS, sel],
+             [[PASS, 9], [PASS, len(sel)], [MORE, 9]], ref="203-233"),
+        case("TestSimpleCassandraPolicy", ("cp1", {"query_table": "no-match"}), [CASS_OPTIONS, sel],
+             [[PASS, 9], [DROP, len(sel)], [MORE, 9]], inject=CASS_UNAUTH, logs=[0, 1], ref="235-282"),
+    ]
+    assert sel[5:9] == (0x76).to_bytes(4, "big") and sel[9:13] == (0x6f).to_bytes(4, "big") and len(sel) == 9 + 0x76
+    return {"ref": "proxylib/cassandra/cassandraparser_test.go:79-282",
+            "query": sel[13:13 + 0x6f].decode(), "path": "/query/select/system.local",
+            "connection": {"proto": "cassandra", "conn_id": 1, "ingress": True, "src_id": 1, "dst_id": 2,
+                           "src_addr": "1.1.1.1:34567", "dst_addr": "2.2.2.2:80", "remotes": [1, 3, 4], "port": 80,
+                           "policy_id": 2},
+            "cases": cases}
+
+
 def main():
     data = {
         "note": "Known-answer tests transcribed from the reference's own tests; 'expect' is the reference's asserted outcome.",
@@ -342,6 +386,7 @@ def main():
         "kafka": kafka_section(),
         "memcache": memcache_section(),
         "memcache_ops": memcache_ops_section(),
+        "cassandra": cassandra_section(),
     }
     with open(OUT, "w") as f:
         json.dump(data, f, indent=1, sort_keys=True)

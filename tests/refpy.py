@@ -40,6 +40,14 @@ def load():
         lib.ref_classify.argtypes = [vp, vp, C.c_uint32, vp, vp, vp, vp, C.c_uint32, vp, vp, vp, C.c_int]
         for f in (lib.ref_gunzip, lib.ref_unsnappy):
             f.argtypes = [cp, sz, vp, sz, C.POINTER(sz)]
+        lib.ref_cass_new.restype = vp
+        lib.ref_cass_free.argtypes = [vp]
+        lib.ref_cass_request.argtypes = [vp, vp, vp, cp, C.c_uint32, C.POINTER(C.c_int64), C.POINTER(C.c_int32),
+                                         C.POINTER(vp), vp, C.POINTER(C.c_uint32)]
+        lib.ref_cass_reply.argtypes = [vp, cp, C.c_uint32, C.POINTER(C.c_int64)]
+        lib.ref_cass_parse_query.argtypes = [vp, cp, sz, cp, sz, cp, sz]
+        lib.ref_cass_keyspace.restype = cp
+        lib.ref_cass_keyspace.argtypes = [vp]
         _lib = lib
     return _lib
 
@@ -122,3 +130,50 @@ def unsnappy(data, cap=MAX_PARSE_BUF):
 
 def classify_workload(w, nthreads=1):
     return Policy(w.policy).classify(w.conns, w.arena, w.offsets, w.lengths, w.conn_ids, nthreads)
+
+
+class Cassandra:
+    """One proxylib cassandra parser state (oracle/cassandra_ref.c): keyspace of
+    the last USE and the prepared-statement paths."""
+    PANIC = -1
+
+    def __init__(self, policy=None, conn=None):
+        self._lib = load()
+        self._h = self._lib.ref_cass_new()
+        self.policy = policy  # refpy.Policy
+        self.conn = conn      # one CONN_DTYPE record
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            self._lib.ref_cass_free(self._h)
+
+    def parse_query(self, q):
+        """(status, action, table): status 0 ok, 1 invalid, 2 panic."""
+        b = q.encode() if isinstance(q, str) else q
+        a, t = C.create_string_buffer(1 << 16), C.create_string_buffer(1 << 16)
+        rc = self._lib.ref_cass_parse_query(self._h, b, len(b), a, len(a), t, len(t))
+        return rc, a.value, t.value
+
+    @property
+    def keyspace(self):
+        return self._lib.ref_cass_keyspace(self._h)
+
+    def request(self, data):
+        """One request-direction OnData step: (op, n, rule, path, inject)."""
+        from cilium_amd.engine import conns_array
+        c = conns_array([self.conn]) if not isinstance(self.conn, np.ndarray) else self.conn
+        n, rule = C.c_int64(0), C.c_int32(0)
+        path = C.c_void_p(0)
+        inj = C.create_string_buffer(65600)
+        il = C.c_uint32(0)
+        op = self._lib.ref_cass_request(self._h, self.policy._h, c.ctypes.data, data, len(data), C.byref(n),
+                                        C.byref(rule), C.byref(path), inj, C.byref(il))
+        p = C.string_at(path.value) if path.value else None
+        if path.value:
+            C.CDLL(None).free(path)
+        return op, n.value, rule.value, p, inj.raw[:il.value]
+
+    def reply(self, data):
+        n = C.c_int64(0)
+        op = self._lib.ref_cass_reply(self._h, data, len(data), C.byref(n))
+        return op, n.value

@@ -1,0 +1,126 @@
+"""cassandra on the GPU: the cassandra kernels bit-exact against the oracle
+(random frames: every query form, keyspace USE / PREPARE in batch order,
+Unicode lower-casing, invalid UTF-8, comments, panics, short / reply /
+compressed / oversized frames, EXECUTE and BATCH, an NFA-fallback table
+regex, remote-restricted groups, the port-0 entry), alone and mixed with
+HTTP; the reference's proxylib cases (proxylib/cassandra/cassandraparser_test.go:79-282)
+through OnData; and the PREPARE -> RESULT -> EXECUTE flow and the access log
+against the oracle's parser state."""
+import numpy as np
+import pytest
+
+from cilium_amd import api, gen
+from cilium_amd import proxylib as P
+from test_gpu_http import assert_same, wl_from_reqs
+
+pytestmark = pytest.mark.gpu
+
+
+def test_cassandra_parity(engine, oracle):
+    w = gen.cassandra_workload(30000)
+    engine.update_policy(w.policy)
+    engine.set_connections(w.conns)
+    got = engine.classify(w.arena, w.offsets, w.lengths, w.conn_ids)
+    assert_same(got, oracle.classify_workload(w, 8), w)
+    assert len(set(got[1].tolist())) >= 8  # many rules, incl. the NFA one and port 0, allow something
+
+
+def test_cassandra_one_connection_keyspace_order(engine, oracle):
+    """All requests on one connection: every request's keyspace is the last USE
+    before it in the batch."""
+    w = gen.cassandra_workload(4000, nconns=1, seed=5)
+    engine.update_policy(w.policy)
+    engine.set_connections(w.conns)
+    got = engine.classify(w.arena, w.offsets, w.lengths, w.conn_ids)
+    assert_same(got, oracle.classify_workload(w, 1), w)
+
+
+def test_cassandra_mixed_with_http(engine, oracle):
+    r = gen.cassandra_workload(3000, nconns=16)
+    h = gen.http_workload(2, 3000, nconns=16)
+    pol = {"policies": r.policy["policies"] + [dict(h.policy["policies"][0], name="http")]}
+    conns = np.concatenate([r.conns, h.conns])
+    conns["policy"][16:] = 1
+    reqs = [bytes(r.arena[int(o):int(o) + int(n)]) for o, n in zip(r.offsets, r.lengths)] + \
+           [bytes(h.arena[int(o):int(o) + int(n)]) for o, n in zip(h.offsets, h.lengths)]
+    ids = np.concatenate([r.conn_ids, h.conn_ids + 16])
+    perm = np.random.default_rng(3).permutation(len(reqs))
+    w = wl_from_reqs([reqs[i] for i in perm], pol, conns, ids[perm])
+    engine.update_policy(w.policy)
+    engine.set_connections(w.conns)
+    got = engine.classify(w.arena, w.offsets, w.lengths, w.conn_ids)
+    assert_same(got, oracle.classify_workload(w, 8), w)
+
+
+def _kat_policy(name, rule):
+    return api.policy_set(api.network_policy(name, 2, ingress=[
+        (80, [api.port_rule(remote_policies=[1, 3, 4], l7proto="cassandra", l7=[rule])])]))
+
+
+def test_reference_op_sequences(kats):
+    K = kats["cassandra"]
+    mid = P.open_module([("node-id", "host~127.0.0.1~cassandra~localdomain")])
+    try:
+        for i, c in enumerate(K["cases"]):
+            if c["l7_rule"]:
+                P.policy_update(mid, _kat_policy(c["policy_name"], c["l7_rule"]))
+            conn = P.Connection(mid, "cassandra", 100 + i, True, 1, 2, "1.1.1.1:34567", "2.2.2.2:80",
+                                c["policy_name"], 1024)
+            assert conn.result == P.OK
+            res, ops = conn.on_data(False, [bytes.fromhex(b) for b in c["data"]], 8)
+            assert res == P.OK, c["name"]
+            assert [list(o) for o in ops] == c["ops"], (c["name"], ops)
+            assert conn.take_inject(True) == bytes.fromhex(c["inject"]), c["name"]
+            conn.close()
+    finally:
+        P.close_module(mid)
+
+
+def test_prepare_result_execute_flow(oracle):
+    """USE, PREPARE, the RESULT/prepared reply and EXECUTE through OnData, step
+    for step against the oracle's parser (op, length, injected bytes)."""
+    pol = gen.cassandra_policy()
+    mid = P.open_module([("node-id", "host~127.0.0.1~cassandra2~localdomain")])
+    try:
+        P.policy_update(mid, pol)
+        conn = P.Connection(mid, "cassandra", 777, True, 100, 2, "1.1.1.1:1", "2.2.2.2:%d" % gen.CASS_PORT, "cs", 4096)
+        assert conn.result == P.OK
+        ref = oracle.Cassandra(oracle.Policy(pol), gen.make_conns(1, 0, gen.CASS_PORT, True, 5, [100]))
+        q = gen.cass_query_frame
+        steps = [
+            (False, [q("select * from users", stream=1), q("use ks1", stream=2), q("select * from t", stream=3)]),
+            (False, [q("select * from t", 0x09, stream=9)]),                      # PREPARE under ks1
+            (False, [gen.cass_frame(0x0A, b"\x00\x02ab\x00\x00", stream=4)]),      # EXECUTE: not yet bound
+            (True, [bytes([0x84, 0, 0, 9, 8]) + (10).to_bytes(4, "big") + (4).to_bytes(4, "big") + b"\x00\x02ab\x00\x00"]),
+            (False, [q("use ks2", stream=5), gen.cass_frame(0x0A, b"\x00\x02ab\x00\x00", stream=6),
+                     q("select * from t", stream=7)]),                             # EXECUTE keeps ks1
+            (False, [q("insert into users x", stream=8), gen.cass_frame(0x05, b"")]),
+            (False, [gen.cass_frame(0x0D, b"\x00\x00\x01")]),                      # BATCH: PARSER_ERROR
+        ]
+        for reply, frames in steps:
+            res, ops = conn.on_data(reply, frames, 16)
+            # connection.go:138-172: an ERROR op does not advance or stop the
+            # loop, so it repeats until the ops slice is full
+            want, data, inj = [], b"".join(frames), b""
+            want_res = P.OK
+            while len(want) < 16:
+                if reply:
+                    op, n = ref.reply(data)
+                else:
+                    op, n, rule, path, i2 = ref.request(data)
+                    inj += i2
+                if op == -1:
+                    want_res = P.PARSER_ERROR
+                    break
+                want.append((op, n))
+                if op == P.MORE:
+                    break
+                if op in (P.PASS, P.DROP):
+                    data = data[n:]
+            assert res == want_res, (frames, res, ops)
+            if res == P.OK:
+                assert ops == want, (frames, ops, want)
+                assert conn.take_inject(True) == inj
+        conn.close()
+    finally:
+        P.close_module(mid)
