@@ -32,7 +32,14 @@ Besides the device-resident rate (`value`) the line reports:
   * e2e        -- pinned host arena -> H2D -> classify -> D2H, the unique
                   shard in 8 chunks on 2 streams (PCIe-inclusive; never `value`);
   * cpu_baseline -- the oracle (C restatement) on the host: all cores the
-                  process may use, and one core, with nproc and the CPU model.
+                  process may use, and one core, with nproc and the CPU model;
+  * latency    -- per-request latency of the drop-in paths (p50/p90/p99 us):
+                  one request per l7g_classify_host call (the Envoy adapter's
+                  Allowed()), requests through the asynchronous batcher
+                  (l7g_batcher, 8 submitting threads at a fixed offered rate)
+                  and proxylib OnData with one memcached request per call
+                  (tests/native/latency_main.cc), next to the oracle deciding
+                  one request per call on one core.
 
 Usage:  python bench.py [--gpus N --steps K --warmup W --workload cfgX]
         (N > 1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
@@ -182,6 +189,48 @@ def e2e_pipeline(torch, eng, w, dev, nchunks=8, reps=3):
     return float(np.median(ts)), moved, (h_v.numpy().copy(), h_r.numpy().copy(), h_c.numpy().view(np.uint32).copy())
 
 
+def latency_leg(gen, refpy, iters=2000):
+    """Drop-in path latency (rank 0, N = 1): tests/native/bin/latency_main on
+    cfg2's HTTP requests and memcached text requests, and the oracle deciding
+    the same requests one call at a time on one core."""
+    import subprocess
+    exe = os.path.join(ROOT, "tests", "native", "bin", "latency_main")
+    if not os.path.exists(exe):
+        return {"error": "tests/native/bin/latency_main not built"}
+    h = gen.http_workload(2, 512)
+    mreqs = [r for r in gen.memcache_requests(4000, 5) if r[0] < 0x80 and r.endswith(b"\r\n")][:512]
+    mcp = gen.mc_policy()
+    pol = {"policies": h.policy["policies"] + [dict(mcp["policies"][0], name="mc-lat")]}
+    c0 = h.conns[0]
+    hreqs = [bytes(h.arena[int(o):int(o) + int(n)]) for o, n in zip(h.offsets, h.lengths)]
+    lines = [json.dumps(pol), f"{int(c0['policy'])} {int(c0['port'])} {int(c0['ingress'])} {int(c0['src_id'])} "
+                              f"{int(c0['dst_id'])}", f"mc mc-lat {gen.MC_PORT} 3005"]
+    lines += [r.hex() for r in hreqs] + ["--"] + [r.hex() for r in mreqs]
+    try:
+        r = subprocess.run([exe, str(iters)], input="\n".join(lines) + "\n", capture_output=True, text=True,
+                           timeout=180)
+        out = json.loads(r.stdout) if r.returncode == 0 else {"error": f"rc {r.returncode}: {r.stderr[-300:]}"}
+    except Exception as e:  # the latency leg never fails the bench line
+        out = {"error": repr(e)}
+    # the oracle, one request per call, one core (ctypes call overhead included)
+    P = refpy.Policy(pol)
+    conns = np.concatenate([h.conns[:1], gen.make_conns(1, 1, gen.MC_PORT, True, gen.PROTO_MEMCACHE, [3005])])
+    conns["flags"][1] = 1
+
+    def one_by_one(reqs, cid):
+        ts = []
+        for q in reqs * max(1, iters // len(reqs)):
+            a = np.frombuffer(q, np.uint8)
+            t0 = time.perf_counter()
+            P.classify(conns, a, np.zeros(1, np.uint64), np.array([len(q)], np.uint32), np.array([cid], np.uint32), 1)
+            ts.append((time.perf_counter() - t0) * 1e6)
+        ts.sort()
+        return {"n": len(ts), "p50_us": ts[len(ts) // 2], "p99_us": ts[int(0.99 * (len(ts) - 1))]}
+    out["oracle_one_core"] = {"http": one_by_one(hreqs, 0), "memcached": one_by_one(mreqs, 1),
+                              "note": "refpy.Policy.classify with n=1 per call (ctypes overhead included)"}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -192,6 +241,7 @@ def main():
     ap.add_argument("--unique", type=int, default=0, help="unique requests generated (tiled up to --requests)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--no-latency", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0, help="oracle threads (0 = every usable core)")
     ap.add_argument("--profile-steps", type=int, default=3, help="extra steps with per-kernel HIP events")
     args = ap.parse_args()
@@ -358,6 +408,10 @@ def main():
                "nproc": cinfo["nproc"], "usable_cores": cinfo["usable_cores"], "affinity_cores": cinfo["affinity_cores"],
                "cgroup_cpu_quota": cinfo["cgroup_cpu_quota"], "cpu_model": cinfo["model"]}
 
+    latency = None
+    if rank == 0 and world == 1 and not args.no_latency:
+        latency = latency_leg(gen, refpy)
+
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
@@ -425,6 +479,11 @@ def main():
                           "note": "all kernels of one l7g_classify call, one HIP event pair on the stream"},
         "kernels": kernels,
         "cpu_baseline": cpu,
+        "algorithmic_bytes_note": "per request len_i + 16 + 9 (SURVEY §8(d)); memcached counts only the bytes its "
+                                  "parser must inspect (the command line, or the 24-byte header + extras + key; a "
+                                  "storage command's data block is framed by length and never read), which lowers "
+                                  "its frac against the len_i + 25 definition",
+        "latency": latency,
         "e2e": None if e2e is None else {
             "verdicts_per_s": round(e2e["requests"] / e2e["s"], 1), "ms_per_pass": round(e2e["s"] * 1e3, 3),
             "requests_per_pass": e2e["requests"], "pcie_gbps": round(e2e["bytes"] / e2e["s"] / 1e9, 2),

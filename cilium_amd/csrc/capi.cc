@@ -88,14 +88,21 @@ constexpr size_t kMaxStreamScratch = 16;  // beyond: the least recently used one
 // l7g_classify_host's per-thread staging: its own stream, device arena and
 // request arrays (grow-only), so host-buffer calls from different threads
 // overlap instead of queueing on one stream.
+// Inputs go over as ONE copy from a pinned staging buffer ([off u64 | len u32 |
+// conn u32 | arena], packed by the host) and outputs come back as ONE copy
+// ([verdict u8 | rule i32 | consumed u32]): a one-request call is two DMA
+// transfers, not seven pageable ones.
 struct HostCtx {
     hipStream_t s = nullptr;
-    uint8_t *arena = nullptr, *req = nullptr;
-    size_t arena_cap = 0, n_cap = 0;
+    uint8_t *dev = nullptr;        // device: [inputs | outputs]
+    uint8_t *pin_in = nullptr;     // pinned host staging of the inputs
+    uint8_t *pin_out = nullptr;    // pinned host staging of the outputs
+    size_t in_cap = 0, out_cap = 0;
     ~HostCtx() {
         if (s) hipStreamSynchronize(s);
-        if (arena) hipFree(arena);
-        if (req) hipFree(req);
+        if (dev) hipFree(dev);
+        if (pin_in) hipHostFree(pin_in);
+        if (pin_out) hipHostFree(pin_out);
         if (s) hipStreamDestroy(s);
     }
 };
@@ -705,41 +712,53 @@ int l7g_classify_host(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, c
         }
         H = slot.get();
     }
-    // grow-only device staging: arena (+64 B so aligned 16-byte reads stay inside) and per-request arrays
-    // (the previous call of this thread has synchronised its stream, so nothing still reads them)
-    const size_t need_a = arena_len + 64, need_n = std::max<uint32_t>(n, 1);
-    if (need_a > H->arena_cap) {
-        if (H->arena) hipFree(H->arena);
-        H->arena = nullptr;
-        H->arena_cap = 0;
-        size_t cap = std::max<size_t>(need_a, 1 << 16);
-        if ((rc = hipMalloc(&H->arena, cap)) != hipSuccess) return (int)rc;
-        H->arena_cap = cap;
+    // grow-only staging: inputs [off | len | conn | arena (+64 B so aligned
+    // 16-byte reads stay inside)], outputs [verdict | rule | consumed]
+    const size_t nn = std::max<uint32_t>(n, 1);
+    const size_t a_off = (nn * 16 + 255) & ~(size_t)255;
+    const size_t need_in = a_off + arena_len + 64;
+    const size_t need_out = nn * 9 + 64;
+    if (need_in > H->in_cap || need_out > H->out_cap) {
+        if (H->dev) hipFree(H->dev);
+        if (H->pin_in) hipHostFree(H->pin_in);
+        if (H->pin_out) hipHostFree(H->pin_out);
+        H->dev = H->pin_in = H->pin_out = nullptr;
+        H->in_cap = std::max(need_in, (size_t)1 << 16);
+        H->out_cap = std::max(need_out, (size_t)1 << 14);
+        if ((rc = hipMalloc(&H->dev, H->in_cap + H->out_cap)) != hipSuccess) { H->in_cap = H->out_cap = 0; return (int)rc; }
+        if ((rc = hipHostMalloc(&H->pin_in, H->in_cap, hipHostMallocDefault)) != hipSuccess ||
+            (rc = hipHostMalloc(&H->pin_out, H->out_cap, hipHostMallocDefault)) != hipSuccess) {
+            H->in_cap = H->out_cap = 0;
+            return (int)rc;
+        }
     }
-    if (need_n > H->n_cap) {
-        if (H->req) hipFree(H->req);
-        H->req = nullptr;
-        H->n_cap = 0;
-        size_t cap = std::max<size_t>(need_n, 1024);
-        if ((rc = hipMalloc(&H->req, cap * 25)) != hipSuccess) return (int)rc;
-        H->n_cap = cap;
+    // (the previous call of this thread synchronised its stream: the staging is free)
+    uint8_t *pi = H->pin_in;
+    if (n) {
+        memcpy(pi, off, (size_t)n * 8);
+        memcpy(pi + nn * 8, len, (size_t)n * 4);
+        memcpy(pi + nn * 12, conn, (size_t)n * 4);
     }
-    uint8_t *base = H->req;
-    const size_t cap = H->n_cap;
-    uint64_t *d_o = (uint64_t *)base;
-    uint32_t *d_l = (uint32_t *)(base + cap * 8), *d_c = (uint32_t *)(base + cap * 12), *d_cons = (uint32_t *)(base + cap * 16);
-    int32_t *d_r = (int32_t *)(base + cap * 20);
-    uint8_t *d_v = base + cap * 24;
+    if (arena_len) memcpy(pi + a_off, arena, arena_len);
+    uint8_t *d_in = H->dev, *d_out = H->dev + H->in_cap;
+    const uint64_t *d_o = (const uint64_t *)d_in;
+    const uint32_t *d_l = (const uint32_t *)(d_in + nn * 8), *d_c = (const uint32_t *)(d_in + nn * 12);
+    uint8_t *d_v = d_out;
+    int32_t *d_r = (int32_t *)(d_out + ((nn + 3) & ~(size_t)3));
+    uint32_t *d_cons = (uint32_t *)(d_out + ((nn + 3) & ~(size_t)3) + nn * 4);
     hipStream_t s = H->s;
-    if (arena_len) rc = hipMemcpyAsync(H->arena, arena, arena_len, hipMemcpyHostToDevice, s);
-    if (rc == hipSuccess && n) rc = hipMemcpyAsync(d_o, off, n * 8, hipMemcpyHostToDevice, s);
-    if (rc == hipSuccess && n) rc = hipMemcpyAsync(d_l, len, n * 4, hipMemcpyHostToDevice, s);
-    if (rc == hipSuccess && n) rc = hipMemcpyAsync(d_c, conn, n * 4, hipMemcpyHostToDevice, s);
-    if (rc == hipSuccess) rc = (hipError_t)l7g_classify(e, H->arena, arena_len, d_o, d_l, d_c, n, d_v, d_r, d_cons, nullptr, s);
-    if (rc == hipSuccess && n) rc = hipMemcpyAsync(verdict, d_v, n, hipMemcpyDeviceToHost, s);
-    if (rc == hipSuccess && n) rc = hipMemcpyAsync(rule, d_r, n * 4, hipMemcpyDeviceToHost, s);
-    if (rc == hipSuccess && n) rc = hipMemcpyAsync(consumed, d_cons, n * 4, hipMemcpyDeviceToHost, s);
+    rc = hipMemcpyAsync(d_in, pi, a_off + arena_len, hipMemcpyHostToDevice, s);
+    if (rc == hipSuccess)
+        rc = (hipError_t)l7g_classify(e, d_in + a_off, arena_len, d_o, d_l, d_c, n, d_v, d_r, d_cons, nullptr, s);
+    const size_t out_bytes = ((nn + 3) & ~(size_t)3) + nn * 8;
+    if (rc == hipSuccess && n) rc = hipMemcpyAsync(H->pin_out, d_out, out_bytes, hipMemcpyDeviceToHost, s);
     if (rc == hipSuccess) rc = hipStreamSynchronize(s);
+    if (rc == hipSuccess && n) {
+        const uint8_t *po = H->pin_out;
+        memcpy(verdict, po, n);
+        memcpy(rule, po + ((nn + 3) & ~(size_t)3), (size_t)n * 4);
+        memcpy(consumed, po + ((nn + 3) & ~(size_t)3) + nn * 4, (size_t)n * 4);
+    }
     return (int)rc;
 }
 

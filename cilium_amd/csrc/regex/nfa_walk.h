@@ -11,6 +11,12 @@
 
 #include "../device_tables.h"
 
+#if defined(__HIPCC__)
+#define L7_NFA_INL __host__ __device__ __forceinline__
+#else
+#define L7_NFA_INL inline
+#endif
+
 namespace l7 {
 
 // empty-width condition bits (the C_* of re_dfa.cc) and previous-byte context
@@ -56,22 +62,25 @@ L7_HD inline uint32_t nfa_decode(const uint8_t *s, uint32_t i, uint32_t n, uint3
     return r;
 }
 
-// Streaming walk: nfa_begin, one nfa_step per rune (r, and c = the first
-// byte of its encoding, which the empty-width conditions look at), nfa_end.
+// Streaming walk (for text the caller produces rune by rune, e.g. the
+// lowered cassandra table name): nfa_begin, one nfa_step per rune (r, and c =
+// the first byte of its encoding, which the empty-width conditions look at),
+// nfa_end.  Same step as nfa_run below, which keeps its own loop so its state
+// stays in registers in the pre-pass kernels.
 struct NfaRun {
     uint64_t S[kNfaMaxWords];
     uint32_t prev;
     bool dead;
 };
 
-L7_HD inline void nfa_begin(NfaRun &R) {
+L7_NFA_INL void nfa_begin(NfaRun &R) {
 #pragma unroll
     for (int w = 0; w < kNfaMaxWords; w++) R.S[w] = w == 0 ? 1 : 0;  // the virtual start position
     R.prev = NP_START;
     R.dead = false;
 }
 
-L7_HD inline void nfa_step(const uint8_t *pool, uint64_t off, NfaRun &R, uint32_t r, uint32_t c) {
+L7_NFA_INL void nfa_step(const uint8_t *pool, uint64_t off, NfaRun &R, uint32_t r, uint32_t c) {
     if (R.dead) return;
     const DevNfa *d = (const DevNfa *)(pool + off);
     const uint32_t W = d->W, nivl = d->nivl;
@@ -120,7 +129,7 @@ L7_HD inline void nfa_step(const uint8_t *pool, uint64_t off, NfaRun &R, uint32_
     R.prev = (r == '\n' ? NP_NL : 0u) | (r < 128 && nfa_word_byte(r) ? NP_WORD : 0u);
 }
 
-L7_HD inline bool nfa_end(const uint8_t *pool, uint64_t off, const NfaRun &R) {
+L7_NFA_INL bool nfa_end(const uint8_t *pool, uint64_t off, const NfaRun &R) {
     if (R.dead) return false;
     const DevNfa *d = (const DevNfa *)(pool + off);
     const uint32_t W = d->W;
@@ -135,15 +144,68 @@ L7_HD inline bool nfa_end(const uint8_t *pool, uint64_t off, const NfaRun &R) {
 
 // Run the NFA at pool + off over s[0, n); true = accepted.
 L7_HD inline bool nfa_run(const uint8_t *pool, uint64_t off, const uint8_t *s, uint32_t n) {
-    NfaRun R;
-    nfa_begin(R);
-    for (uint32_t i = 0; i < n && !R.dead;) {
+    const DevNfa *d = (const DevNfa *)(pool + off);
+    const uint32_t W = d->W, nivl = d->nivl;
+    const uint64_t *T = (const uint64_t *)(pool + d->t_off);
+    const uint32_t *ivl = (const uint32_t *)(pool + d->ivl_off);
+    const uint64_t *B = (const uint64_t *)(pool + d->b_off);
+    const uint16_t *ascii = (const uint16_t *)(pool + d->ascii_off);
+    const uint64_t *Acc = (const uint64_t *)(pool + d->acc_off);
+    uint64_t S[kNfaMaxWords];
+#pragma unroll
+    for (int w = 0; w < kNfaMaxWords; w++) S[w] = w == 0 ? 1 : 0;  // the virtual start position
+    uint32_t prev = NP_START;
+    for (uint32_t i = 0; i < n;) {
+        const uint32_t c = s[i];
         uint32_t width;
         const uint32_t r = nfa_decode(s, i, n, &width);
-        nfa_step(pool, off, R, r, s[i]);
+        const uint32_t k = d->condmap[nfa_cond(prev, (int)c)];
+        uint32_t iv;
+        if (r < 128) {
+            iv = ascii[r];
+        } else {  // last interval starting at or below r
+            uint32_t lo = 0, hi = nivl;
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (ivl[mid] <= r) lo = mid;
+                else hi = mid;
+            }
+            iv = lo;
+        }
+        uint64_t N[kNfaMaxWords];
+#pragma unroll
+        for (int u = 0; u < kNfaMaxWords; u++) N[u] = 0;
+#pragma unroll
+        for (int w = 0; w < kNfaMaxWords; w++) {
+            if ((uint32_t)w >= W) break;
+            uint64_t x = S[w];
+            while (x) {
+                const uint32_t j = (uint32_t)__builtin_ctzll(x) >> 3;
+                const uint32_t v = (uint32_t)(x >> (8 * j)) & 0xFF;
+                x &= ~(0xFFull << (8 * j));
+                const uint64_t *row = T + (((uint64_t)k * 8 * W + 8 * (uint32_t)w + j) * 256 + v) * W;
+#pragma unroll
+                for (int u = 0; u < kNfaMaxWords; u++)
+                    if ((uint32_t)u < W) N[u] |= row[u];
+            }
+        }
+        uint64_t any = 0;
+#pragma unroll
+        for (int u = 0; u < kNfaMaxWords; u++) {
+            if ((uint32_t)u < W) N[u] &= B[(uint64_t)iv * W + u];
+            S[u] = N[u];
+            any |= N[u];
+        }
+        if (!any) return false;
+        prev = (r == '\n' ? NP_NL : 0u) | (r < 128 && nfa_word_byte(r) ? NP_WORD : 0u);
         i += width;
     }
-    return nfa_end(pool, off, R);
+    const uint32_t k = d->condmap[nfa_cond(prev, -1)];
+    uint64_t hit = 0;
+#pragma unroll
+    for (int u = 0; u < kNfaMaxWords; u++)
+        if ((uint32_t)u < W) hit |= S[u] & Acc[(uint64_t)k * W + u];
+    return hit != 0;
 }
 
 }  // namespace l7

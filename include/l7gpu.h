@@ -149,6 +149,28 @@ int l7g_classify_host(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, c
 
 int l7g_stats(l7g_engine *e, l7g_stats_t *out);
 
+/* Asynchronous batching for callers that decide one request at a time on an
+ * event loop -- Envoy's cilium.l7policy decodeHeaders
+ * (envoy/cilium_l7policy.cc:127-182), which would return StopIteration and
+ * resume (continueDecoding / sendLocalReply) from the callback.  Submitted
+ * requests are copied into the batcher's arena; a flusher thread classifies
+ * them in one l7g_classify_host launch once max_requests are pending or the
+ * oldest has waited max_wait_us, then calls each request's callback (from the
+ * flusher thread, in submission order).  A device failure answers every
+ * request of that flush L7G_UNSUPPORTED. */
+typedef void (*l7g_done_fn)(void *ctx, uint8_t verdict, int32_t rule, uint32_t consumed);
+typedef struct l7g_batcher l7g_batcher;
+l7g_batcher *l7g_batcher_create(l7g_engine *e, uint32_t max_requests, uint32_t max_wait_us);
+/* 0 = queued; -1 = the batcher is shutting down (callback not called). */
+int l7g_batcher_submit(l7g_batcher *b, const uint8_t *req, uint32_t len, uint32_t conn, l7g_done_fn done, void *ctx);
+/* Flushes now and returns once every request submitted before the call has
+ * had its callback. */
+int l7g_batcher_flush(l7g_batcher *b);
+/* Flushes what is pending, then stops the flusher thread. */
+void l7g_batcher_destroy(l7g_batcher *b);
+/* Requests classified and launches made so far (for latency accounting). */
+void l7g_batcher_stats(l7g_batcher *b, uint64_t *requests, uint64_t *launches);
+
 /* Measurement hook (bench.py): with profiling on, l7g_classify records HIP
  * events on its stream around each kernel it launches; l7g_profile_last waits
  * for the last call and returns the device time in ms of its four stages

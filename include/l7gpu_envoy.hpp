@@ -11,12 +11,17 @@
 //     headers, as Envoy's HeaderMap holds them) are written back as an
 //     HTTP/1.1 request head, which the device frames and classifies -- the
 //     same bytes Envoy's codec parsed them from;
-//   * AllowedBatch classifies any number of requests in one l7g_classify_host.
+//   * AllowedBatch classifies any number of requests in one l7g_classify_host;
+//   * AllowedAsync queues one request on an l7g_batcher and calls back with
+//     the verdict once the batcher's launch (shared with every other
+//     worker's requests) completes: decodeHeaders returns StopIteration and
+//     the callback resumes the stream (continueDecoding) or sends the 403.
 // Remote identity: the source on ingress, the destination on egress
 // (cilium_l7policy.cc:144-150), which the engine applies to the registered
 // connection's src_id / dst_id.
 #pragma once
 #include <cstdint>
+#include <functional>
 #include <map>
 #include <mutex>
 #include <stdexcept>
@@ -76,6 +81,24 @@ public:
         if (rules) *rules = r;
     }
 
+    // Asynchronous form: done(allowed, rule) runs on the batcher's flusher
+    // thread once the request's launch has completed.
+    void AllowedAsync(l7g_batcher *b, const std::string &policy_name, bool ingress, uint32_t port,
+                      uint64_t remote_id, const Headers &headers, std::function<void(bool, int32_t)> done) {
+        std::vector<uint8_t> head;
+        Head(headers, &head);
+        uint32_t slot;
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            slot = Slot(AllowedRequest{policy_name, ingress, port, remote_id, &headers});
+        }
+        auto *cb = new std::function<void(bool, int32_t)>(std::move(done));
+        if (l7g_batcher_submit(b, head.data(), (uint32_t)head.size(), slot, &Trampoline, cb) != 0) {
+            delete cb;
+            throw std::runtime_error("l7g_batcher_submit: batcher is shutting down");
+        }
+    }
+
     // A policy update may renumber policies: forget the resolved connections.
     void PolicyUpdated() {
         std::lock_guard<std::mutex> g(mu_);
@@ -86,6 +109,12 @@ private:
     l7g_engine *e_;
     std::mutex mu_;
     std::map<std::tuple<std::string, bool, uint32_t, uint64_t>, uint32_t> slots_;
+
+    static void Trampoline(void *ctx, uint8_t verdict, int32_t rule, uint32_t) {
+        auto *cb = (std::function<void(bool, int32_t)> *)ctx;
+        (*cb)(verdict == L7G_ALLOW, verdict == L7G_ALLOW ? rule : -1);
+        delete cb;
+    }
 
     uint32_t Slot(const AllowedRequest &q) {
         auto key = std::make_tuple(q.policy_name, q.ingress, q.port, q.remote_id);

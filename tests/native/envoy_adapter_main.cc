@@ -2,9 +2,13 @@
 // on the GPU box).  stdin: the policy JSON on the first line, then one request
 // per line: policy_name \t ingress \t port \t remote_id \t name=value \t ...
 // stdout: per request "<allowed> <rule>" (the batch form), then a second pass
-// through the single-request Allowed() for the first 8 requests.
+// through the single-request Allowed() for the first 8 requests, then every
+// request through AllowedAsync on an l7g_batcher (4 submitting threads,
+// flush at 8 requests or 200 us), "<allowed> <rule>" in request order.
+#include <atomic>
 #include <iostream>
 #include <sstream>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -44,6 +48,25 @@ int main() {
     for (size_t i = 0; i < rq.size(); i++) std::cout << (int)v[i] << " " << r[i] << "\n";
     for (size_t i = 0; i < rq.size() && i < 8; i++)
         std::cout << (int)m.Allowed(rq[i].policy_name, rq[i].ingress, rq[i].port, rq[i].remote_id, hs[i]) << "\n";
+    // asynchronous: four "worker threads" submit interleaved requests
+    l7g_batcher *b = l7g_batcher_create(e, 8, 200);
+    std::vector<int> av(rq.size(), -9), ar(rq.size(), -9);
+    std::atomic<size_t> got{0};
+    std::vector<std::thread> ws;
+    for (int t = 0; t < 4; t++)
+        ws.emplace_back([&, t] {
+            for (size_t i = (size_t)t; i < rq.size(); i += 4)
+                m.AllowedAsync(b, rq[i].policy_name, rq[i].ingress, rq[i].port, rq[i].remote_id, hs[i],
+                               [&, i](bool ok, int32_t rule) { av[i] = ok; ar[i] = rule; got++; });
+        });
+    for (auto &w : ws) w.join();
+    l7g_batcher_flush(b);
+    uint64_t nreq = 0, nl = 0;
+    l7g_batcher_stats(b, &nreq, &nl);
+    l7g_batcher_destroy(b);
+    if (got != rq.size()) { std::cerr << "async: " << got << " of " << rq.size() << " callbacks\n"; return 4; }
+    for (size_t i = 0; i < rq.size(); i++) std::cout << av[i] << " " << ar[i] << "\n";
+    std::cerr << "async: " << nreq << " requests in " << nl << " launches\n";
     l7g_engine_destroy(e);
     return 0;
 }

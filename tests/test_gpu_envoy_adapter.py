@@ -2,7 +2,8 @@
 shape over the batch C-ABI, driven by tests/native/envoy_adapter_main.cc on the
 GPU.  The 19 Envoy integration verdicts (envoy/cilium_integration_test.cc,
 tests/golden/reference_kats.json) come back through Allowed() from decoded
-headers, and the batched form agrees with the oracle's rule ids."""
+headers, through AllowedAsync on the asynchronous batcher (l7g_batcher, four
+submitting threads), and the batched form agrees with the oracle's rule ids."""
 import json
 import os
 import re
@@ -47,9 +48,12 @@ def test_envoy_kats_through_allowed(kats, oracle):
     n = len(h["cases"])
     batch = [tuple(int(x) for x in ln.split()) for ln in out[:n]]
     single = [int(x) for x in out[n:n + min(n, 8)]]
+    k = n + min(n, 8)
+    asyn = [tuple(int(x) for x in ln.split()) for ln in out[k:k + n]]
     want = [1 if case["expect"] == "ALLOW" else 0 for case in h["cases"]]
     assert [b[0] for b in batch] == want
     assert single == want[:len(single)]
+    assert asyn == batch  # the batcher's verdicts and rule ids equal the synchronous batch
     # rule ids as the oracle resolves them for the same requests
     names = [p["name"] for p in h["policy"]["policies"]]
     conns = [{"policy": names.index(c["conn"]["policy_name"]) if c["conn"]["policy_name"] in names else -1,

@@ -1,6 +1,7 @@
 """Proxy statistics (l7g_flow_stats) on the GPU: per (policy, proto, port,
-direction) received / forwarded / denied / error counts equal the outputs'
-aggregation, accumulate across calls and reset."""
+direction) received / forwarded / denied / error counts equal the aggregation
+of the ORACLE's verdicts for the same stream (pkg/endpoint/endpoint.go:2207-2233
+UpdateProxyStatistics), accumulate across calls and reset."""
 import collections
 
 import numpy as np
@@ -18,7 +19,7 @@ def expected(w, v):
         if x > PARSE_ERROR or cid >= len(w.conns):
             continue
         c = w.conns[cid]
-        if c["proto"] not in (1, 2, 3):
+        if c["proto"] not in (1, 2, 3, 4, 5):
             continue
         k = (int(c["policy"]), int(c["proto"]), int(c["port"]), int(c["ingress"]))
         e = out[k]
@@ -27,15 +28,15 @@ def expected(w, v):
     return {k: tuple(v) for k, v in out.items()}
 
 
-def test_flow_stats_mixed(engine):
+def test_flow_stats_mixed(engine, oracle):
     w = gen.mixed_workload(60000)
     engine.update_policy(w.policy)
     engine.set_connections(w.conns)
     engine.flow_stats_enable(True)
     try:
         engine.flow_stats(reset=True)
-        v, _, _ = engine.classify(w.arena, w.offsets, w.lengths, w.conn_ids)
-        want = expected(w, v)
+        engine.classify(w.arena, w.offsets, w.lengths, w.conn_ids)
+        want = expected(w, oracle.classify_workload(w, 8)[0])
         assert engine.flow_stats() == want
         assert len({k[1] for k in want}) == 3  # every protocol has flows
         engine.classify(w.arena, w.offsets, w.lengths, w.conn_ids)
