@@ -124,9 +124,31 @@ struct ImgHeader {         // 80 B, at offset 0 of every image
     uint16_t name_states;
     uint32_t nfa_off;      // DevNfaRef[nnfa]
     uint8_t nnfa;
-    uint8_t pad2[11];
+    uint8_t ntab_bits;     // name table: 2^ntab_bits DevNameEnt (0: none)
+    uint8_t pad2[2];
+    uint32_t ntab_off;     // DevNameEnt[1 << ntab_bits]
+    uint32_t ntab_mul;     // multiplier of l7_name_hash, chosen so the names do not collide
 };
 static_assert(sizeof(ImgHeader) == 80, "ImgHeader layout");
+
+// Header-name table (the framer's one-probe shortcut for the name DFA): the
+// names of the name DFA that are at most 15 bytes of [0-9a-z-], lower-cased
+// and zero-padded, each in its own slot (a collision-free multiplier is
+// searched at compile time).  A header name of <= 15 bytes of [0-9A-Za-z-]
+// has NI_* flags info iff its lower-cased bytes equal the slot's name, else 0:
+// exactly name_info of the DFA state the name walks to.
+struct DevNameEnt {        // 32 B
+    uint32_t w[4];         // lower-cased name bytes, zero past len
+    uint8_t len;           // 0: empty slot
+    uint8_t info;          // NI_* flags
+    uint8_t pad[10];
+};
+L7_HD inline uint32_t l7_name_hash(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t len, uint32_t mul,
+                                   uint32_t bits) {
+    uint32_t x = w0 ^ (w1 * 0x85EBCA6Bu) ^ (w2 * 0xC2B2AE35u) ^ (w3 * 0x27D4EB2Fu) ^ len;
+    x ^= x >> 15;
+    return (x * mul) >> (32 - bits);
+}
 
 // Bit-parallel rune NFA (the fallback for a pattern whose DFA alone exceeds
 // the state budget; re_dfa.h BitNfa, walked by regex/nfa_walk.h).  One DevNfa

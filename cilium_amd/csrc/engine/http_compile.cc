@@ -136,7 +136,9 @@ struct NameDfa {
     std::vector<uint8_t> info;    // [state]
 };
 
-NameDfa BuildNameDfa(const std::vector<std::string> &custom) {
+// The names the framer must recognise, with their NI_* flags (a custom name
+// equal to a fixed one merges into it).
+std::vector<std::pair<std::string, uint8_t>> NameCandidates(const std::vector<std::string> &custom) {
     std::vector<std::pair<std::string, uint8_t>> cands = {
         {"host", NI_HOST}, {"content-length", NI_CL}, {"transfer-encoding", NI_TE}};
     for (size_t q = 0; q < custom.size(); q++) {
@@ -145,6 +147,52 @@ NameDfa BuildNameDfa(const std::vector<std::string> &custom) {
             if (c.first == custom[q]) { c.second |= (uint8_t)(q + 1); merged = true; }
         if (!merged) cands.emplace_back(custom[q], (uint8_t)(q + 1));
     }
+    return cands;
+}
+
+// DevNameEnt table of the candidates that a <= 15-byte [0-9A-Za-z-] name can
+// equal (device_tables.h); bits = 0 if no collision-free multiplier is found.
+std::vector<DevNameEnt> BuildNameTable(const std::vector<std::string> &custom, uint32_t *bits_out, uint32_t *mul_out) {
+    std::vector<DevNameEnt> ents;
+    for (auto &cd : NameCandidates(custom)) {
+        const std::string &s = cd.first;
+        bool ok = !s.empty() && s.size() <= 15;
+        for (unsigned char ch : s) ok = ok && ((ch >= '0' && ch <= '9') || (ch >= 'a' && ch <= 'z') || ch == '-');
+        if (!ok) continue;  // no fast-path name can equal it
+        DevNameEnt e{};
+        memcpy(e.w, s.data(), s.size());
+        e.len = (uint8_t)s.size();
+        e.info = cd.second;
+        ents.push_back(e);
+    }
+    uint32_t bits = 1;
+    while ((1u << bits) < 2 * ents.size()) bits++;
+    uint64_t seed = 0x9E3779B97F4A7C15ull;
+    for (; bits <= 8; bits++) {
+        for (int tries = 0; tries < 4096; tries++) {
+            seed = seed * 6364136223846793005ull + 1442695040888963407ull;
+            const uint32_t mul = (uint32_t)(seed >> 32) | 1u;
+            std::vector<DevNameEnt> tab((size_t)1 << bits);
+            bool clash = false;
+            for (auto &e : ents) {
+                DevNameEnt &t = tab[l7_name_hash(e.w[0], e.w[1], e.w[2], e.w[3], e.len, mul, bits)];
+                if (t.len) { clash = true; break; }
+                t = e;
+            }
+            if (!clash) {
+                *bits_out = bits;
+                *mul_out = mul;
+                return tab;
+            }
+        }
+    }
+    *bits_out = 0;
+    *mul_out = 0;
+    return {};
+}
+
+NameDfa BuildNameDfa(const std::vector<std::string> &custom) {
+    const std::vector<std::pair<std::string, uint8_t>> cands = NameCandidates(custom);
     NameDfa d;
     // classes: 0 = not a tchar, 1 = tchar spelling none of the names, 2.. = name bytes
     int byte_cls[256];
@@ -443,6 +491,11 @@ int HttpCompiler::Compile(const std::vector<const HttpRule *> &rules, uint8_t te
         H.name_cls_off = Append(img, nd.cls, 256);
         H.name_trans_off = Append(img, nd.trans.data(), nd.trans.size());
         H.name_info_off = Append(img, nd.info.data(), nd.info.size());
+        uint32_t bits = 0, mul = 0;
+        const std::vector<DevNameEnt> tab = BuildNameTable(custom, &bits, &mul);
+        H.ntab_bits = (uint8_t)bits;
+        H.ntab_mul = mul;
+        H.ntab_off = Append(img, tab.data(), tab.size());
     }
     for (size_t k = 0; k < built.size(); k++) {
         const re::DFA &d = built[k].d;

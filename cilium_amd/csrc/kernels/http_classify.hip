@@ -57,6 +57,9 @@ namespace {
 #ifndef L7G_HTTP_WIN
 #define L7G_HTTP_WIN 256
 #endif
+#ifndef L7G_HTTP_FASTLINE  // header lines 16 bytes at a time (fast_line, the skip's LF check)
+#define L7G_HTTP_FASTLINE 1
+#endif
 constexpr int kWaves = L7G_HTTP_WAVES;
 constexpr int kBlock = 64 * kWaves;
 constexpr uint32_t kWin = L7G_HTTP_WIN;        // bytes per lane window
@@ -174,6 +177,7 @@ struct Img {
     __device__ __forceinline__ uint32_t u16(uint32_t o) const { return *(const uint16_t *)(p + o); }
     __device__ __forceinline__ uint32_t u32(uint32_t o) const { return *(const uint32_t *)(p + o); }
     __device__ __forceinline__ uint64_t u64(uint32_t o) const { return *(const uint64_t *)(p + o); }
+    __device__ __forceinline__ uint4 u128(uint32_t o) const { return *(const uint4 *)(p + o); }  // o 16-byte aligned
 };
 template <bool kLds>
 __device__ __forceinline__ uint32_t uni(uint32_t v) {
@@ -401,6 +405,108 @@ __device__ __forceinline__ uint32_t find_stop(const Cursor &C, uint32_t pa, uint
     return lim;
 }
 
+// OWS after a header name is over (L.pa at the value's first byte, inside the
+// window): a value nobody looks at is skipped, anything else is walked.
+template <bool kLds>
+__device__ __forceinline__ void ows_done(const Img<kLds> &I, Lane &L) {
+    if (L.slot == kNoSlot && !(L.ninfo & (NI_CL | NI_TE))) {
+        L.mode = M_SKIP;
+    } else {
+        L.mode = M_VALUE;
+        if (L.slot != kNoSlot) {
+            slot_begin(I, L, L.slot);
+        } else {
+            L.st = 0;
+            L.dcls = L.dtrans = 0;
+        }
+        L.in_ows = false;
+        L.clv = 0;
+        L.ndig = 0;
+        L.cl_bad = L.cl_ws = false;
+    }
+}
+
+// Header name -> slot, as at the end of M_NAME (L.ninfo set).
+template <bool kLds>
+__device__ __forceinline__ void name_slot(const Img<kLds> &I, Lane &L) {
+    uint32_t s = kNoSlot;
+    if (L.ninfo & NI_HOST) s = SLOT_AUTHORITY;
+    else if (L.ninfo & NI_CUSTOM) s = SLOT_CUSTOM0 + (L.ninfo & NI_CUSTOM) - 1;
+    if (s != kNoSlot && ((L.present >> s) & 1)) s = kNoSlot;                // first occurrence only
+    if (s != kNoSlot && !((HDR_U32(I, ref_slots) >> s) & 1)) s = kNoSlot;  // nobody looks at it
+    L.slot = s;
+}
+
+// bit i (0..15) set iff byte i of the 16 bytes is SP or HT
+__device__ __forceinline__ uint32_t ws_mask(uint4 w) {
+    auto eq = [](uint32_t x, uint32_t b) {  // bit 7 of byte i set iff byte i == b
+        const uint32_t t = x ^ b;
+        return ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;
+    };
+    return nib(eq(w.x, 0x20202020u) | eq(w.x, 0x09090909u)) | nib(eq(w.y, 0x20202020u) | eq(w.y, 0x09090909u)) << 4 |
+           nib(eq(w.z, 0x20202020u) | eq(w.z, 0x09090909u)) << 8 | nib(eq(w.w, 0x20202020u) | eq(w.w, 0x09090909u)) << 12;
+}
+
+// A header line's start, 16 bytes at a time (L.mode == M_LINE, L.pa + 16 <=
+// lim): the 16 bytes at L.pa are cut out of two window chunks at once.
+//   "\r\n"                        -> end of the header block (M_ENDLF's work);
+//   name of 1..15 [0-9A-Za-z-] + ":" -> the name's flags from the image's name
+//                                    table in one probe (instead of a DFA step
+//                                    per byte), its slot, and OWS over when it
+//                                    ends inside the 16 bytes;
+//   anything else                 -> left to the byte-wise framer (M_LINE).
+// The outcome is exactly the byte-wise one's (DevNameEnt).
+template <bool kLds>
+__device__ __forceinline__ void fast_line(const Img<kLds> &I, Lane &L, const Cursor &C, const uint64_t *nfa_bits) {
+    const uint32_t k0 = (L.pa - C.w) >> 4, o = L.pa & 15, i = o >> 2, sh = (o & 3) * 8;
+    const uint4 a = C.chunk(k0), b = C.chunk(k0 + 1);  // (b unused when o == 0)
+    const uint32_t d1 = i == 0 ? a.y : i == 1 ? a.z : i == 2 ? a.w : b.x;
+    const uint32_t d0 = i == 0 ? a.x : i == 1 ? a.y : i == 2 ? a.z : a.w;
+    const uint32_t d2 = i == 0 ? a.z : i == 1 ? a.w : i == 2 ? b.x : b.y;
+    const uint32_t d3 = i == 0 ? a.w : i == 1 ? b.x : i == 2 ? b.y : b.z;
+    const uint32_t d4 = i == 0 ? b.x : i == 1 ? b.y : i == 2 ? b.z : b.w;
+    uint4 f;
+    f.x = (uint32_t)((((uint64_t)d1 << 32) | d0) >> sh);
+    f.y = (uint32_t)((((uint64_t)d2 << 32) | d1) >> sh);
+    f.z = (uint32_t)((((uint64_t)d3 << 32) | d2) >> sh);
+    f.w = (uint32_t)((((uint64_t)d4 << 32) | d3) >> sh);
+    const uint32_t b0 = f.x & 0xFF;
+    if (b0 == '\r') {  // M_LINE -> M_ENDLF -> headers_done
+        if (((f.x >> 8) & 0xFF) != '\n') {
+            finish(L, V_PARSE_ERROR);
+        } else {
+            L.pa += 2;
+            headers_done(I, L, nfa_bits);
+        }
+        return;
+    }
+    const uint32_t e = (uint32_t)__builtin_ctz(nonalnum_mask(f) | 0x10000u);
+    if (e == 0 || e == 16 || byte_of(f, e) != ':') return;  // the byte-wise framer decides
+    const uint32_t nb = HDR_U8(I, ntab_bits);
+    if (nb == 0) return;
+    // lower-cased name bytes (OR 0x20 is exact on [0-9A-Za-z-]), zero past e
+    auto keep = [e](uint32_t j) { return e >= 4 * j + 4 ? 0xFFFFFFFFu : e <= 4 * j ? 0u : (1u << (8 * (e - 4 * j))) - 1u; };
+    const uint32_t w0 = (f.x | 0x20202020u) & keep(0), w1 = (f.y | 0x20202020u) & keep(1);
+    const uint32_t w2 = (f.z | 0x20202020u) & keep(2), w3 = (f.w | 0x20202020u) & keep(3);
+    const uint32_t h = l7_name_hash(w0, w1, w2, w3, e, HDR_U32(I, ntab_mul), nb);
+    const uint32_t ent = HDR_U32(I, ntab_off) + h * (uint32_t)sizeof(DevNameEnt);
+    const uint4 n = I.u128(ent);
+    const uint32_t meta = I.u32(ent + 16);
+    const bool hit = (meta & 0xFF) == e && n.x == w0 && n.y == w1 && n.z == w2 && n.w == w3;
+    L.mark = L.pa;
+    L.ninfo = hit ? (meta >> 8) & 0xFF : 0u;
+    name_slot(I, L);
+    // OWS: the first byte after ':' that is not SP / HT, if among the 16
+    const uint32_t v = (uint32_t)__builtin_ctz((~ws_mask(f) & (0xFFFFu << (e + 1)) & 0xFFFFu) | 0x10000u);
+    if (v < 16) {
+        L.pa += v;
+        ows_done(I, L);
+    } else {
+        L.pa += e + 1;
+        L.mode = M_OWS;
+    }
+}
+
 // ---------------------------------------------------------------- parse one window
 // Consumes [L.pa, min(window end, request end)).  Every loop has a single
 // exit; errors set the mode to M_DONE so later blocks fall through.
@@ -495,6 +601,7 @@ __device__ __forceinline__ void parse_window(const Img<kLds> &I, Lane &L, Cursor
     }
     // ---- header lines
     while (L.mode >= M_LINE && L.mode < M_DONE && L.pa < lim) {
+        if (L7G_HTTP_FASTLINE && L.mode == M_LINE && L.pa + 16 <= lim) fast_line(I, L, C, nfa_bits);
         if (L.mode == M_LINE) {
             if (C.at(L.pa) == '\r') {
                 L.pa++;
@@ -548,12 +655,7 @@ __device__ __forceinline__ void parse_window(const Img<kLds> &I, Lane &L, Cursor
                 } else {
                     L.pa++;
                     L.ninfo = L.nstate >= kNameStart ? I.u8(HDR_U32(I, name_info_off) + L.nstate) : 0;
-                    uint32_t s = kNoSlot;
-                    if (L.ninfo & NI_HOST) s = SLOT_AUTHORITY;
-                    else if (L.ninfo & NI_CUSTOM) s = SLOT_CUSTOM0 + (L.ninfo & NI_CUSTOM) - 1;
-                    if (s != kNoSlot && ((L.present >> s) & 1)) s = kNoSlot;                // first occurrence only
-                    if (s != kNoSlot && !((HDR_U32(I, ref_slots) >> s) & 1)) s = kNoSlot;  // nobody looks at it
-                    L.slot = s;
+                    name_slot(I, L);
                     L.mode = M_OWS;
                 }
             }
@@ -563,28 +665,12 @@ __device__ __forceinline__ void parse_window(const Img<kLds> &I, Lane &L, Cursor
                 const uint32_t c = C.at(L.pa);
                 if (c != ' ' && c != '\t') break;
             }
-            if (L.pa < lim) {
-                if (L.slot == kNoSlot && !(L.ninfo & (NI_CL | NI_TE))) {
-                    L.mode = M_SKIP;
-                } else {
-                    L.mode = M_VALUE;
-                    if (L.slot != kNoSlot) {
-                        slot_begin(I, L, L.slot);
-                    } else {
-                        L.st = 0;
-                        L.dcls = L.dtrans = 0;
-                    }
-                    L.in_ows = false;
-                    L.clv = 0;
-                    L.ndig = 0;
-                    L.cl_bad = L.cl_ws = false;
-                }
-            }
+            if (L.pa < lim) ows_done(I, L);
         }
         if (L.mode == M_VALUE && !(L.ninfo & (NI_CL | NI_TE))) {  // a value some rule looks at: DFA walk only
             // software pipeline as for the target: byte p+1 and its class are
             // read while the transition on byte p is in flight
-            uint32_t c = 0;
+            uint32_t c = 0, nx = 0;  // nx: the byte after c when in hand (| 0x100)
             if (L.pa < lim) {
                 c = C.at(L.pa);
                 uint32_t k = L.dcls ? I.u8(L.dcls + c) : 0;
@@ -605,18 +691,27 @@ __device__ __forceinline__ void parse_window(const Img<kLds> &I, Lane &L, Cursor
                     c1 = c2;
                     k = k1;
                 }
+                if (L7G_HTTP_FASTLINE && L.pa + 1 < lim) nx = c1 | 0x100;
             }
             if (L.pa < lim && !((c < 0x20 && c != '\t') || c == 0x7F)) {  // absorbing: skip to the value's end
                 L.pa = find_stop<1>(C, L.pa, lim);
                 c = L.pa < lim ? C.at(L.pa) : 0;
+                nx = 0;
             }
             if (L.pa < lim) {
                 if (c != '\r') {
                     finish(L, V_PARSE_ERROR);
                 } else {
                     if (L.in_ows) L.st = L.saved;  // trailing OWS is not part of the value
-                    L.pa++;
-                    L.mode = M_LF;
+                    if (nx) {  // M_LF's work on the byte in hand
+                        L.pa += 2;
+                        if (nx != ('\n' | 0x100)) finish(L, V_PARSE_ERROR);
+                        else if (line_done(I, L)) L.mode = M_LINE;
+                        else finish(L, V_PARSE_ERROR);
+                    } else {
+                        L.pa++;
+                        L.mode = M_LF;
+                    }
                 }
             }
         }
@@ -654,7 +749,7 @@ __device__ __forceinline__ void parse_window(const Img<kLds> &I, Lane &L, Cursor
             }
         }
         if (L.mode == M_SKIP) {  // a value nobody looks at: find CR (or a CTL / DEL) 16 bytes a step
-            uint32_t stop = 0;
+            uint32_t stop = 0, next = 0;  // next: the byte after the stop when the chunk holds it (| 0x100)
             while (L.pa < lim) {
                 const uint4 w = C.chunk((L.pa - L.w) >> 4);
                 const uint32_t any = stop_bits(w.x) | stop_bits(w.y) | stop_bits(w.z) | stop_bits(w.w);
@@ -667,6 +762,7 @@ __device__ __forceinline__ void parse_window(const Img<kLds> &I, Lane &L, Cursor
                     const uint32_t c = byte_of(w, p & 15);
                     if (c != '\t') {
                         stop = c | 0x100;
+                        if (L7G_HTTP_FASTLINE && p + 1 < cend && p + 1 < lim) next = byte_of(w, (p + 1) & 15) | 0x100;
                         break;
                     }
                     L.pa++;
@@ -675,6 +771,11 @@ __device__ __forceinline__ void parse_window(const Img<kLds> &I, Lane &L, Cursor
             if (stop) {
                 if (stop != ('\r' | 0x100)) {
                     finish(L, V_PARSE_ERROR);
+                } else if (next) {  // M_LF's work on the byte in hand
+                    L.pa += 2;
+                    if (next != ('\n' | 0x100)) finish(L, V_PARSE_ERROR);
+                    else if (line_done(I, L)) L.mode = M_LINE;
+                    else finish(L, V_PARSE_ERROR);
                 } else {
                     L.pa++;
                     L.mode = M_LF;
@@ -783,13 +884,22 @@ __device__ __forceinline__ void parse_window(const Img<kLds> &I, Lane &L, Cursor
 __device__ __forceinline__ void dma_windows(uint8_t *wave_lds, uint64_t packed, uint32_t lane) {
     const uint32_t plo = (uint32_t)packed, phi = (uint32_t)(packed >> 32);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's earlier LDS reads have landed
+    // every window address first, one wait, then the loads: issued one per
+    // load, the compiler waits on each ds_bpermute in turn (16 serial LDS
+    // round trips per round)
+    uint32_t tlo[kWinChunks], thi[kWinChunks];
 #pragma unroll
     for (int j = 0; j < (int)kWinChunks; j++) {
         const int t = (int)(kWinPerInst * j + lane / kLanesPerWin);
-        const uint32_t tlo = __shfl(plo, t), thi = __shfl(phi, t);
-        const uint32_t c = (lane % kLanesPerWin) ^ win_swizzle((uint32_t)t);
-        if ((tlo | thi) && c <= (tlo & 15)) {
-            const uint8_t *src = (const uint8_t *)((((uint64_t)thi) << 32) | (tlo & ~15u)) + 16 * c;
+        tlo[j] = __shfl(plo, t);
+        thi[j] = __shfl(phi, t);
+    }
+#pragma unroll
+    for (int j = 0; j < (int)kWinChunks; j++) {
+        const uint32_t t = kWinPerInst * j + lane / kLanesPerWin;
+        const uint32_t c = (lane % kLanesPerWin) ^ win_swizzle(t);
+        if ((tlo[j] | thi[j]) && c <= (tlo[j] & 15)) {
+            const uint8_t *src = (const uint8_t *)((((uint64_t)thi[j]) << 32) | (tlo[j] & ~15u)) + 16 * c;
             __builtin_amdgcn_global_load_lds((const void *)src,
                                              (__attribute__((address_space(3))) void *)(wave_lds + j * 1024), 16, 0, 0);
         }
@@ -964,12 +1074,20 @@ __device__ __forceinline__ void build_tile_map(TileMap &T, const Lane &L, uint32
     // lane l reading chunk 4j + (l & 3) of request 16q + (l >> 2), so one load
     // instruction touches 16 requests' 64-byte runs instead of 64 lines
     const uint32_t sub = lane & 3, grp = lane >> 2;
+    // the four requests this lane loads for (fixed for the tile): fetched once,
+    // not per step (the compiler waits on each ds_bpermute where it is used)
+    uint64_t qb[4];
+    uint32_t qn[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        qb[q] = (uint64_t)__shfl((unsigned long long)L.base, 16 * q + (int)grp);
+        qn[q] = (uint32_t)__shfl((int)nch, 16 * q + (int)grp);
+    }
 #define MAP_ISSUE(s, j)                                                                                        \
     do {                                                                                                       \
         _Pragma("unroll") for (int q_ = 0; q_ < 4; q_++) {                                                     \
-            const int src_ = 16 * q_ + (int)grp;                                                               \
-            const uint64_t b_ = (uint64_t)__shfl((unsigned long long)L.base, src_);                            \
-            const uint32_t n_ = (uint32_t)__shfl((int)nch, src_);                                              \
+            const uint64_t b_ = qb[q_];                                                                        \
+            const uint32_t n_ = qn[q_];                                                                        \
             const uint32_t c_ = 4 * (uint32_t)(j) + sub;                                                       \
             const uint64_t a_ = c_ < n_ ? b_ + ((uint64_t)c_ << 4) : dummy;                                    \
             __builtin_amdgcn_global_load_lds((const void *)a_,                                                \

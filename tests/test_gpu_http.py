@@ -201,6 +201,52 @@ def test_header_name_and_version_fast_paths(engine, oracle):
     assert len(set(got[0].tolist())) >= 2
 
 
+def test_header_line_fast_path(engine, oracle):
+    """Header lines taken 16 bytes at a time (the kernel's name-table probe,
+    OWS inside the 16 bytes, the LF check on the byte in hand): known names
+    in every case mix, names one byte off them, 15 / 16 / 17-byte names,
+    OWS runs of SP and HT past the 16 bytes, empty values, bare CR / LF line
+    ends and "\\r" + other at the end of the block, duplicate and Content-Length
+    / Transfer-Encoding lines, at every window offset.  Kernel vs oracle."""
+    import random
+    rng = random.Random(7)
+    rules = api.http_rules_from_api([
+        api.PortRuleHTTP(method="GET", path="/a/.*", host="svc-[0-9]+"),
+        api.PortRuleHTTP(path="/b/.*", headers=["x-b2: yes"]),
+        api.PortRuleHTTP(path="/c", host="h"),
+        api.PortRuleHTTP(path="/a/p.*", headers=["Accept-Language-X: en"]),
+        api.PortRuleHTTP(path="/b/pp.*", headers=["X-Token: 123"]),
+    ])
+    pol = api.policy_set(api.network_policy("ep", 1, ingress=[(80, [api.port_rule(http=rules)])]))
+    good = [b"Host", b"HOST", b"hOsT", b"X-Token", b"x-token", b"X-TOKEN", b"x-b2", b"X-B2", b"Accept-Language-X",
+            b"accept-language-x", b"User-Agent", b"Accept", b"X-Pad"]
+    odd = [b"Hos", b"Hostx", b"X-Toke", b"X-Tokenn", b"x-b", b"x-b22", b"Accept-Language", b"Content-Length",
+           b"content-length", b"CONTENT-LENGTH", b"Content-Lengt", b"Transfer-Encoding", b"transfer-encoding",
+           b"A" * 15, b"B" * 16, b"C" * 17, b"a-b-c-d-e-f-g-h", b"X9", b"9", b"-", b"X_Y", b"X.Y", b"X Y", b"X\tY", b""]
+    ows = [b"", b" ", b"  ", b"\t", b" \t ", b" " * 15, b" " * 16, b"\t" * 20]
+    vals = [b"", b"yes", b"en", b"123", b"[0-9]+", b"12a", b"svc-12", b"h", b"chunked", b"0", b"5", b"x" * 40, b"yes ",
+            b"a\x01b"]
+    bad_eols = [b"\n", b"\r", b"\rx"]
+    reqs = []
+    for i in range(4000):
+        path = rng.choice([b"/a/", b"/b/"]) + b"p" * rng.choice([0, 1, 5, 100, 180, 200, 215, 230, 240]) \
+            if rng.random() < 0.8 else rng.choice([b"/c", b"/d"])
+        lines = b""
+        for _ in range(rng.randint(0, 6)):
+            nm = rng.choice(good) if rng.random() < 0.85 else rng.choice(odd)
+            v = rng.choice(vals[:6]) if rng.random() < 0.7 else rng.choice(vals)
+            eol = b"\r\n" if rng.random() < 0.97 else rng.choice(bad_eols)
+            lines += nm + b":" + rng.choice(ows) + v + eol
+        end = b"\r\n" if rng.random() < 0.9 else rng.choice([b"\rx", b"\n", b""])
+        reqs.append(b"GET " + path + b" HTTP/1.1\r\n" + lines + end)
+    conns = gen.make_conns(1, 0, 80, True, PROTO_HTTP, [3])
+    w = wl_from_reqs(reqs, pol, conns)
+    got, ref = both(engine, oracle, w, 4)
+    assert_same(got, ref, w)
+    hist = np.bincount(got[0], minlength=5)
+    assert hist[ALLOW] > 20 and hist[DENY] > 20 and hist[PARSE_ERROR] > 20 and hist[INCOMPLETE] > 20
+
+
 def test_chunked_bodies(engine, oracle):
     """Transfer-Encoding requests get verdicts from their headers
     (envoy/cilium_l7policy.cc:127-182 decides in decodeHeaders); consumed
