@@ -47,6 +47,10 @@
 #include "../device_tables.h"
 #include "gmem.h"
 
+// OCKL's DPP wave reductions (64-bit forms are not declared by hip_runtime.h)
+extern "C" __device__ __attribute__((const)) unsigned long long __ockl_wfred_min_u64(unsigned long long);
+extern "C" __device__ __attribute__((const)) unsigned long long __ockl_wfred_max_u64(unsigned long long);
+
 namespace l7 {
 
 namespace {
@@ -1037,23 +1041,16 @@ __device__ __forceinline__ void build_tile_map(TileMap &T, const Lane &L, uint32
     T.from = 0;
     const uint32_t nch = min(map_nch(L), kMapChunks);
     const uint32_t nseg = (nch + 3) >> 2;  // 64-byte steps of this lane
-    uint32_t smax = nseg;
-    for (int o = 32; o > 0; o >>= 1) smax = max(smax, (uint32_t)__shfl_xor((int)smax, o));
-    smax = (uint32_t)__builtin_amdgcn_readfirstlane((int)smax);
+    // wave reductions by DPP (__ockl_wfred_*): no LDS round trips
+    const uint32_t smax = (uint32_t)__builtin_amdgcn_readfirstlane((int)__ockl_wfred_max_u32(nseg));
     if (smax == 0) return;
     const uint64_t act = __ballot(nch > 0);
     const uint64_t dummy = (uint64_t)__shfl((unsigned long long)L.base, (int)__builtin_ctzll(act));
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // earlier LDS reads of the window area have landed
     {
-        uint64_t lo = nch ? L.base : ~0ull, hi = nch ? L.base + ((uint64_t)nch << 4) : 0ull;
-        uint32_t own = nch;
-        for (int o = 32; o > 0; o >>= 1) {
-            const uint64_t l2 = (uint64_t)__shfl_xor((unsigned long long)lo, o);
-            const uint64_t h2 = (uint64_t)__shfl_xor((unsigned long long)hi, o);
-            lo = l2 < lo ? l2 : lo;
-            hi = h2 > hi ? h2 : hi;
-            own += (uint32_t)__shfl_xor((int)own, o);
-        }
+        uint64_t lo = __ockl_wfred_min_u64(nch ? L.base : ~0ull);
+        uint64_t hi = __ockl_wfred_max_u64(nch ? L.base + ((uint64_t)nch << 4) : 0ull);
+        uint32_t own = __ockl_wfred_add_u32(nch);
         lo = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(lo >> 32)) << 32) |
              (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)lo);
         hi = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(hi >> 32)) << 32) |
