@@ -61,6 +61,12 @@ namespace {
 #ifndef L7G_HTTP_WIN
 #define L7G_HTTP_WIN 256
 #endif
+#ifndef L7G_HTTP_VMAP  // lane-mode tile map streamed through VGPRs, head windows DMA'd meanwhile
+#define L7G_HTTP_VMAP 1
+#endif
+#ifndef L7G_HTTP_MAPDEPTH  // 64-byte-per-lane map steps in flight (VGPR mode)
+#define L7G_HTTP_MAPDEPTH 4
+#endif
 #ifndef L7G_HTTP_FASTLINE  // header lines 16 bytes at a time (fast_line, the skip's LF check)
 #define L7G_HTTP_FASTLINE 1
 #endif
@@ -523,11 +529,24 @@ __device__ __forceinline__ void parse_window(const Img<kLds> &I, Lane &L, Cursor
 
     // ---- request line
     if (L.mode == M_METHOD) {  // 1*tchar SP
+        // software pipeline as for the target: byte p+2 and the class of byte
+        // p+1 are read while the transition on byte p is in flight
         uint32_t c = 0;
-        for (; L.pa < lim; L.pa++) {
+        if (L.pa < lim) {
             c = C.at(L.pa);
-            if (!is_tchar(c)) break;
-            dfa_step(I, L, c);
+            uint32_t k = L.dcls ? I.u8(L.dcls + c) : 0;
+            uint32_t c1 = L.pa + 1 < lim ? C.at(L.pa + 1) : 0;
+            while (is_tchar(c)) {
+                const uint32_t p1 = L.pa + 1;
+                const uint32_t c2 = p1 + 1 < lim ? C.at(p1 + 1) : 0;
+                const uint32_t k1 = L.dcls ? I.u8(L.dcls + c1) : 0;
+                if (L.st) L.st = I.u16(L.dtrans + 2 * (L.st * L.dncls + k));
+                L.pa = p1;
+                if (p1 >= lim) break;
+                c = c1;
+                c1 = c2;
+                k = k1;
+            }
         }
         if (L.pa < lim) {
             if (c != ' ' || L.pa == L.mark) {
@@ -885,7 +904,7 @@ __device__ __forceinline__ void parse_window(const Img<kLds> &I, Lane &L, Cursor
 // window at address `win` into LDS slot t (chunk c stored at position
 // c ^ (t & 15)).  packed = window address | hi (addresses are 16-byte aligned;
 // 0 = nothing to load).
-__device__ __forceinline__ void dma_windows(uint8_t *wave_lds, uint64_t packed, uint32_t lane) {
+__device__ __forceinline__ void dma_windows_issue(uint8_t *wave_lds, uint64_t packed, uint32_t lane) {
     const uint32_t plo = (uint32_t)packed, phi = (uint32_t)(packed >> 32);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's earlier LDS reads have landed
     // every window address first, one wait, then the loads: issued one per
@@ -908,7 +927,17 @@ __device__ __forceinline__ void dma_windows(uint8_t *wave_lds, uint64_t packed, 
                                              (__attribute__((address_space(3))) void *)(wave_lds + j * 1024), 16, 0, 0);
         }
     }
+}
+__device__ __forceinline__ void dma_windows(uint8_t *wave_lds, uint64_t packed, uint32_t lane) {
+    dma_windows_issue(wave_lds, packed, lane);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+// the DMA word of a lane's next window (0: nothing to load)
+__device__ __forceinline__ uint64_t window_packed(Lane &L) {
+    if (L.done) return 0;
+    L.w = L.pa & ~15u;
+    const uint32_t hi = min(L.lena - 1 - L.w, kWin - 1) >> 4;
+    return (L.base + L.w) | hi;
 }
 
 // ---------------------------------------------------------------- value-stop map of a tile
@@ -965,6 +994,8 @@ template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
+
+__device__ __forceinline__ uint4 u4(gm_u32x4 v) { return make_uint4(v.x, v.y, v.z, v.w); }
 
 __device__ __forceinline__ uint32_t byte_at32(uint4 a, uint4 b, uint32_t i) {
     // byte i (0..31) of the 32 bytes a, b (little endian)
@@ -1034,7 +1065,9 @@ __device__ __forceinline__ void map_span(TileMap &T, const Lane &L, uint32_t lan
     T.off = 0;
 }
 
-__device__ __forceinline__ void build_tile_map(TileMap &T, const Lane &L, uint32_t lane, uint8_t *wave_lds) {
+// Returns true when the lane-mode map also DMA'd the tile's first head
+// windows (window_packed of every lane) into the window area.
+__device__ __forceinline__ bool build_tile_map(TileMap &T, Lane &L, uint32_t lane, uint8_t *wave_lds) {
 #pragma unroll
     for (int q = 0; q < (int)kMapWords; q++) T.m[q] = 0;
     T.off = kMapChunks;
@@ -1043,7 +1076,7 @@ __device__ __forceinline__ void build_tile_map(TileMap &T, const Lane &L, uint32
     const uint32_t nseg = (nch + 3) >> 2;  // 64-byte steps of this lane
     // wave reductions by DPP (__ockl_wfred_*): no LDS round trips
     const uint32_t smax = (uint32_t)__builtin_amdgcn_readfirstlane((int)__ockl_wfred_max_u32(nseg));
-    if (smax == 0) return;
+    if (smax == 0) return false;
     const uint64_t act = __ballot(nch > 0);
     const uint64_t dummy = (uint64_t)__shfl((unsigned long long)L.base, (int)__builtin_ctzll(act));
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // earlier LDS reads of the window area have landed
@@ -1059,12 +1092,12 @@ __device__ __forceinline__ void build_tile_map(TileMap &T, const Lane &L, uint32
         const uint64_t span = (hi - lo) >> 4;
         if (span <= kSpanChunksMax && span <= (uint64_t)own + (own >> 3)) {
             map_span(T, L, lane, wave_lds, lo, (uint32_t)span, nch);
-            return;
+            return false;
         }
     }
     T.off = kMapChunks - 4 * smax;
     T.from = 4 * kSkipSteps;
-    if (smax <= kSkipSteps) return;  // every request fits its head window
+    if (smax <= kSkipSteps) return false;  // every request fits its head window
     // lanes with nothing (more) to load still issue theirs, at a chunk of the
     // tile, so every step is four loads and vmcnt counts stay exact
     // four lanes per request: load q of step j covers requests 16q..16q+15,
@@ -1092,6 +1125,55 @@ __device__ __forceinline__ void build_tile_map(TileMap &T, const Lane &L, uint32
                                              16, 0, 0);                                                        \
         }                                                                                                      \
     } while (0)
+#if L7G_HTTP_VMAP
+#undef MAP_ISSUE
+    // The head windows go into the window area now (the map does not use it),
+    // so their DMA overlaps the map stream; the map's 64-byte steps land in
+    // VGPRs, kMapDepth of them in flight (the LDS ring held four).
+    dma_windows_issue(wave_lds, window_packed(L), lane);
+    constexpr int kMapDepth = L7G_HTTP_MAPDEPTH;
+    gm_u32x4 buf[kMapDepth][4];
+    // Loads and waits are written out (inline asm): the compiler's own wait
+    // placement drains every load at the loop head (vmcnt(0)), which leaves
+    // one memory latency per kMapDepth steps.  Slot s is waited for with the
+    // 4 (kMapDepth - 1) loads of the later slots still in flight (vmcnt
+    // retires in issue order; the window DMA above was issued first).
+#define MAP_LOAD(s, j)                                                                                         \
+    do {                                                                                                       \
+        _Pragma("unroll") for (int q_ = 0; q_ < 4; q_++) {                                                     \
+            const uint32_t c_ = 4 * (uint32_t)(j) + sub;                                                       \
+            const uint64_t a_ = c_ < qn[q_] ? qb[q_] + ((uint64_t)c_ << 4) : dummy;                            \
+            asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(buf[s][q_]) : "v"(a_) : "memory");           \
+        }                                                                                                      \
+    } while (0)
+#pragma unroll
+    for (int s = 0; s < kMapDepth; s++) MAP_LOAD(s, kSkipSteps + (uint32_t)s);
+    for (uint32_t j0 = kSkipSteps; j0 < smax; j0 += kMapDepth) {
+#pragma unroll
+        for (int s = 0; s < kMapDepth; s++) {
+            const uint32_t j = j0 + s;
+            asm volatile("s_waitcnt vmcnt(%4)"
+                         : "+v"(buf[s][0]), "+v"(buf[s][1]), "+v"(buf[s][2]), "+v"(buf[s][3])
+                         : "n"(4 * (kMapDepth - 1)));
+            // block q, bit l: request 16q + (l >> 2), chunk 4j + (l & 3)
+            const uint64_t M0 = __ballot(stop_any(u4(buf[s][0])) != 0), M1 = __ballot(stop_any(u4(buf[s][1])) != 0);
+            const uint64_t M2 = __ballot(stop_any(u4(buf[s][2])) != 0), M3 = __ballot(stop_any(u4(buf[s][3])) != 0);
+            MAP_LOAD(s, j + kMapDepth);
+            if (j < smax) {
+                const uint32_t qo = lane >> 4;
+                const uint64_t Mq = qo == 0 ? M0 : qo == 1 ? M1 : qo == 2 ? M2 : M3;
+                uint32_t nb = (uint32_t)(Mq >> (4 * (lane & 15))) & 0xFu;
+                if (4 * j >= nch) nb = 0;
+#pragma unroll
+                for (int q = 0; q < (int)kMapWords - 1; q++) T.m[q] = __builtin_amdgcn_alignbit(T.m[q + 1], T.m[q], 4);
+                T.m[kMapWords - 1] = (T.m[kMapWords - 1] >> 4) | (nb << 28);
+            }
+        }
+    }
+#undef MAP_LOAD
+    wait_vmcnt<0>();
+    return true;
+#else
 #pragma unroll
     for (int s = 0; s < kMapSlots; s++) MAP_ISSUE(s, kSkipSteps + (uint32_t)s);
     for (uint32_t j0 = kSkipSteps; j0 < smax; j0 += kMapSlots) {
@@ -1127,6 +1209,8 @@ __device__ __forceinline__ void build_tile_map(TileMap &T, const Lane &L, uint32
     }
     wait_vmcnt<0>();
 #undef MAP_ISSUE
+    return false;
+#endif
 }
 
 // Lanes with L.scan set: skip the rest of the value with the lane's map.
@@ -1236,20 +1320,16 @@ __device__ __forceinline__ void run_tile(Lane &L, const uint8_t *img, uint8_t *w
     }
     PH_DECL
     TileMap TM;
-    build_tile_map(TM, L, lane, wave_lds);
+    bool loaded = build_tile_map(TM, L, lane, wave_lds);  // true: the first windows are in
     PH_MARK(2);
     Cursor C;
     C.slot = wave_lds + lane * kWin;
     C.swz = win_swizzle(lane) << 4;
     while (__any(!L.done)) {
-        uint64_t packed = 0;
-        if (!L.done) {
-            L.w = L.pa & ~15u;
-            const uint32_t hi = min(L.lena - 1 - L.w, kWin - 1) >> 4;
-            packed = (L.base + L.w) | hi;
-        }
+        const uint64_t packed = window_packed(L);
         PH_MARK(3);
-        dma_windows(wave_lds, packed, lane);
+        if (!loaded) dma_windows(wave_lds, packed, lane);
+        loaded = false;
         PH_MARK(0);
         if (!L.done) {
             parse_window(I, L, C, O.nfa_bits);
