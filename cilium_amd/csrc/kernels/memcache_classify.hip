@@ -194,6 +194,176 @@ __device__ __forceinline__ void classify_cmd(const uint32_t cw[4], uint32_t clen
     else fr = F_BAD;
 }
 
+// ---- SWAR text tokenizer (the common case of the text path)
+// bit i (0..15) set iff byte i of the chunk equals b
+__device__ __forceinline__ uint32_t eq_mask(uint4 w, uint32_t b) {
+    const uint32_t bb = b * 0x01010101u;
+    auto e = [bb](uint32_t x) {
+        const uint32_t t = x ^ bb;
+        return ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;
+    };
+    auto nib = [](uint32_t s) { return __builtin_amdgcn_ubfe((s >> 7) * 0x204081u, 21, 4); };
+    return nib(e(w.x)) | nib(e(w.y)) << 4 | nib(e(w.z)) << 8 | nib(e(w.w)) << 12;
+}
+// bit i set iff byte i is an ASCII white space (0x09..0x0D or 0x20: unicode.IsSpace below 0x80)
+__device__ __forceinline__ uint32_t ascii_space_mask(uint4 w) {
+    auto sp = [](uint32_t x) {
+        const uint32_t t = x & 0x7F7F7F7Fu;
+        // 0x09..0x0D: t - 0x09 < 5 per byte (no borrow across bytes: t >= 0 and the high bit is clear)
+        const uint32_t ge9 = (t + 0x77777777u) & 0x80808080u;   // t >= 0x09
+        const uint32_t ge14 = (t + 0x72727272u) & 0x80808080u;  // t >= 0x0E
+        const uint32_t tt = t ^ 0x20202020u;
+        const uint32_t is20 = ~(((tt & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | tt) & 0x80808080u;
+        return ((ge9 & ~ge14) | is20) & ~x & 0x80808080u;  // high bit of the byte clear
+    };
+    auto nib = [](uint32_t s) { return __builtin_amdgcn_ubfe((s >> 7) * 0x204081u, 21, 4); };
+    return nib(sp(w.x)) | nib(sp(w.y)) << 4 | nib(sp(w.z)) << 8 | nib(sp(w.w)) << 12;
+}
+__device__ __forceinline__ uint32_t chunk_byte(uint4 w, uint32_t q) {
+    const bool upper = (q & 8) != 0;
+    const uint32_t lo = upper ? w.z : w.x, hi = upper ? w.w : w.y;
+    return __builtin_amdgcn_perm(hi, lo, (q & 7) | 0x0C0C0C00u);
+}
+
+// True when the command line (up to its first "\r\n", or all the data) holds
+// no byte that may start a multi-byte White_Space rune (0xC2, 0xE1, 0xE2,
+// 0xE3): text_fast's token masks are then exactly bytes.Fields' split.
+__device__ __forceinline__ bool text_ascii_spaces(const uint8_t *b, uint32_t len) {
+    const uint64_t a = (uint64_t)b;
+    const uint32_t a0 = (uint32_t)(a & 15);
+    const uint64_t base = a - a0;
+    const uint32_t end = a0 + len;
+    bool prev_cr = false;
+    for (uint32_t cb = 0; cb < end; cb += 16) {
+        const uint4 w = gload16(base + cb);
+        uint32_t valid = end >= cb + 16 ? 0xFFFFu : (1u << (end - cb)) - 1u;
+        if (cb == 0) valid &= 0xFFFFu << a0;
+        const uint32_t CR = eq_mask(w, '\r'), LF = eq_mask(w, '\n');
+        if (prev_cr && (LF & valid & 1u)) return true;
+        const uint32_t crlf = CR & (LF >> 1) & valid & (valid >> 1);
+        const uint32_t line = crlf ? valid & ((1u << __builtin_ctz(crlf)) - 1u) : valid;
+        const uint32_t H = eq_mask(w, 0xC2) | eq_mask(w, 0xE1) | eq_mask(w, 0xE2) | eq_mask(w, 0xE3);
+        if (H & line) return false;
+        if (crlf) return true;
+        prev_cr = (CR & valid) >> 15;
+    }
+    return true;
+}
+
+// Text command line state (the byte-wise and the SWAR tokenizer fill the same)
+struct TextLine {
+    uint32_t lf;           // position of the line's "\r\n" (found)
+    bool found;
+    uint32_t nt;           // tokens started
+    uint32_t cw[4], clen;  // first token, packed (<= 16 bytes kept)
+    int fr;
+    uint32_t cmd_id;
+    bool a_ok, a_bad, a_neg;  // strconv.Atoi(tokens[4])
+    uint32_t a_n;
+    uint64_t a_v;
+};
+
+// next byte of the first token (the first 16 are kept; selects, not an
+// indexed store, so cw stays in registers)
+__device__ __forceinline__ void cmd_byte(TextLine &T, uint32_t c) {
+    const uint32_t v = T.clen < 16 ? c << ((T.clen & 3) * 8) : 0u, wi = T.clen >> 2;
+    T.cw[0] |= wi == 0 ? v : 0u;
+    T.cw[1] |= wi == 1 ? v : 0u;
+    T.cw[2] |= wi == 2 ? v : 0u;
+    T.cw[3] |= wi == 3 ? v : 0u;
+    T.clen++;
+}
+
+__device__ __forceinline__ void atoi_step(TextLine &T, uint32_t c) {
+    if (T.a_n == 0 && (c == '+' || c == '-')) { T.a_neg = c == '-'; T.a_ok = false; /* until a digit */ }
+    else if (c < '0' || c > '9') { T.a_ok = false; T.a_bad = true; }
+    else {
+        const uint64_t d = c - '0';
+        if (T.a_v > (~0ull - d) / 10) T.a_bad = true;
+        else T.a_v = T.a_v * 10 + d;
+        if (T.a_v > 0x7FFFFFFFFFFFFFFFull + (T.a_neg ? 1u : 0u)) T.a_bad = true;
+        T.a_ok = !T.a_bad;
+    }
+    T.a_n++;
+}
+
+__device__ __forceinline__ bool is_key_tok(const TextLine &T) {
+    return (T.fr == F_GET && T.nt >= 2) || (T.fr == F_GAT && T.nt >= 3) || ((T.fr == F_STORAGE || T.fr == F_KEY1) && T.nt == 2);
+}
+
+// The command line 16 bytes at a time: per chunk the masks of ASCII spaces,
+// CR and LF give the line end (the first "\r\n") and the token runs; only the
+// bytes of the tokens that matter are visited one by one (the command, the
+// keys through the key DFAs, tokens[4] of a storage command), every other
+// byte is passed over by mask.  Only for lines text_ascii_spaces accepts (a
+// byte that may start a multi-byte White_Space rune sends the line to the
+// byte-wise tokenizer).
+template <bool kNfa>
+__device__ __forceinline__ void text_fast(const Image &I, Keys &K, const uint8_t *b, uint32_t len, TextLine &T) {
+    const uint64_t a = (uint64_t)b;
+    const uint32_t a0 = (uint32_t)(a & 15);
+    const uint64_t base = a - a0;
+    const uint32_t end = a0 + len;  // request bytes are chunk positions [a0, end)
+    bool in_tok = false, key_tok = false, prev_cr = false;
+    uint32_t kstart = 0;
+    for (uint32_t cb = 0; cb < end; cb += 16) {
+        const uint4 w = gload16(base + cb);  // global, not flat (gmem.h)
+        uint32_t valid = end >= cb + 16 ? 0xFFFFu : (1u << (end - cb)) - 1u;
+        if (cb == 0) valid &= 0xFFFFu << a0;
+        const uint32_t S = ascii_space_mask(w), CR = eq_mask(w, '\r'), LF = eq_mask(w, '\n');
+        // the line end: a CR whose next byte is LF (the CR possibly the previous chunk's last byte)
+        uint32_t le = 16;  // first byte of "\r\n" in this chunk (16: none; -1 handled by prev_cr)
+        bool ended = false;
+        if (prev_cr && (LF & valid & 1u)) {
+            T.found = true;
+            T.lf = cb - 1 - a0;
+            ended = true;
+            le = 0;  // nothing of this chunk is on the line
+        } else {
+            const uint32_t crlf = CR & (LF >> 1) & valid & (valid >> 1);
+            if (crlf) {
+                le = (uint32_t)__builtin_ctz(crlf);
+                T.found = true;
+                T.lf = cb + le - a0;
+                ended = true;
+            }
+        }
+        const uint32_t line = valid & ((1u << le) - 1u);  // this chunk's bytes on the line
+        uint32_t m = ~S & line;  // token bytes
+        uint32_t q = 0;          // next position of this chunk to look at
+        for (;;) {
+            if (!in_tok) {
+                const uint32_t mm = m & (0xFFFFu << q);
+                if (!mm) break;
+                q = (uint32_t)__builtin_ctz(mm);
+                T.nt++;
+                key_tok = is_key_tok(T);
+                kstart = cb + q - a0;
+                in_tok = true;
+            }
+            // token bytes [q, e) of this chunk
+            const uint32_t e = (uint32_t)__builtin_ctz((~m & (0xFFFFu << q)) | 0x10000u);
+            if (T.nt == 1) {
+                for (uint32_t k = q; k < e; k++) cmd_byte(T, chunk_byte(w, k));
+            } else if (key_tok) {
+                for (uint32_t k = q; k < e; k++) keys_step(I, K, chunk_byte(w, k));
+            } else if (T.fr == F_STORAGE && T.nt == 5) {
+                for (uint32_t k = q; k < e; k++) atoi_step(T, chunk_byte(w, k));
+            }
+            // the token closes at e: a space on the line, or the line end
+            const bool closes = e < 16 && (((line >> e) & 1u) || (ended && e == le));
+            if (!closes) break;  // it runs on into the next chunk (or the data ends)
+            if (T.nt == 1) classify_cmd(T.cw, T.clen, T.fr, T.cmd_id);
+            if (key_tok) keys_end<kNfa>(I, K, b, kstart, cb + e - a0);
+            in_tok = false;
+            q = e;
+        }
+        if (ended) return;
+        prev_cr = (CR & valid) >> 15;
+    }
+    // the data ends before any "\r\n": incomplete (T.found false)
+}
+
 }  // namespace
 
 // sel: this protocol's request indices (partition_kernel, mixed batches), else
@@ -284,82 +454,75 @@ __device__ __forceinline__ void mc_loop(Batch B, McTables T, const uint8_t *imag
                 frame = (uint32_t)(body + 24u);  // uint32 arithmetic, then int()
             } else {
                 // ---- text command line
-                Reader R{b, ~0ull, 0, 0, 0, 0};
-                uint32_t i = 0, lf = 0;
-                bool found = false;
-                uint32_t nt = 0;              // tokens started
-                uint32_t cw[4] = {0, 0, 0, 0}, clen = 0;
-                int fr = F_NONE;
-                uint32_t cmd_id = kMcOther;
-                bool key_tok = false;         // current token is a key
-                uint32_t kstart = 0;          // its first byte
-                bool a_ok = false, a_bad = false, a_neg = false;  // strconv.Atoi(tokens[4])
-                uint32_t a_n = 0;
-                uint64_t a_v = 0;
-                // One token per round: its bytes in a tight loop, then the
-                // token-end work (command id, key DFA accept masks) once.  A
-                // wave runs its lanes' divergent paths one after the other, so
-                // token-end work inside the byte loop was paid in nearly every
-                // byte step (some lane is always at a token end).
-                for (;;) {
-                    bool tok = false;  // spaces up to the next token or the line end
-                    while (i < len) {
-                        const uint32_t c = rd(R, i);
-                        if (c == '\r' && i + 1 < len && b[i + 1] == '\n') { lf = i; found = true; break; }
-                        const uint32_t sp = space_len(b, i, len, c);
-                        if (!sp) { tok = true; break; }
-                        i += sp;
-                    }
-                    if (!tok) break;  // line end, or the data ends: incomplete
-                    nt++;
-                    key_tok = (fr == F_GET && nt >= 2) || (fr == F_GAT && nt >= 3) ||
-                              ((fr == F_STORAGE || fr == F_KEY1) && nt == 2);
-                    kstart = i;
-                    bool ended = false;  // by a space or the line end (not consumed here)
-                    while (i < len) {
-                        const uint32_t c = rd(R, i);
-                        if ((c == '\r' && i + 1 < len && b[i + 1] == '\n') || space_len(b, i, len, c)) { ended = true; break; }
-                        if (nt == 1) {
-                            if (clen < 16) cw[clen >> 2] |= c << ((clen & 3) * 8);
-                            clen++;
-                        } else if (key_tok) {
-                            keys_step(I, K, c);
+                TextLine T;
+                T.lf = 0;
+                T.found = false;
+                T.nt = 0;
+                T.cw[0] = T.cw[1] = T.cw[2] = T.cw[3] = 0;
+                T.clen = 0;
+                T.fr = F_NONE;
+                T.cmd_id = kMcOther;
+                T.a_ok = T.a_bad = T.a_neg = false;
+                T.a_n = 0;
+                T.a_v = 0;
+                if (text_ascii_spaces(b, len)) {
+                    text_fast<kNfa>(I, K, b, len, T);
+                } else {  // a possible multi-byte space: the byte-wise tokenizer
+                    Reader R{b, ~0ull, 0, 0, 0, 0};
+                    uint32_t i = 0;
+                    bool key_tok = false;         // current token is a key
+                    uint32_t kstart = 0;          // its first byte
+                    // One token per round: its bytes in a tight loop, then the
+                    // token-end work (command id, key DFA accept masks) once.
+                    for (;;) {
+                        bool tok = false;  // spaces up to the next token or the line end
+                        while (i < len) {
+                            const uint32_t c = rd(R, i);
+                            if (c == '\r' && i + 1 < len && b[i + 1] == '\n') { T.lf = i; T.found = true; break; }
+                            const uint32_t sp = space_len(b, i, len, c);
+                            if (!sp) { tok = true; break; }
+                            i += sp;
                         }
-                        if (fr == F_STORAGE && nt == 5) {
-                            if (a_n == 0 && (c == '+' || c == '-')) { a_neg = c == '-'; a_ok = false; /* until a digit */ }
-                            else if (c < '0' || c > '9') { a_ok = false; a_bad = true; }
-                            else {
-                                const uint64_t d = c - '0';
-                                if (a_v > (~0ull - d) / 10) a_bad = true;
-                                else a_v = a_v * 10 + d;
-                                if (a_v > 0x7FFFFFFFFFFFFFFFull + (a_neg ? 1u : 0u)) a_bad = true;
-                                a_ok = !a_bad;
+                        if (!tok) break;  // line end, or the data ends: incomplete
+                        T.nt++;
+                        key_tok = is_key_tok(T);
+                        kstart = i;
+                        bool ended = false;  // by a space or the line end (not consumed here)
+                        while (i < len) {
+                            const uint32_t c = rd(R, i);
+                            if ((c == '\r' && i + 1 < len && b[i + 1] == '\n') || space_len(b, i, len, c)) { ended = true; break; }
+                            if (T.nt == 1) {
+                                cmd_byte(T, c);
+                            } else if (key_tok) {
+                                keys_step(I, K, c);
                             }
-                            a_n++;
+                            if (T.fr == F_STORAGE && T.nt == 5) atoi_step(T, c);
+                            i++;
                         }
-                        i++;
+                        if (!ended) break;  // the data ends inside the token: incomplete
+                        if (T.nt == 1) classify_cmd(T.cw, T.clen, T.fr, T.cmd_id);
+                        if (key_tok) keys_end<kNfa>(I, K, b, kstart, i);
                     }
-                    if (!ended) break;  // the data ends inside the token: incomplete
-                    if (nt == 1) classify_cmd(cw, clen, fr, cmd_id);
-                    if (key_tok) keys_end<kNfa>(I, K, b, kstart, i);
                 }
-                if (!found) {  // MORE 1 if the data ends in '\r', else MORE 2
+                if (!T.found) {  // MORE 1 if the data ends in '\r', else MORE 2
                     verdict = V_INCOMPLETE;
                     consumed = (len > 0 && b[len - 1] == '\r') ? 1 : 2;
                     break;
                 }
+                const uint32_t nt = T.nt;
+                const int fr = T.fr;
                 if (nt == 0) break;  // tokens[0] panics
                 if (fr == F_BAD) break;  // ERROR, 0
                 if (fr == F_GAT && nt < 2) break;  // tokens[2:] panics
                 if ((fr == F_STORAGE || fr == F_KEY1) && nt < 2) break;  // tokens[1:2] panics
-                frame = (uint64_t)lf + 2;
+                frame = (uint64_t)T.lf + 2;
                 if (fr == F_STORAGE) {
                     if (nt < 5) break;  // tokens[4] panics
-                    if (!a_ok) break;
-                    const int64_t nb = a_neg ? (int64_t)(0 - a_v) : (int64_t)a_v;
+                    if (!T.a_ok) break;
+                    const int64_t nb = T.a_neg ? (int64_t)(0 - T.a_v) : (int64_t)T.a_v;
                     frame = frame + (uint64_t)nb + 2u;  // Go int arithmetic
                 }
-                cmdmask = u64at(I, hdr32(I, MC_OFF(text_off))) + (size_t)cmd_id * I.nch;
+                cmdmask = u64at(I, hdr32(I, MC_OFF(text_off))) + (size_t)T.cmd_id * I.nch;
             }
             staged = true;
         } while (false);
