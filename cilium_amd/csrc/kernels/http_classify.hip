@@ -65,7 +65,10 @@ namespace {
 #define L7G_HTTP_VMAP 1
 #endif
 #ifndef L7G_HTTP_MAPDEPTH  // 64-byte-per-lane map steps in flight (VGPR mode)
-#define L7G_HTTP_MAPDEPTH 4
+#define L7G_HTTP_MAPDEPTH 3
+#endif
+#ifndef L7G_HTTP_LPR  // lanes per request in the lane-mode map (4: 64-byte steps, 8: 128-byte steps)
+#define L7G_HTTP_LPR 8
 #endif
 #ifndef L7G_HTTP_FASTLINE  // header lines 16 bytes at a time (fast_line, the skip's LF check)
 #define L7G_HTTP_FASTLINE 1
@@ -1125,7 +1128,66 @@ __device__ __forceinline__ bool build_tile_map(TileMap &T, Lane &L, uint32_t lan
                                              16, 0, 0);                                                        \
         }                                                                                                      \
     } while (0)
-#if L7G_HTTP_VMAP
+#if L7G_HTTP_VMAP && L7G_HTTP_LPR == 8
+#undef MAP_ISSUE
+    // As below with eight lanes per request: a step is 128 bytes (a whole
+    // line) per request, load q covers requests 8q..8q+7, so every load
+    // instruction touches 8 full lines.
+    {
+        dma_windows_issue(wave_lds, window_packed(L), lane);
+        const uint32_t smax8 = (smax + 1) >> 1, skip8 = kWin / 128;
+        T.off = kMapChunks - 8 * smax8;
+        const uint32_t sub8 = lane & 7, grp8 = lane >> 3;
+        uint64_t qb8[8];
+        uint32_t qn8[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            qb8[q] = (uint64_t)__shfl((unsigned long long)L.base, 8 * q + (int)grp8);
+            qn8[q] = (uint32_t)__shfl((int)nch, 8 * q + (int)grp8);
+        }
+        constexpr int kMapDepth = L7G_HTTP_MAPDEPTH;
+        gm_u32x4 buf[kMapDepth][8];
+#define MAP_LOAD8(s, j)                                                                                        \
+    do {                                                                                                       \
+        _Pragma("unroll") for (int q_ = 0; q_ < 8; q_++) {                                                     \
+            const uint32_t c_ = 8 * (uint32_t)(j) + sub8;                                                      \
+            const uint64_t a_ = c_ < qn8[q_] ? qb8[q_] + ((uint64_t)c_ << 4) : dummy;                          \
+            asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(buf[s][q_]) : "v"(a_) : "memory");           \
+        }                                                                                                      \
+    } while (0)
+#pragma unroll
+        for (int s = 0; s < kMapDepth; s++) MAP_LOAD8(s, skip8 + (uint32_t)s);
+        for (uint32_t j0 = skip8; j0 < smax8; j0 += kMapDepth) {
+#pragma unroll
+            for (int s = 0; s < kMapDepth; s++) {
+                const uint32_t j = j0 + s;
+                asm volatile("s_waitcnt vmcnt(%8)"
+                             : "+v"(buf[s][0]), "+v"(buf[s][1]), "+v"(buf[s][2]), "+v"(buf[s][3]), "+v"(buf[s][4]),
+                               "+v"(buf[s][5]), "+v"(buf[s][6]), "+v"(buf[s][7])
+                             : "n"(8 * (kMapDepth - 1)));
+                // block q, bit l: request 8q + (l >> 3), chunk 8j + (l & 7)
+                uint64_t M[8];
+#pragma unroll
+                for (int q = 0; q < 8; q++) M[q] = __ballot(stop_any(u4(buf[s][q])) != 0);
+                MAP_LOAD8(s, j + kMapDepth);
+                if (j < smax8) {
+                    const uint32_t qo = lane >> 3;
+                    uint64_t Mq = M[0];
+#pragma unroll
+                    for (int q = 1; q < 8; q++) Mq = qo == (uint32_t)q ? M[q] : Mq;
+                    uint32_t nb = (uint32_t)(Mq >> (8 * (lane & 7))) & 0xFFu;
+                    if (8 * j >= nch) nb = 0;
+#pragma unroll
+                    for (int q = 0; q < (int)kMapWords - 1; q++) T.m[q] = __builtin_amdgcn_alignbit(T.m[q + 1], T.m[q], 8);
+                    T.m[kMapWords - 1] = (T.m[kMapWords - 1] >> 8) | (nb << 24);
+                }
+            }
+        }
+#undef MAP_LOAD8
+        wait_vmcnt<0>();
+        return true;
+    }
+#elif L7G_HTTP_VMAP
 #undef MAP_ISSUE
     // The head windows go into the window area now (the map does not use it),
     // so their DMA overlaps the map stream; the map's 64-byte steps land in
