@@ -204,23 +204,35 @@ struct DevKafkaRule {      // 24 B
     uint8_t has_topic;
     uint8_t pad[3];
 };
+static_assert(sizeof(DevKafkaRule) == 24, "DevKafkaRule layout");
+struct DevKafkaTopicEnt {  // 48 B: a rule set's rules of one topic (dense, by interned topic id)
+    uint32_t p0;           // position of the list's first rule
+    uint32_t off, cnt;     // the list: cnt u32 rule positions at index[off] (cnt 0: no rule)
+    uint32_t pad;
+    DevKafkaRule r0;       // rules[rule_first + p0]
+    uint32_t pad2[2];
+};
+static_assert(sizeof(DevKafkaTopicEnt) == 48, "DevKafkaTopicEnt layout");
 struct DevKafkaRuleset {   // 36 B
     uint32_t rule_first, nrules;     // rules in evaluation order
     uint32_t topicless_off, ntopicless;  // u32 rule positions (Topic == "") in index[]
     uint32_t topics_off, ntopics;    // sorted (topic_id, list_off, list_cnt) triples in index[]
     uint32_t bykey_off;              // 65 (off, cnt) pairs in index[]: key 0..63, 64 = other kinds
-    uint32_t tdense_off;             // (list_off, list_cnt) per interned topic id in index[]; ~0u = use the
+    uint32_t tdense_off;             // DevKafkaTopicEnt per interned topic id in index[]; ~0u = use the
                                      // sorted directory (rule set x topic count over the dense budget)
     uint8_t any;                     // rules.Kafka != nil (pkg/proxy/kafka.go:139-142)
     uint8_t pad[3];
 };
-struct DevStrSlot {        // 16 B open-addressing slot (topics, client ids)
-    uint32_t hash;         // FNV-1a (case-sensitive)
+struct DevStrSlot {        // 32 B open-addressing slot (topics, client ids)
+    uint32_t hash;         // l7_whash (case-sensitive)
     uint32_t str_off;
     uint16_t len;
     uint16_t used;
     int32_t id;
+    uint32_t pre[4];       // the string's first 16 bytes, zero-padded: a string of <= 16
+                           // bytes compares in the slot, without the string table
 };
+static_assert(sizeof(DevStrSlot) == 32, "DevStrSlot layout");
 // Topic / client-id hash of the Kafka string tables (host compiler and
 // kernel): the string's 32-bit little-endian words, the last one zero-padded,
 // then its length.  Strings sit 4-byte aligned and zero-padded in `strings`,

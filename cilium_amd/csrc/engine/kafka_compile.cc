@@ -1,6 +1,7 @@
 #include "kafka_compile.h"
 
 #include <algorithm>
+#include <cstring>
 
 namespace l7 {
 
@@ -34,6 +35,7 @@ void BuildHash(const std::unordered_map<std::string, int> &ids, std::vector<uint
         d.len = (uint16_t)s.size();
         d.used = 1;
         d.id = (int32_t)id;
+        memcpy(d.pre, s.data(), std::min<size_t>(s.size(), sizeof d.pre));
         strings.resize((strings.size() + 3) & ~(size_t)3, 0);  // 4-byte aligned, zero-padded
         d.str_off = (uint32_t)strings.size();
         strings.insert(strings.end(), s.begin(), s.end());
@@ -144,13 +146,22 @@ int KafkaCompiler::Compile(const std::vector<const KafkaRule *> &rules, bool any
     // Dense (off, cnt) per interned topic id: one lookup instead of a binary
     // search per request topic.  Bounded so many rule sets over many topics
     // keep to the sorted directory.
+    // Each entry (DevKafkaTopicEnt, 48 B, 16-byte aligned) also carries the
+    // list's first rule and its position, so the common case -- the first
+    // rule decides -- is one table read after the topic's hash probe.
     rs.tdense_off = ~0u;
-    if (!by_topic.empty() && I.index.size() + 2 * I.ntopics <= kDenseTopicBudget) {
+    constexpr size_t kEntU32 = sizeof(DevKafkaTopicEnt) / 4;
+    if (!by_topic.empty() && I.index.size() + 3 + kEntU32 * I.ntopics <= kDenseTopicBudget) {
+        I.index.resize((I.index.size() + 3) & ~(size_t)3, 0);
         rs.tdense_off = (uint32_t)I.index.size();
-        I.index.resize(I.index.size() + 2 * I.ntopics, 0);
+        I.index.resize(I.index.size() + kEntU32 * I.ntopics, 0);
         for (size_t t = 0; t < dir.size(); t += 3) {
-            I.index[rs.tdense_off + 2 * dir[t]] = dir[t + 1];
-            I.index[rs.tdense_off + 2 * dir[t] + 1] = dir[t + 2];
+            DevKafkaTopicEnt e{};
+            e.off = dir[t + 1];
+            e.cnt = dir[t + 2];
+            e.p0 = I.index[e.off];
+            e.r0 = I.rules[rs.rule_first + e.p0];
+            memcpy(&I.index[rs.tdense_off + kEntU32 * dir[t]], &e, sizeof e);
         }
     }
     std::vector<uint32_t> keydir;

@@ -77,23 +77,31 @@ __device__ __forceinline__ uint32_t le_load4(Cur &c, const uint8_t *p) {
 
 // Interned id of the request string s[0, n) (topic or client id), -1 if the
 // rule tables do not know it: word hash (l7_whash_*), linear probing, then a
-// word-wise compare against the 4-byte aligned, zero-padded table string.
+// word-wise compare: the first 16 bytes against the slot's copy (the words
+// were read for the hash), the rest against the 4-byte aligned, zero-padded
+// table string.
 __device__ __forceinline__ int32_t str_lookup(const DevStrSlot *tab, uint32_t mask, const uint8_t *strings, Cur &cur,
                                               const uint8_t *s, uint32_t n) {
     uint32_t h = kWHashSeed;
+    uint32_t p0 = 0, p1 = 0, p2 = 0, p3 = 0;  // the first 16 bytes, zero-padded
     for (uint32_t i = 0; i < n; i += 4) {
         const uint32_t r = n - i;
         const uint32_t keep = r >= 4 ? 0xFFFFFFFFu : (1u << (8 * r)) - 1u;
-        h = l7_whash_step(h, le_load4(cur, s + i) & keep);
+        const uint32_t w = le_load4(cur, s + i) & keep;
+        h = l7_whash_step(h, w);
+        p0 = i == 0 ? w : p0;
+        p1 = i == 4 ? w : p1;
+        p2 = i == 8 ? w : p2;
+        p3 = i == 12 ? w : p3;
     }
     h = l7_whash_final(h, n);
     for (uint32_t slot = h & mask;; slot = (slot + 1) & mask) {
         const DevStrSlot e = tab[slot];
         if (!e.used) return -1;
         if (e.hash == h && e.len == n) {
+            bool eq = e.pre[0] == p0 && e.pre[1] == p1 && e.pre[2] == p2 && e.pre[3] == p3;
             const uint32_t *t = reinterpret_cast<const uint32_t *>(strings + e.str_off);
-            bool eq = true;
-            for (uint32_t i = 0; i < n && eq; i += 4) {
+            for (uint32_t i = 16; i < n && eq; i += 4) {
                 const uint32_t r = n - i;
                 const uint32_t keep = r >= 4 ? 0xFFFFFFFFu : (1u << (8 * r)) - 1u;
                 eq = t[i >> 2] == (le_load4(cur, s + i) & keep);
@@ -133,9 +141,21 @@ __device__ __forceinline__ uint32_t topic_first(const KafkaTables &T, const DevK
     if (tid < 0 || rs.ntopics == 0) return kInf;
     uint32_t off, cnt;
     if (rs.tdense_off != ~0u) {
-        const uint2 e = *reinterpret_cast<const uint2 *>(T.index + rs.tdense_off + 2 * (uint32_t)tid);
-        off = e.x;
-        cnt = e.y;
+        const uint4 *ep = reinterpret_cast<const uint4 *>(T.index + rs.tdense_off +
+                                                          (uint32_t)(sizeof(DevKafkaTopicEnt) / 4) * (uint32_t)tid);
+        const uint4 e0 = ep[0], e1 = ep[1], e2 = ep[2];
+        off = e0.y;
+        cnt = e0.z;
+        if (cnt == 0) return kInf;
+        DevKafkaRule r0;
+        const uint32_t w[6] = {e1.x, e1.y, e1.z, e1.w, e2.x, e2.y};
+        __builtin_memcpy(&r0, w, sizeof r0);
+        if (rule_matches(r0, q)) return e0.x;
+        for (uint32_t i = 1; i < cnt; i++) {
+            uint32_t p = T.index[off + i];
+            if (rule_matches(T.rules[rs.rule_first + p], q)) return p;
+        }
+        return kInf;
     } else {
         const uint32_t *dir = T.index + rs.topics_off;
         uint32_t lo = 0, hi = rs.ntopics;
