@@ -33,6 +33,11 @@ namespace l7 {
 namespace {
 
 constexpr int kBlock = 256;
+// key DFAs walked per pass over the line (more DFAs: more passes)
+#ifndef L7G_MC_DFAS
+#define L7G_MC_DFAS 4
+#endif
+constexpr int kMcPassDfas = L7G_MC_DFAS < kMcMaxDfas ? L7G_MC_DFAS : kMcMaxDfas;
 constexpr uint32_t kMcLdsImages = 32 * 1024;  // LDS budget for the staged rule-set images
 // waves per SIMD the common kernel is built for (experiments: -DL7G_MC_WAVES=N)
 #ifndef L7G_MC_WAVES
@@ -59,26 +64,6 @@ __device__ __forceinline__ uint32_t rd(Reader &r, uint32_t i) {
     const uint32_t k = (uint32_t)(a >> 2) & 3;
     const uint32_t w = k == 0 ? r.w0 : k == 1 ? r.w1 : k == 2 ? r.w2 : r.w3;
     return (w >> ((a & 3) * 8)) & 0xFF;
-}
-
-// Length of the Unicode White_Space rune starting at b[i] (unicode.IsSpace),
-// 0 if none.  Multi-byte spaces begin with a UTF-8 lead byte, and a lead byte
-// is always a rune start when a buffer is decoded from its beginning, so the
-// test needs no decoding context (see oracle/memcache_ref.c mc_space_len).
-__device__ __forceinline__ uint32_t space_len(const uint8_t *b, uint32_t i, uint32_t len, uint32_t c) {
-    if (c == ' ' || (c >= 0x09 && c <= 0x0D)) return 1;
-    if (c < 0xC2 || c > 0xE3 || i + 1 >= len) return 0;
-    const uint32_t c1 = b[i + 1];
-    if (c == 0xC2) return (c1 == 0x85 || c1 == 0xA0) ? 2 : 0;
-    if (i + 2 >= len) return 0;
-    const uint32_t c2 = b[i + 2];
-    if (c == 0xE1) return (c1 == 0x9A && c2 == 0x80) ? 3 : 0;
-    if (c == 0xE2) {
-        if (c1 == 0x80) return ((c2 >= 0x80 && c2 <= 0x8A) || c2 == 0xA8 || c2 == 0xA9 || c2 == 0xAF) ? 3 : 0;
-        return (c1 == 0x81 && c2 == 0x9F) ? 3 : 0;
-    }
-    if (c == 0xE3) return (c1 == 0x80 && c2 == 0x80) ? 3 : 0;
-    return 0;
 }
 
 // text command name bytes packed little-endian into 4 words (compile-time)
@@ -122,13 +107,13 @@ __device__ __forceinline__ uint32_t hdr32(const Image &I, int byte_off) { return
 #define MC_OFF(field) ((int)offsetof(McImgHeader, field))
 
 struct Keys {
-    uint32_t st[kMcMaxDfas];   // DFA states of the key being read
+    uint32_t st[kMcPassDfas];   // DFA states of the key being read
     uint64_t all[kMcMaxChunks];  // AND over finished keys of their pass masks
 };
 
 __device__ __forceinline__ void keys_reset(const Image &I, Keys &K) {
 #pragma unroll
-    for (int d = 0; d < kMcMaxDfas; d++)
+    for (int d = 0; d < kMcPassDfas; d++)
         if ((uint32_t)d < I.dn) {
             const DevDfa *dd = (const DevDfa *)(I.p + kMcDfaOff) + I.d0 + d;
             K.st[d] = dd->start;
@@ -137,7 +122,7 @@ __device__ __forceinline__ void keys_reset(const Image &I, Keys &K) {
 
 __device__ __forceinline__ void keys_step(const Image &I, Keys &K, uint32_t c) {
 #pragma unroll
-    for (int d = 0; d < kMcMaxDfas; d++)
+    for (int d = 0; d < kMcPassDfas; d++)
         if ((uint32_t)d < I.dn && K.st[d] != 0) {
             const DevDfa *dd = (const DevDfa *)(I.p + kMcDfaOff) + I.d0 + d;
             const uint32_t cls = I.p[dd->cls_off + c];
@@ -171,7 +156,7 @@ __device__ __forceinline__ void keys_end(const Image &I, Keys &K, const uint8_t 
         if ((uint32_t)c >= I.nch) break;
         uint64_t own = 0, acc = 0;
 #pragma unroll
-        for (int d = 0; d < kMcMaxDfas; d++)
+        for (int d = 0; d < kMcPassDfas; d++)
             if ((uint32_t)d < I.dn) {
                 const DevDfa *dd = (const DevDfa *)(I.p + kMcDfaOff) + I.d0 + d;
                 own |= owned[(I.d0 + d) * I.nch + c];
@@ -225,32 +210,7 @@ __device__ __forceinline__ uint32_t chunk_byte(uint4 w, uint32_t q) {
     return __builtin_amdgcn_perm(hi, lo, (q & 7) | 0x0C0C0C00u);
 }
 
-// True when the command line (up to its first "\r\n", or all the data) holds
-// no byte that may start a multi-byte White_Space rune (0xC2, 0xE1, 0xE2,
-// 0xE3): text_fast's token masks are then exactly bytes.Fields' split.
-__device__ __forceinline__ bool text_ascii_spaces(const uint8_t *b, uint32_t len) {
-    const uint64_t a = (uint64_t)b;
-    const uint32_t a0 = (uint32_t)(a & 15);
-    const uint64_t base = a - a0;
-    const uint32_t end = a0 + len;
-    bool prev_cr = false;
-    for (uint32_t cb = 0; cb < end; cb += 16) {
-        const uint4 w = gload16(base + cb);
-        uint32_t valid = end >= cb + 16 ? 0xFFFFu : (1u << (end - cb)) - 1u;
-        if (cb == 0) valid &= 0xFFFFu << a0;
-        const uint32_t CR = eq_mask(w, '\r'), LF = eq_mask(w, '\n');
-        if (prev_cr && (LF & valid & 1u)) return true;
-        const uint32_t crlf = CR & (LF >> 1) & valid & (valid >> 1);
-        const uint32_t line = crlf ? valid & ((1u << __builtin_ctz(crlf)) - 1u) : valid;
-        const uint32_t H = eq_mask(w, 0xC2) | eq_mask(w, 0xE1) | eq_mask(w, 0xE2) | eq_mask(w, 0xE3);
-        if (H & line) return false;
-        if (crlf) return true;
-        prev_cr = (CR & valid) >> 15;
-    }
-    return true;
-}
-
-// Text command line state (the byte-wise and the SWAR tokenizer fill the same)
+// Text command line state
 struct TextLine {
     uint32_t lf;           // position of the line's "\r\n" (found)
     bool found;
@@ -295,9 +255,8 @@ __device__ __forceinline__ bool is_key_tok(const TextLine &T) {
 // CR and LF give the line end (the first "\r\n") and the token runs; only the
 // bytes of the tokens that matter are visited one by one (the command, the
 // keys through the key DFAs, tokens[4] of a storage command), every other
-// byte is passed over by mask.  Only for lines text_ascii_spaces accepts (a
-// byte that may start a multi-byte White_Space rune sends the line to the
-// byte-wise tokenizer).
+// byte is passed over by mask.  The split is exactly bytes.Fields' (Unicode
+// White_Space, multi-byte runes included).
 template <bool kNfa>
 __device__ __forceinline__ void text_fast(const Image &I, Keys &K, const uint8_t *b, uint32_t len, TextLine &T) {
     const uint64_t a = (uint64_t)b;
@@ -305,12 +264,44 @@ __device__ __forceinline__ void text_fast(const Image &I, Keys &K, const uint8_t
     const uint64_t base = a - a0;
     const uint32_t end = a0 + len;  // request bytes are chunk positions [a0, end)
     bool in_tok = false, key_tok = false, prev_cr = false;
-    uint32_t kstart = 0;
+    uint32_t kstart = 0, carry = 0;  // carry: bytes of this chunk that end a space rune begun in the last one
     for (uint32_t cb = 0; cb < end; cb += 16) {
         const uint4 w = gload16(base + cb);  // global, not flat (gmem.h)
         uint32_t valid = end >= cb + 16 ? 0xFFFFu : (1u << (end - cb)) - 1u;
         if (cb == 0) valid &= 0xFFFFu << a0;
-        const uint32_t S = ascii_space_mask(w), CR = eq_mask(w, '\r'), LF = eq_mask(w, '\n');
+        uint32_t S = ascii_space_mask(w) | carry;
+        const uint32_t CR = eq_mask(w, '\r'), LF = eq_mask(w, '\n');
+        carry = 0;
+        // multi-byte White_Space runes (unicode.IsSpace): U+0085, U+00A0 (C2 xx),
+        // U+1680 (E1 9A 80), U+2000-U+200A, U+2028, U+2029, U+202F (E2 80 xx),
+        // U+205F (E2 81 9F), U+3000 (E3 80 80).  Their lead bytes never continue
+        // another rune, so each is judged on its own, as bytes.Fields' decoder
+        // meets it (the bytes are in this chunk or the next)
+        uint32_t lead = (eq_mask(w, 0xC2) | eq_mask(w, 0xE1) | eq_mask(w, 0xE2) | eq_mask(w, 0xE3)) & valid;
+        if (lead) {
+            uint4 wn = make_uint4(0, 0, 0, 0);
+            if (lead >> 14 && cb + 16 < end) wn = gload16(base + cb + 16);  // holds a request byte: same page
+            while (lead) {
+                const uint32_t i = (uint32_t)__builtin_ctz(lead);
+                lead &= lead - 1;
+                const uint32_t r = cb + i - a0;  // request position
+                const uint32_t c0 = chunk_byte(w, i);
+                const uint32_t c1 = i + 1 < 16 ? chunk_byte(w, i + 1) : chunk_byte(wn, i - 15);
+                const uint32_t c2 = i + 2 < 16 ? chunk_byte(w, i + 2) : chunk_byte(wn, i - 14);
+                uint32_t L = 0;
+                if (c0 == 0xC2) {
+                    if (r + 1 < len && (c1 == 0x85 || c1 == 0xA0)) L = 2;
+                } else if (r + 2 < len) {
+                    if ((c0 == 0xE1 && c1 == 0x9A && c2 == 0x80) || (c0 == 0xE3 && c1 == 0x80 && c2 == 0x80) ||
+                        (c0 == 0xE2 && ((c1 == 0x80 && ((c2 >= 0x80 && c2 <= 0x8A) || c2 == 0xA8 || c2 == 0xA9 || c2 == 0xAF)) ||
+                                        (c1 == 0x81 && c2 == 0x9F))))
+                        L = 3;
+                }
+                const uint32_t bits = ((1u << L) - 1u) << i;
+                S |= bits & 0xFFFFu;
+                carry |= bits >> 16;
+            }
+        }
         // the line end: a CR whose next byte is LF (the CR possibly the previous chunk's last byte)
         uint32_t le = 16;  // first byte of "\r\n" in this chunk (16: none; -1 handled by prev_cr)
         bool ended = false;
@@ -425,11 +416,11 @@ __device__ __forceinline__ void mc_loop(Batch B, McTables T, const uint8_t *imag
         uint64_t frame = 0;
         bool staged = false;  // framing succeeded: match against the rules
         // More key DFAs than one pass walks: re-read the request once per
-        // group of kMcMaxDfas (framing is identical in every pass).
+        // group of kMcPassDfas (framing is identical in every pass).
         if (!in_arena) verdict = V_UNSUPPORTED;  // out of contract: nothing is read
-        for (uint32_t d0 = 0; in_arena; d0 += kMcMaxDfas) {
+        for (uint32_t d0 = 0; in_arena; d0 += kMcPassDfas) {
         I.d0 = d0;
-        I.dn = I.ndfa - d0 < (uint32_t)kMcMaxDfas ? I.ndfa - d0 : (uint32_t)kMcMaxDfas;
+        I.dn = I.ndfa - d0 < (uint32_t)kMcPassDfas ? I.ndfa - d0 : (uint32_t)kMcPassDfas;
         keys_reset(I, K);
         do {
             uint32_t mode = conn.flags & 3;
@@ -465,45 +456,7 @@ __device__ __forceinline__ void mc_loop(Batch B, McTables T, const uint8_t *imag
                 T.a_ok = T.a_bad = T.a_neg = false;
                 T.a_n = 0;
                 T.a_v = 0;
-                if (text_ascii_spaces(b, len)) {
-                    text_fast<kNfa>(I, K, b, len, T);
-                } else {  // a possible multi-byte space: the byte-wise tokenizer
-                    Reader R{b, ~0ull, 0, 0, 0, 0};
-                    uint32_t i = 0;
-                    bool key_tok = false;         // current token is a key
-                    uint32_t kstart = 0;          // its first byte
-                    // One token per round: its bytes in a tight loop, then the
-                    // token-end work (command id, key DFA accept masks) once.
-                    for (;;) {
-                        bool tok = false;  // spaces up to the next token or the line end
-                        while (i < len) {
-                            const uint32_t c = rd(R, i);
-                            if (c == '\r' && i + 1 < len && b[i + 1] == '\n') { T.lf = i; T.found = true; break; }
-                            const uint32_t sp = space_len(b, i, len, c);
-                            if (!sp) { tok = true; break; }
-                            i += sp;
-                        }
-                        if (!tok) break;  // line end, or the data ends: incomplete
-                        T.nt++;
-                        key_tok = is_key_tok(T);
-                        kstart = i;
-                        bool ended = false;  // by a space or the line end (not consumed here)
-                        while (i < len) {
-                            const uint32_t c = rd(R, i);
-                            if ((c == '\r' && i + 1 < len && b[i + 1] == '\n') || space_len(b, i, len, c)) { ended = true; break; }
-                            if (T.nt == 1) {
-                                cmd_byte(T, c);
-                            } else if (key_tok) {
-                                keys_step(I, K, c);
-                            }
-                            if (T.fr == F_STORAGE && T.nt == 5) atoi_step(T, c);
-                            i++;
-                        }
-                        if (!ended) break;  // the data ends inside the token: incomplete
-                        if (T.nt == 1) classify_cmd(T.cw, T.clen, T.fr, T.cmd_id);
-                        if (key_tok) keys_end<kNfa>(I, K, b, kstart, i);
-                    }
-                }
+                text_fast<kNfa>(I, K, b, len, T);
                 if (!T.found) {  // MORE 1 if the data ends in '\r', else MORE 2
                     verdict = V_INCOMPLETE;
                     consumed = (len > 0 && b[len - 1] == '\r') ? 1 : 2;
@@ -526,7 +479,7 @@ __device__ __forceinline__ void mc_loop(Batch B, McTables T, const uint8_t *imag
             }
             staged = true;
         } while (false);
-        if (!staged || d0 + kMcMaxDfas >= I.ndfa) break;
+        if (!staged || d0 + kMcPassDfas >= I.ndfa) break;
         }
         do {
             if (!staged) break;
