@@ -35,7 +35,7 @@ namespace {
 constexpr int kBlock = 256;
 // key DFAs walked per pass over the line (more DFAs: more passes)
 #ifndef L7G_MC_DFAS
-#define L7G_MC_DFAS 4
+#define L7G_MC_DFAS 1
 #endif
 constexpr int kMcPassDfas = L7G_MC_DFAS < kMcMaxDfas ? L7G_MC_DFAS : kMcMaxDfas;
 constexpr uint32_t kMcLdsImages = 32 * 1024;  // LDS budget for the staged rule-set images
