@@ -27,9 +27,10 @@
 
 namespace l7 {
 hipError_t LaunchHttpClassify(const Batch &B, const HttpTables &T, const uint32_t *sel, const uint32_t *sel_count,
-                              bool any_cold, bool answer_other, hipStream_t stream);
+                              bool any_cold, bool answer_other, uint32_t *tile_ctr, hipStream_t stream);
 hipError_t LaunchKafkaClassify(const Batch &B, const KafkaTables &T, const uint32_t *sel, const uint32_t *sel_count,
-                               bool answer_other, uint32_t *zlist, uint32_t *zcount, hipStream_t stream);
+                               bool answer_other, uint32_t *zlist, uint32_t *zcount, uint32_t *work,
+                               hipStream_t stream);
 hipError_t LaunchKafkaInflate(const Batch &B, const uint32_t *zlist, const uint32_t *zcount, uint8_t *region,
                               hipStream_t stream);
 uint32_t KafkaInflateBlocks();
@@ -71,6 +72,8 @@ struct StreamScratch {
     // cassandra USE list: [count | n request indices] (grow-only)
     uint32_t *d_use = nullptr;
     size_t use_cap = 0;
+    // work counters of unpartitioned batches (HTTP tile counters), allocated on first use
+    uint32_t *d_work = nullptr;
     // completion of the last call's kernels on this stream
     hipEvent_t done_ev = nullptr;
     bool launched = false;
@@ -80,10 +83,12 @@ struct StreamScratch {
         if (d_nfa) hipFree(d_nfa);
         if (d_hist) hipFree(d_hist);
         if (d_use) hipFree(d_use);
+        if (d_work) hipFree(d_work);
         if (done_ev) hipEventDestroy(done_ev);
     }
 };
-constexpr size_t kMaxStreamScratch = 16;  // beyond: the least recently used one is handed over
+constexpr size_t kMaxStreamScratch = 16;
+constexpr uint32_t kDynTilesMin = 1u << 18;  // unpartitioned HTTP batches from this size take tiles from a counter  // beyond: the least recently used one is handed over
 
 // l7g_classify_host's per-thread staging: its own stream, device arena and
 // request arrays (grow-only), so host-buffer calls from different threads
@@ -348,6 +353,7 @@ hipError_t Upload(l7g_engine *e) {
         MT.nrulesets = (uint32_t)M.rulesets.size();
         MT.images_len = (uint32_t)M.images.size();
         MT.nfa_pool = M.nfa_pool.empty() ? nullptr : d + m_nfa;
+        MT.max_chunks = (uint32_t)M.max_chunks;
         R2Tables &RT = e->rt;
         RT.rulesets = (const DevRuleset *)(d + r_rs);
         RT.images = d + r_img;
@@ -587,7 +593,9 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
             if (rc == hipSuccess) S->sel_cap = need;
         }
         if (rc != hipSuccess) return (int)rc;
-        cnt = S->d_sel;  // [0, L7_KAFKA_CLASSES) Kafka classes, memcached retrievals, binary, HTTP, other text; [31] compressed Kafka
+        // [0, L7_KAFKA_CLASSES) Kafka classes, memcached retrievals, binary, HTTP, other text;
+        // [28, 29] HTTP tile counters (hot, general launch), [30] Kafka work counter; [31] compressed Kafka
+        cnt = S->d_sel;
         sel_k = S->d_sel + 32;
         sel_m = sel_k + L7_KAFKA_CLASSES * (size_t)n;
         sel_h = sel_m + (size_t)n;
@@ -627,11 +635,22 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
     if (rc == hipSuccess && run[0]) rc = LaunchPartition(B, sel_k, sel_m, sel_h, cnt, s);
     mark(1);
     if (rc == hipSuccess && run[1] && nfa) rc = LaunchHttpNfa(B, ht, s);
+    // tile counters: in the partition counts (zeroed above), or, for a large
+    // unpartitioned batch, two words zeroed here (a small batch keeps the fixed
+    // stride and saves the memset)
+    uint32_t *tile_ctr = cnt ? cnt + 28 : nullptr;
+    if (rc == hipSuccess && run[1] && !cnt && n >= kDynTilesMin) {
+        if (!S->d_work) rc = hipMalloc(&S->d_work, 4 * sizeof(uint32_t));
+        if (rc == hipSuccess) rc = hipMemsetAsync(S->d_work, 0, 2 * sizeof(uint32_t), s);
+        tile_ctr = S->d_work;
+    }
     if (rc == hipSuccess && run[1])
-        rc = LaunchHttpClassify(B, ht, sel_h, cnt ? cnt + L7_KAFKA_CLASSES + 2 : nullptr, e->any_cold, !partitioned, s);
+        rc = LaunchHttpClassify(B, ht, sel_h, cnt ? cnt + L7_KAFKA_CLASSES + 2 : nullptr, e->any_cold, !partitioned,
+                                tile_ctr, s);
     mark(2);
     uint32_t *zcount = cnt ? cnt + 31 : nullptr;
-    if (rc == hipSuccess && run[2]) rc = LaunchKafkaClassify(B, e->kt, sel_k, cnt, !partitioned, sel_z, zcount, s);
+    if (rc == hipSuccess && run[2])
+        rc = LaunchKafkaClassify(B, e->kt, sel_k, cnt, !partitioned, sel_z, zcount, cnt ? cnt + 30 : nullptr, s);
     // requests with gzip / snappy messages: decoded, their sets read, failures answered
     if (rc == hipSuccess && run[2] && sel_z) {
         // the engine's one decode region: after the previous inflate launch on any stream

@@ -300,6 +300,7 @@ struct McTables {
     uint32_t nrulesets;
     uint32_t images_len;       // bytes of all images (staged in LDS when they fit)
     const uint8_t *nfa_pool;   // DevNfa pool (null: no keyRegex on the NFA fallback)
+    uint32_t max_chunks;       // most 64-rule chunks of any rule set (1: the one-chunk kernel)
 };
 
 // ---------------- r2d2 ----------------

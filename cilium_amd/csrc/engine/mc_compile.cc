@@ -219,6 +219,7 @@ int McCompiler::Compile(const std::vector<const McRule *> &rules, uint8_t termin
     I.images.insert(I.images.end(), img.begin(), img.end());
     I.rulesets.push_back(rs);
     I.rules += nr;
+    I.max_chunks = std::max(I.max_chunks, nch);
     I.dfas += dfas.size();
     I.dfa_states += states;
     return (int)I.rulesets.size() - 1;

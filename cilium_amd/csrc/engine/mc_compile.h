@@ -25,6 +25,7 @@ struct McImage {
     std::vector<uint8_t> images;
     std::vector<uint8_t> nfa_pool;  // DevNfa tables of keyRegex patterns over the DFA budget
     size_t rules = 0, dfas = 0, dfa_states = 0, nfas = 0;
+    size_t max_chunks = 0;  // most 64-rule chunks of any rule set (selects the kernel instantiation)
 };
 
 class McCompiler {

@@ -73,6 +73,9 @@ namespace {
 #ifndef L7G_HTTP_FASTLINE  // header lines 16 bytes at a time (fast_line, the skip's LF check)
 #define L7G_HTTP_FASTLINE 1
 #endif
+#ifndef L7G_HTTP_DYN  // tiles after the first from a per-launch counter (0: static stride; 1: taken at the tile's start; 2: at its end)
+#define L7G_HTTP_DYN 2
+#endif
 constexpr int kWaves = L7G_HTTP_WAVES;
 constexpr int kBlock = 64 * kWaves;
 constexpr uint32_t kWin = L7G_HTTP_WIN;        // bytes per lane window
@@ -1430,7 +1433,7 @@ __device__ __forceinline__ void run_tile(Lane &L, const uint8_t *img, uint8_t *w
 template <bool kHot>
 __global__ __launch_bounds__(kBlock) void http_classify_kernel(Batch B, HttpTables T, const uint32_t *__restrict__ sel,
                                                                const uint32_t *__restrict__ sel_count,
-                                                               uint32_t answer_other) {
+                                                               uint32_t answer_other, uint32_t *__restrict__ tile_ctr) {
     const uint8_t *__restrict__ arena = B.arena;
     const uint32_t n = B.n, nconns = B.nconns;
     __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
@@ -1454,7 +1457,23 @@ __global__ __launch_bounds__(kBlock) void http_classify_kernel(Batch B, HttpTabl
     uint8_t *wave_lds = lds + wave * kWaveLds;
     const uint32_t m = sel ? *sel_count : n;
     const uint32_t ntiles = (m + 63) / 64;
-    for (uint32_t tile = blockIdx.x * kWaves + wave; tile < ntiles; tile += gridDim.x * kWaves) {
+    // Tiles: the first by position, the rest (when the launcher passes a zeroed
+    // counter) taken one at a time by whichever wave is free, so the waves of
+    // the persistent grid finish together whatever their tiles cost; else a
+    // fixed stride.
+    const uint32_t stride = gridDim.x * kWaves;
+    for (uint32_t tile = blockIdx.x * kWaves + wave, next; tile < ntiles; tile = next) {
+#if L7G_HTTP_DYN == 1
+        if (tile_ctr) {
+            uint32_t t = 0;
+            if (lane == 0) t = atomicAdd(tile_ctr, 1u);
+            next = stride + __builtin_amdgcn_readfirstlane(t);
+        } else {
+            next = tile + stride;
+        }
+#else
+        next = tile + stride;
+#endif
         Lane L;
         const uint32_t slot = tile * 64 + lane;
         L.idx = sel ? (slot < m ? sel[slot] : n) : slot;
@@ -1493,6 +1512,13 @@ __global__ __launch_bounds__(kBlock) void http_classify_kernel(Batch B, HttpTabl
             }
         }
         run_tile<kHot>(L, img, wave_lds, lane, O);
+#if L7G_HTTP_DYN == 2
+        if (tile_ctr) {
+            uint32_t t = 0;
+            if (lane == 0) t = atomicAdd(tile_ctr, 1u);
+            next = stride + __builtin_amdgcn_readfirstlane(t);
+        }
+#endif
     }
 }
 
@@ -1500,7 +1526,7 @@ __global__ __launch_bounds__(kBlock) void http_classify_kernel(Batch B, HttpTabl
 // 512-thread workgroup per CU; the hot-rule-set kernel, then (only if some
 // HTTP connection uses another rule set) the general one.
 hipError_t LaunchHttpClassify(const Batch &B, const HttpTables &T, const uint32_t *sel, const uint32_t *sel_count,
-                              bool any_cold, bool answer_other, hipStream_t stream) {
+                              bool any_cold, bool answer_other, uint32_t *tile_ctr, hipStream_t stream) {
     if (B.n == 0) return hipSuccess;
     static int num_cus = 0;
     if (num_cus == 0) {
@@ -1514,10 +1540,13 @@ hipError_t LaunchHttpClassify(const Batch &B, const HttpTables &T, const uint32_
     blocks = min(blocks, (uint32_t)num_cus);
     const bool hot = T.hot_ruleset >= 0;
     const uint32_t other = answer_other ? 1u : 0u;
+    // tile_ctr: two zeroed counters (hot, general launch) or null (fixed stride)
     if (hot)
-        hipLaunchKernelGGL(http_classify_kernel<true>, dim3(blocks), dim3(kBlock), 0, stream, B, T, sel, sel_count, other);
+        hipLaunchKernelGGL(http_classify_kernel<true>, dim3(blocks), dim3(kBlock), 0, stream, B, T, sel, sel_count, other,
+                           tile_ctr);
     if (!hot || any_cold)
-        hipLaunchKernelGGL(http_classify_kernel<false>, dim3(blocks), dim3(kBlock), 0, stream, B, T, sel, sel_count, other);
+        hipLaunchKernelGGL(http_classify_kernel<false>, dim3(blocks), dim3(kBlock), 0, stream, B, T, sel, sel_count, other,
+                           tile_ctr ? tile_ctr + 1 : nullptr);
     return hipGetLastError();
 }
 

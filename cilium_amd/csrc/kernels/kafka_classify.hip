@@ -19,7 +19,10 @@ namespace l7 {
 
 namespace {
 
-constexpr int kBlock = 256;
+#ifndef L7G_KAFKA_BLOCK  // threads per workgroup: the CRC tables are shared by its waves
+#define L7G_KAFKA_BLOCK 512
+#endif
+constexpr int kBlock = L7G_KAFKA_BLOCK;
 
 // readMessageSet on the shared position; 0 ok, -1 error; zflag is set when a
 // compressed message was passed
@@ -183,32 +186,30 @@ __device__ __forceinline__ uint32_t topic_first(const KafkaTables &T, const DevK
 #define L7G_KAFKA_WAVES 6
 #endif
 #ifndef L7G_KAFKA_MAX_BLOCKS
-#define L7G_KAFKA_MAX_BLOCKS 8192  // grid-stride beyond this
+#define L7G_KAFKA_MAX_BLOCKS 8192  // grid-stride beyond this (fixed-stride launches)
+#endif
+#ifndef L7G_KAFKA_DYN  // persistent grid, waves take 64 entries at a time from a per-launch counter
+#define L7G_KAFKA_DYN 1
+#endif
+#ifndef L7G_KAFKA_GRIDMUL  // fixed-stride launches: grid = this many rounds of resident workgroups (0: L7G_KAFKA_MAX_BLOCKS cap)
+#define L7G_KAFKA_GRIDMUL 0
+#endif
+#ifndef L7G_KAFKA_ORDER  // 1: the length classes longest first (the long requests start first, the short ones fill the tail)
+#define L7G_KAFKA_ORDER 1
 #endif
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(L7G_KAFKA_WAVES, 8))) void kafka_classify_kernel(
     Batch B, KafkaTables T, const uint32_t *__restrict__ sel, const uint32_t *__restrict__ sel_count,
-    uint32_t answer_other, uint32_t *__restrict__ zlist, uint32_t *__restrict__ zcount) {
+    uint32_t answer_other, uint32_t *__restrict__ zlist, uint32_t *__restrict__ zcount, uint32_t *__restrict__ work) {
     const uint32_t n = B.n, nconns = B.nconns;
     const uint8_t *__restrict__ arena = B.arena;
     const uint32_t *__restrict__ conn_ids = B.conn_ids;
     const DevConn *__restrict__ conns = B.conns;
-    static_assert(kBlock == 256, "one CRC table entry per thread");
-    __shared__ uint32_t crctab[kCrcSlices * 256];
+    static_assert(kBlock >= 256, "one CRC table entry per thread");
+    __shared__ uint32_t crctab[kCrcTables * 256];
     // per wave: the CRC's 64-byte-per-lane staging area (crc32_ieee_staged)
     __shared__ __attribute__((aligned(16))) uint8_t crcstage[kBlock / 64][4096];
     uint8_t *stage = crcstage[threadIdx.x >> 6];
-    {
-        const uint32_t t = threadIdx.x;
-        uint32_t c = t;
-        for (int k = 0; k < 8; k++) c = (c & 1) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
-        crctab[t] = c;
-        __syncthreads();
-        for (int k = 1; k < kCrcSlices; k++) {
-            const uint32_t prev = crctab[(k - 1) * 256 + t];
-            crctab[k * 256 + t] = (prev >> 8) ^ crctab[prev & 0xFF];
-            __syncthreads();
-        }
-    }
+    crc_tables_init(crctab, threadIdx.x);
     // sel: this protocol's request indices from partition_kernel (mixed batches), else all n
     // (L7_KAFKA_CLASSES length classes, class c at sel + c * n, sel_count[c] entries each)
     constexpr int kCls = L7_KAFKA_CLASSES;
@@ -218,11 +219,33 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(L7G_KAFK
         m = 0;
         for (int c = 0; c < kCls; c++) { kc[c] = sel_count[c]; m += kc[c]; }
     }
+#if L7G_KAFKA_DYN
+    // Entries after the grid's first sweep are taken 64 at a time (one per
+    // lane) by whichever wave is free, from a per-launch counter the launcher
+    // zeroes, so the persistent grid's waves finish together; else (no
+    // counter) a fixed stride.  A lane whose entry is past the list end has no
+    // later one either, so the loop may run divergent.
+    const uint32_t stride = gridDim.x * kBlock;
+    auto next_entry = [&](uint32_t i) -> uint32_t {
+        if (!work) return i + stride;
+        const uint32_t lane = threadIdx.x & 63;
+        uint32_t t = 0;
+        if (lane == (uint32_t)__builtin_amdgcn_readfirstlane(lane)) t = atomicAdd(work, 64u);
+        return stride + __builtin_amdgcn_readfirstlane(t) + lane;
+    };
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < m; i = next_entry(i)) {
+#else
     for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < m; i += gridDim.x * kBlock) {
+#endif
         uint32_t idx = i;
         if (sel) {
+#if L7G_KAFKA_ORDER == 1
+            uint32_t c = kCls - 1, j = i;
+            while (c > 0 && j >= kc[c]) { j -= kc[c]; c--; }
+#else
             uint32_t c = 0, j = i;
             while (c < kCls - 1 && j >= kc[c]) { j -= kc[c]; c++; }
+#endif
             idx = sel[(size_t)c * n + j];
         }
         const uint32_t ci = conn_ids[idx];
@@ -415,12 +438,46 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(L7G_KAFK
 hipError_t KafkaPhaseTimes(uint64_t *, bool) { return hipErrorNotSupported; }
 
 hipError_t LaunchKafkaClassify(const Batch &B, const KafkaTables &T, const uint32_t *sel, const uint32_t *sel_count,
-                               bool answer_other, uint32_t *zlist, uint32_t *zcount, hipStream_t stream) {
+                               bool answer_other, uint32_t *zlist, uint32_t *zcount, uint32_t *work,
+                               hipStream_t stream) {
     if (B.n == 0) return hipSuccess;
     uint32_t blocks = (B.n + kBlock - 1) / kBlock;
+#if L7G_KAFKA_DYN
+    // persistent grid: as many workgroups as the CUs hold at once
+    static int resident = 0;
+    if (resident == 0) {
+        int dev = 0, cus = 0, per_cu = 0;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kafka_classify_kernel, kBlock, 0) == hipSuccess &&
+            cus > 0 && per_cu > 0)
+            resident = cus * per_cu;
+        else
+            resident = L7G_KAFKA_MAX_BLOCKS;
+    }
+    if (!work) blocks = blocks > L7G_KAFKA_MAX_BLOCKS ? L7G_KAFKA_MAX_BLOCKS : blocks;
+    else if (blocks > (uint32_t)resident) blocks = (uint32_t)resident;
+#else
+    work = nullptr;
+#if L7G_KAFKA_GRIDMUL
+    static int resident = 0;
+    if (resident == 0) {
+        int dev = 0, cus = 0, per_cu = 0;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kafka_classify_kernel, kBlock, 0) == hipSuccess &&
+            cus > 0 && per_cu > 0)
+            resident = cus * per_cu * L7G_KAFKA_GRIDMUL;
+        else
+            resident = L7G_KAFKA_MAX_BLOCKS;
+    }
+    if (blocks > (uint32_t)resident) blocks = (uint32_t)resident;
+#else
     if (blocks > L7G_KAFKA_MAX_BLOCKS) blocks = L7G_KAFKA_MAX_BLOCKS;
+#endif
+#endif
     hipLaunchKernelGGL(kafka_classify_kernel, dim3(blocks), dim3(kBlock), 0, stream, B, T, sel, sel_count,
-                       answer_other ? 1u : 0u, zlist, zcount);
+                       answer_other ? 1u : 0u, zlist, zcount, work);
     return hipGetLastError();
 }
 

@@ -43,7 +43,6 @@ constexpr uint32_t kMcLdsImages = 32 * 1024;  // LDS budget for the staged rule-
 #ifndef L7G_MC_WAVES
 #define L7G_MC_WAVES 5
 #endif
-#define L7G_MC_OCCUPANCY __attribute__((amdgpu_waves_per_eu(L7G_MC_WAVES, 8)))
 
 // 16-byte aligned register window over one request (the arena is readable up
 // to the 16-byte boundary after its last byte; see include/l7gpu.h).
@@ -106,12 +105,14 @@ __device__ __forceinline__ uint32_t hdr32(const Image &I, int byte_off) { return
 
 #define MC_OFF(field) ((int)offsetof(McImgHeader, field))
 
+template <int kCh>
 struct Keys {
     uint32_t st[kMcPassDfas];   // DFA states of the key being read
-    uint64_t all[kMcMaxChunks];  // AND over finished keys of their pass masks
+    uint64_t all[kCh];          // AND over finished keys of their pass masks
 };
 
-__device__ __forceinline__ void keys_reset(const Image &I, Keys &K) {
+template <int kCh>
+__device__ __forceinline__ void keys_reset(const Image &I, Keys<kCh> &K) {
 #pragma unroll
     for (int d = 0; d < kMcPassDfas; d++)
         if ((uint32_t)d < I.dn) {
@@ -120,7 +121,8 @@ __device__ __forceinline__ void keys_reset(const Image &I, Keys &K) {
         }
 }
 
-__device__ __forceinline__ void keys_step(const Image &I, Keys &K, uint32_t c) {
+template <int kCh>
+__device__ __forceinline__ void keys_step(const Image &I, Keys<kCh> &K, uint32_t c) {
 #pragma unroll
     for (int d = 0; d < kMcPassDfas; d++)
         if ((uint32_t)d < I.dn && K.st[d] != 0) {
@@ -135,24 +137,25 @@ __device__ __forceinline__ void keys_step(const Image &I, Keys &K, uint32_t c) {
 // pass owns it) or one of the pass's DFAs accepts the key.  The first pass
 // also runs the NFA-fallback matchers over the key bytes b[k0, k1): a rule
 // whose predicate one of them is fails if it rejects the key.
-__device__ __forceinline__ void keys_nfa(const Image &I, Keys &K, const uint8_t *b, uint32_t k0, uint32_t k1) {
+template <int kCh>
+__device__ __forceinline__ void keys_nfa(const Image &I, Keys<kCh> &K, const uint8_t *b, uint32_t k0, uint32_t k1) {
     const DevNfaRef *refs = (const DevNfaRef *)(I.p + hdr32(I, MC_OFF(nfa_off)));
     for (uint32_t k = 0; k < I.nnfa; k++) {
         const DevNfaRef ref = refs[k];
         if (nfa_run(I.nfa_pool, ref.nfa, b + k0, k1 - k0)) continue;
         const uint64_t *own = u64at(I, ref.mask_off);
 #pragma unroll
-        for (int c = 0; c < kMcMaxChunks; c++)
+        for (int c = 0; c < kCh; c++)
             if ((uint32_t)c < I.nch) K.all[c] &= ~own[c];
     }
 }
 
-template <bool kNfa>
-__device__ __forceinline__ void keys_end(const Image &I, Keys &K, const uint8_t *b, uint32_t k0, uint32_t k1) {
+template <bool kNfa, int kCh>
+__device__ __forceinline__ void keys_end(const Image &I, Keys<kCh> &K, const uint8_t *b, uint32_t k0, uint32_t k1) {
     if (kNfa && I.nnfa && I.d0 == 0) keys_nfa(I, K, b, k0, k1);
     const uint64_t *owned = u64at(I, hdr32(I, MC_OFF(owned_off)));
 #pragma unroll
-    for (int c = 0; c < kMcMaxChunks; c++) {
+    for (int c = 0; c < kCh; c++) {
         if ((uint32_t)c >= I.nch) break;
         uint64_t own = 0, acc = 0;
 #pragma unroll
@@ -257,8 +260,8 @@ __device__ __forceinline__ bool is_key_tok(const TextLine &T) {
 // keys through the key DFAs, tokens[4] of a storage command), every other
 // byte is passed over by mask.  The split is exactly bytes.Fields' (Unicode
 // White_Space, multi-byte runes included).
-template <bool kNfa>
-__device__ __forceinline__ void text_fast(const Image &I, Keys &K, const uint8_t *b, uint32_t len, TextLine &T) {
+template <bool kNfa, int kCh>
+__device__ __forceinline__ void text_fast(const Image &I, Keys<kCh> &K, const uint8_t *b, uint32_t len, TextLine &T) {
     const uint64_t a = (uint64_t)b;
     const uint32_t a0 = (uint32_t)(a & 15);
     const uint64_t base = a - a0;
@@ -345,7 +348,7 @@ __device__ __forceinline__ void text_fast(const Image &I, Keys &K, const uint8_t
             const bool closes = e < 16 && (((line >> e) & 1u) || (ended && e == le));
             if (!closes) break;  // it runs on into the next chunk (or the data ends)
             if (T.nt == 1) classify_cmd(T.cw, T.clen, T.fr, T.cmd_id);
-            if (key_tok) keys_end<kNfa>(I, K, b, kstart, cb + e - a0);
+            if (key_tok) keys_end<kNfa, kCh>(I, K, b, kstart, cb + e - a0);
             in_tok = false;
             q = e;
         }
@@ -365,7 +368,7 @@ __device__ __forceinline__ void text_fast(const Image &I, Keys &K, const uint8_t
 // kLds: `images` is the workgroup's LDS copy.  The two cases are separate
 // instantiations so that every image read compiles to a ds_read (LDS) or a
 // global_load: one pointer that may be either makes them all flat loads.
-template <bool kNfa, bool kLds>
+template <bool kNfa, bool kLds, int kCh>
 __device__ __forceinline__ void mc_loop(Batch B, McTables T, const uint8_t *images, const uint32_t *__restrict__ sel,
                                         const uint32_t *__restrict__ sel2, const uint32_t *__restrict__ sel_count,
                                         uint32_t answer_other) {
@@ -409,9 +412,9 @@ __device__ __forceinline__ void mc_loop(Batch B, McTables T, const uint8_t *imag
         int32_t rule = -1;
         uint32_t consumed = 0;
         const bool in_arena = l7_in_arena(off, len, B.arena_len);
-        Keys K;
+        Keys<kCh> K;
 #pragma unroll
-        for (int c = 0; c < kMcMaxChunks; c++) K.all[c] = ~0ull;
+        for (int c = 0; c < kCh; c++) K.all[c] = ~0ull;
         const uint64_t *cmdmask = nullptr;
         uint64_t frame = 0;
         bool staged = false;  // framing succeeded: match against the rules
@@ -441,7 +444,7 @@ __device__ __forceinline__ void mc_loop(Batch B, McTables T, const uint8_t *imag
                 cmdmask = u64at(I, hdr32(I, MC_OFF(op_off))) + (size_t)b[1] * I.nch;
                 Reader R{b, ~0ull, 0, 0, 0, 0};
                 for (uint32_t i = 24 + extras, e = 24 + extras + keylen; i < e; i++) keys_step(I, K, rd(R, i));
-                keys_end<kNfa>(I, K, b, 24 + extras, 24 + extras + keylen);
+                keys_end<kNfa, kCh>(I, K, b, 24 + extras, 24 + extras + keylen);
                 frame = (uint32_t)(body + 24u);  // uint32 arithmetic, then int()
             } else {
                 // ---- text command line
@@ -456,7 +459,7 @@ __device__ __forceinline__ void mc_loop(Batch B, McTables T, const uint8_t *imag
                 T.a_ok = T.a_bad = T.a_neg = false;
                 T.a_n = 0;
                 T.a_v = 0;
-                text_fast<kNfa>(I, K, b, len, T);
+                text_fast<kNfa, kCh>(I, K, b, len, T);
                 if (!T.found) {  // MORE 1 if the data ends in '\r', else MORE 2
                     verdict = V_INCOMPLETE;
                     consumed = (len > 0 && b[len - 1] == '\r') ? 1 : 2;
@@ -490,7 +493,7 @@ __device__ __forceinline__ void mc_loop(Batch B, McTables T, const uint8_t *imag
             const int32_t *ids = (const int32_t *)(I.p + hdr32(I, MC_OFF(rule_off)));
             verdict = (uint8_t)I.terminal;
 #pragma unroll
-            for (int c = 0; c < kMcMaxChunks; c++) {
+            for (int c = 0; c < kCh; c++) {
                 if ((uint32_t)c >= I.nch) break;
                 const uint64_t ok = empty[c] | (cmdmask[c] & K.all[c]);
                 if (ok) { verdict = V_ALLOW; rule = ids[c * 64 + __builtin_ctzll(ok)]; break; }
@@ -502,7 +505,7 @@ __device__ __forceinline__ void mc_loop(Batch B, McTables T, const uint8_t *imag
     }
 }
 
-template <bool kNfa>
+template <bool kNfa, int kCh>
 __device__ __forceinline__ void mc_classify(Batch B, McTables T, const uint32_t *__restrict__ sel,
                                             const uint32_t *__restrict__ sel2, const uint32_t *__restrict__ sel_count,
                                             uint32_t answer_other) {
@@ -515,9 +518,9 @@ __device__ __forceinline__ void mc_classify(Batch B, McTables T, const uint32_t 
         const uint32_t n16 = (T.images_len + 15) / 16;
         for (uint32_t i = threadIdx.x; i < n16; i += kBlock) ((uint4 *)mc_lds)[i] = ((const uint4 *)T.images)[i];
         __syncthreads();
-        mc_loop<kNfa, true>(B, T, mc_lds, sel, sel2, sel_count, answer_other);
+        mc_loop<kNfa, true, kCh>(B, T, mc_lds, sel, sel2, sel_count, answer_other);
     } else {
-        mc_loop<kNfa, false>(B, T, T.images, sel, sel2, sel_count, answer_other);
+        mc_loop<kNfa, false, kCh>(B, T, T.images, sel, sel2, sel_count, answer_other);
     }
 }
 
@@ -525,19 +528,23 @@ __device__ __forceinline__ void mc_classify(Batch B, McTables T, const uint32_t 
 // mixed-stream memcached requests: 4 waves (100 VGPRs, no spill) 0.91 ms,
 // 6 waves 0.79-0.82, 7 waves 0.79, 8 waves 0.84 -- the spills grow);
 // the NFA variant keeps its registers.
-__global__ __launch_bounds__(kBlock) L7G_MC_OCCUPANCY void memcache_classify_kernel(Batch B, McTables T,
+// kCh: 64-rule chunks the kernel carries per request (1 when every rule set
+// has at most 64 rules: 6 fewer registers per lane than the 4-chunk build).
+// (the 4-chunk build holds 6 more registers: 4 waves per SIMD, where it does not spill)
+template <int kCh>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kCh == 1 ? L7G_MC_WAVES : 4, 8))) void memcache_classify_kernel(Batch B, McTables T,
                                                                                   const uint32_t *__restrict__ sel,
                                                                                   const uint32_t *__restrict__ sel2,
                                                                                   const uint32_t *__restrict__ sel_count,
                                                                                   uint32_t answer_other) {
-    mc_classify<false>(B, T, sel, sel2, sel_count, answer_other);
+    mc_classify<false, kCh>(B, T, sel, sel2, sel_count, answer_other);
 }
 __global__ __launch_bounds__(kBlock) void memcache_classify_nfa_kernel(Batch B, McTables T,
                                                                        const uint32_t *__restrict__ sel,
                                                                        const uint32_t *__restrict__ sel2,
                                                                        const uint32_t *__restrict__ sel_count,
                                                                        uint32_t answer_other) {
-    mc_classify<true>(B, T, sel, sel2, sel_count, answer_other);
+    mc_classify<true, kMcMaxChunks>(B, T, sel, sel2, sel_count, answer_other);
 }
 
 hipError_t LaunchMemcacheClassify(const Batch &B, const McTables &T, const uint32_t *sel, const uint32_t *sel2,
@@ -549,9 +556,12 @@ hipError_t LaunchMemcacheClassify(const Batch &B, const McTables &T, const uint3
     if (T.nfa_pool)
         hipLaunchKernelGGL(memcache_classify_nfa_kernel, dim3(blocks), dim3(kBlock), lds, stream, B, T, sel, sel2, sel_count,
                            answer_other ? 1u : 0u);
-    else
-        hipLaunchKernelGGL(memcache_classify_kernel, dim3(blocks), dim3(kBlock), lds, stream, B, T, sel, sel2, sel_count,
+    else if (T.max_chunks <= 1)
+        hipLaunchKernelGGL(memcache_classify_kernel<1>, dim3(blocks), dim3(kBlock), lds, stream, B, T, sel, sel2, sel_count,
                            answer_other ? 1u : 0u);
+    else
+        hipLaunchKernelGGL(memcache_classify_kernel<kMcMaxChunks>, dim3(blocks), dim3(kBlock), lds, stream, B, T, sel, sel2,
+                           sel_count, answer_other ? 1u : 0u);
     return hipGetLastError();
 }
 
