@@ -17,7 +17,7 @@ namespace {
 constexpr uint32_t kMaxParseBuf = 6553500;
 constexpr int kCrcSlices = 8;
 #ifndef L7G_KAFKA_CRCSTREAMS  // independent CRC chains per 64-byte batch (1, 2 or 4)
-#define L7G_KAFKA_CRCSTREAMS 2
+#define L7G_KAFKA_CRCSTREAMS 1
 #endif
 // Shift tables after the 8 slicing tables: Zn[j][b] = T_{n-1-j}[b], so that
 // crc(v, n zero bytes) = Zn[0][v & 0xFF] ^ ... ^ Zn[3][v >> 24] (the register
@@ -274,91 +274,89 @@ __device__ __forceinline__ uint32_t cur_word_at(const Cur &c, uint32_t k) {
 // memory latency per batch -- the second buffer costs LDS, not VGPRs.  (cfg3:
 // 0.929 -> 0.919 ms; holding the next batch in registers instead spills.)
 // Correct under any exec mask: each active lane stages and reads only its own
-// bytes, and every batch is exactly four loads, so vmcnt counts are exact.
-__device__ __forceinline__ uint32_t crc32_ieee_staged(const uint32_t *tab, Cur &cur, const uint8_t *p, uint32_t n,
-                                                      uint8_t *stage) {
-    const uint32_t tabaddr = (uint32_t)(uintptr_t)tab;
-    uint32_t c = 0xFFFFFFFFu;
+// bytes, and a batch is waited for with vmcnt(0).  In pieces, so that the
+// message-set walk can interleave them (read_message_set in kafka_classify).
+
+// bytes before the first 16-byte boundary (at most 15, one chunk) in 8-, 4-
+// and 1-byte steps; returns how many were hashed into c
+__device__ __forceinline__ uint32_t crc_head(uint32_t tabaddr, Cur &cur, const uint8_t *p, uint32_t n, uint32_t &c) {
     uint32_t i = 0;
-    {
-        // up to the first 16-byte boundary: one chunk, in 8-, 4- and 1-byte steps
-        const uint32_t k0 = (uint32_t)((uintptr_t)p & 15);
-        uint32_t h = (16 - k0) & 15;
-        if (h > n) h = n;
-        if (h >= 4) {
-            cur_fill(cur, (uintptr_t)p);
-            if (h >= 8) {
-                c = crc_step8(tabaddr, cur_word_at(cur, k0) ^ c, cur_word_at(cur, k0 + 4));
-                i = 8;
-            }
-            if (h - i >= 4) {
-                c = crc_step4(tabaddr, cur_word_at(cur, k0 + i) ^ c);
-                i += 4;
-            }
+    const uint32_t k0 = (uint32_t)((uintptr_t)p & 15);
+    uint32_t h = (16 - k0) & 15;
+    if (h > n) h = n;
+    if (h >= 4) {
+        cur_fill(cur, (uintptr_t)p);
+        if (h >= 8) {
+            c = crc_step8(tabaddr, cur_word_at(cur, k0) ^ c, cur_word_at(cur, k0 + 4));
+            i = 8;
         }
-        if (i < h) {
-            cur_fill(cur, (uintptr_t)p);
-            c = crc_bytes3(tabaddr, c, cur_word_at(cur, k0 + i), h - i);
-            i = h;
+        if (h - i >= 4) {
+            c = crc_step4(tabaddr, cur_word_at(cur, k0 + i) ^ c);
+            i += 4;
         }
     }
-    if (i + 64 <= n) {
-        const uint32_t la = (uint32_t)(uintptr_t)(stage + 16 * (threadIdx.x & 63));
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#define CRC_STAGE(q)                                                                                     \
-    do {                                                                                                 \
-        _Pragma("unroll") for (int k_ = 0; k_ < 4; k_++)                                                 \
-            __builtin_amdgcn_global_load_lds((const void *)((q) + 16 * k_),                              \
-                                             (__attribute__((address_space(3))) void *)(stage + k_ * 1024), 16, 0, 0); \
-    } while (0)
-        CRC_STAGE(p + i);
-        uint4 v0, v1, v2, v3;
-        for (;;) {
-            asm volatile("s_waitcnt vmcnt(0)\n\t"
-                         "ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:1024\n\t"
-                         "ds_read_b128 %2, %4 offset:2048\n\tds_read_b128 %3, %4 offset:3072\n\t"
-                         "s_waitcnt lgkmcnt(0)"
-                         : "=v"(v0), "=v"(v1), "=v"(v2), "=v"(v3)
-                         : "v"(la)
-                         : "memory");
-            const bool more = i + 128 <= n;
-            if (more) CRC_STAGE(p + i + 64);
+    if (i < h) {
+        cur_fill(cur, (uintptr_t)p);
+        c = crc_bytes3(tabaddr, c, cur_word_at(cur, k0 + i), h - i);
+        i = h;
+    }
+    return i;
+}
+// the 64 bytes at q (16-byte aligned) into the lane's staging slot
+__device__ __forceinline__ void crc_stage(uint8_t *stage, const uint8_t *q) {
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        __builtin_amdgcn_global_load_lds((const void *)(q + 16 * k),
+                                         (__attribute__((address_space(3))) void *)(stage + k * 1024), 16, 0, 0);
+}
+// one staged 64-byte batch hashed into c; the next one (if any) staged meanwhile
+__device__ __forceinline__ uint32_t crc_batch(const uint32_t *tab, uint8_t *stage, uint32_t c, const uint8_t *next) {
+    const uint32_t la = (uint32_t)(uintptr_t)(stage + 16 * (threadIdx.x & 63));
+    uint4 v0, v1, v2, v3;
+    asm volatile("s_waitcnt vmcnt(0)\n\t"
+                 "ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:1024\n\t"
+                 "ds_read_b128 %2, %4 offset:2048\n\tds_read_b128 %3, %4 offset:3072\n\t"
+                 "s_waitcnt lgkmcnt(0)"
+                 : "=v"(v0), "=v"(v1), "=v"(v2), "=v"(v3)
+                 : "v"(la)
+                 : "memory");
+    if (next) crc_stage(stage, next);
 #if L7G_KAFKA_CRCSTREAMS == 1
 #pragma unroll
-            for (int j = 0; j < 8; j++) {
-                const uint4 x = j < 2 ? v0 : j < 4 ? v1 : j < 6 ? v2 : v3;
-                const uint32_t lo = ((j & 1) ? x.z : x.x) ^ c, hi = (j & 1) ? x.w : x.y;
-                c = crc_slice8(tab, lo, hi);
-            }
-#elif L7G_KAFKA_CRCSTREAMS == 2
-            // two independent chains (bytes 0-31 from c, bytes 32-63 from 0),
-            // joined by the 32-zero-byte shift: 5 dependent lookup rounds, not 8
-            uint32_t ca = c, cb = 0;
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const uint4 xa = j < 2 ? v0 : v1, xb = j < 2 ? v2 : v3;
-                ca = crc_slice8(tab, ((j & 1) ? xa.z : xa.x) ^ ca, (j & 1) ? xa.w : xa.y);
-                cb = crc_slice8(tab, ((j & 1) ? xb.z : xb.x) ^ cb, (j & 1) ? xb.w : xb.y);
-            }
-            c = crc_shift(tab + kCrcZ32, ca) ^ cb;
-#else
-            // four chains of 16 bytes, joined by the 48/32/16-zero-byte shifts: 3 rounds
-            uint32_t c0 = c, c1 = 0, c2 = 0, c3 = 0;
-#pragma unroll
-            for (int j = 0; j < 2; j++) {
-                c0 = crc_slice8(tab, (j ? v0.z : v0.x) ^ c0, j ? v0.w : v0.y);
-                c1 = crc_slice8(tab, (j ? v1.z : v1.x) ^ c1, j ? v1.w : v1.y);
-                c2 = crc_slice8(tab, (j ? v2.z : v2.x) ^ c2, j ? v2.w : v2.y);
-                c3 = crc_slice8(tab, (j ? v3.z : v3.x) ^ c3, j ? v3.w : v3.y);
-            }
-            c = crc_shift(tab + kCrcZ48, c0) ^ crc_shift(tab + kCrcZ32, c1) ^ crc_shift(tab + kCrcZ16, c2) ^ c3;
-#endif
-            i += 64;
-            if (!more) break;
-        }
-#undef CRC_STAGE
+    for (int j = 0; j < 8; j++) {
+        const uint4 x = j < 2 ? v0 : j < 4 ? v1 : j < 6 ? v2 : v3;
+        const uint32_t lo = ((j & 1) ? x.z : x.x) ^ c, hi = (j & 1) ? x.w : x.y;
+        c = crc_slice8(tab, lo, hi);
     }
-    // the rest from 16-byte aligned chunks: 8-byte steps, then one 4-byte step, then bytes
+#elif L7G_KAFKA_CRCSTREAMS == 2
+    // two independent chains (bytes 0-31 from c, bytes 32-63 from 0), joined
+    // by the 32-zero-byte shift: 5 dependent lookup rounds, not 8
+    uint32_t ca = c, cb = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const uint4 xa = j < 2 ? v0 : v1, xb = j < 2 ? v2 : v3;
+        ca = crc_slice8(tab, ((j & 1) ? xa.z : xa.x) ^ ca, (j & 1) ? xa.w : xa.y);
+        cb = crc_slice8(tab, ((j & 1) ? xb.z : xb.x) ^ cb, (j & 1) ? xb.w : xb.y);
+    }
+    c = crc_shift(tab + kCrcZ32, ca) ^ cb;
+#else
+    // four chains of 16 bytes, joined by the 48/32/16-zero-byte shifts: 3 rounds
+    uint32_t c0 = c, c1 = 0, c2 = 0, c3 = 0;
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+        c0 = crc_slice8(tab, (j ? v0.z : v0.x) ^ c0, j ? v0.w : v0.y);
+        c1 = crc_slice8(tab, (j ? v1.z : v1.x) ^ c1, j ? v1.w : v1.y);
+        c2 = crc_slice8(tab, (j ? v2.z : v2.x) ^ c2, j ? v2.w : v2.y);
+        c3 = crc_slice8(tab, (j ? v3.z : v3.x) ^ c3, j ? v3.w : v3.y);
+    }
+    c = crc_shift(tab + kCrcZ48, c0) ^ crc_shift(tab + kCrcZ32, c1) ^ crc_shift(tab + kCrcZ16, c2) ^ c3;
+#endif
+    return c;
+}
+// the rest (fewer than 64 bytes, from i, 16-byte aligned) from the cursor's
+// chunks: 8-byte steps, then one 4-byte step, then bytes
+__device__ __forceinline__ uint32_t crc_tail(uint32_t tabaddr, Cur &cur, const uint8_t *p, uint32_t n, uint32_t i,
+                                             uint32_t c) {
     for (; i + 8 <= n; i += 8) {
         const uintptr_t a = (uintptr_t)(p + i);
         cur_fill(cur, a);
@@ -377,7 +375,24 @@ __device__ __forceinline__ uint32_t crc32_ieee_staged(const uint32_t *tab, Cur &
         cur_fill(cur, a);
         c = crc_bytes3(tabaddr, c, cur_word_at(cur, (uint32_t)(a & 15)), n - i);
     }
-    return ~c;
+    return c;
+}
+__device__ __forceinline__ uint32_t crc32_ieee_staged(const uint32_t *tab, Cur &cur, const uint8_t *p, uint32_t n,
+                                                      uint8_t *stage) {
+    const uint32_t tabaddr = (uint32_t)(uintptr_t)tab;
+    uint32_t c = 0xFFFFFFFFu;
+    uint32_t i = crc_head(tabaddr, cur, p, n, c);
+    if (i + 64 <= n) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        crc_stage(stage, p + i);
+        for (;;) {
+            const bool more = i + 128 <= n;
+            c = crc_batch(tab, stage, c, more ? p + i + 64 : nullptr);
+            i += 64;
+            if (!more) break;
+        }
+    }
+    return ~crc_tail(tabaddr, cur, p, n, i, c);
 }
 
 }  // namespace

@@ -20,7 +20,10 @@ namespace l7 {
 
 namespace {
 constexpr int kBlock = 256;
-constexpr int kPer = 16;
+#ifndef L7G_PART_PER  // rows (of 256 requests) per workgroup
+#define L7G_PART_PER 8
+#endif
+constexpr int kPer = L7G_PART_PER;
 constexpr int kWaves = kBlock / 64;
 // list classes: 0..kKafkaClasses-1 Kafka by kind / length, then memcached
 // text, memcached binary, then HTTP
@@ -34,9 +37,10 @@ static_assert(kKafkaClasses + 4 <= 31, "counts[31] holds the compressed-Kafka co
 // Kafka list class: the decode path a lane takes is set by the request kind
 // and, for produce, by how many message bytes it hashes, so fetch requests,
 // the other kinds, and produce requests by length each get lists of their own.
-__device__ __forceinline__ uint8_t kafka_class(const uint8_t *b, uint32_t len) {
+// kind: the request's api key bytes (bytes 4-5), 0xFFFF if it has none
+__device__ __forceinline__ uint8_t kafka_class(uint32_t kind, uint32_t len) {
     if (kKafkaClasses == 1) return 0;
-    const uint32_t kind = len >= 6 ? (uint32_t)b[4] << 8 | b[5] : 0xFFFF;
+    if (len < 6) kind = 0xFFFF;
     if (kKafkaClasses == 12) {  // fetch by length (topic / partition count), other kinds, produce in 9 bins
         if (kind == 1) return len < 128 ? 0 : 1;
         if (kind != 0) return 2;
@@ -71,17 +75,56 @@ __global__ __launch_bounds__(kBlock) void partition_kernel(Batch B, uint32_t *__
     const uint64_t below = (1ull << lane) - 1;
     uint8_t p[kPer];  // class + 1, 0 = none
     uint32_t cnt[kClasses] = {};
+    // The rows' loads go out phase by phase (connection ids, connections,
+    // offsets / lengths, first bytes), so a block waits four memory latencies,
+    // not four per row.
+    uint32_t ci[kPer], pw[kPer];
+#pragma unroll
+    for (int r = 0; r < kPer; r++) {
+        const uint64_t idx = start + (uint64_t)r * kBlock + threadIdx.x;
+        ci[r] = idx < n ? B.conn_ids[idx] : 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for (int r = 0; r < kPer; r++) {  // proto | flags << 8 of the connection, PROTO_NONE if unknown
+        pw[r] = PROTO_NONE;
+        if (ci[r] < B.nconns) {
+            const DevConn c = B.conns[ci[r]];
+            pw[r] = (uint32_t)c.proto | (uint32_t)c.flags << 8;
+        }
+    }
+    uint64_t off[kPer];
+    uint32_t len[kPer];
+#pragma unroll
+    for (int r = 0; r < kPer; r++) {
+        const uint64_t idx = start + (uint64_t)r * kBlock + threadIdx.x;
+        const uint32_t proto = pw[r] & 0xFF;
+        off[r] = 0;
+        len[r] = 0;
+        if (proto == PROTO_KAFKA || proto == PROTO_MEMCACHE) {
+            off[r] = B.offs[idx];
+            len[r] = B.lens[idx];
+        }
+    }
+    uint32_t hb[kPer];  // Kafka: the api key bytes 4-5 (0xFFFF: none); memcached: the first byte (0: none)
+#pragma unroll
+    for (int r = 0; r < kPer; r++) {
+        const uint32_t proto = pw[r] & 0xFF;
+        hb[r] = 0;
+        if (proto == PROTO_KAFKA) {
+            const bool ok = l7_in_arena(off[r], len[r], B.arena_len) && len[r] >= 6;
+            hb[r] = ok ? (uint32_t)B.arena[off[r] + 4] << 8 | B.arena[off[r] + 5] : 0xFFFFu;
+        } else if (proto == PROTO_MEMCACHE) {
+            hb[r] = len[r] > 0 && l7_in_arena(off[r], 1, B.arena_len) ? B.arena[off[r]] : 0u;
+        }
+    }
 #pragma unroll
     for (int r = 0; r < kPer; r++) {
         const uint64_t idx = start + (uint64_t)r * kBlock + threadIdx.x;
         uint8_t cls = 0;
         if (idx < n) {
-            const uint32_t ci = B.conn_ids[idx];
-            const uint8_t proto = ci < B.nconns ? B.conns[ci].proto : PROTO_NONE;
+            const uint32_t proto = pw[r] & 0xFF;
             if (proto == PROTO_KAFKA) {
-                const uint32_t len = B.lens[idx];
-                const uint64_t off = B.offs[idx];
-                cls = 1 + kafka_class(B.arena + off, l7_in_arena(off, len, B.arena_len) ? len : 0);
+                cls = 1 + kafka_class(hb[r], l7_in_arena(off[r], len[r], B.arena_len) ? len[r] : 0);
             }
             else if (proto == PROTO_MEMCACHE) {
                 // the parser the connection chose, else the one this buffer's
@@ -90,9 +133,8 @@ __global__ __launch_bounds__(kBlock) void partition_kernel(Batch B, uint32_t *__
                 // their own and a wave runs only one of them
                 // (text: retrievals -- get / gets / gat / gats -- apart from the
                 // rest, whose lines are longer and parse more tokens)
-                uint32_t mode = B.conns[ci].flags & 3;
-                const uint64_t off = B.offs[idx];
-                const uint32_t c0 = B.lens[idx] > 0 && l7_in_arena(off, 1, B.arena_len) ? B.arena[off] : 0u;
+                uint32_t mode = (pw[r] >> 8) & 3;
+                const uint32_t c0 = hb[r];
                 if (mode == 0) mode = c0 >= 0x80 ? 2 : 1;
                 cls = 1 + (mode == 2 ? kMcBinary : c0 == 'g' ? kMcText : kMcText2);
             }
@@ -122,9 +164,9 @@ __global__ __launch_bounds__(kBlock) void partition_kernel(Batch B, uint32_t *__
         }
     }
     __syncthreads();
-    uint32_t off[kClasses];
+    uint32_t lo[kClasses];
 #pragma unroll
-    for (int c = 0; c < kClasses; c++) off[c] = s_off[wave][c];
+    for (int c = 0; c < kClasses; c++) lo[c] = s_off[wave][c];
 #pragma unroll
     for (int r = 0; r < kPer; r++) {
         const uint32_t idx = (uint32_t)(start + (uint64_t)r * kBlock + threadIdx.x);
@@ -132,14 +174,14 @@ __global__ __launch_bounds__(kBlock) void partition_kernel(Batch B, uint32_t *__
         for (int c = 0; c < kClasses; c++) {
             const uint64_t mk = __ballot(p[r] == c + 1);
             if (p[r] == c + 1) {
-                const uint32_t pos = off[c] + __popcll(mk & below);
+                const uint32_t pos = lo[c] + __popcll(mk & below);
                 if (c < kKafkaClasses) sel_kafka[(size_t)c * n + pos] = idx;
                 else if (c == kMcText) sel_mc[pos] = idx;
                 else if (c == kMcBinary) sel_mc[n - 1 - pos] = idx;  // binary from the list's end
                 else if (c == kHttp) sel_http[pos] = idx;
                 else sel_http[n - 1 - pos] = idx;  // other text commands from the HTTP list's end
             }
-            off[c] += __popcll(mk);
+            lo[c] += __popcll(mk);
         }
     }
 }

@@ -128,7 +128,8 @@ int l7g_conn_update(l7g_engine *e, uint32_t index, const l7g_conn_t *conn, char 
  * followed by per-verdict totals (added atomically, so calls on different
  * streams may share one array).  Batches with Kafka requests or with more
  * than one protocol use a scratch of 32 + (L7_KAFKA_CLASSES + 3) n uint32 (the
- * partition lists; 32 + 11 n with 8 classes); scratch is kept per stream (up to
+ * partition lists and work counters; 32 + 11 n with 8 classes), HTTP-only
+ * batches of 2^18 or more requests 4 words (tile counters); scratch is kept per stream (up to
  * 16 streams, then handed over least recently used first), so calls on
  * different streams run concurrently and calls on one stream are ordered by
  * it.  With Kafka rules the engine also holds ONE 1 GiB decode region for
