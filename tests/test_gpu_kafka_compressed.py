@@ -154,3 +154,16 @@ def test_mixed_with_plain_cfg3(engine, oracle):
                      np.random.default_rng(3).integers(0, len(w3.conns), len(mixed)))
     got, ref = both(engine, oracle, w)
     assert_same(got, ref, w)
+
+
+def test_snappy_decode_go_vectors(engine, oracle):
+    """The snappy vectors derived from the reference's vendored decoder
+    (tests/test_snappy_decode_go.py) as snappy-coded messages of produce
+    requests: the inflate kernel's verdicts equal the oracle's, and a vector
+    Decode rejects makes its request PARSE_ERROR."""
+    from test_snappy_decode_go import VECTORS
+    reqs = [gen.k_produce(0, 1, "c", [(TOPIC, [(0, [gen.k_message(src, attributes=2)])])]) for _, src, _, _ in VECTORS]
+    got = run(engine, oracle, reqs)
+    for (name, _, expected, where), v in zip(VECTORS, got):
+        if expected is None:
+            assert v == PARSE_ERROR, f"{name}: {where}"
