@@ -282,10 +282,22 @@ def main():
         f"({w.arena.nbytes / 1e9:.2f} GB) x {tiles} = {n} requests in {time.time() - t0:.1f}s")
 
     eng = Engine(local)
-    # the policy arrives at rank 0 (the NPDS client) and is broadcast to every rank over RCCL
-    policy = l7dist.broadcast_policy(full.policy, dist, device=dev) if dist is not None else full.policy
-    eng.update_policy(policy)
+    # the policy arrives at rank 0 (the NPDS client), which compiles it for the
+    # node's connections and broadcasts the compiled tables over RCCL; the other
+    # ranks install them without compiling
+    t_c = time.time()
+    if dist is not None:
+        l7dist.broadcast_tables(eng, dist, device=dev, policy=full.policy if rank == 0 else None,
+                                conns=full.conns if rank == 0 else None)
+    else:
+        eng.update_policy(full.policy)
     eng.set_connections(w.conns)
+    compile_s, compiled = time.time() - t_c, eng.tables_compiled
+    other_compiled = 0
+    if dist is not None:  # rule sets the ranks > 0 compiled themselves (0: all installed from rank 0's image)
+        oc = torch.tensor([compiled if rank else 0], dtype=torch.int64, device=dev)
+        dist.all_reduce(oc)
+        other_compiled = int(oc.item())
     nrules = eng.nrules
 
     d_arena = torch.from_numpy(np.ascontiguousarray(w.arena)).to(dev)
@@ -472,6 +484,8 @@ def main():
                    "protocol_mix": {k: v["requests"] for k, v in pbytes.items()},
                    "parallelism": f"dp{world}" + (" (connection-sharded stream) + RCCL counter all-reduce"
                                                   if world > 1 else "")},
+        "tables": {"rank0_compile_s": round(compile_s, 3), "rank0_rulesets_compiled": compiled if rank == 0 else None,
+                   "rulesets_compiled_by_other_ranks": other_compiled},
         "scanned_gbps": round(step_alg * world * args.steps / elapsed / 1e9, 2),
         "roofline": roofline,
         "step_roofline": {"algorithmic_bytes_per_launch": step_alg, "kernel_ms": round(kernel_ms, 4),

@@ -41,6 +41,7 @@ EXPORTS = (
     "l7g_debug_kafka_phase_times", "l7g_kafka_deny_response", "l7g_debug_regex_nfa", "l7g_policy_update_proto", "l7g_kafka_corr_create", "l7g_kafka_corr_destroy",
     "l7g_kafka_corr_requests", "l7g_kafka_corr_responses", "l7g_kafka_corr_gc", "l7g_kafka_corr_size",
     "l7g_flow_stats_enable", "l7g_flow_stats",
+    "l7g_tables_export", "l7g_tables_import", "l7g_tables_compiled", "l7g_tables_digest",
 )
 
 
@@ -78,6 +79,12 @@ def load(path=None):
     lib.l7g_policy_nrules.restype = C.c_int32
     lib.l7g_policy_nrules.argtypes = [vp]
     lib.l7g_conns_set.argtypes = [vp, vp, C.c_uint32, cp, sz]
+    lib.l7g_tables_export.argtypes = [vp, vp, sz, C.POINTER(sz)]
+    lib.l7g_tables_import.argtypes = [vp, cp, sz, cp, sz]
+    lib.l7g_tables_compiled.restype = C.c_uint64
+    lib.l7g_tables_compiled.argtypes = [vp]
+    lib.l7g_tables_digest.restype = C.c_uint64
+    lib.l7g_tables_digest.argtypes = [vp]
     lib.l7g_conn_update.argtypes = [vp, C.c_uint32, vp, cp, sz]
     lib.l7g_classify.argtypes = [vp, vp, C.c_uint64, vp, vp, vp, C.c_uint32, vp, vp, vp, vp, vp]
     lib.l7g_classify_host.argtypes = [vp, vp, C.c_uint64, vp, vp, vp, C.c_uint32, vp, vp, vp]

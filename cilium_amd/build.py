@@ -62,6 +62,10 @@ def build(verbose=False, jobs=8, timing=False, variant=None, defines=()):
     compiled with -DL7G_PHASE_TIMING; see l7g_debug_phase_times).  variant=NAME
     builds libl7gpu_NAME.so with extra -D defines (kernel experiments only;
     the product is always libl7gpu.so)."""
+    if not variant and not timing and defines:
+        # the product is built from its sources as they stand: a -D define could
+        # only reach it through an experiment, and none may change a verdict
+        raise ValueError("libl7gpu.so takes no -D defines; build a variant (variant=NAME) for experiments")
     srcs = sources()
     newest_header = max([os.path.getmtime(h) for h in headers()] + [0])
     if timing:

@@ -38,7 +38,8 @@ uint32_t KafkaInflateRegionBytes();
 hipError_t LaunchMemcacheClassify(const Batch &B, const McTables &T, const uint32_t *sel, const uint32_t *sel2,
                                   const uint32_t *sel_count, bool answer_other, hipStream_t stream);
 hipError_t LaunchR2d2Classify(const Batch &B, const R2Tables &T, bool answer_other, hipStream_t stream);
-hipError_t LaunchCassandraClassify(const Batch &B, const CassTables &T, uint32_t *use_list, uint32_t *use_count,
+size_t CassandraScratchBytes(uint32_t n);
+hipError_t LaunchCassandraClassify(const Batch &B, const CassTables &T, void *scratch, size_t scratch_bytes,
                                    bool answer_other, hipStream_t stream);
 hipError_t LaunchCounters(const uint8_t *verdict, const int32_t *rule, uint32_t n, uint32_t nrules,
                           uint64_t *counters, uint32_t *scratch, hipStream_t stream);
@@ -70,7 +71,7 @@ struct StreamScratch {
     // counter histogram scratch (kernels/counters.hip), allocated on first use
     uint32_t *d_hist = nullptr;
     // cassandra USE list: [count | n request indices] (grow-only)
-    uint32_t *d_use = nullptr;
+    void *d_use = nullptr;  // cassandra: USE keys, sorted keys, sort temp (bytes)
     size_t use_cap = 0;
     // work counters of unpartitioned batches (HTTP tile counters), allocated on first use
     uint32_t *d_work = nullptr;
@@ -125,6 +126,9 @@ struct l7g_engine {
     std::vector<DevConn> conns;
     uint8_t *d_blob = nullptr;
     size_t blob_bytes = 0;
+    // the policy version's source (l7g_tables_export ships it with the compiled tables)
+    std::string policy_src;
+    int policy_form = 0, policy_px = 0;
     DevConn *d_conns = nullptr;
     size_t conns_cap = 0;
     HttpTables ht{};
@@ -308,22 +312,42 @@ bool ResolveConns(l7g_engine *e, std::string *err) {
     return true;
 }
 
+// The device table blob: every compiler's image, each 256-byte aligned.
+struct BlobLayout {
+    size_t o_rs, o_img, o_nfa, k_rs, k_r, k_idx, k_th, k_ch, k_s, m_rs, m_img, m_nfa, r_rs, r_img, r_nfa, c_rs, c_img,
+        c_nfa, c_low;
+};
+BlobLayout AssembleBlob(const l7g_engine *e, std::vector<uint8_t> &blob) {
+    BlobLayout L;
+    const HttpImage &H = e->hc->image();
+    L.o_rs = Put(blob, H.rulesets); L.o_img = Put(blob, H.images); L.o_nfa = Put(blob, H.nfa_pool);
+    const KafkaImage &K = e->kc->image();
+    L.k_rs = Put(blob, K.rulesets); L.k_r = Put(blob, K.rules); L.k_idx = Put(blob, K.index);
+    L.k_th = Put(blob, K.topic_hash); L.k_ch = Put(blob, K.client_hash); L.k_s = Put(blob, K.strings);
+    const McImage &M = e->mc->image();
+    L.m_rs = Put(blob, M.rulesets); L.m_img = Put(blob, M.images); L.m_nfa = Put(blob, M.nfa_pool);
+    const R2Image &R = e->r2->image();
+    L.r_rs = Put(blob, R.rulesets); L.r_img = Put(blob, R.images); L.r_nfa = Put(blob, R.nfa_pool);
+    const CassImage &CI = e->cs->image();
+    L.c_rs = Put(blob, CI.rulesets); L.c_img = Put(blob, CI.images); L.c_nfa = Put(blob, CI.nfa_pool);
+    L.c_low = Put(blob, CI.lower);
+    return L;
+}
+
 hipError_t Upload(l7g_engine *e) {
     hipError_t rc;
     if (e->tables_dirty) {
         std::vector<uint8_t> blob;
+        const BlobLayout L = AssembleBlob(e, blob);
+        const size_t o_rs = L.o_rs, o_img = L.o_img, o_nfa = L.o_nfa, k_rs = L.k_rs, k_r = L.k_r, k_idx = L.k_idx,
+                     k_th = L.k_th, k_ch = L.k_ch, k_s = L.k_s, m_rs = L.m_rs, m_img = L.m_img, m_nfa = L.m_nfa,
+                     r_rs = L.r_rs, r_img = L.r_img, r_nfa = L.r_nfa, c_rs = L.c_rs, c_img = L.c_img, c_nfa = L.c_nfa,
+                     c_low = L.c_low;
         const HttpImage &H = e->hc->image();
-        size_t o_rs = Put(blob, H.rulesets), o_img = Put(blob, H.images), o_nfa = Put(blob, H.nfa_pool);
         const KafkaImage &K = e->kc->image();
-        size_t k_rs = Put(blob, K.rulesets), k_r = Put(blob, K.rules), k_idx = Put(blob, K.index),
-               k_th = Put(blob, K.topic_hash), k_ch = Put(blob, K.client_hash), k_s = Put(blob, K.strings);
         const McImage &M = e->mc->image();
-        size_t m_rs = Put(blob, M.rulesets), m_img = Put(blob, M.images), m_nfa = Put(blob, M.nfa_pool);
         const R2Image &R = e->r2->image();
-        size_t r_rs = Put(blob, R.rulesets), r_img = Put(blob, R.images), r_nfa = Put(blob, R.nfa_pool);
         const CassImage &CI = e->cs->image();
-        size_t c_rs = Put(blob, CI.rulesets), c_img = Put(blob, CI.images), c_nfa = Put(blob, CI.nfa_pool),
-               c_low = Put(blob, CI.lower);
         uint8_t *d = nullptr;
         if ((rc = hipMalloc(&d, blob.size())) != hipSuccess) return rc;
         if ((rc = hipMemcpy(d, blob.data(), blob.size(), hipMemcpyHostToDevice)) != hipSuccess) { hipFree(d); return rc; }
@@ -438,6 +462,9 @@ void l7g_engine_destroy(l7g_engine *e) {
 }
 
 static int PolicySwap(l7g_engine *e, std::unique_ptr<PolicySet> ps, char *err, size_t errlen);
+static int SwapIn(l7g_engine *e, std::unique_ptr<PolicySet> ps, std::unique_ptr<HttpCompiler> hc,
+                  std::unique_ptr<KafkaCompiler> kc, std::unique_ptr<McCompiler> mc, std::unique_ptr<R2Compiler> r2,
+                  std::unique_ptr<CassCompiler> cs, char *err, size_t errlen);
 
 int l7g_policy_update(l7g_engine *e, const char *json, size_t len, char *err, size_t errlen) {
     return l7g_policy_update_view(e, (const uint8_t *)json, len, 0, 0, err, errlen);
@@ -461,7 +488,13 @@ int l7g_policy_update_view(l7g_engine *e, const uint8_t *buf, size_t len, int pr
                                : LoadPolicySet((const char *)buf, len, ps.get(), &m);
     if (!ok) { set_err(err, errlen, m); return -1; }
     if (proxylib && !ps->px_nack.empty()) { set_err(err, errlen, ps->px_nack); return -1; }
-    return PolicySwap(e, std::move(ps), err, errlen);
+    const int rc = PolicySwap(e, std::move(ps), err, errlen);
+    if (rc == 0) {
+        e->policy_src.assign((const char *)buf, len);
+        e->policy_form = proto_form;
+        e->policy_px = proxylib;
+    }
+    return rc;
 }
 
 extern "C" {
@@ -469,12 +502,21 @@ extern "C" {
 // Swap in a loaded policy version; on a compile failure the previous version
 // stays in force (an NPDS NACK).  Caller holds e->mu.
 static int PolicySwap(l7g_engine *e, std::unique_ptr<PolicySet> ps, char *err, size_t errlen) {
-    std::string m;
     auto hc = std::make_unique<HttpCompiler>(ps.get());
     auto kc = std::make_unique<KafkaCompiler>(ps.get());
     auto mc = std::make_unique<McCompiler>(ps.get());
     auto r2 = std::make_unique<R2Compiler>(ps.get());
     auto cs = std::make_unique<CassCompiler>(ps.get());
+    return SwapIn(e, std::move(ps), std::move(hc), std::move(kc), std::move(mc), std::move(r2), std::move(cs), err,
+                  errlen);
+}
+
+// Swap in a policy version with its compilers (fresh, or holding imported
+// tables); on a compile failure the previous version stays in force.
+static int SwapIn(l7g_engine *e, std::unique_ptr<PolicySet> ps, std::unique_ptr<HttpCompiler> hc,
+                  std::unique_ptr<KafkaCompiler> kc, std::unique_ptr<McCompiler> mc, std::unique_ptr<R2Compiler> r2,
+                  std::unique_ptr<CassCompiler> cs, char *err, size_t errlen) {
+    std::string m;
     std::swap(e->ps, ps);
     std::swap(e->hc, hc);
     std::swap(e->kc, kc);
@@ -494,6 +536,72 @@ static int PolicySwap(l7g_engine *e, std::unique_ptr<PolicySet> ps, char *err, s
         return -1;
     }
     return 0;
+}
+
+// ---- compiled tables across ranks (engine/serial.h)
+constexpr uint64_t kTablesMagic = 0x3154473754L;  // "T7G1"
+
+int l7g_tables_export(l7g_engine *e, uint8_t *buf, size_t cap, size_t *len) {
+    std::lock_guard<std::mutex> g(e->mu);
+    Ser s;
+    s.u64(kTablesMagic);
+    s.u64((uint64_t)e->policy_form);
+    s.u64((uint64_t)e->policy_px);
+    s.str(e->policy_src);
+    e->hc->Save(s);
+    e->kc->Save(s);
+    e->mc->Save(s);
+    e->r2->Save(s);
+    e->cs->Save(s);
+    if (len) *len = s.out.size();
+    if (!buf || cap < s.out.size()) return -2;
+    memcpy(buf, s.out.data(), s.out.size());
+    return 0;
+}
+
+int l7g_tables_import(l7g_engine *e, const uint8_t *buf, size_t len, char *err, size_t errlen) {
+    std::lock_guard<std::mutex> g(e->mu);
+    Des d(buf, len);
+    if (d.u64() != kTablesMagic) { set_err(err, errlen, "not an l7g_tables_export image"); return -1; }
+    const int form = (int)d.u64(), px = (int)d.u64();
+    const std::string src = d.str();
+    if (!d.ok) { set_err(err, errlen, "truncated tables image"); return -1; }
+    auto ps = std::make_unique<PolicySet>();
+    std::string m;
+    const bool ok = form ? LoadPolicySetProto((const uint8_t *)src.data(), src.size(), ps.get(), &m)
+                         : LoadPolicySet(src.data(), src.size(), ps.get(), &m);
+    if (!ok) { set_err(err, errlen, m); return -1; }
+    auto hc = std::make_unique<HttpCompiler>(ps.get());
+    auto kc = std::make_unique<KafkaCompiler>(ps.get());
+    auto mc = std::make_unique<McCompiler>(ps.get());
+    auto r2 = std::make_unique<R2Compiler>(ps.get());
+    auto cs = std::make_unique<CassCompiler>(ps.get());
+    if (!hc->Load(d) || !kc->Load(d) || !mc->Load(d) || !r2->Load(d) || !cs->Load(d) || d.p != d.end) {
+        set_err(err, errlen, "corrupt tables image");
+        return -1;
+    }
+    const int rc = SwapIn(e, std::move(ps), std::move(hc), std::move(kc), std::move(mc), std::move(r2), std::move(cs),
+                          err, errlen);
+    if (rc == 0) {
+        e->policy_src = src;
+        e->policy_form = form;
+        e->policy_px = px;
+    }
+    return rc;
+}
+
+uint64_t l7g_tables_compiled(l7g_engine *e) {
+    std::lock_guard<std::mutex> g(e->mu);
+    return e->hc->compiled + e->kc->compiled + e->mc->compiled + e->r2->compiled + e->cs->compiled;
+}
+
+uint64_t l7g_tables_digest(l7g_engine *e) {
+    std::lock_guard<std::mutex> g(e->mu);
+    std::vector<uint8_t> blob;
+    AssembleBlob(e, blob);
+    uint64_t h = 1469598103934665603ull;  // FNV-1a 64
+    for (uint8_t b : blob) h = (h ^ b) * 1099511628211ull;
+    return h;
 }
 
 int32_t l7g_policy_index(l7g_engine *e, const char *name, size_t len) {
@@ -594,7 +702,8 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
         }
         if (rc != hipSuccess) return (int)rc;
         // [0, L7_KAFKA_CLASSES) Kafka classes, memcached retrievals, binary, HTTP, other text;
-        // [28, 29] HTTP tile counters (hot, general launch), [30] Kafka work counter; [31] compressed Kafka
+        // [26, 27] Kafka entry counters (produce, other kinds), [28, 29] HTTP tile counters (hot, general
+        // launch); [31] compressed Kafka
         cnt = S->d_sel;
         sel_k = S->d_sel + 32;
         sel_m = sel_k + L7_KAFKA_CLASSES * (size_t)n;
@@ -650,7 +759,7 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
     mark(2);
     uint32_t *zcount = cnt ? cnt + 31 : nullptr;
     if (rc == hipSuccess && run[2])
-        rc = LaunchKafkaClassify(B, e->kt, sel_k, cnt, !partitioned, sel_z, zcount, cnt ? cnt + 30 : nullptr, s);
+        rc = LaunchKafkaClassify(B, e->kt, sel_k, cnt, !partitioned, sel_z, zcount, cnt ? cnt + 26 : nullptr, s);
     // requests with gzip / snappy messages: decoded, their sets read, failures answered
     if (rc == hipSuccess && run[2] && sel_z) {
         // the engine's one decode region: after the previous inflate launch on any stream
@@ -666,17 +775,19 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
     if (rc == hipSuccess && e->has_r2) rc = LaunchR2d2Classify(B, e->rt, !partitioned, s);
     // cassandra (proxylib): the batch's USE requests, then one lane per request
     if (rc == hipSuccess && e->has_cs) {
-        if ((size_t)n + 1 > S->use_cap) {
+        const size_t need = CassandraScratchBytes(n);
+        if (need == 0) rc = hipErrorInvalidValue;
+        if (rc == hipSuccess && need > S->use_cap) {
             if (S->d_use) {
                 if (S->launched) rc = hipEventSynchronize(S->done_ev);
                 hipFree(S->d_use);
                 S->d_use = nullptr;
                 S->use_cap = 0;
             }
-            if (rc == hipSuccess) rc = hipMalloc(&S->d_use, ((size_t)n + 1) * sizeof(uint32_t));
-            if (rc == hipSuccess) S->use_cap = (size_t)n + 1;
+            if (rc == hipSuccess) rc = hipMalloc(&S->d_use, need);
+            if (rc == hipSuccess) S->use_cap = need;
         }
-        if (rc == hipSuccess) rc = LaunchCassandraClassify(B, e->ct, S->d_use + 1, S->d_use, !partitioned, s);
+        if (rc == hipSuccess) rc = LaunchCassandraClassify(B, e->ct, S->d_use, S->use_cap, !partitioned, s);
     }
     mark(4);
     // proxy statistics (accumulated on the device until read)

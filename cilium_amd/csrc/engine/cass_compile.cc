@@ -58,6 +58,7 @@ uint32_t Append(std::vector<uint8_t> &img, const T *p, size_t n) {
 }  // namespace
 
 int CassCompiler::Compile(const std::vector<const CassRule *> &rules, uint8_t terminal, std::string *err) {
+    compiled++;
     const size_t nr = rules.size();
     if (nr > (size_t)kCassMaxChunks * 64) {
         *err = "cassandra rule set has " + std::to_string(nr) + " rules (device limit " +

@@ -10,6 +10,7 @@
 
 #include "../device_tables.h"
 #include "../policy/policy.h"
+#include "serial.h"
 
 namespace l7 {
 
@@ -29,6 +30,21 @@ public:
     const CassImage &image() const { return img_; }
     int max_dfa_states = 4096;
     int max_single_dfa_states = 65535;
+
+    // compiled state of this policy version (engine/serial.h): written by the
+    // rank that compiled it, installed by the others without compiling
+    void Save(Ser &s) const {
+        s.vec(img_.rulesets); s.vec(img_.images); s.vec(img_.nfa_pool);
+        s.cache(cache_); s.smap(nfa_cache_);
+        s.vec(img_.lower); s.u64(img_.rules); s.u64(img_.dfas); s.u64(img_.nfas);
+    }
+    bool Load(Des &d) {
+        d.vec(img_.rulesets); d.vec(img_.images); d.vec(img_.nfa_pool);
+        d.cache(cache_); d.smap(nfa_cache_);
+        d.vec(img_.lower); img_.rules = d.u64(); img_.dfas = d.u64(); img_.nfas = d.u64();
+        return d.ok;
+    }
+    size_t compiled = 0;  // rule sets compiled (not taken from the cache) since construction
 
 private:
     const PolicySet *ps_;

@@ -295,6 +295,7 @@ uint32_t Append(std::vector<uint8_t> &img, const T *p, size_t n) {
 }  // namespace
 
 int HttpCompiler::Compile(const std::vector<const HttpRule *> &rules, uint8_t terminal, std::string *err) {
+    compiled++;
     // custom header names used anywhere in the rule set
     std::vector<std::string> custom;
     for (auto *r : rules)

@@ -104,6 +104,7 @@ int KafkaCompiler::RulesetFor(int policy, bool ingress, uint32_t port, uint64_t 
 static constexpr size_t kDenseTopicBudget = size_t(64) << 20;  // u32 entries in index[] (256 MiB)
 
 int KafkaCompiler::Compile(const std::vector<const KafkaRule *> &rules, bool any) {
+    compiled++;
     KafkaImage &I = img_;
     DevKafkaRuleset rs{};
     rs.any = any ? 1 : 0;

@@ -23,6 +23,7 @@
 
 #include "../device_tables.h"
 #include "../policy/policy.h"
+#include "serial.h"
 
 namespace l7 {
 
@@ -42,6 +43,22 @@ public:
     // proxylib: the proxylib "kafka" parser's view of the port entries
     int RulesetFor(int policy, bool ingress, uint32_t port, uint64_t src_id, bool proxylib, std::string *err);
     const KafkaImage &image() const { return img_; }
+
+    // compiled state of this policy version (engine/serial.h): written by the
+    // rank that compiled it, installed by the others without compiling
+    void Save(Ser &s) const {
+        s.vec(img_.rulesets); s.vec(img_.rules); s.vec(img_.index); s.vec(img_.topic_hash); s.vec(img_.client_hash);
+        s.vec(img_.strings); s.u64(img_.topic_mask); s.u64(img_.client_mask); s.u64(img_.ntopics);
+        s.umap(topic_id_); s.umap(client_id_); s.cache(cache_);
+    }
+    bool Load(Des &d) {
+        d.vec(img_.rulesets); d.vec(img_.rules); d.vec(img_.index); d.vec(img_.topic_hash); d.vec(img_.client_hash);
+        d.vec(img_.strings); img_.topic_mask = (uint32_t)d.u64(); img_.client_mask = (uint32_t)d.u64();
+        img_.ntopics = d.u64();
+        d.umap(topic_id_); d.umap(client_id_); d.cache(cache_);
+        return d.ok;
+    }
+    size_t compiled = 0;  // rule sets compiled (not taken from the cache) since construction
 
 private:
     const PolicySet *ps_;

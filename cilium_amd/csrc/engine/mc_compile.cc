@@ -65,6 +65,7 @@ std::unique_ptr<re::Node> LiteralAst(const std::string &v, bool prefix) {
 }  // namespace
 
 int McCompiler::Compile(const std::vector<const McRule *> &rules, uint8_t terminal, std::string *err) {
+    compiled++;
     const size_t nr = rules.size();
     if (nr > (size_t)kMcMaxChunks * 64) {
         *err = "memcache rule set has " + std::to_string(nr) + " rules (device limit " + std::to_string(kMcMaxChunks * 64) + ")";

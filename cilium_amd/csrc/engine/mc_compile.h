@@ -17,6 +17,7 @@
 
 #include "../device_tables.h"
 #include "../policy/policy.h"
+#include "serial.h"
 
 namespace l7 {
 
@@ -36,6 +37,22 @@ public:
     const McImage &image() const { return img_; }
     int max_dfa_states = 4096;
     int max_single_dfa_states = 65535;  // a pattern the NFA cannot take (see HttpCompiler)
+
+    // compiled state of this policy version (engine/serial.h): written by the
+    // rank that compiled it, installed by the others without compiling
+    void Save(Ser &s) const {
+        s.vec(img_.rulesets); s.vec(img_.images); s.vec(img_.nfa_pool);
+        s.cache(cache_); s.smap(nfa_cache_);
+        s.u64(img_.rules); s.u64(img_.dfas); s.u64(img_.dfa_states); s.u64(img_.nfas); s.u64(img_.max_chunks);
+    }
+    bool Load(Des &d) {
+        d.vec(img_.rulesets); d.vec(img_.images); d.vec(img_.nfa_pool);
+        d.cache(cache_); d.smap(nfa_cache_);
+        img_.rules = d.u64(); img_.dfas = d.u64(); img_.dfa_states = d.u64(); img_.nfas = d.u64();
+        img_.max_chunks = d.u64();
+        return d.ok;
+    }
+    size_t compiled = 0;  // rule sets compiled (not taken from the cache) since construction
 
 private:
     const PolicySet *ps_;

@@ -48,6 +48,7 @@ uint32_t Append(std::vector<uint8_t> &img, const T *p, size_t n) {
 }  // namespace
 
 int R2Compiler::Compile(const std::vector<const R2Rule *> &rules, uint8_t terminal, std::string *err) {
+    compiled++;
     const size_t nr = rules.size();
     if (nr > (size_t)kR2MaxChunks * 64) {
         *err = "r2d2 rule set has " + std::to_string(nr) + " rules (device limit " + std::to_string(kR2MaxChunks * 64) + ")";

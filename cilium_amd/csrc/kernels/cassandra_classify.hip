@@ -21,11 +21,14 @@
 // Keyspace: a batch's requests on one connection are read in batch order, as
 // proxylib's OnData reads a connection's frames, so the keyspace of request i
 // is the one set by the last USE (a QUERY or PREPARE "use x") before i on the
-// same connection; none => "".  cassandra_use_kernel lists the USE requests
-// first (an unordered list; the lane takes the largest index below its own,
-// so the list order does not matter); a lane scans the list only when its
-// table needs the keyspace.
+// same connection; none => "".  cassandra_use_kernel writes one key per
+// request, (connection << 32 | index) for a USE request and ~0 otherwise; the
+// keys are radix-sorted (hipcub), and a lane whose table needs the keyspace
+// finds the last USE on its connection before it by one binary search over
+// them: O(n log n) per batch however many USE requests it holds (a scan of an
+// unordered USE list per lane was O(n x #USE), quadratic on a USE-heavy batch).
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include "../device_tables.h"
 #include "cass_parse.h"
@@ -65,12 +68,17 @@ __device__ __forceinline__ bool frame_of(const uint8_t *b, uint32_t len, Frame *
     return true;
 }
 
-// QUERY / PREPARE: the long string at 9; false = the slice expressions panic
-__device__ __forceinline__ bool query_of(const uint8_t *b, uint32_t fl, uint32_t *qn) {
-    if (fl < 13) return false;
+// QUERY / PREPARE: the long string at 9; false = the slice expressions panic.
+// The frame is data[0:fl] of the bytes.Join buffer (cassandraparser.go:174,
+// :211); Go bounds data[9:13] and data[13:13+ql] by the slice's capacity, so
+// they read on into the bytes after the frame and panic only past the
+// buffer's end (cap = the request's buffer length; a single-slice join's
+// allocator slack is not restated: parity unpinned, oracle/cassandra_ref.c).
+__device__ __forceinline__ bool query_of(const uint8_t *b, uint32_t cap, uint32_t *qn) {
+    if (cap < 13) return false;
     const uint32_t ql = be32(b + 9);
     const uint32_t end = 13u + ql;  // uint32 arithmetic, as in Go
-    if (end < 13u || end > fl) return false;
+    if (end < 13u || end > cap) return false;
     *qn = ql;
     return true;
 }
@@ -107,11 +115,11 @@ struct NfaSink {
 
 }  // namespace
 
-// The batch's USE requests (any order): use_list[*use_count] = request index.
-__global__ __launch_bounds__(kBlock) void cassandra_use_kernel(Batch B, CassTables T, uint32_t *__restrict__ use_list,
-                                                               uint32_t *__restrict__ use_count) {
+// One key per request: (connection << 32 | index) for a USE request, ~0 otherwise.
+__global__ __launch_bounds__(kBlock) void cassandra_use_kernel(Batch B, CassTables T, uint64_t *__restrict__ keys) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= B.n) return;
+    keys[i] = ~0ull;
     const uint32_t ci = B.conn_ids[i];
     if (ci >= B.nconns || B.conns[ci].proto != PROTO_CASSANDRA) return;
     const uint64_t off = B.offs[i];
@@ -120,7 +128,7 @@ __global__ __launch_bounds__(kBlock) void cassandra_use_kernel(Batch B, CassTabl
     const uint8_t *b = B.arena + off;
     Frame F;
     uint32_t qn;
-    if (!frame_of(b, len, &F) || (F.op != 0x07 && F.op != 0x09) || !query_of(b, F.fl, &qn)) return;
+    if (!frame_of(b, len, &F) || (F.op != 0x07 && F.op != 0x09) || !query_of(b, len, &qn)) return;
     // cheap pre-check: the first token must be "use" (ASCII only: no other rune lowers to u, s or e)
     uint32_t p = 0;
     while (p < qn) {
@@ -131,12 +139,11 @@ __global__ __launch_bounds__(kBlock) void cassandra_use_kernel(Batch B, CassTabl
     }
     if (p + 3 > qn || (b[13 + p] | 0x20) != 'u' || (b[14 + p] | 0x20) != 's' || (b[15 + p] | 0x20) != 'e') return;
     const CassQuery Q = cass_parse_query(b + 13, qn, T.lower, T.nlower);
-    if (Q.status == CQ_OK && Q.is_use) use_list[atomicAdd(use_count, 1u)] = i;
+    if (Q.status == CQ_OK && Q.is_use) keys[i] = (uint64_t)ci << 32 | i;
 }
 
 __global__ __launch_bounds__(kBlock) void cassandra_classify_kernel(Batch B, CassTables T,
-                                                                    const uint32_t *__restrict__ use_list,
-                                                                    const uint32_t *__restrict__ use_count,
+                                                                    const uint64_t *__restrict__ use_keys,
                                                                     uint32_t answer_other) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= B.n) return;
@@ -169,7 +176,7 @@ __global__ __launch_bounds__(kBlock) void cassandra_classify_kernel(Batch B, Cas
             verdict = F.verdict;
             consumed = F.consumed;
         } else if (F.op == 0x07 || F.op == 0x09) {
-            if (!query_of(b, F.fl, &qn)) {
+            if (!query_of(b, len, &qn)) {
                 verdict = V_PARSE_ERROR;  // slice bounds panic
             } else {
                 Q = cass_parse_query(b + 13, qn, T.lower, T.nlower);
@@ -180,7 +187,7 @@ __global__ __launch_bounds__(kBlock) void cassandra_classify_kernel(Batch B, Cas
         } else if (F.op == 0x0D) {
             verdict = V_PARSE_ERROR;  // Uint16(data[10:11]) panics
         } else if (F.op == 0x0A) {
-            if (F.fl < 11 || 11u + be16(b + 9) > F.fl) verdict = V_PARSE_ERROR;  // panic
+            if (len < 11 || 11u + be16(b + 9) > len) verdict = V_PARSE_ERROR;  // panic (capacity-bounded, as above)
             else { verdict = V_PARSE_ERROR; consumed = 2; }                      // no prepared statement here
         } else {  // "/" + opcode name: every rule matches
             verdict = H->nrules ? V_ALLOW : H->terminal;
@@ -192,12 +199,15 @@ __global__ __launch_bounds__(kBlock) void cassandra_classify_kernel(Batch B, Cas
             const uint8_t *ks = nullptr;
             CassQuery K{};
             if (Q.seg3 == S3_KS_TABLE) {
-                const uint32_t nu = *use_count;
-                int64_t best = -1;
-                for (uint32_t u = 0; u < nu; u++) {
-                    const uint32_t j = use_list[u];
-                    if (j < i && (int64_t)j > best && B.conn_ids[j] == ci) best = j;
+                // the largest sorted key below (ci << 32 | i), if it is on connection ci
+                const uint64_t probe = (uint64_t)ci << 32 | i;
+                uint32_t lo = 0, hi = B.n;  // first key >= probe
+                while (lo < hi) {
+                    const uint32_t mid = lo + ((hi - lo) >> 1);
+                    if (use_keys[mid] < probe) lo = mid + 1; else hi = mid;
                 }
+                int64_t best = -1;
+                if (lo > 0 && (use_keys[lo - 1] >> 32) == ci) best = (int64_t)(use_keys[lo - 1] & 0xFFFFFFFFu);
                 if (best >= 0) {
                     const uint8_t *bj = B.arena + B.offs[best];
                     const uint32_t qj = be32(bj + 9);
@@ -256,15 +266,34 @@ __global__ __launch_bounds__(kBlock) void cassandra_classify_kernel(Batch B, Cas
     B.consumed[i] = consumed;
 }
 
-hipError_t LaunchCassandraClassify(const Batch &B, const CassTables &T, uint32_t *use_list, uint32_t *use_count,
+// Scratch bytes LaunchCassandraClassify needs for a batch of n requests.
+size_t CassandraScratchBytes(uint32_t n) {
+    size_t temp = 0;
+    if (hipcub::DeviceRadixSort::SortKeys(nullptr, temp, (const uint64_t *)nullptr, (uint64_t *)nullptr, (int)n, 0, 64) !=
+        hipSuccess)
+        return 0;
+    const size_t kb = ((size_t)n * sizeof(uint64_t) + 256 + 255) & ~(size_t)255;  // as LaunchCassandraClassify lays it out
+    return 2 * kb + ((temp + 255) & ~(size_t)255);
+}
+
+// scratch: CassandraScratchBytes(B.n) bytes (256-byte aligned)
+hipError_t LaunchCassandraClassify(const Batch &B, const CassTables &T, void *scratch, size_t scratch_bytes,
                                    bool answer_other, hipStream_t stream) {
     if (B.n == 0) return hipSuccess;
-    hipError_t rc = hipMemsetAsync(use_count, 0, sizeof(uint32_t), stream);
-    if (rc != hipSuccess) return rc;
+    const size_t kb = ((size_t)B.n * sizeof(uint64_t) + 256 + 255) & ~(size_t)255;
+    uint64_t *keys = (uint64_t *)scratch;
+    uint64_t *sorted = (uint64_t *)((uint8_t *)scratch + kb);
+    void *temp = (uint8_t *)scratch + 2 * kb;
+    if (scratch_bytes < 2 * kb) return hipErrorInvalidValue;
+    size_t temp_bytes = scratch_bytes - 2 * kb;
     const dim3 grid((B.n + kBlock - 1) / kBlock);
-    hipLaunchKernelGGL(cassandra_use_kernel, grid, dim3(kBlock), 0, stream, B, T, use_list, use_count);
-    hipLaunchKernelGGL(cassandra_classify_kernel, grid, dim3(kBlock), 0, stream, B, T, use_list, use_count,
-                       answer_other ? 1u : 0u);
+    hipLaunchKernelGGL(cassandra_use_kernel, grid, dim3(kBlock), 0, stream, B, T, keys);
+    hipError_t rc = hipGetLastError();
+    if (rc != hipSuccess) return rc;
+    // connection ids are < 2^32 and request indices < 2^32: all 64 bits
+    rc = hipcub::DeviceRadixSort::SortKeys(temp, temp_bytes, keys, sorted, (int)B.n, 0, 64, stream);
+    if (rc != hipSuccess) return rc;
+    hipLaunchKernelGGL(cassandra_classify_kernel, grid, dim3(kBlock), 0, stream, B, T, sorted, answer_other ? 1u : 0u);
     return hipGetLastError();
 }
 

@@ -43,9 +43,7 @@ __device__ __forceinline__ int read_message_set(Cur &cur, const uint8_t *b, uint
         KDec md{b, at, at + (uint32_t)msize, -1, 0, &cur};
         uint32_t crc = (uint32_t)dec_int(md, 4);
         if (msize <= 4) break;
-#ifndef L7G_KAFKA_EXP_NOCRC  // timing experiment only (verdicts then differ): no CRC work
         if (crc != crc32_ieee_staged(crctab, cur, b + at + 4, (uint32_t)msize - 4, stage)) break;  // stop, no drain
-#endif
         dec_skip(md, 1);
         int8_t attr = (int8_t)dec_int(md, 1);
         if (version >= 1) dec_skip(md, 8);
@@ -88,9 +86,6 @@ __device__ __forceinline__ uint32_t le_load4(Cur &c, const uint8_t *p) {
 // table string.
 __device__ __forceinline__ int32_t str_lookup(const DevStrSlot *tab, uint32_t mask, const uint8_t *strings, Cur &cur,
                                               const uint8_t *s, uint32_t n) {
-#ifdef L7G_KAFKA_EXP_NOLOOKUP  // timing experiment only (verdicts then differ): no table lookups
-    return -1;
-#endif
     uint32_t h = kWHashSeed;
     uint32_t p0 = 0, p1 = 0, p2 = 0, p3 = 0;  // the first 16 bytes, zero-padded
     for (uint32_t i = 0; i < n; i += 4) {

@@ -4,7 +4,7 @@
 //   OnNewConnection            proxylib/proxylib.go:57-74, connection.go:65-101
 //   OnData                     proxylib/proxylib.go:98-108, connection.go:104-174
 //   Close                      proxylib/proxylib.go:112-116
-// and three parsers (the registry of parserfactory.go:68-71):
+// and five parsers (the registry of parserfactory.go:68-71):
 //   "memcache"  proxylib/memcached/parser.go:186-202 with text/parser.go:72-330
 //               and binary/parser.go:58-205;
 //   "http"      HTTP/1 requests with Envoy's cilium.l7policy verdict
@@ -18,7 +18,9 @@
 //               query and matches the path; the host keeps the parser's
 //               state (the frame that set the keyspace, the PREPARE frames by
 //               stream id and by prepared id) and replays it to the device as
-//               extra requests of the same launch (see CassClassify).
+//               extra requests of the same launch (see CassClassify);
+//   "r2d2"      proxylib/r2d2/r2d2parser.go:140-214: one request per line,
+//               denied => DROP and "ERROR\r\n" injected.
 // HTTP and Kafka connections use proxylib's policymap semantics
 // (L7G_CONN_PROXYLIB: no port entry => drop, SrcId as the remote).
 //
@@ -541,7 +543,7 @@ struct Connection {
             if (d.size() - p < 11 || d[p + 4] != 0x0A || (d[p] & 0x80) || (d[p + 1] & 1)) continue;
             const uint32_t fl = 9 + Be32(d, p + 5);
             const uint32_t il = Be16(d, p + 9);
-            if (fl > d.size() - p || 11u + il > fl) continue;
+            if (fl > d.size() - p || 11u + il > d.size() - p) continue;  // (capacity-bounded slices)
             auto it = cass_by_id.find(d.substr(p + 11, il));
             if (it == cass_by_id.end()) continue;
             const std::string u = it->second.first.empty() ? CassEmptyUse() : it->second.first;
@@ -589,14 +591,15 @@ struct Connection {
         const uint32_t fl = 9 + rl;
         const std::string f = d.substr(0, fl);
         if (r) {  // cassandraParseReply (:605-642): RESULT / prepared binds a prepared id
+            // (slices of data[0:fl] are bounded by the joined buffer's capacity, d.size())
             if ((f[0] & 0x80) && !(f[1] & 1) && f[4] == 0x08) {
-                if (fl < 13) throw Panic();
-                if (Be32(f, 9) == 4) {
-                    if (fl < 15) throw Panic();
-                    const uint32_t il = Be16(f, 13);
-                    if (15u + il > fl) throw Panic();
+                if (d.size() < 13) throw Panic();
+                if (Be32(d, 9) == 4) {
+                    if (d.size() < 15) throw Panic();
+                    const uint32_t il = Be16(d, 13);
+                    if (15u + il > d.size()) throw Panic();
                     auto it = cass_by_stream.find((uint16_t)Be16(f, 2));
-                    if (it != cass_by_stream.end()) cass_by_id[f.substr(15, il)] = it->second;
+                    if (it != cass_by_stream.end()) cass_by_id[d.substr(15, il)] = it->second;
                 }
             }
             *n = fl;
@@ -613,7 +616,7 @@ struct Connection {
                 m[2] = (uint8_t)f[2];
                 m[3] = (uint8_t)f[3];
                 Inject(true, m, sizeof m);
-                Inject(true, f.data() + 9, 2 + Be16(f, 9));
+                Inject(true, d.data() + 9, 2 + Be16(d, 9));
             }
             *n = res.consumed;
             return FILTEROP_ERROR;
@@ -629,10 +632,16 @@ struct Connection {
                 if (k != std::string::npos) path.replace(k, 7, "execute");
             }
         } else if (f[4] == 0x07 || f[4] == 0x09) {
+            // the bytes the parse read: the frame, or up to the query's end when its
+            // slice runs past the frame into the buffer (capacity-bounded, as above);
+            // kept whole so that a replay to the device parses the same query
+            size_t ext = fl;
+            if (d.size() >= 13 && 13u + (uint64_t)Be32(d, 9) <= d.size()) ext = std::max<size_t>(ext, 13u + Be32(d, 9));
+            const std::string fx = d.substr(0, ext);
             const std::string use_before = cass_use;
-            path = CassPath(f, use_before);
-            if (CassIsUse(f)) cass_use = f;
-            if (f[4] == 0x09) cass_by_stream[(uint16_t)Be16(f, 2)] = {use_before, f};
+            path = CassPath(fx, use_before);
+            if (CassIsUse(fx)) cass_use = fx;
+            if (f[4] == 0x09) cass_by_stream[(uint16_t)Be16(f, 2)] = {use_before, fx};
         }
         std::vector<std::string> parts;
         for (size_t a = 0;;) {

@@ -3,9 +3,13 @@
 One process per GPU.  Requests are independent given their connection, so
 the data path shards by connection with no collective; the two exchange
 steps are
-  * policy distribution: the policy set (cilium.NetworkPolicy list, JSON)
-    arrives at rank 0 (the NPDS client, proxylib/proxylib/instance.go:168-219)
-    and is broadcast as bytes; every rank compiles the same immutable tables;
+  * compiled tables: the policy set (cilium.NetworkPolicy list) arrives at
+    rank 0 (the NPDS client, proxylib/proxylib/instance.go:168-219), which
+    compiles it (regex -> DFA / NFA, Kafka topic views) for every connection
+    of the node and broadcasts the compiled image (l7g_tables_export: the
+    policy source plus every rule set's device bytes and the rule-list ->
+    rule-set cache); the other ranks install it (l7g_tables_import) without
+    compiling -- one compile per node, not one per GPU;
   * per-rule hit counters: one all-reduce(sum) of the (rules + 8) uint64
     counters per batch (the UpdateProxyStatistics feed,
     pkg/endpoint/endpoint.go:2207-2233).
@@ -34,6 +38,39 @@ def broadcast_policy(policy, dist, src=0, device=None):
         buf.copy_(torch.frombuffer(bytearray(b), dtype=torch.uint8))
     dist.broadcast(buf, src)
     return bytes(buf.cpu().numpy().tobytes())
+
+
+def _broadcast_bytes(b, dist, src, device):
+    import torch
+    rank = dist.get_rank()
+    n = torch.tensor([len(b) if rank == src else 0], dtype=torch.int64, device=device)
+    dist.broadcast(n, src)
+    buf = torch.empty(int(n.item()), dtype=torch.uint8, device=device)
+    if rank == src:
+        buf.copy_(torch.frombuffer(bytearray(b), dtype=torch.uint8))
+    dist.broadcast(buf, src)
+    return bytes(buf.cpu().numpy().tobytes())
+
+
+def broadcast_tables(engine, dist, src=0, device=None, policy=None, conns=None):
+    """Rank `src` compiles (`policy` and the node's connection table `conns`,
+    both read on `src` only) and broadcasts its compiled tables; every other
+    rank installs them into `engine` without compiling.  Returns the image
+    bytes.  Over RCCL (backend "nccl", device = the rank's GPU) on the box,
+    gloo on CPU in the tests."""
+    rank = dist.get_rank()
+    if rank == src:
+        if policy is not None:
+            engine.update_policy(policy)
+        if conns is not None:
+            engine.set_connections(conns)
+        image = engine.export_tables()
+    else:
+        image = None
+    image = _broadcast_bytes(image, dist, src, device)
+    if rank != src:
+        engine.import_tables(image)
+    return image
 
 
 def allreduce_counters(counters, dist):

@@ -55,6 +55,33 @@ class Engine:
         if self._lib.l7g_policy_update_proto(self._h, b, len(b), err, 1024) != 0:
             raise PolicyError(err.value.decode(errors="replace"))
 
+    def export_tables(self):
+        """The current policy version's compiled tables (l7g_tables_export):
+        what rank 0 broadcasts so that the other ranks install them without
+        compiling (cilium_amd/dist.py)."""
+        n = C.c_size_t(0)
+        self._lib.l7g_tables_export(self._h, None, 0, C.byref(n))
+        buf = (C.c_uint8 * max(n.value, 1))()
+        if self._lib.l7g_tables_export(self._h, buf, n.value, C.byref(n)) != 0:
+            raise RuntimeError("l7g_tables_export failed")
+        return bytes(buf)[:n.value]
+
+    def import_tables(self, image):
+        b = bytes(image)
+        err = C.create_string_buffer(1024)
+        if self._lib.l7g_tables_import(self._h, b, len(b), err, 1024) != 0:
+            raise PolicyError(err.value.decode(errors="replace"))
+
+    @property
+    def tables_compiled(self):
+        """Rule sets this engine compiled itself since its policy version was installed."""
+        return int(self._lib.l7g_tables_compiled(self._h))
+
+    @property
+    def tables_digest(self):
+        """FNV-1a 64 of the device table blob (equal <=> byte-identical tables)."""
+        return int(self._lib.l7g_tables_digest(self._h))
+
     def policy_index(self, name):
         b = name.encode()
         return self._lib.l7g_policy_index(self._h, b, len(b))

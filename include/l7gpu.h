@@ -103,6 +103,24 @@ int l7g_policy_update_proto(l7g_engine *e, const uint8_t *buf, size_t len, char 
 int32_t l7g_policy_index(l7g_engine *e, const char *name, size_t len);
 int32_t l7g_policy_nrules(l7g_engine *e);
 
+/* Compiled tables across GPUs (the NPDS receiver is rank 0,
+ * proxylib/proxylib/instance.go:168-219): one rank compiles, the others install.
+ * l7g_tables_export writes the current policy version -- its source bytes and
+ * every compiler's rule sets (device images plus the rule-list -> rule-set
+ * cache) -- into buf; *len = the bytes needed.  Returns 0, or -2 when buf is
+ * NULL or cap is too small (only *len is set).  l7g_tables_import installs such
+ * an image: the policy is parsed, not compiled, and the connections are
+ * re-resolved against the imported rule sets (one the exporter did not compile
+ * is compiled here).  Same atomic swap / NACK as l7g_policy_update. */
+int l7g_tables_export(l7g_engine *e, uint8_t *buf, size_t cap, size_t *len);
+int l7g_tables_import(l7g_engine *e, const uint8_t *buf, size_t len, char *err, size_t errlen);
+/* Rule sets this engine compiled itself since its policy version was installed
+ * (0 on a rank that imported every rule set it uses). */
+uint64_t l7g_tables_compiled(l7g_engine *e);
+/* FNV-1a 64 of the device table blob the engine installs (equal digests <=>
+ * byte-identical tables). */
+uint64_t l7g_tables_digest(l7g_engine *e);
+
 /* Replaces the connection table (connection i = conns[i]); compiles the rule
  * sets the connections need.  0 = ok. */
 int l7g_conns_set(l7g_engine *e, const l7g_conn_t *conns, uint32_t n, char *err, size_t errlen);

@@ -10,7 +10,12 @@
  * reply bookkeeping and inject buffers stay on the host exactly as in
  * proxylib/proxylib/connection.go:118-174.
  *
- * Registered parsers: "memcache" (proxylib/memcached), "http" and "kafka"
+ * Registered parsers (the registry of proxylib/proxylib/parserfactory.go:68-71
+ * and each parser's init()): "memcache" (proxylib/memcached), "r2d2"
+ * (proxylib/r2d2/r2d2parser.go: a denied request is answered "ERROR\r\n"),
+ * "cassandra" (proxylib/cassandra/cassandraparser.go: denials answered with
+ * the unauthorized error frame 0x2100; the host keeps the parser's keyspace /
+ * prepared-statement state), and "http" and "kafka"
  * (the Envoy-filter protocols run through proxylib's policymap semantics:
  * policymap.go:150-236 -- installed entries only, no port entry => drop, SrcId
  * as the remote in both directions).  HTTP: a denied request is DROPped and

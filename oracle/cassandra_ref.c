@@ -285,8 +285,15 @@ static char *join_path(const char *op, const char *action, const char *table) {
 
 /* cassandraParseRequest on a complete frame; returns 0 (ok, *path set),
  * FILTEROP error code 2 (INVALID_FRAME_TYPE, *unprepared set for an EXECUTE
- * without a cached path) or -1 (panic). */
-static int parse_request(ref_cass *st, const uint8_t *d, uint32_t n, char **path, int *unprepared) {
+ * without a cached path) or -1 (panic).  The frame is data[0:fl] of the
+ * bytes.Join buffer (:174, :211): a Go slice expression is bounded by the
+ * slice's capacity, not its length, so data[9:13] and data[13:13+ql] read on
+ * into the bytes that follow the frame in the buffer and panic only past its
+ * end (cap = the buffer length n; bytes.Join of two or more slices allocates
+ * exactly n -- a single slice is copied by append, whose capacity Go rounds
+ * up to its allocator's size class; reads into that zeroed slack are not
+ * restated: parity unpinned there, no reference test reaches it). */
+static int parse_request(ref_cass *st, const uint8_t *d, uint32_t cap, char **path, int *unprepared) {
     *path = NULL;
     *unprepared = 0;
     if (d[0] & 0x80) return 2;
@@ -294,10 +301,10 @@ static int parse_request(ref_cass *st, const uint8_t *d, uint32_t n, char **path
     const uint8_t op = d[4];
     const char *name = op < 17 ? kOpcodes[op] : "";
     if (op == 0x07 || op == 0x09) {
-        if (n < 13) return -1;
+        if (cap < 13) return -1;
         const uint32_t ql = be32(d + 9);
         const uint32_t end = 13u + ql;  /* uint32 arithmetic, as in Go */
-        if (end < 13u || end > n) return -1;
+        if (end < 13u || end > cap) return -1;
         char *action, *table;
         int rc = parse_query(st, d + 13, ql, &action, &table);
         if (rc == Q_PANIC) return -1;
@@ -322,9 +329,9 @@ static int parse_request(ref_cass *st, const uint8_t *d, uint32_t n, char **path
     }
     if (op == 0x0D) return -1;  /* Uint16(data[10:11]) */
     if (op == 0x0A) {
-        if (n < 11) return -1;
+        if (cap < 11) return -1;
         const uint16_t il = be16(d + 9);
-        if (11u + il > n) return -1;
+        if (11u + il > cap) return -1;
         for (int k = 0; k < st->nbi; k++)
             if (st->bi[k].idlen == il && !memcmp(st->bi[k].id, d + 11, il) && st->bi[k].path[0]) {
                 *path = sdup(st->bi[k].path);
@@ -338,7 +345,9 @@ static int parse_request(ref_cass *st, const uint8_t *d, uint32_t n, char **path
     return 0;
 }
 
-/* cassandraParseReply (:605-642) on a complete frame; -1 = panic */
+/* cassandraParseReply (:605-642) on a complete frame; -1 = panic.  n: the
+ * capacity its slices are bounded by (the joined buffer's length, as in
+ * parse_request). */
 static int parse_reply(ref_cass *st, const uint8_t *d, uint32_t n) {
     if ((d[0] & 0x80) != 0x80) return 0;
     if (d[1] & 0x01) return 0;
@@ -427,7 +436,7 @@ int ref_cass_request(ref_cass *st, const ref_policy *pol, const ref_conn_t *c, c
     const uint32_t fl = 9 + rl;
     char *path;
     int unprepared;
-    int rc = parse_request(st, d, fl, &path, &unprepared);
+    int rc = parse_request(st, d, n, &path, &unprepared);
     if (rc < 0) return -1;
     if (rc > 0) {
         if (unprepared) {  /* sendUnpreparedMsg (:586-601): header + [short bytes] id */
@@ -465,7 +474,7 @@ int ref_cass_reply(ref_cass *st, const uint8_t *d, uint32_t n, int64_t *nout) {
     if (rl > 268435456u) { *nout = 3; return 4; }
     const int64_t missing = 9 + (int64_t)rl - (int64_t)n;
     if (missing > 0) { *nout = missing; return 0; }
-    if (parse_reply(st, d, 9 + rl) < 0) return -1;
+    if (parse_reply(st, d, n) < 0) return -1;
     *nout = 9 + (int64_t)rl;
     return 1;
 }

@@ -1,8 +1,9 @@
 """bench.py's N > 1 path on CPU (gloo), launched by torchrun from
 tests/test_dist_torchrun.py: the same stream on every rank (bench.make_workload,
-fixed seed), rank 0's policy broadcast, the stream sharded by connection with
-each protocol's bytes balanced (cilium_amd/dist.py, what bench.py calls), each
-rank's tables compiled by the product compiler (host-only engine), per-rank
+fixed seed), rank 0's compiled tables broadcast (installed, not compiled, by the other
+ranks), the stream sharded by connection with
+each protocol's bytes balanced (cilium_amd/dist.py, what bench.py calls), rank
+0's tables compiled by the product compiler (host-only engine), per-rank
 counters all-reduced, parity counts summed, timings MAX-reduced.  The device
 verdicts are stood in for by the oracle here (no GPU): this checks the
 exchange, the sharding and the counter path, not the kernels."""
@@ -34,12 +35,16 @@ def main():
         import cilium_amd
         from cilium_amd import dist as l7dist, gen
         full = bench.make_workload(gen, "cfg5", args.unique)
-        policy = l7dist.broadcast_policy(full.policy if rank == 0 else None, dist)
         _, shards = l7dist.shard_by_connection(full.conn_ids, full.lengths, len(full.conns), world, full.conns["proto"])
         w = gen.select(full, shards[rank], name=f"{full.name}[rank {rank}/{world}]")
         eng = cilium_amd.Engine(-1)
-        eng.update_policy(policy)
+        # rank 0 compiles, the others install its compiled tables (bench.py's path)
+        image = l7dist.broadcast_tables(eng, dist, policy=full.policy if rank == 0 else None,
+                                        conns=full.conns if rank == 0 else None)
         eng.set_connections(w.conns)
+        policy = full.policy  # for the oracle, which stands in for the device verdicts
+        compiled = torch.tensor([eng.tables_compiled if rank else 0], dtype=torch.int64)
+        dist.all_reduce(compiled)
         nr = eng.nrules
         t0 = time.perf_counter()
         v, r, c = refpy.Policy(policy).classify(w.conns, w.arena, w.offsets, w.lengths, w.conn_ids)
@@ -60,6 +65,7 @@ def main():
         if rank == 0:
             json.dump({"world": world, "n_full": full.n, "counters": cnt.tolist(), "max_s": float(t.item()),
                        "per_rank": [p.tolist() for p in per], "nrules": nr,
+                       "compiled_by_other_ranks": int(compiled.item()),
                        "stats": {k: v for k, v in eng.stats().items() if k.startswith(("http", "kafka", "mc"))}},
                       open(args.out, "w"))
     finally:

@@ -1,0 +1,108 @@
+"""Compiled tables broadcast from rank 0: rank 0
+compiles the node's policy for every connection and broadcasts the compiled
+image (cilium_amd/dist.py broadcast_tables over gloo here, RCCL on the box);
+ranks > 0 install it without compiling a single rule set, and every rank's
+device table blob is byte-identical to rank 0's and to a local compile."""
+import os
+import socket
+
+import pytest
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _workload():
+    from cilium_amd import gen
+    return gen.mixed_workload(3000, seed=77)
+
+
+def _worker(rank, world, port, q):
+    import sys
+    import torch.distributed as dist
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import cilium_amd
+        from cilium_amd import dist as l7dist
+        w = _workload()
+        eng = cilium_amd.Engine(-1)
+        image = l7dist.broadcast_tables(eng, dist, policy=w.policy if rank == 0 else None,
+                                        conns=w.conns if rank == 0 else None)
+        if rank != 0:
+            eng.set_connections(w.conns)  # this rank's connection table: every rule set is in the image
+        q.put((rank, len(image), eng.tables_digest, eng.tables_compiled, eng.nrules,
+               {k: v for k, v in eng.stats().items() if k.endswith("rulesets")}))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_tables_broadcast(world):
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=500) for _ in range(world))
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    import cilium_amd
+    w = _workload()
+    local = cilium_amd.Engine(-1)
+    local.update_policy(w.policy)
+    local.set_connections(w.conns)
+    assert local.tables_compiled > 0
+    r0 = res[0]
+    assert r0[3] == local.tables_compiled  # rank 0 compiled what a lone engine compiles
+    for rank, n, digest, compiled, nrules, st in res:
+        assert digest == local.tables_digest, rank  # byte-identical installed tables
+        assert nrules == local.nrules and st == r0[5]
+        if rank:
+            assert compiled == 0, (rank, compiled)  # installed, not compiled
+
+
+def test_import_refuses_corrupt_image():
+    import cilium_amd
+    w = _workload()
+    a = cilium_amd.Engine(-1)
+    a.update_policy(w.policy)
+    a.set_connections(w.conns)
+    img = a.export_tables()
+    b = cilium_amd.Engine(-1)
+    for bad in (img[:len(img) // 2], b"x" * 64, img[:-1]):
+        with pytest.raises(cilium_amd.PolicyError):
+            b.import_tables(bad)
+    b.import_tables(img)
+    b.set_connections(w.conns)
+    assert b.tables_digest == a.tables_digest and b.tables_compiled == 0
+
+
+def test_connection_outside_image_compiles_locally():
+    """A rank whose connections need a rule set the exporter never compiled
+    compiles just that one (same tables as compiling everything locally)."""
+    import numpy as np
+    import cilium_amd
+    w = _workload()
+    a = cilium_amd.Engine(-1)
+    a.update_policy(w.policy)
+    a.set_connections(w.conns[:1])
+    b = cilium_amd.Engine(-1)
+    b.import_tables(a.export_tables())
+    b.set_connections(w.conns)
+    c = cilium_amd.Engine(-1)
+    c.update_policy(w.policy)
+    c.set_connections(w.conns)
+    assert b.tables_compiled > 0
+    assert np.array_equal(np.array(sorted(b.stats().items())), np.array(sorted(c.stats().items())))

@@ -32,6 +32,7 @@ def test_torchrun_sharded_counters(tmp_path, world):
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=500, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     res = json.load(open(out))
+    assert res["compiled_by_other_ranks"] == 0  # ranks > 0 installed rank 0's compiled tables
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import bench

@@ -124,3 +124,60 @@ def test_prepare_result_execute_flow(oracle):
         conn.close()
     finally:
         P.close_module(mid)
+
+
+def test_use_heavy_batch_linear(engine, oracle):
+    """half of a large batch is USE frames on many connections, the
+    rest undotted-table SELECTs that need each connection's keyspace.  The
+    keyspace lookup is a sorted-key binary search (O(n log n) per batch), so
+    this finishes in well under a second; the scan it replaced was O(n x #USE).
+    Bit-exact against the oracle."""
+    import time
+    n, nconns = 200000, 512
+    rng = np.random.default_rng(11)
+    reqs = []
+    for i in range(n):
+        if rng.random() < 0.5:
+            reqs.append(gen.cass_query_frame(f"use ks{int(rng.integers(0, 4))}"))
+        else:
+            reqs.append(gen.cass_query_frame("select * from users"))
+    arena, offs, lens = gen.pack(reqs)
+    conns = gen.make_conns(nconns, 0, gen.CASS_PORT, True, gen.PROTO_CASSANDRA, [7] * nconns)
+    w = gen.Workload("cass-use", arena, offs, lens, rng.integers(0, nconns, size=n).astype(np.uint32), conns,
+                     gen.cassandra_policy())
+    engine.update_policy(w.policy)
+    engine.set_connections(w.conns)
+    engine.classify(w.arena, w.offsets, w.lengths, w.conn_ids)  # warm
+    t0 = time.perf_counter()
+    got = engine.classify(w.arena, w.offsets, w.lengths, w.conn_ids)
+    dt = time.perf_counter() - t0
+    assert_same(got, oracle.classify_workload(w, 8), w)
+    assert dt < 1.0, dt
+
+
+def test_query_slice_bounded_by_buffer(engine, oracle):
+    """cassandraParseRequest slices data[0:fl] of the joined buffer, so
+    data[9:13] and data[13:13+ql] are bounded by the buffer, not the frame
+    (cassandraparser.go:174, :211, :492-494): a QUERY frame too short for its
+    query length parses the bytes that follow it when the buffer holds them,
+    and panics only past the buffer's end.  Bit-exact against the oracle."""
+    q = b"select * from ks1.users"
+    full = gen.cass_query_frame(q)
+    body_short = len(q).to_bytes(4, "big") + q[:5]  # the frame ends inside the query
+    short = gen.cass_frame(0x07, body_short)
+    tail = q[5:] + b"\x00\x01\x00"
+    reqs_bufs = [
+        short + tail,        # query runs on into the buffer: parsed
+        short,               # buffer ends inside the query: panic
+        gen.cass_frame(0x07, b"\x00\x00"),            # frame shorter than 13 bytes, nothing follows: panic
+        gen.cass_frame(0x07, b"\x00\x00") + b"\x00\x00\x00\x00\x00",  # ... more bytes follow: ql read from them
+        full,
+    ]
+    arena, offs, lens = gen.pack(reqs_bufs)
+    conns = gen.make_conns(1, 0, gen.CASS_PORT, True, gen.PROTO_CASSANDRA, [7])
+    w = gen.Workload("cass-cap", arena, offs, lens, np.zeros(len(reqs_bufs), np.uint32), conns, gen.cassandra_policy())
+    engine.update_policy(w.policy)
+    engine.set_connections(w.conns)
+    got = engine.classify(w.arena, w.offsets, w.lengths, w.conn_ids)
+    assert_same(got, oracle.classify_workload(w, 1), w)
+    assert got[0][0] in (0, 1) and got[0][1] == 2  # the first parsed, the second panicked (PARSE_ERROR)
