@@ -29,8 +29,8 @@ namespace l7 {
 hipError_t LaunchHttpClassify(const Batch &B, const HttpTables &T, const uint32_t *sel, const uint32_t *sel_count,
                               bool any_cold, bool answer_other, uint32_t *tile_ctr, hipStream_t stream);
 hipError_t LaunchKafkaClassify(const Batch &B, const KafkaTables &T, const uint32_t *sel, const uint32_t *sel_count,
-                               bool answer_other, uint32_t *zlist, uint32_t *zcount, uint32_t *work,
-                               hipStream_t stream);
+                               bool answer_other, uint32_t *zlist, uint32_t *zcount, uint32_t *work, uint32_t *fbn,
+                               uint32_t *fbl, hipStream_t stream);
 hipError_t LaunchKafkaInflate(const Batch &B, const uint32_t *zlist, const uint32_t *zcount, uint8_t *region,
                               hipStream_t stream);
 uint32_t KafkaInflateBlocks();
@@ -88,8 +88,13 @@ struct StreamScratch {
         if (done_ev) hipEventDestroy(done_ev);
     }
 };
-constexpr size_t kMaxStreamScratch = 16;
-constexpr uint32_t kDynTilesMin = 1u << 18;  // unpartitioned HTTP batches from this size take tiles from a counter  // beyond: the least recently used one is handed over
+constexpr size_t kMaxStreamScratch = 16;   // per-stream scratch sets; beyond: the least recently used one is handed over
+constexpr uint32_t kDynTilesMin = 1u << 18;  // unpartitioned HTTP batches from this size take tiles from a counter
+// l7g_classify_host calls up to this size run zero-copy (kernels on the pinned staging)
+constexpr uint32_t kZeroCopyMaxRequests = 256;
+constexpr size_t kZeroCopyMaxBytes = 256 * 1024;
+// batches below this size skip the protocol split when one classifier can walk them alone
+constexpr uint32_t kPartitionMin = 4096;
 
 // l7g_classify_host's per-thread staging: its own stream, device arena and
 // request arrays (grow-only), so host-buffer calls from different threads
@@ -684,12 +689,14 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
     // (a Kafka-only or memcached-only engine partitions too: the kind / length
     // lists keep the Kafka kernel's waves converged, 1.55 -> 0.99 ms on cfg3,
     // and the text / binary lists the memcached kernel's)
-    const bool partitioned = nproto > 1 || e->has_kafka || e->has_mc;
+    // (a small memcached-only batch gains nothing from converged waves: its one
+    // kernel walks the batch itself, one launch fewer on the latency path)
+    const bool partitioned = nproto > 1 || e->has_kafka || (e->has_mc && n >= kPartitionMin);
     StreamScratch *S = nullptr;
     if ((rc = GetScratch(e, s, &S)) != hipSuccess) return (int)rc;
-    uint32_t *sel_k = nullptr, *sel_m = nullptr, *sel_h = nullptr, *sel_z = nullptr, *cnt = nullptr;
+    uint32_t *sel_k = nullptr, *sel_m = nullptr, *sel_h = nullptr, *sel_z = nullptr, *sel_f = nullptr, *cnt = nullptr;
     if (partitioned) {
-        const size_t need = 32 + (L7_KAFKA_CLASSES + 3) * (size_t)n;
+        const size_t need = 32 + (L7_KAFKA_CLASSES + 4) * (size_t)n;
         if (need > S->sel_cap) {
             if (S->d_sel) {  // the previous call on this stream may still use it
                 if (S->launched) rc = hipEventSynchronize(S->done_ev);
@@ -702,13 +709,14 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
         }
         if (rc != hipSuccess) return (int)rc;
         // [0, L7_KAFKA_CLASSES) Kafka classes, memcached retrievals, binary, HTTP, other text;
-        // [26, 27] Kafka entry counters (produce, other kinds), [28, 29] HTTP tile counters (hot, general
-        // launch); [31] compressed Kafka
+        // [26] Kafka entry counter, [27] Kafka requests handed to the exact walk, [28, 29] HTTP tile
+        // counters (hot, general launch); [31] compressed Kafka
         cnt = S->d_sel;
         sel_k = S->d_sel + 32;
         sel_m = sel_k + L7_KAFKA_CLASSES * (size_t)n;
         sel_h = sel_m + (size_t)n;
         sel_z = sel_h + (size_t)n;
+        sel_f = sel_z + (size_t)n;
         if (rc == hipSuccess) rc = hipMemsetAsync(cnt, 0, 32 * sizeof(uint32_t), s);
         if (rc == hipSuccess && e->has_kafka && !e->d_zreg) {
             rc = hipEventCreateWithFlags(&e->zreg_ev, hipEventDisableTiming);
@@ -759,7 +767,8 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
     mark(2);
     uint32_t *zcount = cnt ? cnt + 31 : nullptr;
     if (rc == hipSuccess && run[2])
-        rc = LaunchKafkaClassify(B, e->kt, sel_k, cnt, !partitioned, sel_z, zcount, cnt ? cnt + 26 : nullptr, s);
+        rc = LaunchKafkaClassify(B, e->kt, sel_k, cnt, !partitioned, sel_z, zcount, cnt ? cnt + 26 : nullptr,
+                                 cnt ? cnt + 27 : nullptr, sel_f, s);
     // requests with gzip / snappy messages: decoded, their sets read, failures answered
     if (rc == hipSuccess && run[2] && sel_z) {
         // the engine's one decode region: after the previous inflate launch on any stream
@@ -870,18 +879,34 @@ int l7g_classify_host(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, c
         memcpy(pi + nn * 12, conn, (size_t)n * 4);
     }
     if (arena_len) memcpy(pi + a_off, arena, arena_len);
+    // A small call (the Envoy adapter's Allowed(), one OnData) is latency, not
+    // bandwidth: the kernels read the inputs from and write the verdicts to the
+    // pinned staging in place (zero-copy, over PCIe), so the call is one launch
+    // and a synchronise instead of copy, launch, copy, synchronise.
+    static const bool zc_on = [] {
+        const char *v = getenv("L7G_SYNC_ZEROCOPY");
+        return !(v && v[0] == '0');
+    }();
+    const bool zc = zc_on && n <= kZeroCopyMaxRequests && a_off + arena_len <= kZeroCopyMaxBytes;
     uint8_t *d_in = H->dev, *d_out = H->dev + H->in_cap;
+    if (zc) {
+        void *dp = nullptr;
+        if ((rc = hipHostGetDevicePointer(&dp, H->pin_in, 0)) != hipSuccess) return (int)rc;
+        d_in = (uint8_t *)dp;
+        if ((rc = hipHostGetDevicePointer(&dp, H->pin_out, 0)) != hipSuccess) return (int)rc;
+        d_out = (uint8_t *)dp;
+    }
     const uint64_t *d_o = (const uint64_t *)d_in;
     const uint32_t *d_l = (const uint32_t *)(d_in + nn * 8), *d_c = (const uint32_t *)(d_in + nn * 12);
     uint8_t *d_v = d_out;
     int32_t *d_r = (int32_t *)(d_out + ((nn + 3) & ~(size_t)3));
     uint32_t *d_cons = (uint32_t *)(d_out + ((nn + 3) & ~(size_t)3) + nn * 4);
     hipStream_t s = H->s;
-    rc = hipMemcpyAsync(d_in, pi, a_off + arena_len, hipMemcpyHostToDevice, s);
+    if (!zc) rc = hipMemcpyAsync(d_in, pi, a_off + arena_len, hipMemcpyHostToDevice, s);
     if (rc == hipSuccess)
         rc = (hipError_t)l7g_classify(e, d_in + a_off, arena_len, d_o, d_l, d_c, n, d_v, d_r, d_cons, nullptr, s);
     const size_t out_bytes = ((nn + 3) & ~(size_t)3) + nn * 8;
-    if (rc == hipSuccess && n) rc = hipMemcpyAsync(H->pin_out, d_out, out_bytes, hipMemcpyDeviceToHost, s);
+    if (rc == hipSuccess && n && !zc) rc = hipMemcpyAsync(H->pin_out, d_out, out_bytes, hipMemcpyDeviceToHost, s);
     if (rc == hipSuccess) rc = hipStreamSynchronize(s);
     if (rc == hipSuccess && n) {
         const uint8_t *po = H->pin_out;

@@ -172,20 +172,27 @@ int l7g_stats(l7g_engine *e, l7g_stats_t *out);
  * event loop -- Envoy's cilium.l7policy decodeHeaders
  * (envoy/cilium_l7policy.cc:127-182), which would return StopIteration and
  * resume (continueDecoding / sendLocalReply) from the callback.  Submitted
- * requests are copied into the batcher's arena; a flusher thread classifies
- * them in one l7g_classify_host launch once max_requests are pending or the
- * oldest has waited max_wait_us, then calls each request's callback (from the
- * flusher thread, in submission order).  A device failure answers every
- * request of that flush L7G_UNSUPPORTED. */
+ * requests are copied into one of the batcher's sharded queues (the calling
+ * thread's); two flusher threads each take everything pending once
+ * max_requests are pending or the oldest has waited max_wait_us, classify it
+ * with one l7g_classify_host launch on their own stream (so one batch is on
+ * the device while the next is gathered), and call each request's callback
+ * from the flusher thread -- batches in the order they were taken, a thread's
+ * requests in submission order.  A device failure answers every request of
+ * that flush L7G_UNSUPPORTED.  A callback must not call l7g_batcher_flush or
+ * l7g_batcher_destroy (from a flusher thread both return at once, doing
+ * nothing). */
 typedef void (*l7g_done_fn)(void *ctx, uint8_t verdict, int32_t rule, uint32_t consumed);
 typedef struct l7g_batcher l7g_batcher;
 l7g_batcher *l7g_batcher_create(l7g_engine *e, uint32_t max_requests, uint32_t max_wait_us);
-/* 0 = queued; -1 = the batcher is shutting down (callback not called). */
+/* 0 = queued; -1 = the batcher is shutting down; -2 = backpressure: 64 x
+ * max_requests requests are already waiting (the callback is not called; the
+ * caller decides the request itself or retries). */
 int l7g_batcher_submit(l7g_batcher *b, const uint8_t *req, uint32_t len, uint32_t conn, l7g_done_fn done, void *ctx);
 /* Flushes now and returns once every request submitted before the call has
- * had its callback. */
+ * had its callback (0); -1 when called from a callback. */
 int l7g_batcher_flush(l7g_batcher *b);
-/* Flushes what is pending, then stops the flusher thread. */
+/* Flushes what is pending, then stops the flusher threads. */
 void l7g_batcher_destroy(l7g_batcher *b);
 /* Requests classified and launches made so far (for latency accounting). */
 void l7g_batcher_stats(l7g_batcher *b, uint64_t *requests, uint64_t *launches);

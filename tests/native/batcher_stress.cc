@@ -1,0 +1,77 @@
+// Batcher threading on a host-only engine (no GPU needed: every flush is
+// answered L7G_UNSUPPORTED, which still runs the sharded queues, both
+// flusher threads, batch-ordered callbacks, flush and backpressure).
+// Checks: every request's callback exactly once, a thread's callbacks in its
+// submission order, flush() returns only after its requests were answered,
+// flush() from a callback returns -1, submit beyond the backpressure cap
+// returns -2.  stdout: one JSON object.
+#include <atomic>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "../../include/l7gpu.h"
+
+static std::atomic<uint64_t> g_calls{0};
+static std::atomic<int> g_bad{0};
+static std::vector<std::atomic<uint32_t>> *g_next;  // per thread: the next sequence number expected
+static l7g_batcher *g_b = nullptr;
+static std::atomic<int> g_flush_rc{1};
+
+static void done(void *ctx, uint8_t verdict, int32_t rule, uint32_t consumed) {
+    const uint64_t v = (uint64_t)(uintptr_t)ctx;
+    const uint32_t t = (uint32_t)(v >> 32), seq = (uint32_t)v;
+    if (verdict != L7G_UNSUPPORTED || rule != -1 || consumed != 0) g_bad++;
+    if ((*g_next)[t].load() != seq) g_bad++;  // out of order or twice
+    (*g_next)[t].store(seq + 1);
+    if (t == 0 && seq == 7) g_flush_rc = l7g_batcher_flush(g_b);  // re-entry: must not deadlock
+    g_calls++;
+}
+
+int main() {
+    char err[256];
+    l7g_engine *e = l7g_engine_create(L7G_HOST_ONLY, err, sizeof err);
+    if (!e) { printf("{\"error\": \"%s\"}\n", err); return 1; }
+    const int T = 8, N = 20000;
+    std::vector<std::atomic<uint32_t>> next(T);
+    for (auto &x : next) x = 0;
+    g_next = &next;
+    g_b = l7g_batcher_create(e, 256, 50);
+    std::atomic<int> rejected{0};
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; t++)
+        th.emplace_back([t, &rejected] {
+            uint8_t req[64];
+            memset(req, 'a', sizeof req);
+            for (uint32_t i = 0; i < (uint32_t)N; i++) {
+                int rc;
+                while ((rc = l7g_batcher_submit(g_b, req, 16 + (i % 48), 0, done,
+                                                (void *)(uintptr_t)((uint64_t)t << 32 | i))) == -2)
+                    rejected++, std::this_thread::yield();
+                if (rc != 0) { g_bad++; return; }
+            }
+        });
+    for (auto &x : th) x.join();
+    const int frc = l7g_batcher_flush(g_b);
+    const uint64_t after_flush = g_calls.load();
+    // backpressure: a batcher whose flushers cannot keep up (huge wait) refuses past 64 x max_requests
+    l7g_batcher *slow = l7g_batcher_create(e, 4, 5000000);
+    int queued = 0, refused = 0;
+    uint8_t one = 'x';
+    for (int i = 0; i < 1000; i++) {
+        const int rc = l7g_batcher_submit(slow, &one, 1, 0, [](void *, uint8_t, int32_t, uint32_t) {}, nullptr);
+        if (rc == 0) queued++; else if (rc == -2) refused++;
+    }
+    l7g_batcher_destroy(slow);
+    uint64_t reqs = 0, launches = 0;
+    l7g_batcher_stats(g_b, &reqs, &launches);
+    l7g_batcher_destroy(g_b);
+    l7g_engine_destroy(e);
+    printf("{\"calls\": %llu, \"after_flush\": %llu, \"expected\": %d, \"bad\": %d, \"flush_rc\": %d, "
+           "\"reentrant_flush_rc\": %d, \"launches\": %llu, \"queued\": %d, \"refused\": %d, \"rejected\": %d}\n",
+           (unsigned long long)g_calls.load(), (unsigned long long)after_flush, T * N, g_bad.load(), frc,
+           g_flush_rc.load(), (unsigned long long)launches, queued, refused, rejected.load());
+    return 0;
+}

@@ -93,7 +93,7 @@ int main(int argc, char **argv) {
     std::ostringstream bat;
     bat << "[";
     const struct { int threads; double rate_per_thread; uint32_t n, wait_us; } cfgs[] = {
-        {8, 20000.0, 256, 100}, {8, 100000.0, 1024, 200}};
+        {8, 20000.0, 256, 100}, {8, 100000.0, 1024, 200}, {8, 600000.0, 4096, 200}};
     bool firstc = true;
     for (auto &cf : cfgs) {
         l7g_batcher *b = l7g_batcher_create(e, cf.n, cf.wait_us);

@@ -1,0 +1,23 @@
+"""l7g_batcher's threading on the CPU (tests/native/batcher_stress.cc on a
+host-only engine): sharded submit from 8 threads, two flushers, every callback
+once and in each thread's submission order, flush, re-entrant flush refused,
+backpressure past 64 x max_requests."""
+import json
+import subprocess
+
+import pytest
+
+from cilium_amd import build as b
+
+
+@pytest.mark.timeout(300)
+def test_batcher_threads_order_flush_backpressure():
+    exe = [x for x in b.build_test_natives() if x.endswith("batcher_stress")][0]
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr
+    d = json.loads(r.stdout)
+    assert d["bad"] == 0, d
+    assert d["calls"] == d["expected"] == d["after_flush"], d  # flush returned after every callback
+    assert d["flush_rc"] == 0 and d["reentrant_flush_rc"] == -1, d
+    assert d["launches"] < d["expected"] // 8, d  # batched, not one launch per request
+    assert d["queued"] == 4 * 64 and d["refused"] == 1000 - 4 * 64, d
