@@ -10,8 +10,9 @@ GPU -- 50 % HTTP (cfg2's 64 rules), 30 % Kafka (cfg3's ~1k rules), 20 %
 memcached text + binary -- built from a 2M-request unique stream.
 
 Multi-GPU (N > 1, one process per GPU): every rank generates the SAME unique
-stream (same seed, same policy), rank 0's policy bytes are broadcast over
-RCCL, and the stream is sharded by connection (whole connections per rank,
+stream (same seed, same policy), rank 0 compiles the policy for the node's
+connections and broadcasts the compiled tables over RCCL (the other ranks
+install them without compiling: l7g_tables_import), and the stream is sharded by connection (whole connections per rank,
 each protocol's bytes balanced over ranks: cilium_amd/dist.py).  Each rank
 tiles its shard up to the per-GPU request count (weak scaling), classifies it
 every step and all-reduces the counters.  Every rank checks every verdict of
@@ -365,7 +366,7 @@ def main():
     verdict = d_v.cpu().numpy()
     rule = d_r.cpu().numpy()
     consumed = d_c.cpu().numpy().view(np.uint32)
-    pol = refpy.Policy(policy)
+    pol = refpy.Policy(full.policy)
     t1 = time.perf_counter()
     rv, rr, rc = pol.classify(w.conns, w.arena, w.offsets, w.lengths, w.conn_ids, threads)
     cpu_all_s = time.perf_counter() - t1

@@ -4,81 +4,83 @@
 // loop (envoy/cilium_l7policy.cc:127-182).  One device launch per request is
 // all latency and no throughput, so callers submit requests here instead and
 // get a callback.  Layout (round 4):
-//   * submit appends to one of kShards pending queues (the calling thread's
-//     shard, picked once per thread), each under its own lock, into storage
-//     that keeps its capacity between flushes -- eight submitting threads do
-//     not serialise on one lock or on a growing vector;
-//   * kFlushers flusher threads each take everything pending (once
-//     max_requests are pending, the oldest has waited max_wait_us, or a flush
-//     is asked for), classify it with one l7g_classify_host call on their own
-//     stream and staging, and run its callbacks -- so one batch is on the
-//     device while the next is being gathered and launched;
+//   * submitters write straight into a pinned batch slot, in the layout the
+//     device copy reads (offsets, lengths, connections, request bytes): a
+//     compare-and-swap reserves an index and an arena range, the submitting
+//     threads copy their bytes in parallel, and no lock is taken;
+//   * kFlushers flusher threads each seal the open slot (once max_requests
+//     are in it, its first request has waited max_wait_us, or a flush is asked
+//     for), open a free one in its place, wait for the sealed slot's last
+//     writers, and classify it where it lies -- one copy to the device (none
+//     for a small batch), one launch, no gather on the host -- on the
+//     flusher's own stream, then run its callbacks; so one batch is on the
+//     device while the next fills;
 //   * callbacks run on the flusher threads, batch after batch in the order
-//     the batches were taken (a thread's requests in submission order); a
+//     the batches were sealed (a thread's requests in submission order); a
 //     callback must not call l7g_batcher_flush or l7g_batcher_destroy (both
 //     return at once, doing nothing, when called from a flusher thread);
-//   * at most max_pending requests wait (max_requests x 64): beyond that
-//     submit returns -2 and the caller answers the request itself.
+//   * a slot holds 2 x max_requests requests (at least 1024) and 2 KiB of
+//     request bytes per request; when both flushers are busy and the open
+//     slot is full, submit returns -2 (backpressure) and the caller answers
+//     the request itself.
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <thread>
 #include <vector>
 
 #include "../../include/l7gpu.h"
+#include "capi_internal.h"
 
 namespace {
 
-constexpr int kShards = 16;
 constexpr int kFlushers = 2;
+constexpr int kSlots = kFlushers + 2;  // one per flusher, the open one, and one ready to open
+constexpr uint64_t kBytesMask = (1ull << 40) - 1;  // Slot::resv = count << 40 | arena bytes
+constexpr uint32_t kMinSlotRequests = 1024;
+constexpr uint64_t kSlotBytesPerRequest = 2048;
 using Clock = std::chrono::steady_clock;
+enum : int { FREE = 0, OPEN = 1, SEALED = 2 };
 
-struct Pending {
-    std::vector<uint8_t> arena;
-    std::vector<uint64_t> off;
-    std::vector<uint32_t> len, conn;
+int64_t now_ns() { return Clock::now().time_since_epoch().count(); }
+
+struct Slot {
+    uint8_t *mem = nullptr;  // pinned; plain malloc when there is no device (a host-only engine)
+    bool pinned = false;
+    uint64_t *off = nullptr;
+    uint32_t *len = nullptr, *conn = nullptr;
+    uint8_t *arena = nullptr;
     std::vector<l7g_done_fn> fn;
     std::vector<void *> ctx;
-    void clear() {  // (capacity kept)
-        arena.clear();
-        off.clear();
-        len.clear();
-        conn.clear();
-        fn.clear();
-        ctx.clear();
-    }
-    size_t n() const { return off.size(); }
+    uint32_t cap_n = 0;
+    uint64_t cap_bytes = 0;
+    std::atomic<uint64_t> resv{0};
+    std::atomic<int32_t> writers{0};  // submitters between their check of `state` and their last store
+    std::atomic<int> state{FREE};
+    std::atomic<int64_t> first_ns{0};  // when its first request was reserved
 };
-
-struct alignas(64) Shard {
-    std::mutex mu;
-    Pending q;
-};
-
-std::atomic<uint32_t> g_next_shard{0};
-thread_local int t_shard = -1;
 
 }  // namespace
 
 struct l7g_batcher {
     l7g_engine *e = nullptr;
     uint32_t max_n = 1;
-    uint64_t max_pending = 64;
     std::chrono::microseconds max_wait{0};
-    Shard shards[kShards];
-    std::atomic<uint64_t> pending{0};
-    std::atomic<int64_t> oldest_ns{0};  // steady-clock time of the first pending submission (0: none)
+    Slot slots[kSlots];
+    std::atomic<int> open_idx{0};
+    std::atomic<bool> stop{false};
+    std::atomic<uint64_t> n_submitted{0};
     // flusher coordination
     std::mutex mu;
     std::condition_variable cv, done_cv;
-    std::atomic<bool> stop{false};
-    uint64_t flush_gen = 0;  // a flush was asked for (flushers take what is pending at once)
-    uint64_t submitted = 0, completed = 0, launches = 0;  // (completed / launches under mu)
-    std::atomic<uint64_t> n_submitted{0};
-    uint64_t take_seq = 0, deliver_seq = 0;  // batch order of callbacks (under mu)
-    std::mutex take_mu;                      // one flusher gathers at a time
+    uint64_t flush_gen = 0;                  // a flush was asked for: seal what is open at once
+    uint64_t completed = 0, launches = 0;    // (under mu)
+    uint64_t seal_seq = 0, deliver_seq = 0;  // batch order of callbacks (under mu)
+    std::mutex seal_mu;
     std::thread th[kFlushers];
 
     bool IsFlusher() const {
@@ -86,74 +88,97 @@ struct l7g_batcher {
             if (t.get_id() == std::this_thread::get_id()) return true;
         return false;
     }
+    void Wake() {
+        // (taken and released so that a flusher between its check and its wait
+        // cannot miss the notification)
+        { std::lock_guard<std::mutex> g(mu); }
+        cv.notify_all();
+    }
+    uint32_t OpenCount() const { return (uint32_t)(slots[open_idx.load()].resv.load() >> 40); }
 
-    // Moves every shard's pending requests into w (offsets rebased); returns the count.
-    size_t Gather(Pending &w) {
-        w.clear();
-        for (auto &s : shards) {
-            std::lock_guard<std::mutex> g(s.mu);
-            Pending &q = s.q;
-            if (!q.n()) continue;
-            const uint64_t base = w.arena.size();
-            w.arena.insert(w.arena.end(), q.arena.begin(), q.arena.end());
-            for (uint64_t o : q.off) w.off.push_back(base + o);
-            w.len.insert(w.len.end(), q.len.begin(), q.len.end());
-            w.conn.insert(w.conn.end(), q.conn.begin(), q.conn.end());
-            w.fn.insert(w.fn.end(), q.fn.begin(), q.fn.end());
-            w.ctx.insert(w.ctx.end(), q.ctx.begin(), q.ctx.end());
-            q.clear();
-        }
-        pending.fetch_sub(w.n());
-        oldest_ns.store(pending.load() ? Clock::now().time_since_epoch().count() : 0);
-        return w.n();
+    // Seals the open slot if it holds requests and a free slot can take its
+    // place; returns its index (and its batch number), or -1.
+    int Seal(uint64_t *seq) {
+        std::lock_guard<std::mutex> g(seal_mu);
+        const int i = open_idx.load();
+        Slot &s = slots[i];
+        if ((s.resv.load() >> 40) == 0) return -1;
+        int j = -1;
+        for (int k = 1; k < kSlots && j < 0; k++)
+            if (slots[(i + k) % kSlots].state.load() == FREE) j = (i + k) % kSlots;
+        if (j < 0) return -1;  // (cannot happen with kSlots = kFlushers + 2; the open slot keeps filling)
+        Slot &t = slots[j];
+        t.resv.store(0);
+        t.first_ns.store(0);
+        t.state.store(OPEN);
+        open_idx.store(j);
+        // seq_cst with the submitters' writers++ then state load: a submitter
+        // either sees SEALED and moves on, or is counted in s.writers
+        s.state.store(SEALED);
+        std::lock_guard<std::mutex> g2(mu);
+        *seq = seal_seq++;
+        return i;
     }
 
     void Run() {
-        Pending work;
         std::vector<uint8_t> v;
         std::vector<int32_t> r;
         std::vector<uint32_t> c;
+        {  // this thread's stream and staging, made now rather than under its first batch
+            uint8_t vv;
+            int32_t rr;
+            uint32_t cc;
+            const Slot &s0 = slots[0];
+            l7g_host_run_pinned(e, 0, 0, s0.off, s0.len, s0.conn, s0.arena, &vv, &rr, &cc);
+        }
         uint64_t seen_flush = 0;
         for (;;) {
             {
                 std::unique_lock<std::mutex> lk(mu);
                 for (;;) {
-                    if (stop && pending.load() == 0) return;
-                    const uint64_t p = pending.load();
+                    const uint32_t p = OpenCount();
+                    if (stop && p == 0) return;
                     if (p >= max_n || (p && (stop || flush_gen != seen_flush))) break;
                     if (p) {
-                        const int64_t o = oldest_ns.load();
+                        int64_t o = slots[open_idx.load()].first_ns.load();
+                        if (o == 0) o = now_ns();  // (its first writer has not stamped it yet)
                         const auto due = Clock::time_point(Clock::duration(o)) + max_wait;
-                        if (o && Clock::now() >= due) break;
-                        cv.wait_until(lk, o ? due : Clock::now() + max_wait);
+                        if (Clock::now() >= due) break;
+                        cv.wait_until(lk, due);
                     } else {
-                        if (flush_gen != seen_flush) { seen_flush = flush_gen; done_cv.notify_all(); }
-                        cv.wait(lk);
+                        if (flush_gen != seen_flush) {
+                            seen_flush = flush_gen;
+                            done_cv.notify_all();
+                        }
+                        cv.wait_for(lk, std::chrono::milliseconds(100));
                     }
                 }
                 seen_flush = flush_gen;
             }
-            uint64_t seq;
-            {
-                std::lock_guard<std::mutex> g(take_mu);
-                if (!Gather(work)) continue;
-                std::lock_guard<std::mutex> g2(mu);
-                seq = take_seq++;
+            uint64_t seq = 0;
+            const int i = Seal(&seq);
+            if (i < 0) {  // the other flusher sealed it first
+                std::this_thread::yield();
+                continue;
             }
-            const size_t n = work.n();
-            v.assign(n, 0);
-            r.assign(n, -1);
-            c.assign(n, 0);
-            const int rc = l7g_classify_host(e, work.arena.data(), work.arena.size(), work.off.data(), work.len.data(),
-                                             work.conn.data(), (uint32_t)n, v.data(), r.data(), c.data());
+            Slot &s = slots[i];
+            while (s.writers.load() != 0) std::this_thread::yield();
+            const uint64_t rv = s.resv.load();
+            const uint32_t n = (uint32_t)(rv >> 40);
+            const uint64_t bytes = rv & kBytesMask;
+            v.resize(n);
+            r.resize(n);
+            c.resize(n);
+            const int rc = l7g_host_run_pinned(e, n, bytes, s.off, s.len, s.conn, s.arena, v.data(), r.data(), c.data());
             {  // callbacks in batch order
                 std::unique_lock<std::mutex> lk(mu);
                 done_cv.wait(lk, [&] { return deliver_seq == seq; });
             }
-            for (size_t i = 0; i < n; i++) {
-                if (rc != 0) work.fn[i](work.ctx[i], L7G_UNSUPPORTED, -1, 0);
-                else work.fn[i](work.ctx[i], v[i], r[i], c[i]);
+            for (uint32_t k = 0; k < n; k++) {
+                if (rc != 0) s.fn[k](s.ctx[k], L7G_UNSUPPORTED, -1, 0);
+                else s.fn[k](s.ctx[k], v[k], r[k], c[k]);
             }
+            s.state.store(FREE);
             {
                 std::lock_guard<std::mutex> g(mu);
                 deliver_seq++;
@@ -161,10 +186,19 @@ struct l7g_batcher {
                 launches++;
             }
             done_cv.notify_all();
-            cv.notify_all();  // the other flusher may have work waiting
+            cv.notify_all();
         }
     }
 };
+
+static void FreeSlots(l7g_batcher *b) {
+    for (auto &s : b->slots) {
+        if (!s.mem) continue;
+        if (s.pinned) l7g_pinned_free(s.mem);
+        else free(s.mem);
+        s.mem = nullptr;
+    }
+}
 
 extern "C" {
 
@@ -172,49 +206,82 @@ l7g_batcher *l7g_batcher_create(l7g_engine *e, uint32_t max_requests, uint32_t m
     if (!e) return nullptr;
     auto *b = new l7g_batcher();
     b->e = e;
-    b->max_n = max_requests ? max_requests : 1;
-    b->max_pending = (uint64_t)b->max_n * 64;
+    b->max_n = std::min<uint32_t>(max_requests ? max_requests : 1, 1u << 20);
     b->max_wait = std::chrono::microseconds(max_wait_us);
-    for (auto &s : b->shards) {
-        s.q.arena.reserve((size_t)b->max_n * 512 / kShards + 4096);
-        s.q.off.reserve(b->max_n / kShards + 64);
+    const uint32_t cap_n = std::max<uint32_t>(2 * b->max_n, kMinSlotRequests);
+    const uint64_t cap_bytes = (uint64_t)cap_n * kSlotBytesPerRequest;
+    const size_t meta = ((size_t)cap_n * 16 + 255) & ~(size_t)255;
+    const size_t total = meta + cap_bytes + 64;  // (+64: aligned 16-byte reads past the last request stay inside)
+    for (auto &s : b->slots) {
+        s.mem = (uint8_t *)l7g_pinned_alloc(total);
+        s.pinned = s.mem != nullptr;
+        if (!s.mem) s.mem = (uint8_t *)malloc(total);
+        if (!s.mem) {
+            FreeSlots(b);
+            delete b;
+            return nullptr;
+        }
+        s.off = (uint64_t *)s.mem;
+        s.len = (uint32_t *)(s.mem + (size_t)cap_n * 8);
+        s.conn = (uint32_t *)(s.mem + (size_t)cap_n * 12);
+        s.arena = s.mem + meta;
+        s.fn.resize(cap_n);
+        s.ctx.resize(cap_n);
+        s.cap_n = cap_n;
+        s.cap_bytes = cap_bytes;
     }
+    b->slots[0].state.store(OPEN);
     for (auto &t : b->th) t = std::thread([b] { b->Run(); });
     return b;
 }
 
 int l7g_batcher_submit(l7g_batcher *b, const uint8_t *req, uint32_t len, uint32_t conn, l7g_done_fn done, void *ctx) {
-    if (b->stop) return -1;  // (unsynchronised read: a submit racing destroy is the caller's error)
-    if (b->pending.load(std::memory_order_relaxed) >= b->max_pending) return -2;
-    if (t_shard < 0) t_shard = (int)(g_next_shard.fetch_add(1) % kShards);
-    Shard &s = b->shards[t_shard];
-    // counted before it is queued, so a gather never takes more than `pending` holds
-    b->n_submitted.fetch_add(1);
-    const uint64_t p = b->pending.fetch_add(1) + 1;
-    {
-        std::lock_guard<std::mutex> g(s.mu);
-        Pending &q = s.q;
-        q.off.push_back(q.arena.size());
-        q.arena.insert(q.arena.end(), req, req + len);
-        q.len.push_back(len);
-        q.conn.push_back(conn);
-        q.fn.push_back(done);
-        q.ctx.push_back(ctx);
+    if (b->stop.load(std::memory_order_relaxed)) return -1;  // (a submit racing destroy is the caller's error)
+    if (len > b->slots[0].cap_bytes) return -2;               // never fits a slot
+    for (int tries = 0;;) {
+        const int i = b->open_idx.load();
+        Slot &s = b->slots[i];
+        s.writers.fetch_add(1);
+        if (s.state.load() != OPEN || b->open_idx.load() != i) {  // sealed under us: take the next one
+            s.writers.fetch_sub(1);
+            continue;
+        }
+        uint64_t rv = s.resv.load(), n, at;
+        bool full = false;
+        for (;;) {
+            n = rv >> 40;
+            at = rv & kBytesMask;
+            if (n + 1 > s.cap_n || at + len > s.cap_bytes) {
+                full = true;
+                break;
+            }
+            if (s.resv.compare_exchange_weak(rv, (n + 1) << 40 | (at + len))) break;
+        }
+        if (full) {
+            s.writers.fetch_sub(1);
+            b->Wake();
+            if (++tries > 1000) return -2;  // both flushers busy and the open slot full: backpressure
+            std::this_thread::yield();
+            continue;
+        }
+        if (n == 0) s.first_ns.store(now_ns());
+        s.off[n] = at;
+        s.len[n] = len;
+        s.conn[n] = conn;
+        s.fn[n] = done;
+        s.ctx[n] = ctx;
+        memcpy(s.arena + at, req, len);
+        s.writers.fetch_sub(1);
+        b->n_submitted.fetch_add(1);
+        if (n == 0 || n + 1 == b->max_n) b->Wake();
+        return 0;
     }
-    if (p == 1) {
-        int64_t z = 0;
-        b->oldest_ns.compare_exchange_strong(z, Clock::now().time_since_epoch().count());
-        b->cv.notify_all();
-    } else if (p == b->max_n) {
-        b->cv.notify_all();
-    }
-    return 0;
 }
 
 int l7g_batcher_flush(l7g_batcher *b) {
     if (b->IsFlusher()) return -1;  // from a callback: it would wait on itself
-    std::unique_lock<std::mutex> lk(b->mu);
     const uint64_t target = b->n_submitted.load();
+    std::unique_lock<std::mutex> lk(b->mu);
     b->flush_gen++;
     b->cv.notify_all();
     b->done_cv.wait(lk, [&] { return b->completed >= target; });
@@ -223,12 +290,10 @@ int l7g_batcher_flush(l7g_batcher *b) {
 
 void l7g_batcher_destroy(l7g_batcher *b) {
     if (!b || b->IsFlusher()) return;  // (from a callback: not allowed, see the header)
-    {
-        std::lock_guard<std::mutex> g(b->mu);
-        b->stop = true;
-    }
-    b->cv.notify_all();
+    b->stop.store(true);
+    b->Wake();
     for (auto &t : b->th) t.join();
+    FreeSlots(b);
     delete b;
 }
 

@@ -29,8 +29,8 @@ namespace l7 {
 hipError_t LaunchHttpClassify(const Batch &B, const HttpTables &T, const uint32_t *sel, const uint32_t *sel_count,
                               bool any_cold, bool answer_other, uint32_t *tile_ctr, hipStream_t stream);
 hipError_t LaunchKafkaClassify(const Batch &B, const KafkaTables &T, const uint32_t *sel, const uint32_t *sel_count,
-                               bool answer_other, uint32_t *zlist, uint32_t *zcount, uint32_t *work, uint32_t *fbn,
-                               uint32_t *fbl, hipStream_t stream);
+                               bool answer_other, uint32_t *zlist, uint32_t *zcount, uint32_t *work,
+                               hipStream_t stream);
 hipError_t LaunchKafkaInflate(const Batch &B, const uint32_t *zlist, const uint32_t *zcount, uint8_t *region,
                               hipStream_t stream);
 uint32_t KafkaInflateBlocks();
@@ -101,8 +101,8 @@ constexpr uint32_t kPartitionMin = 4096;
 // overlap instead of queueing on one stream.
 // Inputs go over as ONE copy from a pinned staging buffer ([off u64 | len u32 |
 // conn u32 | arena], packed by the host) and outputs come back as ONE copy
-// ([verdict u8 | rule i32 | consumed u32]): a one-request call is two DMA
-// transfers, not seven pageable ones.
+// ([verdict u8 | rule i32 | consumed u32]); a small call is not copied at all
+// (the kernels read and write the pinned buffers in place, see HostRun).
 struct HostCtx {
     hipStream_t s = nullptr;
     uint8_t *dev = nullptr;        // device: [inputs | outputs]
@@ -210,8 +210,9 @@ static hipError_t GetScratch(l7g_engine *e, hipStream_t s, StreamScratch **out) 
         }
     }
     // (a handle can be reused by a new stream while the old one's work is
-    // still pending: order the call after that work whatever the stream)
-    if (it->second->launched) {
+    // still pending: order the call after that work whatever the stream;
+    // nothing to wait for once it has completed -- the synchronous callers)
+    if (it->second->launched && hipEventQuery(it->second->done_ev) != hipSuccess) {
         hipError_t rc = hipStreamWaitEvent(s, it->second->done_ev, 0);
         if (rc != hipSuccess) return rc;
     }
@@ -694,9 +695,9 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
     const bool partitioned = nproto > 1 || e->has_kafka || (e->has_mc && n >= kPartitionMin);
     StreamScratch *S = nullptr;
     if ((rc = GetScratch(e, s, &S)) != hipSuccess) return (int)rc;
-    uint32_t *sel_k = nullptr, *sel_m = nullptr, *sel_h = nullptr, *sel_z = nullptr, *sel_f = nullptr, *cnt = nullptr;
+    uint32_t *sel_k = nullptr, *sel_m = nullptr, *sel_h = nullptr, *sel_z = nullptr, *cnt = nullptr;
     if (partitioned) {
-        const size_t need = 32 + (L7_KAFKA_CLASSES + 4) * (size_t)n;
+        const size_t need = 32 + (L7_KAFKA_CLASSES + 3) * (size_t)n;
         if (need > S->sel_cap) {
             if (S->d_sel) {  // the previous call on this stream may still use it
                 if (S->launched) rc = hipEventSynchronize(S->done_ev);
@@ -709,14 +710,13 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
         }
         if (rc != hipSuccess) return (int)rc;
         // [0, L7_KAFKA_CLASSES) Kafka classes, memcached retrievals, binary, HTTP, other text;
-        // [26] Kafka entry counter, [27] Kafka requests handed to the exact walk, [28, 29] HTTP tile
-        // counters (hot, general launch); [31] compressed Kafka
+        // [26] Kafka entry counter, [28, 29] HTTP tile counters (hot, general launch); [31] compressed
+        // Kafka
         cnt = S->d_sel;
         sel_k = S->d_sel + 32;
         sel_m = sel_k + L7_KAFKA_CLASSES * (size_t)n;
         sel_h = sel_m + (size_t)n;
         sel_z = sel_h + (size_t)n;
-        sel_f = sel_z + (size_t)n;
         if (rc == hipSuccess) rc = hipMemsetAsync(cnt, 0, 32 * sizeof(uint32_t), s);
         if (rc == hipSuccess && e->has_kafka && !e->d_zreg) {
             rc = hipEventCreateWithFlags(&e->zreg_ev, hipEventDisableTiming);
@@ -767,8 +767,7 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
     mark(2);
     uint32_t *zcount = cnt ? cnt + 31 : nullptr;
     if (rc == hipSuccess && run[2])
-        rc = LaunchKafkaClassify(B, e->kt, sel_k, cnt, !partitioned, sel_z, zcount, cnt ? cnt + 26 : nullptr,
-                                 cnt ? cnt + 27 : nullptr, sel_f, s);
+        rc = LaunchKafkaClassify(B, e->kt, sel_k, cnt, !partitioned, sel_z, zcount, cnt ? cnt + 26 : nullptr, s);
     // requests with gzip / snappy messages: decoded, their sets read, failures answered
     if (rc == hipSuccess && run[2] && sel_z) {
         // the engine's one decode region: after the previous inflate launch on any stream
@@ -833,78 +832,106 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
     return (int)rc;
 }
 
-int l7g_classify_host(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const uint64_t *off, const uint32_t *len,
-                      const uint32_t *conn, uint32_t n, uint8_t *verdict, int32_t *rule, uint32_t *consumed) {
-    if (e->device < 0) return (int)hipErrorNoDevice;
-    hipError_t rc = hipSetDevice(e->device);
-    if (rc != hipSuccess) return (int)rc;
-    // this thread's stream and staging (the engine lock is held only while
-    // l7g_classify enqueues, so threads' copies and kernels overlap)
-    HostCtx *H = nullptr;
-    {
-        std::lock_guard<std::mutex> g(e->hmu);
-        auto &slot = e->hctx[std::this_thread::get_id()];
-        if (!slot) {
-            auto h = std::make_unique<HostCtx>();
-            if ((rc = hipStreamCreateWithFlags(&h->s, hipStreamNonBlocking)) != hipSuccess) return (int)rc;
-            slot = std::move(h);
-        }
-        H = slot.get();
+}  // extern "C"
+
+// ---- l7g_classify_host's per-thread path, in three steps (the batcher's
+// flushers fill the staging in place and skip the copy)
+
+// this thread's stream and staging (the engine lock is held only while
+// l7g_classify enqueues, so threads' copies and kernels overlap)
+static hipError_t HostCtxFor(l7g_engine *e, HostCtx **out) {
+    std::lock_guard<std::mutex> g(e->hmu);
+    auto &slot = e->hctx[std::this_thread::get_id()];
+    if (!slot) {
+        auto h = std::make_unique<HostCtx>();
+        hipError_t rc;
+        if ((rc = hipStreamCreateWithFlags(&h->s, hipStreamNonBlocking)) != hipSuccess) return rc;
+        slot = std::move(h);
     }
-    // grow-only staging: inputs [off | len | conn | arena (+64 B so aligned
-    // 16-byte reads stay inside)], outputs [verdict | rule | consumed]
+    *out = slot.get();
+    return hipSuccess;
+}
+
+// grow-only staging: inputs [off | len | conn | arena (+64 B so aligned
+// 16-byte reads stay inside)], outputs [verdict | rule | consumed]
+static size_t HostArenaOff(uint32_t n) { return ((size_t)std::max<uint32_t>(n, 1) * 16 + 255) & ~(size_t)255; }
+static hipError_t HostGrow(HostCtx *H, uint32_t n, uint64_t arena_len) {
     const size_t nn = std::max<uint32_t>(n, 1);
-    const size_t a_off = (nn * 16 + 255) & ~(size_t)255;
-    const size_t need_in = a_off + arena_len + 64;
+    const size_t need_in = HostArenaOff(n) + arena_len + 64;
     const size_t need_out = nn * 9 + 64;
-    if (need_in > H->in_cap || need_out > H->out_cap) {
-        if (H->dev) hipFree(H->dev);
-        if (H->pin_in) hipHostFree(H->pin_in);
-        if (H->pin_out) hipHostFree(H->pin_out);
-        H->dev = H->pin_in = H->pin_out = nullptr;
-        H->in_cap = std::max(need_in, (size_t)1 << 16);
-        H->out_cap = std::max(need_out, (size_t)1 << 14);
-        if ((rc = hipMalloc(&H->dev, H->in_cap + H->out_cap)) != hipSuccess) { H->in_cap = H->out_cap = 0; return (int)rc; }
-        if ((rc = hipHostMalloc(&H->pin_in, H->in_cap, hipHostMallocDefault)) != hipSuccess ||
-            (rc = hipHostMalloc(&H->pin_out, H->out_cap, hipHostMallocDefault)) != hipSuccess) {
-            H->in_cap = H->out_cap = 0;
-            return (int)rc;
-        }
-    }
+    if (need_in <= H->in_cap && need_out <= H->out_cap) return hipSuccess;
     // (the previous call of this thread synchronised its stream: the staging is free)
-    uint8_t *pi = H->pin_in;
-    if (n) {
-        memcpy(pi, off, (size_t)n * 8);
-        memcpy(pi + nn * 8, len, (size_t)n * 4);
-        memcpy(pi + nn * 12, conn, (size_t)n * 4);
+    if (H->dev) hipFree(H->dev);
+    if (H->pin_in) hipHostFree(H->pin_in);
+    if (H->pin_out) hipHostFree(H->pin_out);
+    H->dev = H->pin_in = H->pin_out = nullptr;
+    H->in_cap = std::max(need_in + need_in / 4, (size_t)1 << 16);  // (some slack: batches vary)
+    H->out_cap = std::max(need_out + need_out / 4, (size_t)1 << 14);
+    hipError_t rc;
+    if ((rc = hipMalloc(&H->dev, H->in_cap + H->out_cap)) != hipSuccess) { H->in_cap = H->out_cap = 0; return rc; }
+    if ((rc = hipHostMalloc(&H->pin_in, H->in_cap, hipHostMallocDefault)) != hipSuccess ||
+        (rc = hipHostMalloc(&H->pin_out, H->out_cap, hipHostMallocDefault)) != hipSuccess) {
+        H->in_cap = H->out_cap = 0;
+        return rc;
     }
-    if (arena_len) memcpy(pi + a_off, arena, arena_len);
+    return hipSuccess;
+}
+
+// classify a call whose inputs are in pinned host memory (the thread's staging,
+// or a batcher slot), wait for it, copy the answers out
+static hipError_t HostRun(l7g_engine *e, HostCtx *H, uint32_t n, uint64_t arena_len, const uint64_t *p_off,
+                          const uint32_t *p_len, const uint32_t *p_conn, const uint8_t *p_arena, uint8_t *verdict,
+                          int32_t *rule, uint32_t *consumed) {
+    hipError_t rc = hipSuccess;
+    const size_t nn = std::max<uint32_t>(n, 1);
+    const size_t a_off = HostArenaOff(n);
     // A small call (the Envoy adapter's Allowed(), one OnData) is latency, not
     // bandwidth: the kernels read the inputs from and write the verdicts to the
-    // pinned staging in place (zero-copy, over PCIe), so the call is one launch
-    // and a synchronise instead of copy, launch, copy, synchronise.
+    // pinned memory in place (zero-copy, over PCIe), so the call is one launch
+    // and a wait instead of copy, launch, copy, wait.
     static const bool zc_on = [] {
         const char *v = getenv("L7G_SYNC_ZEROCOPY");
         return !(v && v[0] == '0');
     }();
     const bool zc = zc_on && n <= kZeroCopyMaxRequests && a_off + arena_len <= kZeroCopyMaxBytes;
-    uint8_t *d_in = H->dev, *d_out = H->dev + H->in_cap;
+    hipStream_t s = H->s;
+    const uint64_t *d_o;
+    const uint32_t *d_l, *d_c;
+    const uint8_t *d_a;
+    uint8_t *d_out = H->dev + H->in_cap;
     if (zc) {
         void *dp = nullptr;
-        if ((rc = hipHostGetDevicePointer(&dp, H->pin_in, 0)) != hipSuccess) return (int)rc;
-        d_in = (uint8_t *)dp;
-        if ((rc = hipHostGetDevicePointer(&dp, H->pin_out, 0)) != hipSuccess) return (int)rc;
-        d_out = (uint8_t *)dp;
+        auto dev_ptr = [&](const void *h) -> const uint8_t * {
+            if (rc == hipSuccess) rc = hipHostGetDevicePointer(&dp, const_cast<void *>(h), 0);
+            return (const uint8_t *)dp;
+        };
+        d_o = (const uint64_t *)dev_ptr(p_off);
+        d_l = (const uint32_t *)dev_ptr(p_len);
+        d_c = (const uint32_t *)dev_ptr(p_conn);
+        d_a = dev_ptr(p_arena);
+        d_out = (uint8_t *)dev_ptr(H->pin_out);
+        if (rc != hipSuccess) return rc;
+    } else {
+        uint8_t *d_in = H->dev;
+        d_o = (const uint64_t *)d_in;
+        d_l = (const uint32_t *)(d_in + nn * 8);
+        d_c = (const uint32_t *)(d_in + nn * 12);
+        d_a = d_in + a_off;
+        if (p_off == (const uint64_t *)H->pin_in) {  // the thread's staging: one copy of the whole layout
+            rc = hipMemcpyAsync(d_in, H->pin_in, a_off + arena_len, hipMemcpyHostToDevice, s);
+        } else {
+            rc = hipMemcpyAsync((void *)d_o, p_off, (size_t)n * 8, hipMemcpyHostToDevice, s);
+            if (rc == hipSuccess) rc = hipMemcpyAsync((void *)d_l, p_len, (size_t)n * 4, hipMemcpyHostToDevice, s);
+            if (rc == hipSuccess) rc = hipMemcpyAsync((void *)d_c, p_conn, (size_t)n * 4, hipMemcpyHostToDevice, s);
+            if (rc == hipSuccess && arena_len)
+                rc = hipMemcpyAsync((void *)d_a, p_arena, arena_len, hipMemcpyHostToDevice, s);
+        }
     }
-    const uint64_t *d_o = (const uint64_t *)d_in;
-    const uint32_t *d_l = (const uint32_t *)(d_in + nn * 8), *d_c = (const uint32_t *)(d_in + nn * 12);
     uint8_t *d_v = d_out;
     int32_t *d_r = (int32_t *)(d_out + ((nn + 3) & ~(size_t)3));
     uint32_t *d_cons = (uint32_t *)(d_out + ((nn + 3) & ~(size_t)3) + nn * 4);
-    hipStream_t s = H->s;
-    if (!zc) rc = hipMemcpyAsync(d_in, pi, a_off + arena_len, hipMemcpyHostToDevice, s);
     if (rc == hipSuccess)
-        rc = (hipError_t)l7g_classify(e, d_in + a_off, arena_len, d_o, d_l, d_c, n, d_v, d_r, d_cons, nullptr, s);
+        rc = (hipError_t)l7g_classify(e, d_a, arena_len, d_o, d_l, d_c, n, d_v, d_r, d_cons, nullptr, s);
     const size_t out_bytes = ((nn + 3) & ~(size_t)3) + nn * 8;
     if (rc == hipSuccess && n && !zc) rc = hipMemcpyAsync(H->pin_out, d_out, out_bytes, hipMemcpyDeviceToHost, s);
     if (rc == hipSuccess) rc = hipStreamSynchronize(s);
@@ -914,7 +941,75 @@ int l7g_classify_host(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, c
         memcpy(rule, po + ((nn + 3) & ~(size_t)3), (size_t)n * 4);
         memcpy(consumed, po + ((nn + 3) & ~(size_t)3) + nn * 4, (size_t)n * 4);
     }
+    return rc;
+}
+
+int l7g_host_stage(l7g_engine *e, uint32_t n, uint64_t arena_len, uint8_t **arena, uint64_t **off, uint32_t **len,
+                   uint32_t **conn) {
+    if (e->device < 0) return (int)hipErrorNoDevice;
+    hipError_t rc = hipSetDevice(e->device);
+    HostCtx *H = nullptr;
+    if (rc == hipSuccess) rc = HostCtxFor(e, &H);
+    if (rc == hipSuccess) rc = HostGrow(H, n, arena_len);
+    if (rc != hipSuccess) return (int)rc;
+    const size_t nn = std::max<uint32_t>(n, 1);
+    *off = (uint64_t *)H->pin_in;
+    *len = (uint32_t *)(H->pin_in + nn * 8);
+    *conn = (uint32_t *)(H->pin_in + nn * 12);
+    *arena = H->pin_in + HostArenaOff(n);
+    return 0;
+}
+
+int l7g_host_run(l7g_engine *e, uint32_t n, uint64_t arena_len, uint8_t *verdict, int32_t *rule, uint32_t *consumed) {
+    if (e->device < 0) return (int)hipErrorNoDevice;
+    hipError_t rc = hipSetDevice(e->device);
+    HostCtx *H = nullptr;
+    if (rc == hipSuccess) rc = HostCtxFor(e, &H);
+    if (rc == hipSuccess) {
+        const size_t nn = std::max<uint32_t>(n, 1);
+        rc = HostRun(e, H, n, arena_len, (const uint64_t *)H->pin_in, (const uint32_t *)(H->pin_in + nn * 8),
+                     (const uint32_t *)(H->pin_in + nn * 12), H->pin_in + HostArenaOff(n), verdict, rule, consumed);
+    }
     return (int)rc;
+}
+
+int l7g_host_run_pinned(l7g_engine *e, uint32_t n, uint64_t arena_len, const uint64_t *off, const uint32_t *len,
+                        const uint32_t *conn, const uint8_t *arena, uint8_t *verdict, int32_t *rule,
+                        uint32_t *consumed) {
+    if (e->device < 0) return (int)hipErrorNoDevice;
+    hipError_t rc = hipSetDevice(e->device);
+    HostCtx *H = nullptr;
+    if (rc == hipSuccess) rc = HostCtxFor(e, &H);
+    if (rc == hipSuccess) rc = HostGrow(H, n, 0);  // device staging and pinned outputs for n requests
+    if (rc == hipSuccess && HostArenaOff(n) + arena_len + 64 > H->in_cap) rc = HostGrow(H, n, arena_len);
+    if (rc == hipSuccess) rc = HostRun(e, H, n, arena_len, off, len, conn, arena, verdict, rule, consumed);
+    return (int)rc;
+}
+
+void *l7g_pinned_alloc(size_t bytes) {
+    void *p = nullptr;
+    return hipHostMalloc(&p, bytes, hipHostMallocDefault) == hipSuccess ? p : nullptr;
+}
+void l7g_pinned_free(void *p) {
+    if (p) hipHostFree(p);
+}
+
+extern "C" {
+
+int l7g_classify_host(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const uint64_t *off, const uint32_t *len,
+                      const uint32_t *conn, uint32_t n, uint8_t *verdict, int32_t *rule, uint32_t *consumed) {
+    uint8_t *pa;
+    uint64_t *po;
+    uint32_t *pl, *pc;
+    int rc = l7g_host_stage(e, n, arena_len, &pa, &po, &pl, &pc);
+    if (rc != 0) return rc;
+    if (n) {
+        memcpy(po, off, (size_t)n * 8);
+        memcpy(pl, len, (size_t)n * 4);
+        memcpy(pc, conn, (size_t)n * 4);
+    }
+    if (arena_len) memcpy(pa, arena, arena_len);
+    return l7g_host_run(e, n, arena_len, verdict, rule, consumed);
 }
 
 int l7g_stats(l7g_engine *e, l7g_stats_t *out) {

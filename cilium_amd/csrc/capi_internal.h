@@ -13,3 +13,20 @@ struct l7g_engine;
 // in instance.go:168-176); the previous version then stays in force.
 int l7g_policy_update_view(l7g_engine *e, const uint8_t *buf, size_t len, int proto_form, int proxylib, char *err,
                            size_t errlen);
+
+// l7g_classify_host in two steps (the batcher's flushers, csrc/batcher.cc):
+// l7g_host_stage returns the calling thread's pinned staging for a call of n
+// requests over arena_len bytes (grown as needed; valid until the thread's
+// next stage); the caller fills it in place, then l7g_host_run classifies it
+// exactly as l7g_classify_host would and waits.  0 = ok, else a hipError_t.
+int l7g_host_stage(l7g_engine *e, uint32_t n, uint64_t arena_len, uint8_t **arena, uint64_t **off, uint32_t **len,
+                   uint32_t **conn);
+int l7g_host_run(l7g_engine *e, uint32_t n, uint64_t arena_len, uint8_t *verdict, int32_t *rule, uint32_t *consumed);
+// The same with inputs already in pinned host memory (hipHostMalloc: a
+// batcher slot filled in place by its submitters): copied to the device (or
+// read in place for a small call), classified, waited for.
+int l7g_host_run_pinned(l7g_engine *e, uint32_t n, uint64_t arena_len, const uint64_t *off, const uint32_t *len,
+                        const uint32_t *conn, const uint8_t *arena, uint8_t *verdict, int32_t *rule,
+                        uint32_t *consumed);
+void *l7g_pinned_alloc(size_t bytes);  // hipHostMalloc (NULL on failure)
+void l7g_pinned_free(void *p);

@@ -16,7 +16,9 @@ namespace {
 
 constexpr uint32_t kMaxParseBuf = 6553500;
 constexpr int kCrcSlices = 8;
-#define L7G_KAFKA_CRCSTREAMS 1  // independent CRC chains per 64-byte batch (2 and 4 measured slower, round 3)
+#ifndef L7G_KAFKA_CRCSTREAMS  // independent CRC chains per 64-byte batch (1, 2 or 4)
+#define L7G_KAFKA_CRCSTREAMS 1
+#endif
 // Shift tables after the 8 slicing tables: Zn[j][b] = T_{n-1-j}[b], so that
 // crc(v, n zero bytes) = Zn[0][v & 0xFF] ^ ... ^ Zn[3][v >> 24] (the register
 // state is linear: crc(c, A || B) = crc(crc(c, A), 0^|B|) ^ crc(0, B)).
@@ -53,107 +55,50 @@ __device__ __forceinline__ uint32_t crc_shift(const uint32_t *z, uint32_t v) {
 constexpr uint32_t kInf = 0xFFFFFFFFu;
 
 // Per-lane byte cursor: the decoders walk their request forward, so each lane
-// keeps the aligned block it last touched in registers and serves field bytes
-// from it.  CurT<4>: one 16-byte chunk (one dwordx4 load replaces up to 16 byte
-// loads); CurT<16>: a 64-byte block (four dwordx4 loads issued together, so a
-// message header, a topic entry or a request header is one memory latency, not
-// two or three).  A block that holds a request byte never leaves that byte's
-// page, so the aligned over-read is safe for any arena alignment.
-template <int NW>
-struct CurT;
-template <>
-struct CurT<4> {
-    uintptr_t line;  // address of the cached block (~0 = none)
+// keeps the 16-byte aligned chunk it last touched in registers and serves
+// field bytes from it; one dwordx4 load replaces up to 16 byte loads.  A chunk
+// that holds a request byte never leaves that byte's page, so the aligned
+// over-read is safe for any arena alignment.
+struct Cur {
+    uintptr_t line;  // address of the cached chunk (~0 = none)
     uint32_t w0, w1, w2, w3;  // scalars, not an array: a selected array element would put Cur in scratch
 };
-template <>
-struct CurT<8> {
-    uintptr_t line;
-    uint32_t w0, w1, w2, w3, w4, w5, w6, w7;
-};
-template <>
-struct CurT<16> {
-    uintptr_t line;
-    uint32_t w0, w1, w2, w3, w4, w5, w6, w7, w8, w9, w10, w11, w12, w13, w14, w15;
-};
-using Cur = CurT<4>;
-template <int NW>
-__device__ __forceinline__ void cur_fill(CurT<NW> &c, uintptr_t a) {
-    const uintptr_t ln = a & ~(uintptr_t)(NW * 4 - 1);
+__device__ __forceinline__ void cur_fill(Cur &c, uintptr_t a) {
+    const uintptr_t ln = a & ~(uintptr_t)15;
     if (ln != c.line) {
-        if constexpr (NW == 4) {
-            const uint4 v = gload16(ln);
-            c.w0 = v.x; c.w1 = v.y; c.w2 = v.z; c.w3 = v.w;
-        } else if constexpr (NW == 8) {
-            const uint4 v0 = gload16(ln), v1 = gload16(ln + 16);
-            c.w0 = v0.x; c.w1 = v0.y; c.w2 = v0.z; c.w3 = v0.w;
-            c.w4 = v1.x; c.w5 = v1.y; c.w6 = v1.z; c.w7 = v1.w;
-        } else {
-            const uint4 v0 = gload16(ln), v1 = gload16(ln + 16), v2 = gload16(ln + 32), v3 = gload16(ln + 48);
-            c.w0 = v0.x; c.w1 = v0.y; c.w2 = v0.z; c.w3 = v0.w;
-            c.w4 = v1.x; c.w5 = v1.y; c.w6 = v1.z; c.w7 = v1.w;
-            c.w8 = v2.x; c.w9 = v2.y; c.w10 = v2.z; c.w11 = v2.w;
-            c.w12 = v3.x; c.w13 = v3.y; c.w14 = v3.z; c.w15 = v3.w;
-        }
+        const uint4 v = gload16(ln);
+        c.w0 = v.x; c.w1 = v.y; c.w2 = v.z; c.w3 = v.w;
         c.line = ln;
     }
 }
-// word i of the block, 0 past its end (values are copied out before they are
-// selected: a select between struct members becomes a select between their
-// addresses, i.e. a scratch array)
-template <int NW>
-__device__ __forceinline__ uint32_t cur_wordi(const CurT<NW> &c, uint32_t i) {
-    if constexpr (NW == 4) {
-        const uint32_t a = c.w0, b = c.w1, d = c.w2, e = c.w3;
-        return i < 2 ? (i == 0 ? a : b) : i == 2 ? d : i == 3 ? e : 0u;
-    } else if constexpr (NW == 8) {
-        const uint32_t x0 = c.w0, x1 = c.w1, x2 = c.w2, x3 = c.w3, x4 = c.w4, x5 = c.w5, x6 = c.w6, x7 = c.w7;
-        const uint32_t lo4 = (i & 2) ? ((i & 1) ? x3 : x2) : ((i & 1) ? x1 : x0);
-        const uint32_t hi4 = (i & 2) ? ((i & 1) ? x7 : x6) : ((i & 1) ? x5 : x4);
-        return i < 8 ? ((i & 4) ? hi4 : lo4) : 0u;
-    } else {
-        const uint32_t x0 = c.w0, x1 = c.w1, x2 = c.w2, x3 = c.w3, x4 = c.w4, x5 = c.w5, x6 = c.w6, x7 = c.w7;
-        const uint32_t x8 = c.w8, x9 = c.w9, x10 = c.w10, x11 = c.w11, x12 = c.w12, x13 = c.w13, x14 = c.w14,
-                       x15 = c.w15;
-        const uint32_t lo4 = (i & 2) ? ((i & 1) ? x3 : x2) : ((i & 1) ? x1 : x0);
-        const uint32_t hi4 = (i & 2) ? ((i & 1) ? x7 : x6) : ((i & 1) ? x5 : x4);
-        const uint32_t lo8 = (i & 2) ? ((i & 1) ? x11 : x10) : ((i & 1) ? x9 : x8);
-        const uint32_t hi8 = (i & 2) ? ((i & 1) ? x15 : x14) : ((i & 1) ? x13 : x12);
-        const uint32_t v = (i & 8) ? ((i & 4) ? hi8 : lo8) : ((i & 4) ? hi4 : lo4);
-        return i < 16 ? v : 0u;
-    }
+// (values are copied out before they are selected: a select between struct
+// members becomes a select between their addresses, i.e. a scratch array)
+__device__ __forceinline__ uint32_t cur_word(const Cur &c, uint32_t k) {
+    const uint32_t a = c.w0, b = c.w1, d = c.w2, e = c.w3;
+    return k < 8 ? (k < 4 ? a : b) : (k < 12 ? d : e);
 }
-template <int NW>
-__device__ __forceinline__ uint32_t cur_word(const CurT<NW> &c, uint32_t k) {
-    return cur_wordi(c, k >> 2);
-}
-template <int NW>
-__device__ __forceinline__ uint32_t cur_byte(CurT<NW> &c, const uint8_t *p) {
+__device__ __forceinline__ uint32_t cur_byte(Cur &c, const uint8_t *p) {
     const uintptr_t a = (uintptr_t)p;
     cur_fill(c, a);
-    const uint32_t k = (uint32_t)(a & (NW * 4 - 1));
+    const uint32_t k = (uint32_t)(a & 15);
     return (cur_word(c, k) >> ((k & 3) * 8)) & 0xFFu;
 }
 
-template <class C>
-struct KDecT {
+struct KDec {
     const uint8_t *b;
     uint32_t pos, end;
     int32_t limit;  // LimitReader remaining, -1 = none (a set is at most kMaxParseBuf)
     int err;        // 0 ok, 1 EOF, 2 ErrUnexpectedEOF, 3 other
-    C *c;
+    Cur *c;
 };
-using KDec = KDecT<Cur>;
 
-template <class D>
-__device__ __forceinline__ uint32_t kavail(const D &d) {
+__device__ __forceinline__ uint32_t kavail(const KDec &d) {
     uint32_t a = d.end - d.pos;
     if (d.limit >= 0 && (uint32_t)d.limit < a) a = (uint32_t)d.limit;
     return a;
 }
 // io.ReadFull(r, buf[:n]); returns start offset, sets d.err on a short read
-template <class D>
-__device__ __forceinline__ uint32_t kread(D &d, uint32_t n) {
+__device__ __forceinline__ uint32_t kread(KDec &d, uint32_t n) {
     uint32_t at = d.pos;
     if (n == 0) return at;
     uint32_t a = kavail(d);
@@ -165,17 +110,18 @@ __device__ __forceinline__ uint32_t kread(D &d, uint32_t n) {
     return at;
 }
 // Big-endian n-byte field (n = 1, 2, 4 or 8).  A field inside the cached
-// block is cut out of two adjacent words (v_alignbyte) and byte-swapped
-// (v_perm); one straddling two blocks is read byte by byte.
+// 16-byte chunk is cut out of two adjacent words (v_alignbyte) and byte-
+// swapped (v_perm); one straddling two chunks is read byte by byte.
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_amdgcn_perm(0, x, 0x00010203u); }
-template <int NW>
-__device__ __forceinline__ uint64_t be_load(CurT<NW> &c, const uint8_t *p, int n) {
+__device__ __forceinline__ uint64_t be_load(Cur &c, const uint8_t *p, int n) {
     const uintptr_t a = (uintptr_t)p;
-    const uint32_t k = (uint32_t)(a & (NW * 4 - 1));
-    if (n <= 4 && k + (uint32_t)n <= NW * 4) {
+    const uint32_t k = (uint32_t)(a & 15);
+    if (n <= 4 && k + (uint32_t)n <= 16) {
         cur_fill(c, a);
+        const uint32_t w0 = c.w0, w1 = c.w1, w2 = c.w2, w3 = c.w3;
         const uint32_t i = k >> 2;
-        const uint32_t lo = cur_wordi(c, i), hi = cur_wordi(c, i + 1);
+        const uint32_t lo = i == 0 ? w0 : i == 1 ? w1 : i == 2 ? w2 : w3;
+        const uint32_t hi = i == 0 ? w1 : i == 1 ? w2 : i == 2 ? w3 : 0u;
         const uint32_t v = bswap32(__builtin_amdgcn_alignbyte(hi, lo, k & 3));  // bytes k..k+3, big-endian
         return n == 4 ? v : v >> (32 - 8 * n);
     }
@@ -184,8 +130,7 @@ __device__ __forceinline__ uint64_t be_load(CurT<NW> &c, const uint8_t *p, int n
     for (int i = 0; i < n; i++) v = (v << 8) | cur_byte(c, p + i);
     return v;
 }
-template <class D>
-__device__ __forceinline__ int64_t dec_int(D &d, int n) {
+__device__ __forceinline__ int64_t dec_int(KDec &d, int n) {
     if (d.err) return 0;
     uint32_t at = kread(d, (uint32_t)n);
     if (d.err) return 0;
@@ -193,14 +138,12 @@ __device__ __forceinline__ int64_t dec_int(D &d, int n) {
     return n == 1 ? (int64_t)(int8_t)v : n == 2 ? (int64_t)(int16_t)v : n == 4 ? (int64_t)(int32_t)v : (int64_t)v;
 }
 // A field whose value is not needed: only the read (and its errors) matter.
-template <class D>
-__device__ __forceinline__ void dec_skip(D &d, int n) {
+__device__ __forceinline__ void dec_skip(KDec &d, int n) {
     if (d.err) return;
     kread(d, (uint32_t)n);
 }
 // DecodeString -> (off, len); len < 1 => ""
-template <class D>
-__device__ __forceinline__ void dec_string(D &d, uint32_t &off, uint32_t &len) {
+__device__ __forceinline__ void dec_string(KDec &d, uint32_t &off, uint32_t &len) {
     off = 0; len = 0;
     if (d.err) return;
     int16_t sl = (int16_t)dec_int(d, 2);
@@ -210,16 +153,14 @@ __device__ __forceinline__ void dec_string(D &d, uint32_t &off, uint32_t &len) {
     off = at; len = (uint32_t)sl;
 }
 // DecodeArrayLen(nullable): -1 null; sets bad on ErrInvalidArrayLen
-template <class D>
-__device__ __forceinline__ int32_t dec_arraylen(D &d, bool nullable, bool &bad) {
+__device__ __forceinline__ int32_t dec_arraylen(KDec &d, bool nullable, bool &bad) {
     int32_t l = (int32_t)dec_int(d, 4);
     bad = false;
     if (l < 0) { if (nullable) return -1; bad = true; return 0; }
     if ((uint32_t)l > kMaxParseBuf) { bad = true; return 0; }
     return l;
 }
-template <class D>
-__device__ __forceinline__ void dec_bytes(D &d) {
+__device__ __forceinline__ void dec_bytes(KDec &d) {
     if (d.err) return;
     int32_t sl = (int32_t)dec_int(d, 4);
     if (d.err || sl < 1) return;
@@ -324,62 +265,6 @@ __device__ __forceinline__ uint32_t cur_word_at(const Cur &c, uint32_t k) {
     const uint32_t lo = i == 0 ? w0 : i == 1 ? w1 : i == 2 ? w2 : w3;
     const uint32_t hi = i == 0 ? w1 : i == 1 ? w2 : i == 2 ? w3 : 0u;
     return __builtin_amdgcn_alignbyte(hi, lo, k & 3);
-}
-
-// CRC32-IEEE of r bytes at byte j of the 16-byte chunk v (j + r <= 16): 8-,
-// 4- and <= 3-byte slicing steps, each step's lookups in flight together.
-__device__ __forceinline__ uint32_t crc_chunk_span(uint32_t tabaddr, uint32_t c, const uint4 &v, uint32_t j, uint32_t r) {
-    auto word_at = [&](uint32_t k) -> uint32_t {  // little-endian bytes k .. k+3 (k <= 12)
-        const uint32_t i = k >> 2;
-        const uint32_t lo = i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w;
-        const uint32_t hi = i == 0 ? v.y : i == 1 ? v.z : i == 2 ? v.w : 0u;
-        return __builtin_amdgcn_alignbyte(hi, lo, k & 3);
-    };
-    if (j == 0 && r == 16) {
-        c = crc_step8(tabaddr, v.x ^ c, v.y);
-        return crc_step8(tabaddr, v.z ^ c, v.w);
-    }
-    uint32_t i = 0;
-    if (r >= 8) {
-        c = crc_step8(tabaddr, word_at(j) ^ c, word_at(j + 4));
-        i = 8;
-    }
-    if (r - i >= 4) {
-        c = crc_step4(tabaddr, word_at(j + i) ^ c);
-        i += 4;
-    }
-    if (i < r) c = crc_bytes3(tabaddr, c, word_at(j + i), r - i);
-    return c;
-}
-// CRC32-IEEE of [p, p + n) in global memory: the aligned 16-byte chunks that
-// hold it, 64 bytes per group, the next group's loads issued before the
-// current one is hashed (two groups in flight per lane, so a lane walking a
-// message waits about one memory latency per 64 bytes less).
-__device__ __forceinline__ uint32_t crc32_ieee_global(uint32_t tabaddr, const uint8_t *p, uint32_t n) {
-    uint32_t c = 0xFFFFFFFFu;
-    if (n == 0) return ~c;
-    const uint64_t a = (uint64_t)(uintptr_t)p, ab = a & ~15ull;
-    const uint32_t j0 = (uint32_t)(a & 15);
-    const uint32_t nch = (j0 + n + 15) >> 4, end = j0 + n;  // end: bytes from ab
-    auto ld = [&](uint32_t k) -> uint4 { return gload16(ab + 16ull * (k < nch ? k : 0)); };
-    uint4 g0 = ld(0), g1 = ld(1), g2 = ld(2), g3 = ld(3);
-    for (uint32_t k = 0; k < nch; k += 4) {
-        const bool more = k + 4 < nch;
-        uint4 h0 = g0, h1 = g1, h2 = g2, h3 = g3;
-        if (more) { h0 = ld(k + 4); h1 = ld(k + 5); h2 = ld(k + 6); h3 = ld(k + 7); }
-        auto one = [&](const uint4 &v, uint32_t kk) {
-            if (kk >= nch) return;
-            const uint32_t from = kk == 0 ? j0 : 0;
-            const uint32_t to = 16 * kk + 16 <= end ? 16 : end - 16 * kk;
-            c = crc_chunk_span(tabaddr, c, v, from, to - from);
-        };
-        one(g0, k);
-        one(g1, k + 1);
-        one(g2, k + 2);
-        one(g3, k + 3);
-        g0 = h0; g1 = h1; g2 = h2; g3 = h3;
-    }
-    return ~c;
 }
 
 // The same CRC with the bulk loads staged through LDS (kafka_classify): the

@@ -1,10 +1,10 @@
 // Batcher threading on a host-only engine (no GPU needed: every flush is
-// answered L7G_UNSUPPORTED, which still runs the sharded queues, both
+// answered L7G_UNSUPPORTED, which still runs the lock-free slots, both
 // flusher threads, batch-ordered callbacks, flush and backpressure).
 // Checks: every request's callback exactly once, a thread's callbacks in its
 // submission order, flush() returns only after its requests were answered,
-// flush() from a callback returns -1, submit beyond the backpressure cap
-// returns -2.  stdout: one JSON object.
+// flush() from a callback returns -1, submit returns -2 while both flushers
+// are busy and the open slot is full, and every accepted request is answered.  stdout: one JSON object.
 #include <atomic>
 #include <cstdio>
 #include <cstring>
@@ -56,22 +56,34 @@ int main() {
     for (auto &x : th) x.join();
     const int frc = l7g_batcher_flush(g_b);
     const uint64_t after_flush = g_calls.load();
-    // backpressure: a batcher whose flushers cannot keep up (huge wait) refuses past 64 x max_requests
-    l7g_batcher *slow = l7g_batcher_create(e, 4, 5000000);
+    // backpressure: callbacks that block until released keep both flushers
+    // busy, so the open slot fills (1024 requests for max_requests = 4) and
+    // submit refuses; after the release every queued request is answered
+    static std::mutex gate;
+    static std::atomic<int> slow_calls{0};
+    gate.lock();
+    l7g_batcher *slow = l7g_batcher_create(e, 4, 50);
     int queued = 0, refused = 0;
     uint8_t one = 'x';
-    for (int i = 0; i < 1000; i++) {
-        const int rc = l7g_batcher_submit(slow, &one, 1, 0, [](void *, uint8_t, int32_t, uint32_t) {}, nullptr);
+    for (int i = 0; i < 5000; i++) {
+        const int rc = l7g_batcher_submit(slow, &one, 1, 0, [](void *, uint8_t, int32_t, uint32_t) {
+            std::lock_guard<std::mutex> g(gate);
+            slow_calls++;
+        }, nullptr);
         if (rc == 0) queued++; else if (rc == -2) refused++;
     }
+    gate.unlock();
+    l7g_batcher_flush(slow);
+    const int slow_answered = slow_calls.load();
     l7g_batcher_destroy(slow);
     uint64_t reqs = 0, launches = 0;
     l7g_batcher_stats(g_b, &reqs, &launches);
     l7g_batcher_destroy(g_b);
     l7g_engine_destroy(e);
     printf("{\"calls\": %llu, \"after_flush\": %llu, \"expected\": %d, \"bad\": %d, \"flush_rc\": %d, "
-           "\"reentrant_flush_rc\": %d, \"launches\": %llu, \"queued\": %d, \"refused\": %d, \"rejected\": %d}\n",
+           "\"reentrant_flush_rc\": %d, \"launches\": %llu, \"queued\": %d, \"refused\": %d, \"rejected\": %d, "
+           "\"slow_answered\": %d}\n",
            (unsigned long long)g_calls.load(), (unsigned long long)after_flush, T * N, g_bad.load(), frc,
-           g_flush_rc.load(), (unsigned long long)launches, queued, refused, rejected.load());
+           g_flush_rc.load(), (unsigned long long)launches, queued, refused, rejected.load(), slow_answered);
     return 0;
 }

@@ -105,7 +105,8 @@ int main(int argc, char **argv) {
         l7g_batcher_flush(b);
         uint64_t warm_req = 0, warm_l = 0;
         l7g_batcher_stats(b, &warm_req, &warm_l);
-        const int per = iters * 4 / cf.threads;
+        // a quarter second of offered load per configuration (at least iters * 4 requests)
+        const int per = std::max(iters * 4 / cf.threads, (int)(cf.rate_per_thread * 0.25));
         std::vector<std::vector<double>> lat(cf.threads);
         struct Ctx { Clock::time_point t0; std::vector<double> *out; std::atomic<int> *left; };
         std::atomic<int> left{per * cf.threads};
@@ -118,14 +119,15 @@ int main(int argc, char **argv) {
                     std::this_thread::sleep_until(start + std::chrono::duration_cast<Clock::duration>(gap * (double)i));
                     const std::string &r = http[(size_t)(i * cf.threads + t) % http.size()];
                     auto *c = new Ctx{Clock::now(), &lat[t], &left};
-                    l7g_batcher_submit(b, (const uint8_t *)r.data(), (uint32_t)r.size(), 0,
+                    while (l7g_batcher_submit(b, (const uint8_t *)r.data(), (uint32_t)r.size(), 0,
                                        [](void *p, uint8_t, int32_t, uint32_t) {
                                            auto *c = (Ctx *)p;
                                            c->out->push_back(std::chrono::duration<double, std::micro>(Clock::now() - c->t0).count());
                                            (*c->left)--;
                                            delete c;
                                        },
-                                       c);
+                                       c) == -2)
+                        std::this_thread::yield();  // backpressure: the batcher's queue is full
                 }
             });
         for (auto &w : ws) w.join();
