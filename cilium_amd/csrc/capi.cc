@@ -95,6 +95,7 @@ constexpr uint32_t kZeroCopyMaxRequests = 256;
 constexpr size_t kZeroCopyMaxBytes = 256 * 1024;
 // batches below this size skip the protocol split when one classifier can walk them alone
 constexpr uint32_t kPartitionMin = 4096;
+constexpr uint32_t kHostScanMax = 4096;  // host calls up to this size check their connections for cold rule sets
 
 // l7g_classify_host's per-thread staging: its own stream, device arena and
 // request arrays (grow-only), so host-buffer calls from different threads
@@ -657,9 +658,14 @@ int l7g_conn_update(l7g_engine *e, uint32_t index, const l7g_conn_t *conn, char 
     return 0;
 }
 
-int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const uint64_t *off, const uint32_t *len,
-                 const uint32_t *conn,
-                 uint32_t n, uint8_t *verdict, int32_t *rule, uint32_t *consumed, uint64_t *counters, void *stream) {
+}  // extern "C"
+
+// l7g_classify; host_conn: the connection indices in host memory as well
+// (l7g_classify_host's calls), so that a small call whose requests all use the
+// hot HTTP rule set skips the general HTTP kernel's launch
+static int Classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const uint64_t *off, const uint32_t *len,
+                    const uint32_t *conn, uint32_t n, uint8_t *verdict, int32_t *rule, uint32_t *consumed,
+                    uint64_t *counters, void *stream, const uint32_t *host_conn) {
     std::lock_guard<std::mutex> g(e->mu);
     if (e->device < 0) return (int)hipErrorNoDevice;
     hipError_t rc = hipSetDevice(e->device);
@@ -693,6 +699,14 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
     // (a small memcached-only batch gains nothing from converged waves: its one
     // kernel walks the batch itself, one launch fewer on the latency path)
     const bool partitioned = nproto > 1 || e->has_kafka || (e->has_mc && n >= kPartitionMin);
+    bool any_cold = e->any_cold;
+    if (any_cold && host_conn && n <= kHostScanMax) {
+        any_cold = false;
+        for (uint32_t i = 0; i < n && !any_cold; i++) {
+            const uint32_t ci = host_conn[i];
+            any_cold = ci < e->conns.size() && e->attrs[ci].proto == PROTO_HTTP && e->conns[ci].ruleset != e->hot_ruleset;
+        }
+    }
     StreamScratch *S = nullptr;
     if ((rc = GetScratch(e, s, &S)) != hipSuccess) return (int)rc;
     uint32_t *sel_k = nullptr, *sel_m = nullptr, *sel_h = nullptr, *sel_z = nullptr, *cnt = nullptr;
@@ -762,7 +776,7 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
         tile_ctr = S->d_work;
     }
     if (rc == hipSuccess && run[1])
-        rc = LaunchHttpClassify(B, ht, sel_h, cnt ? cnt + L7_KAFKA_CLASSES + 2 : nullptr, e->any_cold, !partitioned,
+        rc = LaunchHttpClassify(B, ht, sel_h, cnt ? cnt + L7_KAFKA_CLASSES + 2 : nullptr, any_cold, !partitioned,
                                 tile_ctr, s);
     mark(2);
     uint32_t *zcount = cnt ? cnt + 31 : nullptr;
@@ -832,6 +846,14 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
     return (int)rc;
 }
 
+extern "C" {
+
+int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const uint64_t *off, const uint32_t *len,
+                 const uint32_t *conn, uint32_t n, uint8_t *verdict, int32_t *rule, uint32_t *consumed,
+                 uint64_t *counters, void *stream) {
+    return Classify(e, arena, arena_len, off, len, conn, n, verdict, rule, consumed, counters, stream, nullptr);
+}
+
 }  // extern "C"
 
 // ---- l7g_classify_host's per-thread path, in three steps (the batcher's
@@ -877,23 +899,34 @@ static hipError_t HostGrow(HostCtx *H, uint32_t n, uint64_t arena_len) {
     return hipSuccess;
 }
 
-// classify a call whose inputs are in pinned host memory (the thread's staging,
-// or a batcher slot), wait for it, copy the answers out
-static hipError_t HostRun(l7g_engine *e, HostCtx *H, uint32_t n, uint64_t arena_len, const uint64_t *p_off,
-                          const uint32_t *p_len, const uint32_t *p_conn, const uint8_t *p_arena, uint8_t *verdict,
-                          int32_t *rule, uint32_t *consumed) {
+// where a call's inputs lie in pinned host memory: the thread's staging, or a
+// batcher slot filled in place (its three arrays `stride` entries apart, its
+// request bytes in one piece per lane)
+struct HostIn {
+    const uint64_t *off;
+    const uint32_t *len, *conn;
+    size_t stride;  // > 0: len = (u8 *)off + stride * 8, conn = (u8 *)off + stride * 12
+    const l7g_host_seg *seg;
+    int nseg;  // the arena is these pieces, concatenated
+};
+
+// classify a call whose inputs are in pinned host memory, wait for it, copy
+// the answers out
+static hipError_t HostRun(l7g_engine *e, HostCtx *H, uint32_t n, uint64_t arena_len, const HostIn &in,
+                          uint8_t *verdict, int32_t *rule, uint32_t *consumed) {
     hipError_t rc = hipSuccess;
     const size_t nn = std::max<uint32_t>(n, 1);
     const size_t a_off = HostArenaOff(n);
-    // A small call (the Envoy adapter's Allowed(), one OnData) is latency, not
-    // bandwidth: the kernels read the inputs from and write the verdicts to the
-    // pinned memory in place (zero-copy, over PCIe), so the call is one launch
-    // and a wait instead of copy, launch, copy, wait.
+    // A small call (the Envoy adapter's Allowed(), one OnData, a light batch)
+    // is latency, not bandwidth: the kernels read the inputs from and write the
+    // verdicts to the pinned memory in place (zero-copy, over PCIe), so the
+    // call is one launch and a wait instead of copy, launch, copy, wait.
     static const bool zc_on = [] {
         const char *v = getenv("L7G_SYNC_ZEROCOPY");
         return !(v && v[0] == '0');
     }();
-    const bool zc = zc_on && n <= kZeroCopyMaxRequests && a_off + arena_len <= kZeroCopyMaxBytes;
+    const bool zc = zc_on && (in.nseg == 0 || (in.nseg == 1 && in.seg[0].rows <= 1)) && n <= kZeroCopyMaxRequests &&
+                    a_off + arena_len <= kZeroCopyMaxBytes;
     hipStream_t s = H->s;
     const uint64_t *d_o;
     const uint32_t *d_l, *d_c;
@@ -905,33 +938,48 @@ static hipError_t HostRun(l7g_engine *e, HostCtx *H, uint32_t n, uint64_t arena_
             if (rc == hipSuccess) rc = hipHostGetDevicePointer(&dp, const_cast<void *>(h), 0);
             return (const uint8_t *)dp;
         };
-        d_o = (const uint64_t *)dev_ptr(p_off);
-        d_l = (const uint32_t *)dev_ptr(p_len);
-        d_c = (const uint32_t *)dev_ptr(p_conn);
-        d_a = dev_ptr(p_arena);
+        d_o = (const uint64_t *)dev_ptr(in.off);
+        d_l = (const uint32_t *)dev_ptr(in.len);
+        d_c = (const uint32_t *)dev_ptr(in.conn);
+        d_a = in.nseg ? dev_ptr(in.seg[0].p) : (const uint8_t *)d_o;
         d_out = (uint8_t *)dev_ptr(H->pin_out);
         if (rc != hipSuccess) return rc;
     } else {
         uint8_t *d_in = H->dev;
+        const bool staging = in.off == (const uint64_t *)H->pin_in;
+        const size_t st = staging ? nn : in.stride ? in.stride : nn;
         d_o = (const uint64_t *)d_in;
-        d_l = (const uint32_t *)(d_in + nn * 8);
-        d_c = (const uint32_t *)(d_in + nn * 12);
-        d_a = d_in + a_off;
-        if (p_off == (const uint64_t *)H->pin_in) {  // the thread's staging: one copy of the whole layout
+        d_l = (const uint32_t *)(d_in + st * 8);
+        d_c = (const uint32_t *)(d_in + st * 12);
+        d_a = d_in + HostArenaOff((uint32_t)st);
+        if (staging) {  // the thread's staging: one copy of the whole layout
             rc = hipMemcpyAsync(d_in, H->pin_in, a_off + arena_len, hipMemcpyHostToDevice, s);
         } else {
-            rc = hipMemcpyAsync((void *)d_o, p_off, (size_t)n * 8, hipMemcpyHostToDevice, s);
-            if (rc == hipSuccess) rc = hipMemcpyAsync((void *)d_l, p_len, (size_t)n * 4, hipMemcpyHostToDevice, s);
-            if (rc == hipSuccess) rc = hipMemcpyAsync((void *)d_c, p_conn, (size_t)n * 4, hipMemcpyHostToDevice, s);
-            if (rc == hipSuccess && arena_len)
-                rc = hipMemcpyAsync((void *)d_a, p_arena, arena_len, hipMemcpyHostToDevice, s);
+            if (in.stride) {  // the three arrays in one copy
+                rc = hipMemcpyAsync(d_in, in.off, st * 12 + (size_t)n * 4, hipMemcpyHostToDevice, s);
+            } else {
+                rc = hipMemcpyAsync((void *)d_o, in.off, (size_t)n * 8, hipMemcpyHostToDevice, s);
+                if (rc == hipSuccess) rc = hipMemcpyAsync((void *)d_l, in.len, (size_t)n * 4, hipMemcpyHostToDevice, s);
+                if (rc == hipSuccess) rc = hipMemcpyAsync((void *)d_c, in.conn, (size_t)n * 4, hipMemcpyHostToDevice, s);
+            }
+            uint64_t at = 0;
+            for (int k = 0; k < in.nseg && rc == hipSuccess; k++) {
+                const l7g_host_seg &g = in.seg[k];
+                if (!g.width || !g.rows) continue;
+                if (g.rows == 1)
+                    rc = hipMemcpyAsync((void *)(d_a + at), g.p, g.width, hipMemcpyHostToDevice, s);
+                else
+                    rc = hipMemcpy2DAsync((void *)(d_a + at), g.width, g.p, g.pitch, g.width, g.rows,
+                                          hipMemcpyHostToDevice, s);
+                at += g.width * g.rows;
+            }
         }
     }
     uint8_t *d_v = d_out;
     int32_t *d_r = (int32_t *)(d_out + ((nn + 3) & ~(size_t)3));
     uint32_t *d_cons = (uint32_t *)(d_out + ((nn + 3) & ~(size_t)3) + nn * 4);
     if (rc == hipSuccess)
-        rc = (hipError_t)l7g_classify(e, d_a, arena_len, d_o, d_l, d_c, n, d_v, d_r, d_cons, nullptr, s);
+        rc = (hipError_t)Classify(e, d_a, arena_len, d_o, d_l, d_c, n, d_v, d_r, d_cons, nullptr, s, in.conn);
     const size_t out_bytes = ((nn + 3) & ~(size_t)3) + nn * 8;
     if (rc == hipSuccess && n && !zc) rc = hipMemcpyAsync(H->pin_out, d_out, out_bytes, hipMemcpyDeviceToHost, s);
     if (rc == hipSuccess) rc = hipStreamSynchronize(s);
@@ -967,22 +1015,39 @@ int l7g_host_run(l7g_engine *e, uint32_t n, uint64_t arena_len, uint8_t *verdict
     if (rc == hipSuccess) rc = HostCtxFor(e, &H);
     if (rc == hipSuccess) {
         const size_t nn = std::max<uint32_t>(n, 1);
-        rc = HostRun(e, H, n, arena_len, (const uint64_t *)H->pin_in, (const uint32_t *)(H->pin_in + nn * 8),
-                     (const uint32_t *)(H->pin_in + nn * 12), H->pin_in + HostArenaOff(n), verdict, rule, consumed);
+        const l7g_host_seg seg{H->pin_in + HostArenaOff(n), arena_len, arena_len, 1};
+        const HostIn in{(const uint64_t *)H->pin_in, (const uint32_t *)(H->pin_in + nn * 8),
+                        (const uint32_t *)(H->pin_in + nn * 12), nn, &seg, 1};
+        rc = HostRun(e, H, n, arena_len, in, verdict, rule, consumed);
     }
     return (int)rc;
 }
 
-int l7g_host_run_pinned(l7g_engine *e, uint32_t n, uint64_t arena_len, const uint64_t *off, const uint32_t *len,
-                        const uint32_t *conn, const uint8_t *arena, uint8_t *verdict, int32_t *rule,
-                        uint32_t *consumed) {
+int l7g_host_run_pinned(l7g_engine *e, uint32_t n, const uint64_t *off, size_t stride, const l7g_host_seg *seg,
+                        int nseg, uint8_t *verdict, int32_t *rule, uint32_t *consumed) {
+    if (e->device < 0) return (int)hipErrorNoDevice;
+    hipError_t rc = hipSetDevice(e->device);
+    HostCtx *H = nullptr;
+    uint64_t arena_len = 0;
+    for (int k = 0; k < nseg; k++) arena_len += seg[k].width * seg[k].rows;
+    const uint32_t st = (uint32_t)std::max<size_t>(stride, n);
+    if (rc == hipSuccess) rc = HostCtxFor(e, &H);
+    // device staging for `st` entries' arrays and the arena, pinned outputs for n
+    if (rc == hipSuccess) rc = HostGrow(H, st, arena_len);
+    if (rc == hipSuccess) {
+        const uint8_t *b = (const uint8_t *)off;
+        const HostIn in{off, (const uint32_t *)(b + stride * 8), (const uint32_t *)(b + stride * 12), stride, seg, nseg};
+        rc = HostRun(e, H, n, arena_len, in, verdict, rule, consumed);
+    }
+    return (int)rc;
+}
+
+int l7g_host_reserve(l7g_engine *e, uint32_t n, uint64_t arena_len) {
     if (e->device < 0) return (int)hipErrorNoDevice;
     hipError_t rc = hipSetDevice(e->device);
     HostCtx *H = nullptr;
     if (rc == hipSuccess) rc = HostCtxFor(e, &H);
-    if (rc == hipSuccess) rc = HostGrow(H, n, 0);  // device staging and pinned outputs for n requests
-    if (rc == hipSuccess && HostArenaOff(n) + arena_len + 64 > H->in_cap) rc = HostGrow(H, n, arena_len);
-    if (rc == hipSuccess) rc = HostRun(e, H, n, arena_len, off, len, conn, arena, verdict, rule, consumed);
+    if (rc == hipSuccess) rc = HostGrow(H, n, arena_len);
     return (int)rc;
 }
 

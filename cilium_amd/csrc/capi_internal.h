@@ -23,10 +23,22 @@ int l7g_host_stage(l7g_engine *e, uint32_t n, uint64_t arena_len, uint8_t **aren
                    uint32_t **conn);
 int l7g_host_run(l7g_engine *e, uint32_t n, uint64_t arena_len, uint8_t *verdict, int32_t *rule, uint32_t *consumed);
 // The same with inputs already in pinned host memory (hipHostMalloc: a
-// batcher slot filled in place by its submitters): copied to the device (or
-// read in place for a small call), classified, waited for.
-int l7g_host_run_pinned(l7g_engine *e, uint32_t n, uint64_t arena_len, const uint64_t *off, const uint32_t *len,
-                        const uint32_t *conn, const uint8_t *arena, uint8_t *verdict, int32_t *rule,
-                        uint32_t *consumed);
+// batcher slot filled in place by its submitters): off[0..n), then len and
+// conn `stride` entries further on (len = (u8 *)off + stride * 8, conn =
+// (u8 *)off + stride * 12; stride >= n), and the request bytes as nseg
+// blocks that the device sees concatenated (off[] indexes the concatenation);
+// a block is `rows` rows of `width` bytes, `pitch` bytes apart in host memory
+// (one 2-D copy).  Copied to the device (or, one single-row block and a small
+// call, read in place), classified, waited for.
+struct l7g_host_seg {
+    const uint8_t *p;
+    uint64_t width, pitch;
+    uint32_t rows;
+};
+int l7g_host_run_pinned(l7g_engine *e, uint32_t n, const uint64_t *off, size_t stride, const l7g_host_seg *seg,
+                        int nseg, uint8_t *verdict, int32_t *rule, uint32_t *consumed);
+// Sizes the calling thread's stream and staging for calls of up to n requests
+// over arena_len bytes now, so that no such call reallocates them.
+int l7g_host_reserve(l7g_engine *e, uint32_t n, uint64_t arena_len);
 void *l7g_pinned_alloc(size_t bytes);  // hipHostMalloc (NULL on failure)
 void l7g_pinned_free(void *p);

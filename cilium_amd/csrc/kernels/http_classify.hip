@@ -1449,7 +1449,16 @@ __global__ __launch_bounds__(kBlock) void http_classify_kernel(Batch B, HttpTabl
         const DevRuleset r = T.rulesets[hot];
         const uint4 *src = (const uint4 *)(T.images + r.image_off);
         const uint32_t n16 = (r.image_len + 15) / 16;
-        for (uint32_t i = tid; i < n16; i += kBlock) ((uint4 *)s_img)[i] = src[i];
+        // every load issued before the first store: one memory round trip, not
+        // one per 8 KiB (a small launch -- one request -- waits on this)
+        constexpr uint32_t kIters = (kLdsImageBytes / 16 + kBlock - 1) / kBlock;
+        uint4 t[kIters];
+#pragma unroll
+        for (uint32_t k = 0; k < kIters; k++)
+            if (tid + k * kBlock < n16) t[k] = src[tid + k * kBlock];
+#pragma unroll
+        for (uint32_t k = 0; k < kIters; k++)
+            if (tid + k * kBlock < n16) ((uint4 *)s_img)[tid + k * kBlock] = t[k];
     }
     __syncthreads();
 

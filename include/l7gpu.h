@@ -171,23 +171,28 @@ int l7g_stats(l7g_engine *e, l7g_stats_t *out);
 /* Asynchronous batching for callers that decide one request at a time on an
  * event loop -- Envoy's cilium.l7policy decodeHeaders
  * (envoy/cilium_l7policy.cc:127-182), which would return StopIteration and
- * resume (continueDecoding / sendLocalReply) from the callback.  Submitted
- * requests are copied into one of the batcher's sharded queues (the calling
- * thread's); two flusher threads each take everything pending once
- * max_requests are pending or the oldest has waited max_wait_us, classify it
- * with one l7g_classify_host launch on their own stream (so one batch is on
- * the device while the next is gathered), and call each request's callback
- * from the flusher thread -- batches in the order they were taken, a thread's
- * requests in submission order.  A device failure answers every request of
- * that flush L7G_UNSUPPORTED.  A callback must not call l7g_batcher_flush or
- * l7g_batcher_destroy (from a flusher thread both return at once, doing
- * nothing). */
+ * resume (continueDecoding / sendLocalReply) from the callback.  Submitters
+ * copy their request straight into the open batch slot (pinned host memory in
+ * the layout the device copy reads; a compare-and-swap reserves the place, no
+ * lock).  Two flusher threads each seal the open slot once max_requests are in
+ * it, its first request has waited max_wait_us, or a flush is asked for
+ * (under load a batch can hold up to twice max_requests: requests keep coming
+ * while the slot is sealed), classify it in place with one launch on their own
+ * stream (so one batch is on the device while the next fills), and call each
+ * request's callback from the flusher thread -- batches in the order they
+ * were sealed, a thread's requests in submission order.  A device failure
+ * answers every request of that batch L7G_UNSUPPORTED.  A callback must not
+ * call l7g_batcher_flush or l7g_batcher_destroy (from a flusher thread both
+ * return at once, doing nothing). */
 typedef void (*l7g_done_fn)(void *ctx, uint8_t verdict, int32_t rule, uint32_t consumed);
 typedef struct l7g_batcher l7g_batcher;
+/* Slots hold max(2 x max_requests, 1024) requests and 2 KiB of request bytes
+ * per request each; four slots are allocated (pinned) up front. */
 l7g_batcher *l7g_batcher_create(l7g_engine *e, uint32_t max_requests, uint32_t max_wait_us);
-/* 0 = queued; -1 = the batcher is shutting down; -2 = backpressure: 64 x
- * max_requests requests are already waiting (the callback is not called; the
- * caller decides the request itself or retries). */
+/* 0 = queued; -1 = the batcher is shutting down; -2 = backpressure: both
+ * flushers are busy and the open slot is full, or the request is larger than
+ * a slot (the callback is not called; the caller decides the request itself
+ * or retries). */
 int l7g_batcher_submit(l7g_batcher *b, const uint8_t *req, uint32_t len, uint32_t conn, l7g_done_fn done, void *ctx);
 /* Flushes now and returns once every request submitted before the call has
  * had its callback (0); -1 when called from a callback. */
@@ -196,6 +201,11 @@ int l7g_batcher_flush(l7g_batcher *b);
 void l7g_batcher_destroy(l7g_batcher *b);
 /* Requests classified and launches made so far (for latency accounting). */
 void l7g_batcher_stats(l7g_batcher *b, uint64_t *requests, uint64_t *launches);
+/* Where the flusher threads' time went, summed over both, in ns: [0] waiting
+ * for a sealed slot's entries to be published, [1] the device round trip (copy, launch, wait),
+ * [2] callbacks, [3] waiting for the previous batch's callbacks (ordering);
+ * [4] the largest batch. */
+void l7g_batcher_timing(l7g_batcher *b, uint64_t out[5]);
 
 /* Measurement hook (bench.py): with profiling on, l7g_classify records HIP
  * events on its stream around each kernel it launches; l7g_profile_last waits

@@ -56,6 +56,32 @@ int main() {
     for (auto &x : th) x.join();
     const int frc = l7g_batcher_flush(g_b);
     const uint64_t after_flush = g_calls.load();
+    uint64_t reqs = 0, launches = 0;
+    l7g_batcher_stats(g_b, &reqs, &launches);
+    l7g_batcher_destroy(g_b);
+    // large requests (1-31 KB): slots fill by bytes before they fill by count,
+    // so racing reservations past the arena's end leave holes the flusher
+    // closes up -- still every callback once, in each thread's order
+    for (auto &x : next) x = 0;
+    const uint64_t calls0 = g_calls.load();
+    g_b = l7g_batcher_create(e, 64, 50);
+    std::vector<std::thread> th2;
+    const int N2 = 3000;
+    for (int t = 0; t < T; t++)
+        th2.emplace_back([t, &rejected] {
+            std::vector<uint8_t> req(32768, 'b');
+            for (uint32_t i = 0; i < (uint32_t)N2; i++) {
+                int rc;
+                while ((rc = l7g_batcher_submit(g_b, req.data(), 1000 + (i * 7919u + t * 104729u) % 30000, 0, done,
+                                                (void *)(uintptr_t)((uint64_t)t << 32 | i))) == -2)
+                    rejected++, std::this_thread::yield();
+                if (rc != 0) { g_bad++; return; }
+            }
+        });
+    for (auto &x : th2) x.join();
+    l7g_batcher_flush(g_b);
+    const uint64_t large_calls = g_calls.load() - calls0;
+    l7g_batcher_destroy(g_b);
     // backpressure: callbacks that block until released keep both flushers
     // busy, so the open slot fills (1024 requests for max_requests = 4) and
     // submit refuses; after the release every queued request is answered
@@ -76,14 +102,12 @@ int main() {
     l7g_batcher_flush(slow);
     const int slow_answered = slow_calls.load();
     l7g_batcher_destroy(slow);
-    uint64_t reqs = 0, launches = 0;
-    l7g_batcher_stats(g_b, &reqs, &launches);
-    l7g_batcher_destroy(g_b);
     l7g_engine_destroy(e);
     printf("{\"calls\": %llu, \"after_flush\": %llu, \"expected\": %d, \"bad\": %d, \"flush_rc\": %d, "
            "\"reentrant_flush_rc\": %d, \"launches\": %llu, \"queued\": %d, \"refused\": %d, \"rejected\": %d, "
-           "\"slow_answered\": %d}\n",
+           "\"slow_answered\": %d, \"large_calls\": %llu, \"large_expected\": %d}\n",
            (unsigned long long)g_calls.load(), (unsigned long long)after_flush, T * N, g_bad.load(), frc,
-           g_flush_rc.load(), (unsigned long long)launches, queued, refused, rejected.load(), slow_answered);
+           g_flush_rc.load(), (unsigned long long)launches, queued, refused, rejected.load(), slow_answered,
+           (unsigned long long)large_calls, T * N2);
     return 0;
 }

@@ -107,34 +107,46 @@ int main(int argc, char **argv) {
         l7g_batcher_stats(b, &warm_req, &warm_l);
         // a quarter second of offered load per configuration (at least iters * 4 requests)
         const int per = std::max(iters * 4 / cf.threads, (int)(cf.rate_per_thread * 0.25));
-        std::vector<std::vector<double>> lat(cf.threads);
-        struct Ctx { Clock::time_point t0; std::vector<double> *out; std::atomic<int> *left; };
-        std::atomic<int> left{per * cf.threads};
+        // per-request context and latency slot allocated up front: the callbacks
+        // write one double and touch nothing shared (the harness itself must not
+        // be the bottleneck: a malloc per request freed on the flusher thread was)
+        std::vector<std::vector<double>> lat(cf.threads, std::vector<double>(per, -1.0));
+        struct Ctx { Clock::time_point t0; double *out; };
+        std::vector<std::vector<Ctx>> ctxs(cf.threads, std::vector<Ctx>(per));
+        std::atomic<uint64_t> refused{0}, late_ns{0};
         std::vector<std::thread> ws;
         const auto start = Clock::now();
         for (int t = 0; t < cf.threads; t++)
             ws.emplace_back([&, t] {
                 const auto gap = std::chrono::duration<double>(1.0 / cf.rate_per_thread);
+                int64_t late = 0;  // how far behind its schedule the thread ended (generator-bound if large)
+                uint64_t nref = 0;
                 for (int i = 0; i < per; i++) {
-                    std::this_thread::sleep_until(start + std::chrono::duration_cast<Clock::duration>(gap * (double)i));
+                    const auto due = start + std::chrono::duration_cast<Clock::duration>(gap * (double)i);
+                    if (Clock::now() < due) std::this_thread::sleep_until(due);
+                    if (i == per - 1) late = (Clock::now() - due).count();
                     const std::string &r = http[(size_t)(i * cf.threads + t) % http.size()];
-                    auto *c = new Ctx{Clock::now(), &lat[t], &left};
+                    Ctx *c = &ctxs[t][i];
+                    c->out = &lat[t][i];
+                    c->t0 = Clock::now();
                     while (l7g_batcher_submit(b, (const uint8_t *)r.data(), (uint32_t)r.size(), 0,
-                                       [](void *p, uint8_t, int32_t, uint32_t) {
-                                           auto *c = (Ctx *)p;
-                                           c->out->push_back(std::chrono::duration<double, std::micro>(Clock::now() - c->t0).count());
-                                           (*c->left)--;
-                                           delete c;
-                                       },
-                                       c) == -2)
-                        std::this_thread::yield();  // backpressure: the batcher's queue is full
+                                              [](void *p, uint8_t, int32_t, uint32_t) {
+                                                  auto *c = (Ctx *)p;
+                                                  *c->out = std::chrono::duration<double, std::micro>(Clock::now() - c->t0).count();
+                                              },
+                                              c) == -2)
+                        nref++, std::this_thread::yield();  // backpressure: both flushers busy, open slot full
                 }
+                late_ns += (uint64_t)std::max<int64_t>(late, 0);
+                refused += nref;
             });
         for (auto &w : ws) w.join();
+        const double submit_secs = std::chrono::duration<double>(Clock::now() - start).count();
         l7g_batcher_flush(b);
         const double secs = std::chrono::duration<double>(Clock::now() - start).count();
-        uint64_t nreq = 0, nl = 0;
+        uint64_t nreq = 0, nl = 0, tm[5];
         l7g_batcher_stats(b, &nreq, &nl);
+        l7g_batcher_timing(b, tm);
         l7g_batcher_destroy(b);
         std::vector<double> all;
         for (auto &v : lat) all.insert(all.end(), v.begin(), v.end());
@@ -143,6 +155,10 @@ int main(int argc, char **argv) {
         bat << (firstc ? "" : ", ") << "{\"threads\": " << cf.threads << ", \"offered_per_s\": "
             << cf.threads * cf.rate_per_thread << ", \"max_requests\": " << cf.n << ", \"max_wait_us\": " << cf.wait_us
             << ", \"achieved_per_s\": " << (double)nreq / secs << ", \"launches\": " << nl
+            << ", \"submit_s\": " << submit_secs << ", \"total_s\": " << secs << ", \"refused_retries\": " << refused.load()
+            << ", \"mean_end_lag_us\": " << (double)late_ns.load() / cf.threads / 1e3
+            << ", \"flusher_ms\": {\"ready_wait\": " << tm[0] / 1e6 << ", \"device\": " << tm[1] / 1e6
+            << ", \"callbacks\": " << tm[2] / 1e6 << ", \"order_wait\": " << tm[3] / 1e6 << ", \"max_batch\": " << tm[4] << "}"
             << ", \"latency\": " << pct(all) << "}";
         firstc = false;
     }

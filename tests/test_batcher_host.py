@@ -18,9 +18,11 @@ def test_batcher_threads_order_flush_backpressure():
     assert r.returncode == 0, r.stderr
     d = json.loads(r.stdout)
     assert d["bad"] == 0, d
-    assert d["calls"] == d["expected"] == d["after_flush"], d  # flush returned after every callback
+    assert d["after_flush"] == d["expected"], d  # flush returned after every callback
+    assert d["calls"] == d["expected"] + d["large_expected"], d
     assert d["flush_rc"] == 0 and d["reentrant_flush_rc"] == -1, d
     assert d["launches"] < d["expected"] // 8, d  # batched, not one launch per request
+    assert d["large_calls"] == d["large_expected"], d  # byte-full slots (holes closed up): every callback once
     # both flushers blocked in callbacks: at most two sealed batches and one full open slot are taken
     assert d["refused"] > 0 and d["queued"] + d["refused"] == 5000, d
     assert 1024 <= d["queued"] <= 3 * 1024 and d["slow_answered"] == d["queued"], d
