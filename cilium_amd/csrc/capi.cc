@@ -2,6 +2,7 @@
 // connection table, table upload and kernel dispatch (product code).
 #include <hip/hip_runtime_api.h>
 
+#include <algorithm>
 #include <cstring>
 #include <map>
 #include <thread>
@@ -36,17 +37,19 @@ hipError_t LaunchKafkaInflate(const Batch &B, const uint32_t *zlist, const uint3
 uint32_t KafkaInflateBlocks();
 uint32_t KafkaInflateRegionBytes();
 hipError_t LaunchMemcacheClassify(const Batch &B, const McTables &T, const uint32_t *sel, const uint32_t *sel2,
-                                  const uint32_t *sel_count, bool answer_other, hipStream_t stream);
-hipError_t LaunchR2d2Classify(const Batch &B, const R2Tables &T, bool answer_other, hipStream_t stream);
+                                  const uint32_t *sel_count, bool answer_other, uint32_t scratch_lanes,
+                                  hipStream_t stream);
+hipError_t LaunchR2d2Classify(const Batch &B, const R2Tables &T, bool answer_other, uint32_t scratch_lanes,
+                              hipStream_t stream);
 size_t CassandraScratchBytes(uint32_t n);
 hipError_t LaunchCassandraClassify(const Batch &B, const CassTables &T, void *scratch, size_t scratch_bytes,
-                                   bool answer_other, hipStream_t stream);
+                                   bool answer_other, uint32_t nfa_lanes, hipStream_t stream);
 hipError_t LaunchCounters(const uint8_t *verdict, const int32_t *rule, uint32_t n, uint32_t nrules,
                           uint64_t *counters, uint32_t *scratch, hipStream_t stream);
 size_t CountersScratchBytes();
 hipError_t LaunchFlowStats(const Batch &B, uint32_t nkeys, uint64_t *acc, hipStream_t stream);
 uint32_t FlowStatsMaxKeys();
-hipError_t LaunchHttpNfa(const Batch &B, const HttpTables &T, hipStream_t stream);
+hipError_t LaunchHttpNfa(const Batch &B, const HttpTables &T, uint32_t scratch_lanes, hipStream_t stream);
 hipError_t LaunchPartition(const Batch &B, uint32_t *sel_kafka, uint32_t *sel_mc, uint32_t *sel_http, uint32_t *counts,
                            hipStream_t stream);
 hipError_t HttpPhaseTimes(uint64_t *out, bool reset);
@@ -75,11 +78,15 @@ struct StreamScratch {
     size_t use_cap = 0;
     // work counters of unpartitioned batches (HTTP tile counters), allocated on first use
     uint32_t *d_work = nullptr;
+    // large NFAs' state sets: a lane's 2 W words for each lane of a launch (grow-only)
+    uint64_t *d_bignfa = nullptr;
+    size_t bignfa_bytes = 0;
     // completion of the last call's kernels on this stream
     hipEvent_t done_ev = nullptr;
     bool launched = false;
     uint64_t last_use = 0;
     ~StreamScratch() {
+        if (d_bignfa) hipFree(d_bignfa);
         if (d_sel) hipFree(d_sel);
         if (d_nfa) hipFree(d_nfa);
         if (d_hist) hipFree(d_hist);
@@ -95,7 +102,8 @@ constexpr uint32_t kZeroCopyMaxRequests = 256;
 constexpr size_t kZeroCopyMaxBytes = 256 * 1024;
 // batches below this size skip the protocol split when one classifier can walk them alone
 constexpr uint32_t kPartitionMin = 4096;
-constexpr uint32_t kHostScanMax = 4096;  // host calls up to this size check their connections for cold rule sets
+constexpr uint32_t kHostScanMax = 4096;
+constexpr size_t kNfaScratchBytes = 256ull << 20;  // large NFAs: state-set scratch per stream (lanes in flight)  // host calls up to this size check their connections for cold rule sets
 
 // l7g_classify_host's per-thread staging: its own stream, device arena and
 // request arrays (grow-only), so host-buffer calls from different threads
@@ -368,6 +376,10 @@ hipError_t Upload(l7g_engine *e) {
         T.hot_ruleset = e->hot_ruleset;
         T.nfa_pool = H.nfa_pool.empty() ? nullptr : d + o_nfa;
         T.nfa_bits = nullptr;
+        // large NFAs (W > kNfaMaxWords): 2 W words of scratch per lane, given at launch
+        auto lane_words = [](uint32_t w) { return w > (uint32_t)kNfaMaxWords ? 2 * w : 0u; };
+        T.nfa_scratch = nullptr;
+        T.nfa_lane_words = lane_words(e->hc->nfa_max_words());
         KafkaTables &KT = e->kt;
         KT.rulesets = (const DevKafkaRuleset *)(d + k_rs);
         KT.rules = (const DevKafkaRule *)(d + k_r);
@@ -385,11 +397,15 @@ hipError_t Upload(l7g_engine *e) {
         MT.images_len = (uint32_t)M.images.size();
         MT.nfa_pool = M.nfa_pool.empty() ? nullptr : d + m_nfa;
         MT.max_chunks = (uint32_t)M.max_chunks;
+        MT.nfa_scratch = nullptr;
+        MT.nfa_lane_words = lane_words(e->mc->nfa_max_words());
         R2Tables &RT = e->rt;
         RT.rulesets = (const DevRuleset *)(d + r_rs);
         RT.images = d + r_img;
         RT.nrulesets = (uint32_t)R.rulesets.size();
         RT.nfa_pool = R.nfa_pool.empty() ? nullptr : d + r_nfa;
+        RT.nfa_scratch = nullptr;
+        RT.nfa_lane_words = lane_words(e->r2->nfa_max_words());
         CassTables &CT = e->ct;
         CT.rulesets = (const DevRuleset *)(d + c_rs);
         CT.images = d + c_img;
@@ -397,6 +413,8 @@ hipError_t Upload(l7g_engine *e) {
         CT.nfa_pool = CI.nfa_pool.empty() ? nullptr : d + c_nfa;
         CT.lower = (const uint32_t *)(d + c_low);
         CT.nlower = (uint32_t)(CI.lower.size() / 2);
+        CT.nfa_scratch = nullptr;
+        CT.nfa_lane_words = lane_words(e->cs->nfa_max_words());
         e->tables_dirty = false;
     }
     if (e->conns_dirty) {
@@ -755,6 +773,38 @@ static int Classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, con
         if (rc != hipSuccess) return (int)rc;
         ht.nfa_bits = S->d_nfa;
     }
+    // large NFAs: one scratch for the call's launches (they run one after
+    // another on this stream), as many lanes as a budget allows; the kernels
+    // loop over their requests with that many lanes
+    McTables mt = e->mt;
+    R2Tables rt = e->rt;
+    CassTables ct = e->ct;
+    uint32_t big_lanes = 0;
+    {
+        const uint32_t lw = std::max({ht.nfa_lane_words, mt.nfa_lane_words, rt.nfa_lane_words, ct.nfa_lane_words});
+        if (lw && rc == hipSuccess) {
+            const size_t lane_bytes = (size_t)lw * 8;
+            size_t lanes = std::min<size_t>(((size_t)n + 255) & ~(size_t)255, kNfaScratchBytes / lane_bytes);
+            lanes = std::max<size_t>(lanes & ~(size_t)255, 256);
+            if (lanes * lane_bytes > S->bignfa_bytes) {
+                if (S->d_bignfa) {
+                    if (S->launched) rc = hipEventSynchronize(S->done_ev);
+                    hipFree(S->d_bignfa);
+                    S->d_bignfa = nullptr;
+                    S->bignfa_bytes = 0;
+                }
+                if (rc == hipSuccess) rc = hipMalloc(&S->d_bignfa, lanes * lane_bytes);
+                if (rc == hipSuccess) S->bignfa_bytes = lanes * lane_bytes;
+            }
+            if (rc != hipSuccess) return (int)rc;
+            big_lanes = (uint32_t)(S->bignfa_bytes / lane_bytes);
+            uint64_t *sc = S->d_bignfa;
+            if (ht.nfa_lane_words) { ht.nfa_scratch = sc; ht.nfa_lane_words = lw; }
+            if (mt.nfa_lane_words) { mt.nfa_scratch = sc; mt.nfa_lane_words = lw; }
+            if (rt.nfa_lane_words) { rt.nfa_scratch = sc; rt.nfa_lane_words = lw; }
+            if (ct.nfa_lane_words) { ct.nfa_scratch = sc; ct.nfa_lane_words = lw; }
+        }
+    }
     // profiling: event k is recorded before stage k (partition, http, kafka, memcache), event 4 after the last
     const bool prof = e->profile;
     auto mark = [&](int k) {
@@ -765,7 +815,7 @@ static int Classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, con
     mark(0);
     if (rc == hipSuccess && run[0]) rc = LaunchPartition(B, sel_k, sel_m, sel_h, cnt, s);
     mark(1);
-    if (rc == hipSuccess && run[1] && nfa) rc = LaunchHttpNfa(B, ht, s);
+    if (rc == hipSuccess && run[1] && nfa) rc = LaunchHttpNfa(B, ht, big_lanes, s);
     // tile counters: in the partition counts (zeroed above), or, for a large
     // unpartitioned batch, two words zeroed here (a small batch keeps the fixed
     // stride and saves the memset)
@@ -792,9 +842,10 @@ static int Classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, con
     }
     mark(3);
     if (rc == hipSuccess && run[3])
-        rc = LaunchMemcacheClassify(B, e->mt, sel_m, sel_h, cnt ? cnt + L7_KAFKA_CLASSES : nullptr, !partitioned, s);
+        rc = LaunchMemcacheClassify(B, mt, sel_m, sel_h, cnt ? cnt + L7_KAFKA_CLASSES : nullptr, !partitioned, big_lanes,
+                                    s);
     // r2d2 (proxylib's example line protocol): one lane per request over the whole batch
-    if (rc == hipSuccess && e->has_r2) rc = LaunchR2d2Classify(B, e->rt, !partitioned, s);
+    if (rc == hipSuccess && e->has_r2) rc = LaunchR2d2Classify(B, rt, !partitioned, big_lanes, s);
     // cassandra (proxylib): the batch's USE requests, then one lane per request
     if (rc == hipSuccess && e->has_cs) {
         const size_t need = CassandraScratchBytes(n);
@@ -809,7 +860,7 @@ static int Classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, con
             if (rc == hipSuccess) rc = hipMalloc(&S->d_use, need);
             if (rc == hipSuccess) S->use_cap = need;
         }
-        if (rc == hipSuccess) rc = LaunchCassandraClassify(B, e->ct, S->d_use, S->use_cap, !partitioned, s);
+        if (rc == hipSuccess) rc = LaunchCassandraClassify(B, ct, S->d_use, S->use_cap, !partitioned, big_lanes, s);
     }
     mark(4);
     // proxy statistics (accumulated on the device until read)
@@ -1197,11 +1248,15 @@ int l7g_debug_regex_nfa(const char *pat, size_t patlen, int anchored, const uint
     auto ast = re::Parse(std::string(pat, patlen), &m);
     if (!ast) { set_err(err, errlen, m); return -1; }
     re::BitNfa n;
-    if (!re::BuildBitNfa({ast.get(), anchored != 0}, kNfaMaxWords * 64, &n, &m)) { set_err(err, errlen, m); return -1; }
+    if (!re::BuildBitNfa({ast.get(), anchored != 0}, kNfaMaxPositions, &n, &m, kNfaMaxWords)) {
+        set_err(err, errlen, m);
+        return -1;
+    }
     std::vector<uint8_t> pool;
     const uint64_t off = AppendDevNfa(n, &pool, &m);
     if (off == ~0ull) { set_err(err, errlen, m); return -1; }
-    return nfa_run(pool.data(), off, s, (uint32_t)slen) ? 1 : 0;
+    std::vector<uint64_t> scratch(2 * (size_t)n.W);  // (a large NFA's state sets)
+    return nfa_run(pool.data(), off, s, (uint32_t)slen, scratch.data()) ? 1 : 0;
 }
 
 }  // extern "C"

@@ -156,7 +156,20 @@ L7_HD inline uint32_t l7_name_hash(uint32_t w0, uint32_t w1, uint32_t w2, uint32
 // bytes from the pool start.  t_off: the follow sets tabulated per condition
 // class k, per 8-position chunk j of the state and per value v of that chunk:
 // u64[K][8W][256][W] (T[k][j][v] = OR of Follow_k(8j + b) for the bits b of v).
-constexpr int kNfaMaxWords = 16;  // <= 1024 positions
+constexpr int kNfaMaxWords = 16;  // dense tables, state in registers: <= 1024 positions
+// Past that, sparse rows and the state sets in per-lane global scratch (regex/
+// nfa_walk.h): Go 1.10 caps each repeat at 1000 and nested repeats at a
+// product of 1000 (regexp/syntax repeatIsValid), so a pattern needs about
+// 1000 positions per rune class it writes; this bound is the pattern's size.
+constexpr int kNfaMaxPositions = 1 << 20;
+// Large NFAs (W > kNfaMaxWords) keep their follow sets as sparse rows
+// (re_dfa.h BitNfa): DevNfa::t_off then points at this.
+struct DevNfaSparse {      // 32 B
+    uint64_t row_of_off;   // u32[K][m]: each position's row
+    uint64_t row_ptr_off;  // u32[rows + 1]: each row's first pair
+    uint64_t pair_w_off;   // u32[pairs]: word index
+    uint64_t pair_m_off;   // u64[pairs]: mask
+};
 struct DevNfa {            // 128 B
     uint32_t m, W, K, nivl;
     uint64_t t_off;
@@ -190,6 +203,8 @@ struct HttpTables {
     int32_t hot_ruleset;   // rule set whose image is staged in LDS (-1: none)
     const uint8_t *nfa_pool;   // DevNfa pool (null: no rule set has NFA matchers)
     uint64_t *nfa_bits;        // per request: bit k = NFA matcher k of its rule set accepted
+    uint64_t *nfa_scratch;     // large NFAs: nfa_lane_words per lane of the launch (null: none in the pool)
+    uint32_t nfa_lane_words;
 };
 
 // ---------------- Kafka ----------------
@@ -301,6 +316,8 @@ struct McTables {
     uint32_t images_len;       // bytes of all images (staged in LDS when they fit)
     const uint8_t *nfa_pool;   // DevNfa pool (null: no keyRegex on the NFA fallback)
     uint32_t max_chunks;       // most 64-rule chunks of any rule set (1: the one-chunk kernel)
+    uint32_t nfa_lane_words;   // large NFAs: scratch words per lane of the launch
+    uint64_t *nfa_scratch;     // (null: none in the pool)
 };
 
 // ---------------- r2d2 ----------------
@@ -326,8 +343,9 @@ struct R2Tables {
     const DevRuleset *rulesets;
     const uint8_t *images;
     uint32_t nrulesets;
-    uint32_t pad;
+    uint32_t nfa_lane_words;   // large NFAs: scratch words per lane of the launch
     const uint8_t *nfa_pool;
+    uint64_t *nfa_scratch;     // (null: none in the pool)
 };
 
 // ---------------- cassandra ----------------
@@ -359,7 +377,15 @@ struct CassTables {
     uint32_t nlower;           // (rune, lower) pairs of unicode.ToLower
     const uint8_t *nfa_pool;
     const uint32_t *lower;
+    uint64_t *nfa_scratch;     // large NFAs: nfa_lane_words per lane of the launch (null: none in the pool)
+    uint32_t nfa_lane_words;
 };
+#if defined(__HIPCC__)
+// A lane's large-NFA scratch (2 W words), by its index in the launch
+__device__ __forceinline__ uint64_t *l7_nfa_lane_scratch(uint64_t *base, uint32_t words) {
+    return base ? base + (size_t)(blockIdx.x * blockDim.x + threadIdx.x) * words : nullptr;
+}
+#endif
 
 // FNV-1a over lower-cased ASCII (header names are tchar, i.e. ASCII)
 static inline uint32_t l7_fnv_step(uint32_t h, uint8_t c) {

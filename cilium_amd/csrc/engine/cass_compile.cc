@@ -115,10 +115,22 @@ int CassCompiler::Compile(const std::vector<const CassRule *> &rules, uint8_t te
         }
         if (it != nfa_cache_.end()) { nfas.emplace_back(q, it->second); continue; }
         re::DFA d;
-        std::string e2;
-        if (!re::BuildDFA({{r.table_re.get(), false}}, max_single_dfa_states, &d, &e2)) {
-            *err = "cassandra query_table regex too complex for the device (" + e + "): " + r.table_src;
-            return -1;
+        std::string e2, e3;
+        // the large NFA (sparse rows, state sets in scratch) when one large DFA does not fit
+        re::BitNfa nf;
+        const bool big = re::BuildBitNfa({r.table_re.get(), false}, kNfaMaxPositions, &nf, &e3, kNfaMaxWords);
+        if (!re::BuildDFA({{r.table_re.get(), false}},
+                          big ? LargeNfaDfaBudget(nf.m, max_single_dfa_states) : max_single_dfa_states, &d, &e2)) {
+            if (!big) {
+                *err = "cassandra query_table regex too complex for the device (" + e3 + "): " + r.table_src;
+                return -1;
+            }
+            const uint64_t off = AppendDevNfa(nf, &img_.nfa_pool, err);
+            if (off == ~0ull) return -1;
+            it = nfa_cache_.emplace(r.table_src, off).first;
+            img_.nfas++;
+            nfas.emplace_back(q, it->second);
+            continue;
         }
         parts.push_back({q});
         dfas.push_back(std::move(d));

@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "../device_tables.h"
+#include "nfa_pool.h"
 #include "../policy/policy.h"
 #include "serial.h"
 
@@ -24,6 +25,8 @@ struct CassImage {
 
 class CassCompiler {
 public:
+    // the largest state set (u64 words) among its NFAs (large ones: > kNfaMaxWords)
+    uint32_t nfa_max_words() const { return NfaPoolMaxWords(img_.nfa_pool, nfa_cache_); }
     explicit CassCompiler(const PolicySet *ps);
     // remote = the connection's source identity (connection.go:176-179)
     int RulesetFor(int policy, bool ingress, uint32_t port, uint64_t remote, std::string *err);

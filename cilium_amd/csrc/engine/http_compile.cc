@@ -398,13 +398,24 @@ int HttpCompiler::Compile(const std::vector<const HttpRule *> &rules, uint8_t te
                 nfas.push_back({slot, it->second, p, {}});
                 continue;
             }
-            // too many positions for the NFA: one large DFA if it fits
+            // too many positions for the register NFA: one large DFA if it fits,
+            // else the large NFA (sparse rows, state sets in scratch)
             re::DFA d;
-            std::string e2;
-            if (!re::BuildDFA({{asts[p], true}}, max_single_dfa_states, &d, &e2)) {
-                *err = "regex too complex for the device (" + e + "; DFA over " +
-                       std::to_string(max_single_dfa_states) + " states): " + pats[p].value;
-                return -1;
+            std::string e2, e3;
+            re::BitNfa n;
+            const bool big = re::BuildBitNfa({asts[p], true}, kNfaMaxPositions, &n, &e3, kNfaMaxWords);
+            if (!re::BuildDFA({{asts[p], true}}, big ? LargeNfaDfaBudget(n.m, max_single_dfa_states) : max_single_dfa_states,
+                              &d, &e2)) {
+                if (!big) {
+                    *err = "regex too complex for the device (" + e3 + "): " + pats[p].value;
+                    return -1;
+                }
+                const uint64_t off = AppendDevNfa(n, &img_.nfa_pool, err);
+                if (off == ~0ull) return -1;
+                it = nfa_cache_.emplace(pats[p].value, off).first;
+                img_.nfas++;
+                nfas.push_back({slot, it->second, p, {}});
+                continue;
             }
             groups.push_back({p});
             dfas.push_back(std::move(d));

@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "../device_tables.h"
+#include "nfa_pool.h"
 #include "../policy/policy.h"
 #include "serial.h"
 
@@ -31,6 +32,8 @@ struct HttpImage {
 
 class HttpCompiler {
 public:
+    // the largest state set (u64 words) among its NFAs (large ones: > kNfaMaxWords)
+    uint32_t nfa_max_words() const { return NfaPoolMaxWords(img_.nfa_pool, nfa_cache_); }
     explicit HttpCompiler(const PolicySet *ps) : ps_(ps) {}
     // Returns the rule set index for a connection, compiling it on first use.
     // policy < 0: unknown policy (NetworkPolicyMap::Allowed => deny).

@@ -145,11 +145,22 @@ int McCompiler::Compile(const std::vector<const McRule *> &rules, uint8_t termin
             continue;
         }
         re::DFA d;
-        std::string e2;
-        if (!re::BuildDFA({{pats[p].ast, pats[p].anchored}}, max_single_dfa_states, &d, &e2)) {
-            *err = "memcache key pattern too complex for the device (" + e + "; DFA over " +
-                   std::to_string(max_single_dfa_states) + " states): " + pats[p].src;
-            return -1;
+        std::string e2, e3;
+        // the large NFA (sparse rows, state sets in scratch) when one large DFA does not fit
+        re::BitNfa nf;
+        const bool big = !pats[p].anchored && re::BuildBitNfa({pats[p].ast, false}, kNfaMaxPositions, &nf, &e3, kNfaMaxWords);
+        if (!re::BuildDFA({{pats[p].ast, pats[p].anchored}},
+                          big ? LargeNfaDfaBudget(nf.m, max_single_dfa_states) : max_single_dfa_states, &d, &e2)) {
+            if (!big) {
+                *err = "memcache key pattern too complex for the device (" + (e3.empty() ? e2 : e3) + "): " + pats[p].src;
+                return -1;
+            }
+            const uint64_t off = AppendDevNfa(nf, &img_.nfa_pool, err);
+            if (off == ~0ull) return -1;
+            it = nfa_cache_.emplace(pats[p].src, off).first;
+            img_.nfas++;
+            nfas.emplace_back(p, it->second);
+            continue;
         }
         parts.push_back({p});
         dfas.push_back(std::move(d));

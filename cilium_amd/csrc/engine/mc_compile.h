@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "../device_tables.h"
+#include "nfa_pool.h"
 #include "../policy/policy.h"
 #include "serial.h"
 
@@ -31,6 +32,8 @@ struct McImage {
 
 class McCompiler {
 public:
+    // the largest state set (u64 words) among its NFAs (large ones: > kNfaMaxWords)
+    uint32_t nfa_max_words() const { return NfaPoolMaxWords(img_.nfa_pool, nfa_cache_); }
     explicit McCompiler(const PolicySet *ps) : ps_(ps) {}
     // remote = the connection's source identity (proxylib/proxylib/connection.go:176-179)
     int RulesetFor(int policy, bool ingress, uint32_t port, uint64_t remote, std::string *err);

@@ -1,6 +1,7 @@
 // Device layout of bit-parallel NFAs (product code): BitNfa (re_dfa.h) ->
 // DevNfa + its tables appended to a pool (device_tables.h).
 #pragma once
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -13,13 +14,19 @@ namespace l7 {
 // Appends n's device tables to pool (16-byte aligned); returns the DevNfa
 // offset, or ~0ull with *err when the pool would pass 4 GiB.
 inline uint64_t AppendDevNfa(const re::BitNfa &n, std::vector<uint8_t> *pool, std::string *err) {
-    const size_t W = (size_t)n.W, K = (size_t)n.K;
+    const size_t W = (size_t)n.W, K = (size_t)n.K, m = (size_t)n.m;
     auto align = [&](size_t bytes) {
         size_t off = (pool->size() + 15) & ~(size_t)15;
         pool->resize(off + bytes, 0);
         return off;
     };
-    const size_t t_bytes = K * 8 * W * 256 * W * 8, niv = n.ivl_lo.size();
+    if (n.sparse != (W > (size_t)kNfaMaxWords)) {
+        *err = "NFA table form does not match its size";
+        return ~0ull;
+    }
+    const size_t t_bytes = n.sparse ? sizeof(DevNfaSparse) + K * m * 4 + n.row_ptr.size() * 4 + n.pair_w.size() * 12 + 64
+                                    : K * 8 * W * 256 * W * 8;
+    const size_t niv = n.ivl_lo.size();
     if (pool->size() + t_bytes + niv * (W * 8 + 4) + K * W * 8 + 512 > (1ull << 32)) {
         *err = "NFA tables exceed 4 GiB";
         return ~0ull;
@@ -31,8 +38,20 @@ inline uint64_t AppendDevNfa(const re::BitNfa &n, std::vector<uint8_t> *pool, st
     d.K = (uint32_t)K;
     d.nivl = (uint32_t)niv;
     memcpy(d.condmap, n.condmap, sizeof d.condmap);
-    d.t_off = align(t_bytes);
-    {
+    if (n.sparse) {
+        d.t_off = align(sizeof(DevNfaSparse));
+        DevNfaSparse sp{};
+        sp.row_of_off = align(K * m * 4);
+        memcpy(pool->data() + sp.row_of_off, n.row_of.data(), K * m * 4);
+        sp.row_ptr_off = align(n.row_ptr.size() * 4);
+        memcpy(pool->data() + sp.row_ptr_off, n.row_ptr.data(), n.row_ptr.size() * 4);
+        sp.pair_w_off = align(n.pair_w.size() * 4);
+        memcpy(pool->data() + sp.pair_w_off, n.pair_w.data(), n.pair_w.size() * 4);
+        sp.pair_m_off = align(n.pair_m.size() * 8);
+        memcpy(pool->data() + sp.pair_m_off, n.pair_m.data(), n.pair_m.size() * 8);
+        memcpy(pool->data() + d.t_off, &sp, sizeof sp);
+    } else {
+        d.t_off = align(t_bytes);
         uint64_t *T = (uint64_t *)(pool->data() + d.t_off);
         for (size_t k = 0; k < K; k++)
             for (size_t j = 0; j < 8 * W; j++) {
@@ -63,6 +82,22 @@ inline uint64_t AppendDevNfa(const re::BitNfa &n, std::vector<uint8_t> *pool, st
     memcpy(pool->data() + doff, &d, sizeof d);
     align(16);  // aligned tail: 16-byte reads of the last table stay inside
     return doff;
+}
+
+// A pattern past the register NFA (m > kNfaMaxWords * 64 positions) is tried
+// as one large DFA first (faster to walk), but the subset construction costs
+// about states x positions: its state budget shrinks as the NFA grows, so that
+// a pattern whose DFA explodes (.{1000}x.{1000} unanchored) falls through to
+// the large NFA in well under a second instead of minutes.
+inline int LargeNfaDfaBudget(int m, int cap) { return std::min(cap, std::max(2048, (8 << 20) / std::max(m, 1))); }
+
+// The largest state set (u64 words) among the pool's NFAs (offsets: a
+// compiler's pattern -> DevNfa offset map).
+template <class Map>
+inline uint32_t NfaPoolMaxWords(const std::vector<uint8_t> &pool, const Map &offsets) {
+    uint32_t w = 0;
+    for (const auto &kv : offsets) w = std::max(w, ((const DevNfa *)(pool.data() + kv.second))->W);
+    return w;
 }
 
 }  // namespace l7

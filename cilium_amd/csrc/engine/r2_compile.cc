@@ -103,10 +103,22 @@ int R2Compiler::Compile(const std::vector<const R2Rule *> &rules, uint8_t termin
         }
         if (it != nfa_cache_.end()) { nfas.emplace_back(q, it->second); continue; }
         re::DFA d;
-        std::string e2;
-        if (!re::BuildDFA({{r.file_re.get(), false}}, max_single_dfa_states, &d, &e2)) {
-            *err = "r2d2 file regex too complex for the device (" + e + "): " + r.file_src;
-            return -1;
+        std::string e2, e3;
+        // the large NFA (sparse rows, state sets in scratch) when one large DFA does not fit
+        re::BitNfa nf;
+        const bool big = re::BuildBitNfa({r.file_re.get(), false}, kNfaMaxPositions, &nf, &e3, kNfaMaxWords);
+        if (!re::BuildDFA({{r.file_re.get(), false}}, big ? LargeNfaDfaBudget(nf.m, max_single_dfa_states) : max_single_dfa_states,
+                          &d, &e2)) {
+            if (!big) {
+                *err = "r2d2 file regex too complex for the device (" + e3 + "): " + r.file_src;
+                return -1;
+            }
+            const uint64_t off = AppendDevNfa(nf, &img_.nfa_pool, err);
+            if (off == ~0ull) return -1;
+            it = nfa_cache_.emplace(r.file_src, off).first;
+            img_.nfas++;
+            nfas.emplace_back(q, it->second);
+            continue;
         }
         parts.push_back({q});
         dfas.push_back(std::move(d));

@@ -142,11 +142,8 @@ __global__ __launch_bounds__(kBlock) void cassandra_use_kernel(Batch B, CassTabl
     if (Q.status == CQ_OK && Q.is_use) keys[i] = (uint64_t)ci << 32 | i;
 }
 
-__global__ __launch_bounds__(kBlock) void cassandra_classify_kernel(Batch B, CassTables T,
-                                                                    const uint64_t *__restrict__ use_keys,
-                                                                    uint32_t answer_other) {
-    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    if (i >= B.n) return;
+__device__ __forceinline__ void cassandra_one(const Batch &B, const CassTables &T, const uint64_t *__restrict__ use_keys,
+                                              uint32_t answer_other, uint32_t i, uint64_t *scratch) {
     const uint32_t ci = B.conn_ids[i];
     const DevConn conn = ci < B.nconns ? B.conns[ci] : DevConn{-1, PROTO_NONE, 0, 0xFFFF};
     if (conn.proto != PROTO_CASSANDRA || conn.ruleset < 0 || (uint32_t)conn.ruleset >= T.nrulesets) {
@@ -238,7 +235,7 @@ __global__ __launch_bounds__(kBlock) void cassandra_classify_kernel(Batch B, Cas
                 for (uint32_t k = 0; k < H->nnfa; k++) {
                     const DevNfaRef r = refs[k];
                     NfaSink S{T.nfa_pool, r.nfa, {}};
-                    nfa_begin(S.R);
+                    nfa_begin(S.R, scratch);
                     cass_seg3(Q, q, ks, K.ts, K.te, K.fc, T.lower, T.nlower, S);
                     if (!nfa_end(T.nfa_pool, r.nfa, S.R)) continue;
                     const uint64_t *own = (const uint64_t *)(img + r.mask_off);
@@ -266,6 +263,15 @@ __global__ __launch_bounds__(kBlock) void cassandra_classify_kernel(Batch B, Cas
     B.consumed[i] = consumed;
 }
 
+// grid-stride: a launch with large NFAs has as many lanes as it has scratch for
+__global__ __launch_bounds__(kBlock) void cassandra_classify_kernel(Batch B, CassTables T,
+                                                                    const uint64_t *__restrict__ use_keys,
+                                                                    uint32_t answer_other) {
+    uint64_t *scratch = l7_nfa_lane_scratch(T.nfa_scratch, T.nfa_lane_words);
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < B.n; i += gridDim.x * kBlock)
+        cassandra_one(B, T, use_keys, answer_other, i, scratch);
+}
+
 // Scratch bytes LaunchCassandraClassify needs for a batch of n requests.
 size_t CassandraScratchBytes(uint32_t n) {
     size_t temp = 0;
@@ -277,8 +283,9 @@ size_t CassandraScratchBytes(uint32_t n) {
 }
 
 // scratch: CassandraScratchBytes(B.n) bytes (256-byte aligned)
+// nfa_lanes: lanes T.nfa_scratch holds (when it is set)
 hipError_t LaunchCassandraClassify(const Batch &B, const CassTables &T, void *scratch, size_t scratch_bytes,
-                                   bool answer_other, hipStream_t stream) {
+                                   bool answer_other, uint32_t nfa_lanes, hipStream_t stream) {
     if (B.n == 0) return hipSuccess;
     const size_t kb = ((size_t)B.n * sizeof(uint64_t) + 256 + 255) & ~(size_t)255;
     uint64_t *keys = (uint64_t *)scratch;
@@ -293,7 +300,9 @@ hipError_t LaunchCassandraClassify(const Batch &B, const CassTables &T, void *sc
     // connection ids are < 2^32 and request indices < 2^32: all 64 bits
     rc = hipcub::DeviceRadixSort::SortKeys(temp, temp_bytes, keys, sorted, (int)B.n, 0, 64, stream);
     if (rc != hipSuccess) return rc;
-    hipLaunchKernelGGL(cassandra_classify_kernel, grid, dim3(kBlock), 0, stream, B, T, sorted, answer_other ? 1u : 0u);
+    dim3 cgrid = grid;
+    if (T.nfa_scratch) cgrid.x = max(1u, min(cgrid.x, nfa_lanes / kBlock));
+    hipLaunchKernelGGL(cassandra_classify_kernel, cgrid, dim3(kBlock), 0, stream, B, T, sorted, answer_other ? 1u : 0u);
     return hipGetLastError();
 }
 

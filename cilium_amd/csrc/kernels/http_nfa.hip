@@ -74,11 +74,7 @@ __device__ bool value_span(const uint8_t *r, uint32_t len, uint32_t slot, const 
     return false;
 }
 
-}  // namespace
-
-__global__ __launch_bounds__(kNfaBlock) void http_nfa_kernel(Batch B, HttpTables T) {
-    const uint32_t i = blockIdx.x * kNfaBlock + threadIdx.x;
-    if (i >= B.n) return;
+__device__ __forceinline__ void nfa_request(const Batch &B, const HttpTables &T, uint32_t i, uint64_t *scratch) {
     const uint32_t ci = B.conn_ids[i];
     if (ci >= B.nconns) return;
     const DevConn conn = B.conns[ci];
@@ -96,16 +92,28 @@ __global__ __launch_bounds__(kNfaBlock) void http_nfa_kernel(Batch B, HttpTables
         for (uint32_t k = 0; k < nnfa; k++) {
             const DevNfaRef ref = refs[k];
             uint32_t vo, vl;
-            if (value_span(r, len, ref.slot, img, &vo, &vl) && nfa_run(T.nfa_pool, ref.nfa, r + vo, vl))
+            if (value_span(r, len, ref.slot, img, &vo, &vl) && nfa_run(T.nfa_pool, ref.nfa, r + vo, vl, scratch))
                 bits |= 1ull << k;
         }
     }
     T.nfa_bits[i] = bits;
 }
 
-hipError_t LaunchHttpNfa(const Batch &B, const HttpTables &T, hipStream_t stream) {
+}  // namespace
+
+// grid-stride: a launch with large NFAs has as many lanes as it has scratch for
+__global__ __launch_bounds__(kNfaBlock) void http_nfa_kernel(Batch B, HttpTables T) {
+    uint64_t *scratch = l7_nfa_lane_scratch(T.nfa_scratch, T.nfa_lane_words);
+    for (uint32_t i = blockIdx.x * kNfaBlock + threadIdx.x; i < B.n; i += gridDim.x * kNfaBlock)
+        nfa_request(B, T, i, scratch);
+}
+
+// scratch_lanes: lanes T.nfa_scratch holds (when it is set)
+hipError_t LaunchHttpNfa(const Batch &B, const HttpTables &T, uint32_t scratch_lanes, hipStream_t stream) {
     if (B.n == 0) return hipSuccess;
-    hipLaunchKernelGGL(http_nfa_kernel, dim3((B.n + kNfaBlock - 1) / kNfaBlock), dim3(kNfaBlock), 0, stream, B, T);
+    uint32_t blocks = (B.n + kNfaBlock - 1) / kNfaBlock;
+    if (T.nfa_scratch) blocks = max(1u, min(blocks, scratch_lanes / kNfaBlock));
+    hipLaunchKernelGGL(http_nfa_kernel, dim3(blocks), dim3(kNfaBlock), 0, stream, B, T);
     return hipGetLastError();
 }
 

@@ -98,6 +98,7 @@ struct Image {
     uint32_t d0, dn;  // DFAs [d0, d0+dn) are walked in the current pass over the request
     uint32_t nnfa;    // keyRegex matchers on the NFA fallback (evaluated in the first pass)
     const uint8_t *nfa_pool;
+    uint64_t *nfa_scratch;  // this lane's large-NFA state sets (null: no large NFA in the pool)
 };
 
 __device__ __forceinline__ const uint64_t *u64at(const Image &I, uint32_t off) { return (const uint64_t *)(I.p + off); }
@@ -142,7 +143,7 @@ __device__ __forceinline__ void keys_nfa(const Image &I, Keys<kCh> &K, const uin
     const DevNfaRef *refs = (const DevNfaRef *)(I.p + hdr32(I, MC_OFF(nfa_off)));
     for (uint32_t k = 0; k < I.nnfa; k++) {
         const DevNfaRef ref = refs[k];
-        if (nfa_run(I.nfa_pool, ref.nfa, b + k0, k1 - k0)) continue;
+        if (nfa_run(I.nfa_pool, ref.nfa, b + k0, k1 - k0, I.nfa_scratch)) continue;
         const uint64_t *own = u64at(I, ref.mask_off);
 #pragma unroll
         for (int c = 0; c < kCh; c++)
@@ -405,6 +406,7 @@ __device__ __forceinline__ void mc_loop(Batch B, McTables T, const uint8_t *imag
         }
         I.nnfa = hdr32(I, MC_OFF(nnfa));
         I.nfa_pool = T.nfa_pool;
+        I.nfa_scratch = kNfa ? l7_nfa_lane_scratch(T.nfa_scratch, T.nfa_lane_words) : nullptr;
         const uint64_t off = B.offs[idx];
         const uint32_t len = B.lens[idx];
         const uint8_t *b = B.arena + off;
@@ -547,11 +549,14 @@ __global__ __launch_bounds__(kBlock) void memcache_classify_nfa_kernel(Batch B, 
     mc_classify<true, kMcMaxChunks>(B, T, sel, sel2, sel_count, answer_other);
 }
 
+// scratch_lanes: lanes T.nfa_scratch holds (when it is set)
 hipError_t LaunchMemcacheClassify(const Batch &B, const McTables &T, const uint32_t *sel, const uint32_t *sel2,
-                                  const uint32_t *sel_count, bool answer_other, hipStream_t stream) {
+                                  const uint32_t *sel_count, bool answer_other, uint32_t scratch_lanes,
+                                  hipStream_t stream) {
     if (B.n == 0) return hipSuccess;
     uint32_t blocks = (B.n + kBlock - 1) / kBlock;
     if (blocks > 8192) blocks = 8192;
+    if (T.nfa_scratch) blocks = max(1u, min(blocks, scratch_lanes / kBlock));  // (grid-stride loop)
     const size_t lds = T.images_len && T.images_len <= kMcLdsImages ? ((T.images_len + 15) & ~15u) : 0;
     if (T.nfa_pool)
         hipLaunchKernelGGL(memcache_classify_nfa_kernel, dim3(blocks), dim3(kBlock), lds, stream, B, T, sel, sel2, sel_count,

@@ -41,9 +41,8 @@ __device__ __forceinline__ uint32_t rd(Win &r, const uint8_t *p) {
 
 }  // namespace
 
-__global__ __launch_bounds__(kBlock) void r2d2_classify_kernel(Batch B, R2Tables T, uint32_t answer_other) {
-    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    if (i >= B.n) return;
+__device__ __forceinline__ void r2d2_one(const Batch &B, const R2Tables &T, uint32_t answer_other, uint32_t i,
+                                         uint64_t *scratch) {
     const uint32_t ci = B.conn_ids[i];
     const DevConn conn = ci < B.nconns ? B.conns[ci] : DevConn{-1, PROTO_NONE, 0, 0xFFFF};
     if (conn.proto != PROTO_R2D2 || conn.ruleset < 0 || (uint32_t)conn.ruleset >= T.nrulesets) {
@@ -110,7 +109,7 @@ __global__ __launch_bounds__(kBlock) void r2d2_classify_kernel(Batch B, R2Tables
             const DevNfaRef *refs = (const DevNfaRef *)(img + H->nfa_off);
             for (uint32_t k = 0; k < H->nnfa; k++) {
                 const DevNfaRef r = refs[k];
-                if (!nfa_run(T.nfa_pool, r.nfa, b + f0, f1 - f0)) continue;
+                if (!nfa_run(T.nfa_pool, r.nfa, b + f0, f1 - f0, scratch)) continue;
                 const uint64_t *own = (const uint64_t *)(img + r.mask_off);
 #pragma unroll
                 for (int c = 0; c < kR2MaxChunks; c++)
@@ -137,10 +136,20 @@ __global__ __launch_bounds__(kBlock) void r2d2_classify_kernel(Batch B, R2Tables
     B.consumed[i] = consumed;
 }
 
-hipError_t LaunchR2d2Classify(const Batch &B, const R2Tables &T, bool answer_other, hipStream_t stream) {
+// grid-stride: a launch with large NFAs has as many lanes as it has scratch for
+__global__ __launch_bounds__(kBlock) void r2d2_classify_kernel(Batch B, R2Tables T, uint32_t answer_other) {
+    uint64_t *scratch = l7_nfa_lane_scratch(T.nfa_scratch, T.nfa_lane_words);
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < B.n; i += gridDim.x * kBlock)
+        r2d2_one(B, T, answer_other, i, scratch);
+}
+
+// scratch_lanes: lanes T.nfa_scratch holds (when it is set)
+hipError_t LaunchR2d2Classify(const Batch &B, const R2Tables &T, bool answer_other, uint32_t scratch_lanes,
+                              hipStream_t stream) {
     if (B.n == 0) return hipSuccess;
-    hipLaunchKernelGGL(r2d2_classify_kernel, dim3((B.n + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, B, T,
-                       answer_other ? 1u : 0u);
+    uint32_t blocks = (B.n + kBlock - 1) / kBlock;
+    if (T.nfa_scratch) blocks = max(1u, min(blocks, scratch_lanes / kBlock));
+    hipLaunchKernelGGL(r2d2_classify_kernel, dim3(blocks), dim3(kBlock), 0, stream, B, T, answer_other ? 1u : 0u);
     return hipGetLastError();
 }
 

@@ -62,6 +62,78 @@ L7_HD inline uint32_t nfa_decode(const uint8_t *s, uint32_t i, uint32_t n, uint3
     return r;
 }
 
+// Rune interval (the ASCII table, else the last interval starting at or below r)
+L7_HD inline uint32_t nfa_interval(const uint8_t *pool, const DevNfa *d, uint32_t r) {
+    if (r < 128) return ((const uint16_t *)(pool + d->ascii_off))[r];
+    const uint32_t *ivl = (const uint32_t *)(pool + d->ivl_off);
+    uint32_t lo = 0, hi = d->nivl;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (ivl[mid] <= r) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// ---- large NFAs (W > kNfaMaxWords: sparse rows, device_tables.h
+// DevNfaSparse).  The two state sets live in the caller's scratch (2 W words
+// per lane); only the words [lo, hi] of the current set are live, and the
+// next set is cleared lazily over the words its rows touch.
+L7_HD inline bool nfa_big_step(const uint8_t *pool, const DevNfa *d, const uint64_t *S, uint64_t *N, uint32_t &lo,
+                               uint32_t &hi, uint32_t k, uint32_t iv) {
+    const DevNfaSparse *sp = (const DevNfaSparse *)(pool + d->t_off);
+    const uint32_t *row_of = (const uint32_t *)(pool + sp->row_of_off) + (size_t)k * d->m;
+    const uint32_t *row_ptr = (const uint32_t *)(pool + sp->row_ptr_off);
+    const uint32_t *pw = (const uint32_t *)(pool + sp->pair_w_off);
+    const uint64_t *pm = (const uint64_t *)(pool + sp->pair_m_off);
+    uint32_t nlo = 1, nhi = 0;  // (empty)
+    for (uint32_t w = lo; w <= hi; w++) {
+        uint64_t x = S[w];
+        while (x) {
+            const uint32_t p = w * 64 + (uint32_t)__builtin_ctzll(x);
+            x &= x - 1;
+            const uint32_t row = row_of[p];
+            for (uint32_t e = row_ptr[row], ee = row_ptr[row + 1]; e < ee; e++) {
+                const uint32_t u = pw[e];
+                if (nlo > nhi) {
+                    N[u] = 0;
+                    nlo = nhi = u;
+                } else if (u < nlo) {
+                    for (uint32_t z = u; z < nlo; z++) N[z] = 0;
+                    nlo = u;
+                } else if (u > nhi) {
+                    for (uint32_t z = nhi + 1; z <= u; z++) N[z] = 0;
+                    nhi = u;
+                }
+                N[u] |= pm[e];
+            }
+        }
+    }
+    if (nlo > nhi) return false;
+    const uint64_t *B = (const uint64_t *)(pool + d->b_off) + (size_t)iv * d->W;
+    uint32_t a = 1, b = 0;
+    for (uint32_t u = nlo; u <= nhi; u++) {
+        const uint64_t v = N[u] & B[u];
+        N[u] = v;
+        if (v) {
+            if (a > b) a = u;
+            b = u;
+        }
+    }
+    if (a > b) return false;
+    lo = a;
+    hi = b;
+    return true;
+}
+
+L7_HD inline bool nfa_big_accepts(const uint8_t *pool, const DevNfa *d, const uint64_t *S, uint32_t lo, uint32_t hi,
+                                  uint32_t k) {
+    const uint64_t *Acc = (const uint64_t *)(pool + d->acc_off) + (size_t)k * d->W;
+    uint64_t hit = 0;
+    for (uint32_t u = lo; u <= hi; u++) hit |= S[u] & Acc[u];
+    return hit != 0;
+}
+
 // Streaming walk (for text the caller produces rune by rune, e.g. the
 // lowered cassandra table name): nfa_begin, one nfa_step per rune (r, and c =
 // the first byte of its encoding, which the empty-width conditions look at),
@@ -71,18 +143,37 @@ struct NfaRun {
     uint64_t S[kNfaMaxWords];
     uint32_t prev;
     bool dead;
+    uint64_t *big;     // a large NFA's two state sets (2 W words of scratch; null: none given)
+    uint32_t cur, lo, hi;
 };
 
-L7_NFA_INL void nfa_begin(NfaRun &R) {
+// scratch: 2 W words when the NFA may be a large one (see nfa_run)
+L7_NFA_INL void nfa_begin(NfaRun &R, uint64_t *scratch = nullptr) {
 #pragma unroll
     for (int w = 0; w < kNfaMaxWords; w++) R.S[w] = w == 0 ? 1 : 0;  // the virtual start position
     R.prev = NP_START;
     R.dead = false;
+    R.big = scratch;
+    R.cur = 0;
+    R.lo = R.hi = 0;
+    if (scratch) scratch[0] = 1;
 }
 
 L7_NFA_INL void nfa_step(const uint8_t *pool, uint64_t off, NfaRun &R, uint32_t r, uint32_t c) {
     if (R.dead) return;
     const DevNfa *d = (const DevNfa *)(pool + off);
+    if (d->W > (uint32_t)kNfaMaxWords) {
+        if (!R.big) {  // (the launcher gives scratch whenever the pool holds a large NFA)
+            R.dead = true;
+            return;
+        }
+        uint64_t *S = R.big + (size_t)R.cur * d->W, *N = R.big + (size_t)(R.cur ^ 1) * d->W;
+        const uint32_t k = d->condmap[nfa_cond(R.prev, (int)c)];
+        R.dead = !nfa_big_step(pool, d, S, N, R.lo, R.hi, k, nfa_interval(pool, d, r));
+        R.cur ^= 1;
+        R.prev = (r == '\n' ? NP_NL : 0u) | (r < 128 && nfa_word_byte(r) ? NP_WORD : 0u);
+        return;
+    }
     const uint32_t W = d->W, nivl = d->nivl;
     const uint64_t *T = (const uint64_t *)(pool + d->t_off);
     const uint32_t *ivl = (const uint32_t *)(pool + d->ivl_off);
@@ -133,6 +224,8 @@ L7_NFA_INL bool nfa_end(const uint8_t *pool, uint64_t off, const NfaRun &R) {
     if (R.dead) return false;
     const DevNfa *d = (const DevNfa *)(pool + off);
     const uint32_t W = d->W;
+    if (W > (uint32_t)kNfaMaxWords)
+        return R.big && nfa_big_accepts(pool, d, R.big + (size_t)R.cur * W, R.lo, R.hi, d->condmap[nfa_cond(R.prev, -1)]);
     const uint64_t *Acc = (const uint64_t *)(pool + d->acc_off);
     const uint32_t k = d->condmap[nfa_cond(R.prev, -1)];
     uint64_t hit = 0;
@@ -142,9 +235,32 @@ L7_NFA_INL bool nfa_end(const uint8_t *pool, uint64_t off, const NfaRun &R) {
     return hit != 0;
 }
 
-// Run the NFA at pool + off over s[0, n); true = accepted.
-L7_HD inline bool nfa_run(const uint8_t *pool, uint64_t off, const uint8_t *s, uint32_t n) {
+// A large NFA over s[0, n) with its state sets in scratch (2 W words).
+L7_HD inline bool nfa_run_big(const uint8_t *pool, const DevNfa *d, const uint8_t *s, uint32_t n, uint64_t *scratch) {
+    uint64_t *S = scratch, *N = scratch + d->W;
+    S[0] = 1;  // the virtual start position
+    uint32_t lo = 0, hi = 0, prev = NP_START;
+    for (uint32_t i = 0; i < n;) {
+        const uint32_t c = s[i];
+        uint32_t width;
+        const uint32_t r = nfa_decode(s, i, n, &width);
+        if (!nfa_big_step(pool, d, S, N, lo, hi, d->condmap[nfa_cond(prev, (int)c)], nfa_interval(pool, d, r)))
+            return false;
+        uint64_t *t = S;
+        S = N;
+        N = t;
+        prev = (r == '\n' ? NP_NL : 0u) | (r < 128 && nfa_word_byte(r) ? NP_WORD : 0u);
+        i += width;
+    }
+    return nfa_big_accepts(pool, d, S, lo, hi, d->condmap[nfa_cond(prev, -1)]);
+}
+
+// Run the NFA at pool + off over s[0, n); true = accepted.  scratch: 2 W
+// words for a large NFA (W > kNfaMaxWords); the launchers give every lane its
+// own whenever the pool holds one.
+L7_HD inline bool nfa_run(const uint8_t *pool, uint64_t off, const uint8_t *s, uint32_t n, uint64_t *scratch = nullptr) {
     const DevNfa *d = (const DevNfa *)(pool + off);
+    if (d->W > (uint32_t)kNfaMaxWords) return scratch && nfa_run_big(pool, d, s, n, scratch);
     const uint32_t W = d->W, nivl = d->nivl;
     const uint64_t *T = (const uint64_t *)(pool + d->t_off);
     const uint32_t *ivl = (const uint32_t *)(pool + d->ivl_off);

@@ -475,7 +475,7 @@ bool BuildDFA(const std::vector<Pattern> &pats, int max_states, DFA *out, std::s
     return true;
 }
 
-bool BuildBitNfa(const Pattern &p, int max_positions, BitNfa *out, std::string *err) {
+bool BuildBitNfa(const Pattern &p, int max_positions, BitNfa *out, std::string *err, int dense_words) {
     Nfa nfa;
     nfa.rune_mode = true;
     RuneSet any;
@@ -544,24 +544,37 @@ bool BuildBitNfa(const Pattern &p, int max_positions, BitNfa *out, std::string *
     out->m = m;
     out->W = W;
     out->K = K;
-    out->follow.assign((size_t)K * m * W, 0);
+    out->sparse = W > dense_words;
+    if (out->sparse) {
+        out->row_of.assign((size_t)K * m, 0);
+        out->row_ptr.assign(1, 0);
+    } else {
+        out->follow.assign((size_t)K * m * W, 0);
+    }
     out->acc.assign((size_t)K * W, 0);
     std::vector<int> mark(ns, -1), stack;
+    std::vector<uint64_t> tmp(out->sparse ? W : 0);  // a sparse row being built
+    std::vector<uint32_t> touched;
     int epoch = 0;
     for (int k = 0; k < K; k++) {
         const uint8_t cond = cls_cond[k];
         std::vector<int> memo_to(ns, -1);  // target state -> position whose row is already computed
         for (int pp = 0; pp < m; pp++) {
-            uint64_t *row = &out->follow[((size_t)k * m + pp) * W];
             const int to = to_of[pp];
             if (memo_to[to] >= 0) {
-                const uint64_t *src = &out->follow[((size_t)k * m + memo_to[to]) * W];
-                std::copy(src, src + W, row);
-                if ((out->acc[(size_t)k * W + memo_to[to] / 64] >> (memo_to[to] % 64)) & 1)
+                const int src = memo_to[to];
+                if (out->sparse) {
+                    out->row_of[(size_t)k * m + pp] = out->row_of[(size_t)k * m + src];
+                } else {
+                    const uint64_t *sr = &out->follow[((size_t)k * m + src) * W];
+                    std::copy(sr, sr + W, &out->follow[((size_t)k * m + pp) * W]);
+                }
+                if ((out->acc[(size_t)k * W + src / 64] >> (src % 64)) & 1)
                     out->acc[(size_t)k * W + pp / 64] |= 1ull << (pp % 64);
                 continue;
             }
             memo_to[to] = pp;
+            uint64_t *row = out->sparse ? tmp.data() : &out->follow[((size_t)k * m + pp) * W];
             epoch++;
             bool accepts = false;
             stack.assign(1, to);
@@ -577,6 +590,7 @@ bool BuildBitNfa(const Pattern &p, int max_positions, BitNfa *out, std::string *
                 case K::Rune: {
                     if (st.acc >= 0) accepts = true;
                     const int e = pos_of[q];
+                    if (out->sparse && !row[e / 64]) touched.push_back((uint32_t)(e / 64));
                     row[e / 64] |= 1ull << (e % 64);
                     break;
                 }
@@ -584,6 +598,21 @@ bool BuildBitNfa(const Pattern &p, int max_positions, BitNfa *out, std::string *
                 }
             }
             if (accepts) out->acc[(size_t)k * W + pp / 64] |= 1ull << (pp % 64);
+            if (out->sparse) {  // the row's non-zero words, in word order
+                std::sort(touched.begin(), touched.end());
+                out->row_of[(size_t)k * m + pp] = (uint32_t)(out->row_ptr.size() - 1);
+                for (uint32_t w : touched) {
+                    out->pair_w.push_back(w);
+                    out->pair_m.push_back(row[w]);
+                    row[w] = 0;
+                }
+                touched.clear();
+                out->row_ptr.push_back((uint32_t)out->pair_w.size());
+                if (out->pair_w.size() > (1u << 27)) {
+                    if (err) *err = "NFA follow tables exceed 2^27 entries";
+                    return false;
+                }
+            }
         }
     }
     // ---- rune intervals on which every position's class is constant

@@ -57,18 +57,28 @@ bool BuildDFA(const std::vector<Pattern> &pats, int max_states, DFA *out, std::s
 // where Follow_k(p) is every position reachable from p through the epsilon
 // closure under k, and B[iv] the positions whose class holds the rune
 // interval iv.  The input is accepted iff S & Acc_k(end) != 0.
+//
+// A small automaton (W <= dense_words) keeps Follow_k as dense rows; a large
+// one (up to max_positions, e.g. .{1000}x.{1000}: 2,003 positions) as sparse
+// rows: Follow_k(p) = the (word, mask) pairs of its non-zero words, shared by
+// the positions whose epsilon closures coincide.
 struct BitNfa {
     int m = 0;                    // positions (incl. the virtual start)
     int W = 0;                    // u64 words per state set
     int K = 0;                    // empty-width condition classes
     uint8_t condmap[64] = {0};    // NC_* condition bits (nfa_walk.h) -> class
-    std::vector<uint64_t> follow; // [K][m][W]
+    std::vector<uint64_t> follow; // dense: [K][m][W]
+    bool sparse = false;
+    std::vector<uint32_t> row_of;   // sparse: [K][m] -> row
+    std::vector<uint32_t> row_ptr;  // sparse: [rows + 1] -> first pair
+    std::vector<uint32_t> pair_w;   // sparse: word of each pair
+    std::vector<uint64_t> pair_m;   // sparse: mask of each pair
     std::vector<uint64_t> acc;    // [K][W]
     std::vector<int32_t> ivl_lo;  // rune intervals [ivl_lo[i], ivl_lo[i+1]) (last ends at 0x110000)
     std::vector<uint64_t> b;      // [interval][W]
 };
 // false (and *err) when the pattern needs more than max_positions positions.
-bool BuildBitNfa(const Pattern &p, int max_positions, BitNfa *out, std::string *err);
+bool BuildBitNfa(const Pattern &p, int max_positions, BitNfa *out, std::string *err, int dense_words = 16);
 
 // Reference walk over the compiled tables (used by tests and by the host-side
 // table validator; the product's matching runs on the GPU).

@@ -129,9 +129,32 @@ def test_blowup_patterns_nfa_vs_oracle(oracle, pat):
             assert ca.debug_regex(pat, data, anchored, nfa=True) == ref.match(data, anchored), (pat, data, anchored)
 
 
-def test_nfa_position_limit():
-    with pytest.raises(ValueError, match="NFA positions"):
-        ca.debug_regex(".{1000}.{100}", b"", True, nfa=True)
+# Past 1,024 positions the NFA keeps sparse follow rows and its state sets in
+# scratch (regex/nfa_walk.h nfa_run_big): every repeat count Go accepts.
+LARGE = [".{1000}x.{1000}", "(a|b)*a.{1000}b.{1000}", "(?m)^a.{1000}.{30}$", "\\b[ab]{1000}[ab]{100}\\b",
+         "(?s).{1000}.{25}\u00e9", "(x|y.{600}){1}z[^a]{500}.{400}"]
+
+
+def _large_inputs(pat, rng):
+    yield b""
+    for _ in range(24):
+        n = rng.choice([1000, 1030, 1099, 1100, 1101, 1500, 2000, 2001, 2002, 2003, 2100, 2500, 3200])
+        alphabet = [b"a", b"b", b"x", b"y", b"z", b"c", b" ", b"\n", "\u00e9".encode()]
+        data = bytearray(b"".join(rng.choice(alphabet[:3] if rng.random() < 0.5 else alphabet) for _ in range(n)))
+        if rng.random() < 0.5 and len(data) > 1001:  # a planted x / b at the distance the pattern wants
+            k = rng.randrange(0, len(data) - 1001)
+            data[k] = ord("a")
+            data[k + 1001] = ord(rng.choice("xb"))
+        yield bytes(data)
+
+
+@pytest.mark.parametrize("pat", LARGE)
+def test_large_nfa_vs_oracle(oracle, pat):
+    ref = oracle.Regex(pat)
+    rng = random.Random(sum(pat.encode()))
+    for data in _large_inputs(pat, rng):
+        for anchored in (True, False):
+            assert ca.debug_regex(pat, data, anchored, nfa=True) == ref.match(data, anchored), (pat, len(data), anchored)
 
 
 # Unicode version of Go 1.10 (Unicode 10.0.0): the tables are restricted to the
