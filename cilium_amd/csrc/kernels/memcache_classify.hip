@@ -39,6 +39,9 @@ constexpr int kBlock = 256;
 #endif
 constexpr int kMcPassDfas = L7G_MC_DFAS < kMcMaxDfas ? L7G_MC_DFAS : kMcMaxDfas;
 constexpr uint32_t kMcLdsImages = 32 * 1024;  // LDS budget for the staged rule-set images
+constexpr int kMcWaves = kBlock / 64;
+constexpr int kMcSortPer = 4;                          // list entries per lane per chunk (1: 4.33 ms, 2: 3.82, 4: 3.25, 8: 3.26, 16: 4.41 on cfg5)
+constexpr uint32_t kMcWaveChunk = 64 * kMcSortPer;     // entries a wave orders by parser at a time
 // waves per SIMD the common kernel is built for (experiments: -DL7G_MC_WAVES=N)
 #ifndef L7G_MC_WAVES
 #define L7G_MC_WAVES 5
@@ -361,8 +364,7 @@ __device__ __forceinline__ void text_fast(const Image &I, Keys<kCh> &K, const ui
 
 }  // namespace
 
-// sel: this protocol's request indices (partition_kernel, mixed batches), else
-// requests 0..n-1.  answer_other: answer entries on connections that are not
+// One request.  answer_other: answer entries on connections that are not
 // memcached (single-protocol engines, where partition_kernel does not run).
 // kNfa: the variant that also runs NFA-fallback key matchers (launched only
 // when some memcache rule set has them; the other keeps its registers).
@@ -370,21 +372,12 @@ __device__ __forceinline__ void text_fast(const Image &I, Keys<kCh> &K, const ui
 // instantiations so that every image read compiles to a ds_read (LDS) or a
 // global_load: one pointer that may be either makes them all flat loads.
 template <bool kNfa, bool kLds, int kCh>
-__device__ __forceinline__ void mc_loop(Batch B, McTables T, const uint8_t *images, const uint32_t *__restrict__ sel,
-                                        const uint32_t *__restrict__ sel2, const uint32_t *__restrict__ sel_count,
-                                        uint32_t answer_other) {
-    const uint32_t n = B.n, nconns = B.nconns;
+__device__ __forceinline__ void mc_one(const Batch &B, const McTables &T, const uint8_t *images, uint32_t idx,
+                                       uint32_t answer_other) {
+    const uint32_t nconns = B.nconns;
     const uint32_t *__restrict__ conn_ids = B.conn_ids;
     const DevConn *__restrict__ conns = B.conns;
-    // sel: this protocol's request indices from partition_kernel: sel_count[0]
-    // text retrievals from sel's start, sel_count[1] binary requests from its
-    // end, sel_count[3] other text commands from sel2's end (n slots each);
-    // null: all n
-    const uint32_t ma = sel ? sel_count[0] : n;
-    const uint32_t mb = sel ? ma + sel_count[3] : n;
-    const uint32_t m = sel ? mb + sel_count[1] : n;
-    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < m; i += gridDim.x * kBlock) {
-        const uint32_t idx = !sel ? i : i < ma ? sel[i] : i < mb ? sel2[n - 1 - (i - ma)] : sel[n - 1 - (i - mb)];
+    {
         const uint32_t ci = conn_ids[idx];
         const DevConn conn = ci < nconns ? conns[ci] : DevConn{-1, PROTO_NONE, 0, 0xFFFF};
         if (conn.proto != PROTO_MEMCACHE || conn.ruleset < 0 || (uint32_t)conn.ruleset >= T.nrulesets) {
@@ -393,7 +386,7 @@ __device__ __forceinline__ void mc_loop(Batch B, McTables T, const uint8_t *imag
                 B.rule[idx] = -1;
                 B.consumed[idx] = 0;
             }
-            continue;
+            return;
         }
         const DevRuleset rs = T.rulesets[conn.ruleset];
         Image I;
@@ -504,6 +497,104 @@ __device__ __forceinline__ void mc_loop(Batch B, McTables T, const uint8_t *imag
         B.verdict[idx] = verdict;
         B.rule[idx] = rule;
         B.consumed[idx] = consumed;
+    }
+}
+
+// The parser each of a lane's kMcSortPer entries takes (memcached/parser.go:
+// 186-202: the connection's, else the one its first byte picks), and text
+// retrievals (get / gets / gat / gats) apart from the other commands, whose
+// lines are longer and parse more tokens: 0 text retrieval, 1 other text, 2
+// binary, 3 everything else, 4 no entry.  The loads go out phase by phase
+// (connection ids, connections, offsets / lengths, first bytes) so the lane
+// waits four memory latencies, not four per entry.
+__device__ __forceinline__ void mc_kinds(const Batch &B, const McTables &T, const uint32_t (&ix)[kMcSortPer],
+                                         uint32_t (&kd)[kMcSortPer]) {
+    uint32_t ci[kMcSortPer], fl[kMcSortPer], ln[kMcSortPer];
+    uint64_t of[kMcSortPer];
+#pragma unroll
+    for (int r = 0; r < kMcSortPer; r++) ci[r] = ix[r] != ~0u ? B.conn_ids[ix[r]] : ~0u;
+#pragma unroll
+    for (int r = 0; r < kMcSortPer; r++) {
+        kd[r] = ix[r] == ~0u ? 4 : 3;
+        fl[r] = 0;
+        if (ci[r] < B.nconns) {
+            const DevConn c = B.conns[ci[r]];
+            if (c.proto == PROTO_MEMCACHE && c.ruleset >= 0 && (uint32_t)c.ruleset < T.nrulesets) {
+                kd[r] = 0;
+                fl[r] = c.flags;
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < kMcSortPer; r++) {
+        of[r] = 0;
+        ln[r] = 0;
+        if (kd[r] == 0) {
+            of[r] = B.offs[ix[r]];
+            ln[r] = B.lens[ix[r]];
+            if (ln[r] == 0 || !l7_in_arena(of[r], ln[r], B.arena_len)) kd[r] = 3;
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < kMcSortPer; r++) {
+        if (kd[r] != 0) continue;
+        const uint32_t b0 = B.arena[of[r]];
+        uint32_t mode = fl[r] & 3;
+        if (mode == 0) mode = b0 >= 0x80 ? 2 : 1;
+        kd[r] = mode == 2 ? 2 : b0 == 'g' ? 0 : 1;
+    }
+}
+
+// sel: this protocol's request indices (partition_kernel, mixed batches), else
+// requests 0..n-1.  Each wave takes kMcWaveChunk list entries at a time,
+// reads each one's parser from its first byte (a line the classification
+// reads next anyway), orders them by parser in its own LDS slice (stable:
+// list order within a parser), then classifies them in that order, so the
+// wave mostly runs one parser's path instead of text and binary one after the
+// other.  Waves never wait for each other (no workgroup barrier).
+template <bool kNfa, bool kLds, int kCh>
+__device__ __forceinline__ void mc_loop(Batch B, McTables T, const uint8_t *images, const uint32_t *__restrict__ sel,
+                                        const uint32_t *__restrict__ sel2, const uint32_t *__restrict__ sel_count,
+                                        uint32_t answer_other) {
+    const uint32_t n = B.n;
+    // sel: sel_count[0] entries from sel's start, sel_count[1] from its end,
+    // sel_count[3] from sel2's end (n slots each); null: all n
+    const uint32_t ma = sel ? sel_count[0] : n;
+    const uint32_t mb = sel ? ma + sel_count[3] : n;
+    const uint32_t m = sel ? mb + sel_count[1] : n;
+    __shared__ uint32_t s_idx[kMcWaves][kMcWaveChunk];  // a wave's entries in parser order
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t below = (1ull << lane) - 1;
+    uint32_t *slot = s_idx[wave];
+    for (uint32_t base = (blockIdx.x * kMcWaves + wave) * kMcWaveChunk; base < m;
+         base += gridDim.x * kMcWaves * kMcWaveChunk) {
+        uint32_t ix[kMcSortPer], kd[kMcSortPer];
+#pragma unroll
+        for (int r = 0; r < kMcSortPer; r++) {
+            const uint32_t i = base + r * 64 + lane;
+            ix[r] = i >= m ? ~0u : !sel ? i : i < ma ? sel[i] : i < mb ? sel2[n - 1 - (i - ma)] : sel[n - 1 - (i - mb)];
+        }
+        mc_kinds(B, T, ix, kd);
+        uint32_t lo[4] = {0, 0, 0, 0};  // exclusive offsets, parser-major
+#pragma unroll
+        for (int r = 0; r < kMcSortPer; r++)
+#pragma unroll
+            for (int k = 0; k < 3; k++) lo[k + 1] += __popcll(__ballot(kd[r] <= (uint32_t)k));
+#pragma unroll
+        for (int r = 0; r < kMcSortPer; r++) {
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint64_t mk = __ballot(kd[r] == (uint32_t)k);
+                if (kd[r] == (uint32_t)k) slot[lo[k] + __popcll(mk & below)] = ix[r];
+                lo[k] += __popcll(mk);
+            }
+        }
+        const uint32_t total = min(m - base, kMcWaveChunk);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (uint32_t k = lane; k < total; k += 64) mc_one<kNfa, kLds, kCh>(B, T, images, slot[k], answer_other);
+        __builtin_amdgcn_wave_barrier();  // (the slice is rewritten by the next chunk)
     }
 }
 

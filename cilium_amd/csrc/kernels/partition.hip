@@ -5,13 +5,18 @@
 // stream (cfg5) most of their lanes would only discover "not my protocol" and
 // idle while the others decode.  This kernel writes, for each of those two
 // protocols, the list of request indices that belong to it; the classifiers
-// then walk only their own list.  Kafka requests are further grouped by kind
-// and length class, so a wave of the one-lane-per-request Kafka kernel holds
-// requests that take the same decode path for about as long, and no longer
-// waits on one long produce request among short fetches (a wave runs as long
-// as its longest lane, and divergent paths run one after the other).  One block owns 4096 consecutive requests
-// (16 per lane, protocol kept in registers between the count and the write
-// pass) and takes its slot range with one atomic per protocol.
+// then walk only their own list.  Kafka requests are further grouped by length
+// class, so a wave of the one-lane-per-request Kafka kernel holds requests
+// that take the same decode path for about as long, and no longer waits on one
+// long produce request among short fetches (a wave runs as long as its longest
+// lane, and divergent paths run one after the other).  The class comes from
+// the request's length alone: this kernel reads no request bytes (round 3 read
+// each Kafka request's api key and each memcached request's first byte, one
+// HBM line per request, 5 of its 7 GB per cfg5 launch); the memcached kernel
+// splits text from binary itself, from bytes it reads anyway.  One block owns
+// 2048 consecutive requests (8 per lane, protocol kept in registers between
+// the count and the write pass) and takes its slot range with one atomic per
+// protocol.
 #include <hip/hip_runtime.h>
 
 #include "../device_tables.h"
@@ -20,10 +25,7 @@ namespace l7 {
 
 namespace {
 constexpr int kBlock = 256;
-#ifndef L7G_PART_PER  // rows (of 256 requests) per workgroup
-#define L7G_PART_PER 8
-#endif
-constexpr int kPer = L7G_PART_PER;
+constexpr int kPer = 8;  // rows (of 256 requests) per workgroup
 constexpr int kWaves = kBlock / 64;
 // list classes: 0..kKafkaClasses-1 Kafka by kind / length, then memcached
 // text, memcached binary, then HTTP
@@ -32,24 +34,20 @@ constexpr int kMcText = kKafkaClasses, kMcBinary = kKafkaClasses + 1, kHttp = kK
 constexpr int kMcText2 = kKafkaClasses + 3;  // text commands not starting with 'g' (storage, delete, ...)
 constexpr int kClasses = kKafkaClasses + 4;
 
-static_assert(kKafkaClasses == 1 || kKafkaClasses == 8 || kKafkaClasses == 12, "length classes");
+static_assert(kKafkaClasses == 1 || kKafkaClasses == 8, "length classes");
 static_assert(kKafkaClasses + 4 <= 31, "counts[31] holds the compressed-Kafka count");
 // Kafka list class: the decode path a lane takes is set by the request kind
-// and, for produce, by how many message bytes it hashes, so fetch requests,
-// the other kinds, and produce requests by length each get lists of their own.
-// kind: the request's api key bytes (bytes 4-5), 0xFFFF if it has none
-__device__ __forceinline__ uint8_t kafka_class(uint32_t kind, uint32_t len) {
+// and, for produce, by how many message bytes it hashes.  The length tells the
+// kinds apart well enough to schedule by (requests without message sets --
+// metadata, offsets, heartbeats -- are tens of bytes, a fetch of a few topics
+// and partitions a hundred or two, a produce carries its messages); a request
+// in the "wrong" class only shares a wave with a different path: every class
+// takes every kind, so this is scheduling, not semantics.
+__device__ __forceinline__ uint8_t kafka_class(uint32_t len) {
     if (kKafkaClasses == 1) return 0;
-    if (len < 6) kind = 0xFFFF;
-    if (kKafkaClasses == 12) {  // fetch by length (topic / partition count), other kinds, produce in 9 bins
-        if (kind == 1) return len < 128 ? 0 : 1;
-        if (kind != 0) return 2;
-        return len < 512 ? 3 : len < 896 ? 4 : len < 1280 ? 5 : len < 1664 ? 6 : len < 2048 ? 7
-             : len < 2560 ? 8 : len < 3072 ? 9 : len < 3712 ? 10 : 11;
-    }
-    if (kind == 1) return 0;
-    if (kind != 0) return 1;
-    return len < 384 ? 2 : len < 640 ? 3 : len < 896 ? 4 : len < 1280 ? 5 : len < 2048 ? 6 : 7;
+    if (len < 67) return 1;   // no message set
+    if (len < 211) return 0;  // fetch
+    return len < 384 ? 2 : len < 640 ? 3 : len < 896 ? 4 : len < 1280 ? 5 : len < 2048 ? 6 : 7;  // produce
 }
 }  // namespace
 
@@ -76,8 +74,8 @@ __global__ __launch_bounds__(kBlock) void partition_kernel(Batch B, uint32_t *__
     uint8_t p[kPer];  // class + 1, 0 = none
     uint32_t cnt[kClasses] = {};
     // The rows' loads go out phase by phase (connection ids, connections,
-    // offsets / lengths, first bytes), so a block waits four memory latencies,
-    // not four per row.
+    // Kafka offsets / lengths), so a block waits three memory latencies, not
+    // three per row.
     uint32_t ci[kPer], pw[kPer];
 #pragma unroll
     for (int r = 0; r < kPer; r++) {
@@ -100,21 +98,9 @@ __global__ __launch_bounds__(kBlock) void partition_kernel(Batch B, uint32_t *__
         const uint32_t proto = pw[r] & 0xFF;
         off[r] = 0;
         len[r] = 0;
-        if (proto == PROTO_KAFKA || proto == PROTO_MEMCACHE) {
+        if (proto == PROTO_KAFKA) {
             off[r] = B.offs[idx];
             len[r] = B.lens[idx];
-        }
-    }
-    uint32_t hb[kPer];  // Kafka: the api key bytes 4-5 (0xFFFF: none); memcached: the first byte (0: none)
-#pragma unroll
-    for (int r = 0; r < kPer; r++) {
-        const uint32_t proto = pw[r] & 0xFF;
-        hb[r] = 0;
-        if (proto == PROTO_KAFKA) {
-            const bool ok = l7_in_arena(off[r], len[r], B.arena_len) && len[r] >= 6;
-            hb[r] = ok ? (uint32_t)B.arena[off[r] + 4] << 8 | B.arena[off[r] + 5] : 0xFFFFu;
-        } else if (proto == PROTO_MEMCACHE) {
-            hb[r] = len[r] > 0 && l7_in_arena(off[r], 1, B.arena_len) ? B.arena[off[r]] : 0u;
         }
     }
 #pragma unroll
@@ -124,19 +110,10 @@ __global__ __launch_bounds__(kBlock) void partition_kernel(Batch B, uint32_t *__
         if (idx < n) {
             const uint32_t proto = pw[r] & 0xFF;
             if (proto == PROTO_KAFKA) {
-                cls = 1 + kafka_class(hb[r], l7_in_arena(off[r], len[r], B.arena_len) ? len[r] : 0);
+                cls = 1 + kafka_class(l7_in_arena(off[r], len[r], B.arena_len) ? len[r] : 0);
             }
             else if (proto == PROTO_MEMCACHE) {
-                // the parser the connection chose, else the one this buffer's
-                // first byte picks (memcached/parser.go:186-202): text and
-                // binary requests take different paths, so they get lists of
-                // their own and a wave runs only one of them
-                // (text: retrievals -- get / gets / gat / gats -- apart from the
-                // rest, whose lines are longer and parse more tokens)
-                uint32_t mode = (pw[r] >> 8) & 3;
-                const uint32_t c0 = hb[r];
-                if (mode == 0) mode = c0 >= 0x80 ? 2 : 1;
-                cls = 1 + (mode == 2 ? kMcBinary : c0 == 'g' ? kMcText : kMcText2);
+                cls = 1 + kMcText;  // one list: the memcached kernel splits it by parser itself
             }
             else if (proto == PROTO_HTTP) cls = 1 + kHttp;
             else if (!L7_PROTO_OWNED(proto)) {  // (r2d2, cassandra: their kernels walk the whole batch)
