@@ -41,6 +41,14 @@ extern "C" {
 typedef struct l7g_engine l7g_engine;
 
 enum { L7G_PROTO_HTTP = 1, L7G_PROTO_KAFKA = 2, L7G_PROTO_MEMCACHE = 3, L7G_PROTO_R2D2 = 4, L7G_PROTO_CASSANDRA = 5 };
+/* L7G_PROTO_CASSANDRA keeps no state between l7g_classify calls: a request's
+ * keyspace comes only from the last USE on its connection earlier in the same
+ * batch (a USE from an earlier batch is not remembered, so "t" stays ".t"
+ * rather than "ks.t"), and an EXECUTE is never resolved to its prepared query
+ * (answered L7G_PARSE_ERROR, consumed 2).  The proxylib shim keeps both per
+ * connection (USE keyspace, PREPARE ids) and replays them into each batch, as
+ * cassandraparser.go does; a direct caller that needs the reference's
+ * cross-batch behaviour must do the same. */
 enum {
     L7G_DENY = 0,        /* policy denies (HTTP 403 / Kafka ErrTopicAuthorizationFailed) */
     L7G_ALLOW = 1,       /* policy allows; rule = matched global rule id or -1 */
