@@ -42,6 +42,7 @@ EXPORTS = (
     "l7g_kafka_corr_requests", "l7g_kafka_corr_responses", "l7g_kafka_corr_gc", "l7g_kafka_corr_size",
     "l7g_flow_stats_enable", "l7g_flow_stats",
     "l7g_tables_export", "l7g_tables_import", "l7g_tables_compiled", "l7g_tables_digest",
+    "l7g_frame_streams", "l7g_classify_streams",
 )
 
 
@@ -87,6 +88,9 @@ def load(path=None):
     lib.l7g_tables_digest.argtypes = [vp]
     lib.l7g_conn_update.argtypes = [vp, C.c_uint32, vp, cp, sz]
     lib.l7g_classify.argtypes = [vp, vp, C.c_uint64, vp, vp, vp, C.c_uint32, vp, vp, vp, vp, vp]
+    lib.l7g_frame_streams.argtypes = [vp, vp, C.c_uint64, vp, vp, vp, C.c_uint32, C.c_uint32, vp, vp, vp, vp, vp]
+    lib.l7g_classify_streams.argtypes = [vp, vp, C.c_uint64, vp, vp, vp, C.c_uint32, C.c_uint32, vp, vp, vp, vp, vp, vp,
+                                         vp, vp, vp]
     lib.l7g_classify_host.argtypes = [vp, vp, C.c_uint64, vp, vp, vp, C.c_uint32, vp, vp, vp]
     lib.l7g_stats.argtypes = [vp, C.POINTER(Stats)]
     lib.l7g_debug_regex.argtypes = [cp, sz, C.c_int, cp, sz, cp, sz]

@@ -52,6 +52,10 @@ uint32_t FlowStatsMaxKeys();
 hipError_t LaunchHttpNfa(const Batch &B, const HttpTables &T, uint32_t scratch_lanes, hipStream_t stream);
 hipError_t LaunchPartition(const Batch &B, uint32_t *sel_kafka, uint32_t *sel_mc, uint32_t *sel_http, uint32_t *counts,
                            hipStream_t stream);
+hipError_t LaunchFrameStreams(const uint8_t *arena, uint64_t arena_len, const uint64_t *s_off, const uint32_t *s_len,
+                              const uint32_t *s_conn, uint32_t n, const DevConn *conns, uint32_t nconns,
+                              uint32_t max_frames, uint64_t *frame_off, uint32_t *frame_len, uint32_t *conn_out,
+                              uint32_t *nframes, hipStream_t stream);
 hipError_t HttpPhaseTimes(uint64_t *out, bool reset);
 hipError_t KafkaPhaseTimes(uint64_t *out, bool reset);
 }  // namespace l7
@@ -903,6 +907,32 @@ int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const 
                  const uint32_t *conn, uint32_t n, uint8_t *verdict, int32_t *rule, uint32_t *consumed,
                  uint64_t *counters, void *stream) {
     return Classify(e, arena, arena_len, off, len, conn, n, verdict, rule, consumed, counters, stream, nullptr);
+}
+
+int l7g_frame_streams(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const uint64_t *s_off,
+                      const uint32_t *s_len, const uint32_t *s_conn, uint32_t n, uint32_t max_frames,
+                      uint64_t *frame_off, uint32_t *frame_len, uint32_t *frame_conn, uint32_t *nframes, void *stream) {
+    std::lock_guard<std::mutex> g(e->mu);
+    if (e->device < 0) return (int)hipErrorNoDevice;
+    if (max_frames == 0 || (uint64_t)n * max_frames > 0xFFFFFFFFull) return (int)hipErrorInvalidValue;
+    hipError_t rc = hipSetDevice(e->device);
+    if (rc == hipSuccess) rc = Upload(e);  // (the connection table the walk reads)
+    if (rc == hipSuccess)
+        rc = LaunchFrameStreams(arena, arena_len, s_off, s_len, s_conn, n, e->d_conns, (uint32_t)e->conns.size(),
+                                max_frames, frame_off, frame_len, frame_conn, nframes, (hipStream_t)stream);
+    return (int)rc;
+}
+
+int l7g_classify_streams(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const uint64_t *s_off,
+                         const uint32_t *s_len, const uint32_t *s_conn, uint32_t n, uint32_t max_frames,
+                         uint64_t *frame_off, uint32_t *frame_len, uint32_t *frame_conn, uint32_t *nframes,
+                         uint8_t *verdict, int32_t *rule, uint32_t *consumed, uint64_t *counters, void *stream) {
+    int rc = l7g_frame_streams(e, arena, arena_len, s_off, s_len, s_conn, n, max_frames, frame_off, frame_len,
+                               frame_conn, nframes, stream);
+    if (rc != 0) return rc;
+    // every slot, the empty ones on connection ~0 (answered UNSUPPORTED)
+    return Classify(e, arena, arena_len, frame_off, frame_len, frame_conn, n * max_frames, verdict, rule, consumed,
+                    counters, stream, nullptr);
 }
 
 }  // extern "C"

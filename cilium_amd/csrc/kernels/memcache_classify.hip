@@ -564,6 +564,14 @@ __device__ __forceinline__ void mc_loop(Batch B, McTables T, const uint8_t *imag
     const uint32_t m = sel ? mb + sel_count[1] : n;
     __shared__ uint32_t s_idx[kMcWaves][kMcWaveChunk];  // a wave's entries in parser order
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (m <= 64) {  // one wave's worth (a proxylib OnData): nothing to order, and the
+                    // first bytes would be one more round trip (zero-copy: over PCIe)
+        const uint32_t i = lane;
+        if (blockIdx.x == 0 && wave == 0 && i < m)
+            mc_one<kNfa, kLds, kCh>(B, T, images, !sel ? i : i < ma ? sel[i] : i < mb ? sel2[n - 1 - (i - ma)] : sel[n - 1 - (i - mb)],
+                                    answer_other);
+        return;
+    }
     const uint64_t below = (1ull << lane) - 1;
     uint32_t *slot = s_idx[wave];
     for (uint32_t base = (blockIdx.x * kMcWaves + wave) * kMcWaveChunk; base < m;

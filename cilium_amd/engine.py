@@ -110,6 +110,23 @@ class Engine:
         if rc != 0:
             raise RuntimeError(f"l7g_classify failed: HIP error {rc}")
 
+    def classify_streams_device(self, arena_ptr, arena_len, s_off_ptr, s_len_ptr, s_conn_ptr, n, max_frames,
+                                frame_off_ptr, frame_len_ptr, frame_conn_ptr, nframes_ptr, verdict_ptr=0, rule_ptr=0,
+                                consumed_ptr=0, counters_ptr=0, stream=0):
+        """l7g_frame_streams (no verdict pointers) or l7g_classify_streams: device
+        framing of n connection streams into n * max_frames frame slots."""
+        if verdict_ptr:
+            rc = self._lib.l7g_classify_streams(self._h, arena_ptr, arena_len, s_off_ptr, s_len_ptr, s_conn_ptr, n,
+                                                max_frames, frame_off_ptr, frame_len_ptr, frame_conn_ptr, nframes_ptr,
+                                                verdict_ptr, rule_ptr, consumed_ptr, counters_ptr or None,
+                                                stream or None)
+        else:
+            rc = self._lib.l7g_frame_streams(self._h, arena_ptr, arena_len, s_off_ptr, s_len_ptr, s_conn_ptr, n,
+                                             max_frames, frame_off_ptr, frame_len_ptr, frame_conn_ptr, nframes_ptr,
+                                             stream or None)
+        if rc != 0:
+            raise RuntimeError(f"l7g_frame_streams / l7g_classify_streams failed: HIP error {rc}")
+
     def classify(self, arena, offsets, lengths, conn_ids):
         """Host-buffer convenience: copies to the device, classifies, copies back."""
         arena = np.ascontiguousarray(arena, dtype=np.uint8)

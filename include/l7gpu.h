@@ -24,6 +24,10 @@
  *                                                                  proxylib/proxylib.go:97-110,
  *                                                                  proxylib/memcached/parser.go:186-202,
  *                                                                  proxylib/proxylib/policymap.go:210-236
+ *   l7g_frame_streams   the parsers' framing of a connection's input: proto.ReadReq's size prefix
+ *                                                                  vendor/github.com/optiopay/kafka/proto/messages.go:124-165,
+ *                       memcached text line / binary header        proxylib/memcached/text/parser.go:72-262,
+ *                                                                  proxylib/memcached/binary/parser.go:72-139
  *   counters argument   Endpoint.UpdateProxyStatistics counters    pkg/endpoint/endpoint.go:2207-2233
  *   of l7g_classify     (per-rule allow hits + per-verdict totals, accumulated on the device)
  *
@@ -166,6 +170,36 @@ int l7g_conn_update(l7g_engine *e, uint32_t index, const l7g_conn_t *conn, char 
 int l7g_classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const uint64_t *off, const uint32_t *len,
                  const uint32_t *conn, uint32_t n, uint8_t *verdict, int32_t *rule, uint32_t *consumed,
                  uint64_t *counters, void *stream);
+
+/* Device framing of connection streams (replaces the host scan that proposes
+ * where a connection's frames start: Kafka's BE int32 size prefix,
+ * proto.ReadReq vendor/github.com/optiopay/kafka/proto/messages.go:124-165;
+ * memcached text lines + storage data blocks and binary 24-byte header + body,
+ * proxylib/memcached/{text,binary}/parser.go; HTTP/1 head + Content-Length;
+ * r2d2 lines; cassandra 9-byte header + body).  Stream s is arena[s_off[s],
+ * s_off[s] + s_len[s]) on connection s_conn[s] (a memcached connection without
+ * a chosen parser takes the one the stream's first byte picks).  One device
+ * lane walks each stream; output slots [s * max_frames, (s + 1) * max_frames):
+ * frame k of stream s starts at frame_off (an arena offset) and is handed
+ * frame_len = the bytes from there to the stream's end, as proxylib hands a
+ * parser the joined input; frame_conn = s_conn[s]; nframes[s] frames.  The
+ * walk stops at a frame whose end is not in the stream or cannot be known
+ * before parsing it (a chunked HTTP body, an unreadable size): that frame is
+ * the last, with the rest of the stream, and the classifier's consumed length
+ * says where the next one starts.  Empty slots: length 0, connection ~0.  All
+ * pointers are device memory; asynchronous on `stream`.  0 or a hipError_t. */
+int l7g_frame_streams(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const uint64_t *s_off,
+                      const uint32_t *s_len, const uint32_t *s_conn, uint32_t n, uint32_t max_frames,
+                      uint64_t *frame_off, uint32_t *frame_len, uint32_t *frame_conn, uint32_t *nframes, void *stream);
+/* l7g_frame_streams, then l7g_classify over all n * max_frames slots (the
+ * empty ones answer L7G_UNSUPPORTED): a batch of connection streams in, one
+ * verdict per frame out, with no host pass over the bytes.  A frame is
+ * confirmed when its consumed length equals the distance to the next frame
+ * (or, for the last, when the caller accepts a partial one). */
+int l7g_classify_streams(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const uint64_t *s_off,
+                         const uint32_t *s_len, const uint32_t *s_conn, uint32_t n, uint32_t max_frames,
+                         uint64_t *frame_off, uint32_t *frame_len, uint32_t *frame_conn, uint32_t *nframes,
+                         uint8_t *verdict, int32_t *rule, uint32_t *consumed, uint64_t *counters, void *stream);
 
 /* Same with host buffers: copies in, classifies, copies out, synchronises.
  * Each calling thread gets its own stream and device staging, so calls from

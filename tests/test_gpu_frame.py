@@ -1,0 +1,225 @@
+"""Device framing of connection streams (l7g_frame_streams /
+l7g_classify_streams, kernels/frame.hip) on the GPU.
+
+Each protocol's generated requests are grouped by connection and concatenated
+into one stream per connection (some cut short), the way a proxy receives
+them.  The device walk must find exactly the frame starts the restatement below
+finds -- the parsers' framing as csrc/proxylib/shim.cc scans it on the host
+(Kafka's BE int32 size prefix, vendor/github.com/optiopay/kafka/proto/
+messages.go:124-165; memcached text lines + storage data blocks and binary
+headers, proxylib/memcached/{text,binary}/parser.go; HTTP head +
+Content-Length; r2d2 lines; cassandra 9-byte headers) -- and, for generated
+well-formed requests, exactly the request boundaries.  l7g_classify_streams'
+verdicts, rule ids and consumed lengths for every frame equal the oracle's on
+the same frames."""
+import numpy as np
+import pytest
+import torch
+
+from cilium_amd import gen
+from cilium_amd._lib import PROTO_CASSANDRA, PROTO_HTTP, PROTO_KAFKA, PROTO_MEMCACHE, PROTO_R2D2
+
+pytestmark = pytest.mark.gpu
+
+
+# ---- the framing restatement (shim.cc NextKafka / NextMcBinary / NextMcText / NextLine / NextHttp)
+def _space_len(s, i, n):
+    c = s[i]
+    if c == 0x20 or 0x09 <= c <= 0x0D:
+        return 1
+    if c < 0xC2 or c > 0xE3 or i + 1 >= n:
+        return 0
+    c1 = s[i + 1]
+    if c == 0xC2:
+        return 2 if c1 in (0x85, 0xA0) else 0
+    if i + 2 >= n:
+        return 0
+    c2 = s[i + 2]
+    if c == 0xE1:
+        return 3 if (c1, c2) == (0x9A, 0x80) else 0
+    if c == 0xE2 and c1 == 0x80:
+        return 3 if (0x80 <= c2 <= 0x8A or c2 in (0xA8, 0xA9, 0xAF)) else 0
+    if c == 0xE2 and c1 == 0x81:
+        return 3 if c2 == 0x9F else 0
+    if c == 0xE3:
+        return 3 if (c1, c2) == (0x80, 0x80) else 0
+    return 0
+
+
+def _fields(s):
+    out, i, start, inside, n = [], 0, 0, False, len(s)
+    while i < n:
+        sp = _space_len(s, i, n)
+        if sp:
+            if inside:
+                out.append(s[start:i])
+            inside = False
+            i += sp
+        else:
+            if not inside:
+                start, inside = i, True
+            i += 1
+    if inside:
+        out.append(s[start:])
+    return out
+
+
+def _next(d, p, proto, mode):
+    n = len(d)
+    if proto == PROTO_KAFKA:
+        if n - p < 4:
+            return 0
+        size = int.from_bytes(d[p:p + 4], "big", signed=True)
+        return p + 4 + size if 0 < size and size + 4 <= n - p else 0
+    if proto == PROTO_CASSANDRA:
+        if n - p < 9:
+            return 0
+        fl = 9 + int.from_bytes(d[p + 5:p + 9], "big")
+        return p + fl if fl <= n - p else 0
+    if proto == PROTO_MEMCACHE and mode == 2:
+        if n - p < 24:
+            return 0
+        body = int.from_bytes(d[p + 8:p + 12], "big")
+        return p + 24 + body if body + 24 <= n - p else 0
+    lf = d.find(b"\r\n", p)
+    if lf < 0:
+        return 0
+    if proto == PROTO_R2D2:
+        return lf + 2
+    if proto == PROTO_MEMCACHE:
+        tok = _fields(d[p:lf])
+        nxt = lf + 2
+        if tok and tok[0] in (b"set", b"add", b"replace", b"append", b"prepend", b"cas"):
+            if len(tok) < 5:
+                return 0
+            t = tok[4]
+            digits = t[1:] if t[:1] in (b"+", b"-") else t
+            if not digits or not digits.isdigit():
+                return 0
+            v = int(digits)
+            if t[:1] == b"-" and v:
+                return 0
+            nxt += v + 2
+        return nxt if nxt <= n else 0
+    # HTTP
+    he = d.find(b"\r\n\r\n", p)
+    if he < 0:
+        return 0
+    cl = 0
+    ls = lf + 2
+    while ls < he:
+        le = d.find(b"\r\n", ls)
+        colon = d.find(b":", ls)
+        if 0 <= colon < le:
+            name = d[ls:colon].lower()
+            if name == b"transfer-encoding":
+                return 0
+            if name == b"content-length":
+                v = d[colon + 1:].lstrip(b" \t\r\n\v\f")
+                neg = v[:1] == b"-"
+                v = v[1:] if v[:1] in (b"+", b"-") else v
+                k = 0
+                while k < len(v) and 48 <= v[k] <= 57:
+                    k += 1
+                x = int(v[:k]) if k else 0
+                cl = (-x) % (1 << 64) if neg else min(x, (1 << 64) - 1)
+        ls = le + 2
+    nxt = he + 4 + cl
+    return nxt if he + 4 <= n and cl <= n - (he + 4) else 0
+
+
+def _frames(d, proto, mode, max_frames):
+    out, p = [], 0
+    if proto == PROTO_MEMCACHE and mode == 0 and d:
+        mode = 2 if d[0] >= 0x80 else 1
+    while p < len(d) and len(out) < max_frames:
+        out.append(p)
+        q = _next(d, p, proto, mode)
+        if q <= p:
+            break
+        p = q
+    return out
+
+
+def _streams(w, rng, cut_every=5):
+    """One stream per connection: its requests in order; every cut_every-th
+    stream cut short at a random point."""
+    reqs = [bytes(w.arena[int(o):int(o) + int(n)]) for o, n in zip(w.offsets, w.lengths)]
+    by = {}
+    for q, c in zip(reqs, w.conn_ids):
+        by.setdefault(int(c), []).append(q)
+    conns, streams, bounds = [], [], []
+    for k, (c, qs) in enumerate(sorted(by.items())):
+        s = b"".join(qs)
+        b = list(np.cumsum([0] + [len(q) for q in qs[:-1]]))
+        if k % cut_every == 3 and len(s) > 2:
+            s = s[:int(rng.integers(1, len(s)))]
+        conns.append(c)
+        streams.append(s)
+        bounds.append(b)
+    return conns, streams, bounds
+
+
+def _run(engine, oracle, w, max_frames=64):
+    rng = np.random.default_rng(7)
+    engine.update_policy(w.policy)
+    engine.set_connections(w.conns)
+    conns, streams, bounds = _streams(w, rng)
+    arena = np.frombuffer(b"".join(streams), np.uint8).copy()
+    s_off = np.cumsum([0] + [len(s) for s in streams[:-1]]).astype(np.uint64)
+    s_len = np.array([len(s) for s in streams], np.uint32)
+    s_conn = np.array(conns, np.uint32)
+    n = len(streams)
+    dev = torch.device("cuda", 0)
+    t = lambda a: torch.from_numpy(a.view(np.int64) if a.dtype == np.uint64 else a.view(np.int32) if a.itemsize == 4 else a).to(dev)  # noqa: E731
+    d_arena, d_off, d_len, d_conn = t(arena), t(s_off), t(s_len), t(s_conn)
+    slots = n * max_frames
+    f_off = torch.zeros(slots, dtype=torch.int64, device=dev)
+    f_len = torch.zeros(slots, dtype=torch.int32, device=dev)
+    f_conn = torch.zeros(slots, dtype=torch.int32, device=dev)
+    nfr = torch.zeros(n, dtype=torch.int32, device=dev)
+    v = torch.zeros(slots, dtype=torch.uint8, device=dev)
+    r = torch.zeros(slots, dtype=torch.int32, device=dev)
+    c = torch.zeros(slots, dtype=torch.int32, device=dev)
+    engine.classify_streams_device(d_arena.data_ptr(), arena.nbytes, d_off.data_ptr(), d_len.data_ptr(),
+                                   d_conn.data_ptr(), n, max_frames, f_off.data_ptr(), f_len.data_ptr(),
+                                   f_conn.data_ptr(), nfr.data_ptr(), v.data_ptr(), r.data_ptr(), c.data_ptr())
+    torch.cuda.synchronize()
+    f_off, f_len, f_conn = f_off.cpu().numpy().view(np.uint64), f_len.cpu().numpy().view(np.uint32), \
+        f_conn.cpu().numpy().view(np.uint32)
+    nfr = nfr.cpu().numpy()
+    modes = {i: int(w.conns["flags"][i]) & 3 for i in range(len(w.conns))}
+    whole = 0
+    sel = []
+    for s in range(n):
+        proto = int(w.conns["proto"][conns[s]])
+        want = _frames(streams[s], proto, modes[conns[s]], max_frames)
+        got = [int(x) - int(s_off[s]) for x in f_off[s * max_frames:s * max_frames + nfr[s]]]
+        assert got == want, (s, proto, got[:8], want[:8])
+        assert all(int(x) == len(streams[s]) - g for x, g in zip(f_len[s * max_frames:], got))
+        assert (f_conn[s * max_frames:s * max_frames + nfr[s]] == conns[s]).all()
+        assert (f_len[s * max_frames + nfr[s]:(s + 1) * max_frames] == 0).all()
+        if got == [int(b) for b in bounds[s][:len(got)]]:
+            whole += 1
+        sel.extend(range(s * max_frames, s * max_frames + nfr[s]))
+    sel = np.array(sel)
+    ref = oracle.Policy(w.policy).classify(w.conns, arena, f_off[sel], f_len[sel], f_conn[sel], 8)
+    assert (v.cpu().numpy()[sel] == ref[0]).all()
+    assert (r.cpu().numpy()[sel] == ref[1]).all()
+    assert (c.cpu().numpy().view(np.uint32)[sel] == ref[2]).all()
+    empty = np.setdiff1d(np.arange(slots), sel)
+    assert (v.cpu().numpy()[empty] == 4).all()  # empty slots: UNSUPPORTED
+    return n, whole, len(sel)
+
+
+@pytest.mark.parametrize("proto", ["http", "kafka", "memcache", "r2d2", "cassandra"])
+def test_frame_streams_match_the_scan_and_the_oracle(engine, oracle, proto):
+    w = {"http": lambda: gen.http_workload(2, 3000, nconns=64),
+         "kafka": lambda: gen.kafka_workload(3000, nconns=64),
+         "memcache": lambda: gen.memcache_workload(3000, nconns=64),
+         "r2d2": lambda: gen.r2d2_workload(2000, nconns=32),
+         "cassandra": lambda: gen.cassandra_workload(2000, nconns=16)}[proto]()
+    n, whole, frames = _run(engine, oracle, w)
+    assert frames > n * 2  # several frames per stream
+    if proto in ("http", "kafka"):  # well-formed generated requests: the frames are the requests
+        assert whole >= n * 3 // 4, (whole, n)
