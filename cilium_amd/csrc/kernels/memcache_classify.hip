@@ -617,7 +617,17 @@ __device__ __forceinline__ void mc_classify(Batch B, McTables T, const uint32_t 
     extern __shared__ __attribute__((aligned(16))) uint8_t mc_lds[];
     if (T.images_len && T.images_len <= kMcLdsImages) {
         const uint32_t n16 = (T.images_len + 15) / 16;
-        for (uint32_t i = threadIdx.x; i < n16; i += kBlock) ((uint4 *)mc_lds)[i] = ((const uint4 *)T.images)[i];
+        // every load issued before the first store: one memory round trip per
+        // 32 KiB, not one per 4 KiB (a one-request launch waits on this)
+        constexpr uint32_t kIters = 8;  // kMcLdsImages / (16 * kBlock)
+        static_assert(kIters * 16 * kBlock == kMcLdsImages, "staging rounds");
+        uint4 t[kIters];
+#pragma unroll
+        for (uint32_t k = 0; k < kIters; k++)
+            if (threadIdx.x + k * kBlock < n16) t[k] = ((const uint4 *)T.images)[threadIdx.x + k * kBlock];
+#pragma unroll
+        for (uint32_t k = 0; k < kIters; k++)
+            if (threadIdx.x + k * kBlock < n16) ((uint4 *)mc_lds)[threadIdx.x + k * kBlock] = t[k];
         __syncthreads();
         mc_loop<kNfa, true, kCh>(B, T, mc_lds, sel, sel2, sel_count, answer_other);
     } else {

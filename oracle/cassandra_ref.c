@@ -60,11 +60,6 @@ static void sb_rune(sbuf *b, int32_t r) {  /* utf8.EncodeRune */
     }
 }
 
-static char *sdup(const char *s) {
-    char *d = malloc(strlen(s) + 1);
-    strcpy(d, s);
-    return d;
-}
 
 /* utf8.DecodeRuneInString: (rune, width); invalid => U+FFFD width 1 */
 static int dec(const uint8_t *s, size_t n, int32_t *r) {
@@ -166,8 +161,11 @@ static fields_t go_fields(const uint8_t *s, size_t n) {
 static int feq(const fields_t *f, int i, const char *w) { return f->len[i] == strlen(w) && !memcmp(f->f[i], w, f->len[i]); }
 
 /* ---------------- per-connection parser state ---------------- */
-typedef struct { uint16_t stream; char *path; } by_stream_t;
-typedef struct { char *id; size_t idlen; char *path; } by_id_t;
+/* Paths are Go strings: bytes with a length (a keyspace or table token may
+ * hold any byte, NUL included, e.g. a USE whose query runs on past its frame),
+ * NUL-terminated only for convenience. */
+typedef struct { uint16_t stream; char *path; size_t plen; } by_stream_t;
+typedef struct { char *id; size_t idlen; char *path; size_t plen; } by_id_t;
 struct ref_cass {
     sbuf keyspace;
     by_stream_t *bs; int nbs;
@@ -191,7 +189,8 @@ enum { Q_OK = 0, Q_INVALID = 1, Q_PANIC = 2 };
 
 /* parseQuery (cassandraparser.go:368-469); on Q_OK *action / *table are
  * malloc'd strings. */
-static int parse_query(ref_cass *st, const uint8_t *q, size_t qn, char **action, char **table) {
+static int parse_query(ref_cass *st, const uint8_t *q, size_t qn, char **action, size_t *alen, char **table,
+                       size_t *tlen) {
     while (qn > 0 && q[qn - 1] == ';') qn--;  /* strings.TrimRight(query, ";") */
     sbuf low = {0};
     go_to_lower(q, qn, &low);
@@ -253,7 +252,7 @@ static int parse_query(ref_cass *st, const uint8_t *q, size_t qn, char **action,
         goto out;
     }
     if (!tab.p) sb_put(&tab, "", 0);
-    if (tab.n > 0 && !memchr(tab.p, '.', tab.n) && strcmp((char *)act.p, "use")) {
+    if (tab.n > 0 && !memchr(tab.p, '.', tab.n) && !(act.n == 3 && !memcmp(act.p, "use", 3))) {
         sbuf t2 = {0};
         sb_put(&t2, st->keyspace.p, st->keyspace.n);
         sb_byte(&t2, '.');
@@ -264,7 +263,7 @@ static int parse_query(ref_cass *st, const uint8_t *q, size_t qn, char **action,
     rc = Q_OK;
 out:
     fields_free(&f);
-    if (rc == Q_OK) { *action = (char *)act.p; *table = (char *)tab.p; }
+    if (rc == Q_OK) { *action = (char *)act.p; *alen = act.n; *table = (char *)tab.p; *tlen = tab.n; }
     else { free(act.p); free(tab.p); }
     return rc;
 }
@@ -276,11 +275,23 @@ static const char *kOpcodes[17] = {"error", "startup", "ready", "authenticate", 
 static uint32_t be32(const uint8_t *b) { return (uint32_t)b[0] << 24 | (uint32_t)b[1] << 16 | (uint32_t)b[2] << 8 | b[3]; }
 static uint16_t be16(const uint8_t *b) { return (uint16_t)(b[0] << 8 | b[1]); }
 
-static char *join_path(const char *op, const char *action, const char *table) {
-    size_t n = 3 + strlen(op) + strlen(action) + strlen(table) + 1;
-    char *p = malloc(n);
-    strcpy(p, "/"); strcat(p, op); strcat(p, "/"); strcat(p, action); strcat(p, "/"); strcat(p, table);
+/* "/" + op + "/" + action + "/" + table, with its length */
+static char *join_path(const char *op, const char *action, size_t alen, const char *table, size_t tlen,
+                       size_t *plen) {
+    const size_t ol = strlen(op);
+    *plen = 3 + ol + alen + tlen;
+    char *p = malloc(*plen + 1), *w = p;
+    *w++ = '/'; memcpy(w, op, ol); w += ol;
+    *w++ = '/'; memcpy(w, action, alen); w += alen;
+    *w++ = '/'; memcpy(w, table, tlen); w += tlen;
+    *w = 0;
     return p;
+}
+static char *bdup(const char *s, size_t n) {
+    char *d = malloc(n + 1);
+    memcpy(d, s, n);
+    d[n] = 0;
+    return d;
 }
 
 /* cassandraParseRequest on a complete frame; returns 0 (ok, *path set),
@@ -293,8 +304,9 @@ static char *join_path(const char *op, const char *action, const char *table) {
  * exactly n -- a single slice is copied by append, whose capacity Go rounds
  * up to its allocator's size class; reads into that zeroed slack are not
  * restated: parity unpinned there, no reference test reaches it). */
-static int parse_request(ref_cass *st, const uint8_t *d, uint32_t cap, char **path, int *unprepared) {
+static int parse_request(ref_cass *st, const uint8_t *d, uint32_t cap, char **path, size_t *plen, int *unprepared) {
     *path = NULL;
+    *plen = 0;
     *unprepared = 0;
     if (d[0] & 0x80) return 2;
     if (d[1] & 0x01) return 2;
@@ -306,24 +318,31 @@ static int parse_request(ref_cass *st, const uint8_t *d, uint32_t cap, char **pa
         const uint32_t end = 13u + ql;  /* uint32 arithmetic, as in Go */
         if (end < 13u || end > cap) return -1;
         char *action, *table;
-        int rc = parse_query(st, d + 13, ql, &action, &table);
+        size_t alen, tlen;
+        int rc = parse_query(st, d + 13, ql, &action, &alen, &table, &tlen);
         if (rc == Q_PANIC) return -1;
         if (rc == Q_INVALID) return 2;
-        *path = join_path(name, action, table);
+        *path = join_path(name, action, alen, table, tlen, plen);
         free(action); free(table);
-        if (op == 0x09) {  /* stash, "prepare" -> "execute" (first occurrence) */
+        if (op == 0x09) {  /* stash, "prepare" -> "execute" (strings.Replace, first occurrence) */
             const uint16_t sid = be16(d + 2);
-            char *x = malloc(strlen(*path) + 8);
-            char *hit = strstr(*path, "prepare");
-            if (hit) {
-                size_t pre = (size_t)(hit - *path);
-                memcpy(x, *path, pre); strcpy(x + pre, "execute"); strcat(x, hit + 7);
-            } else strcpy(x, *path);
+            char *x = malloc(*plen + 8);
+            size_t xl = *plen, pre = 0;
+            while (pre + 7 <= *plen && memcmp(*path + pre, "prepare", 7)) pre++;
+            if (pre + 7 <= *plen) {
+                memcpy(x, *path, pre);
+                memcpy(x + pre, "execute", 7);
+                memcpy(x + pre + 7, *path + pre + 7, *plen - pre - 7);
+            } else {
+                memcpy(x, *path, *plen);
+            }
+            x[xl] = 0;
             int k;
             for (k = 0; k < st->nbs; k++) if (st->bs[k].stream == sid) break;
             if (k == st->nbs) { st->bs = realloc(st->bs, (size_t)(st->nbs + 1) * sizeof *st->bs); st->bs[k].stream = sid; st->nbs++; }
             else free(st->bs[k].path);
             st->bs[k].path = x;
+            st->bs[k].plen = xl;
         }
         return 0;
     }
@@ -333,8 +352,9 @@ static int parse_request(ref_cass *st, const uint8_t *d, uint32_t cap, char **pa
         const uint16_t il = be16(d + 9);
         if (11u + il > cap) return -1;
         for (int k = 0; k < st->nbi; k++)
-            if (st->bi[k].idlen == il && !memcmp(st->bi[k].id, d + 11, il) && st->bi[k].path[0]) {
-                *path = sdup(st->bi[k].path);
+            if (st->bi[k].idlen == il && !memcmp(st->bi[k].id, d + 11, il) && st->bi[k].plen) {
+                *path = bdup(st->bi[k].path, st->bi[k].plen);
+                *plen = st->bi[k].plen;
                 return 0;
             }
         *unprepared = 1;
@@ -342,6 +362,7 @@ static int parse_request(ref_cass *st, const uint8_t *d, uint32_t cap, char **pa
     }
     *path = malloc(strlen(name) + 2);
     strcpy(*path, "/"); strcat(*path, name);
+    *plen = strlen(*path);
     return 0;
 }
 
@@ -359,7 +380,7 @@ static int parse_reply(ref_cass *st, const uint8_t *d, uint32_t n) {
     const uint16_t il = be16(d + 13);
     if (15u + il > n) return -1;
     for (int k = 0; k < st->nbs; k++)
-        if (st->bs[k].stream == sid && st->bs[k].path[0]) {
+        if (st->bs[k].stream == sid && st->bs[k].plen) {
             int j;
             for (j = 0; j < st->nbi; j++) if (st->bi[j].idlen == il && !memcmp(st->bi[j].id, d + 15, il)) break;
             if (j == st->nbi) {
@@ -367,29 +388,32 @@ static int parse_reply(ref_cass *st, const uint8_t *d, uint32_t n) {
                 st->bi[j].id = malloc(il + 1u); memcpy(st->bi[j].id, d + 15, il); st->bi[j].idlen = il;
                 st->nbi++;
             } else free(st->bi[j].path);
-            st->bi[j].path = sdup(st->bs[k].path);
+            st->bi[j].path = bdup(st->bs[k].path, st->bs[k].plen);
+            st->bi[j].plen = st->bs[k].plen;
         }
     return 0;
 }
 
 /* ---------------- policy ---------------- */
 /* CassandraRule.Matches (:58-95) */
-static int cass_rule_matches(const ref_mc_rule *r, const char *path) {
+static int cass_rule_matches(const ref_mc_rule *r, const char *path, size_t plen) {
     /* strings.Split(path, "/") */
     int nparts = 1;
-    for (const char *p = path; *p; p++) if (*p == '/') nparts++;
+    for (size_t i = 0; i < plen; i++) if (path[i] == '/') nparts++;
     if (nparts <= 2) return 1;
     if (nparts < 4) return 0;
-    const char *s2 = strchr(strchr(path, '/') + 1, '/') + 1;  /* parts[2] */
-    const char *s3 = strchr(s2, '/') + 1;                     /* parts[3] */
-    const char *e3 = strchr(s3, '/');
-    size_t l2 = (size_t)(s3 - 1 - s2), l3 = e3 ? (size_t)(e3 - s3) : strlen(s3);
+    const char *end = path + plen;
+    const char *s1 = (const char *)memchr(path, '/', plen) + 1;
+    const char *s2 = (const char *)memchr(s1, '/', (size_t)(end - s1)) + 1;  /* parts[2] */
+    const char *s3 = (const char *)memchr(s2, '/', (size_t)(end - s2)) + 1;  /* parts[3] */
+    const char *e3 = (const char *)memchr(s3, '/', (size_t)(end - s3));
+    size_t l2 = (size_t)(s3 - 1 - s2), l3 = e3 ? (size_t)(e3 - s3) : (size_t)(end - s3);
     if (r->cass_action && (strlen(r->cass_action) != l2 || memcmp(r->cass_action, s2, l2))) return 0;
     if (l3 > 0 && r->cass_table && !ref_re_match(r->cass_table, (const uint8_t *)s3, l3, 0)) return 0;
     return 1;
 }
 
-static int cass_port_rules_match(const ref_port *pp, uint64_t remote, const char *path, int32_t *rule) {
+static int cass_port_rules_match(const ref_port *pp, uint64_t remote, const char *path, size_t plen, int32_t *rule) {
     *rule = -1;
     if (!ref_px_have_l7(pp)) return 1;
     if (pp->nrules == 0) return 1;
@@ -399,13 +423,13 @@ static int cass_port_rules_match(const ref_port *pp, uint64_t remote, const char
         if (ref_px_nl7(pr) == 0) return 1;
         if (pr->l7type != L7T_L7 || !pr->l7proto || strcmp(pr->l7proto, "cassandra")) continue;
         for (int k = 0; k < pr->nl7; k++)
-            if (cass_rule_matches(&pr->l7[k], path)) { *rule = pr->l7[k].id; return 1; }
+            if (cass_rule_matches(&pr->l7[k], path, plen)) { *rule = pr->l7[k].id; return 1; }
     }
     return 0;
 }
 
 /* Connection.Matches over the proxylib policymap */
-static int cass_matches(const ref_policy *pol, const ref_conn_t *c, const char *path, int32_t *rule) {
+static int cass_matches(const ref_policy *pol, const ref_conn_t *c, const char *path, size_t plen, int32_t *rule) {
     *rule = -1;
     if (c->policy < 0 || c->policy >= pol->np) return 0;
     const ref_port *ex, *wc;
@@ -413,7 +437,7 @@ static int cass_matches(const ref_policy *pol, const ref_conn_t *c, const char *
     const ref_port *cands[2] = {ex, wc};
     for (int k = 0; k < 2; k++) {
         if (!cands[k] || !ref_px_installed(cands[k])) continue;
-        if (cass_port_rules_match(cands[k], c->src_id, path, rule)) return 1;
+        if (cass_port_rules_match(cands[k], c->src_id, path, plen, rule)) return 1;
     }
     return 0;
 }
@@ -435,8 +459,9 @@ int ref_cass_request(ref_cass *st, const ref_policy *pol, const ref_conn_t *c, c
     if (missing > 0) { *nout = missing; return 0; }
     const uint32_t fl = 9 + rl;
     char *path;
+    size_t plen;
     int unprepared;
-    int rc = parse_request(st, d, n, &path, &unprepared);
+    int rc = parse_request(st, d, n, &path, &plen, &unprepared);
     if (rc < 0) return -1;
     if (rc > 0) {
         if (unprepared) {  /* sendUnpreparedMsg (:586-601): header + [short bytes] id */
@@ -451,7 +476,7 @@ int ref_cass_request(ref_cass *st, const ref_policy *pol, const ref_conn_t *c, c
         *nout = rc;
         return 4;
     }
-    const int ok = cass_matches(pol, c, path, rule);
+    const int ok = cass_matches(pol, c, path, plen, rule);
     if (path_out) *path_out = path; else free(path);
     *nout = fl;
     if (ok) return 1;
@@ -483,7 +508,8 @@ int ref_cass_reply(ref_cass *st, const uint8_t *d, uint32_t n, int64_t *nout) {
  * (updated by a USE); returns Q_OK / Q_INVALID / Q_PANIC. */
 int ref_cass_parse_query(ref_cass *st, const uint8_t *q, size_t n, char *action, size_t alen, char *table, size_t tlen) {
     char *a, *t;
-    int rc = parse_query(st, q, n, &a, &t);
+    size_t al, tl;
+    int rc = parse_query(st, q, n, &a, &al, &t, &tl);
     if (rc == Q_OK) {
         snprintf(action, alen, "%s", a);
         snprintf(table, tlen, "%s", t);

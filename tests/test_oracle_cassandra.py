@@ -185,3 +185,30 @@ def test_batch_api_keyspace_in_order():
     ALLOW, DENY = 1, 0
     assert v.tolist() == [DENY, DENY, ALLOW, DENY, DENY, DENY]
     assert c.tolist() == [len(x) for x in reqs]
+
+
+def test_keyspace_with_nul_bytes():
+    """Go strings hold any byte: a USE whose query runs on past its frame
+    (capacity-bounded slice of the joined input) takes a keyspace token with
+    NUL bytes in it, and the next table is that token + "." + table; the rule
+    regex sees every byte of it (the oracle once cut the path at the first NUL
+    as a C string; found by the device framing test, tests/test_gpu_frame.py)."""
+    pol = refpy.Policy(kat_policy("cpn", {"query_action": "insert", "query_table": "users$"}))
+    conns = conns_array([(0, 80, 1, PROTO_CASSANDRA, 1, 2)])
+
+    def q(s, ql=None):
+        b = s.encode()
+        body = (len(b) if ql is None else ql).to_bytes(4, "big") + b
+        return bytes([4, 0, 0, 1, 7]) + len(body).to_bytes(4, "big") + body
+
+    use = q("use x", ql=100)  # the query is the next 100 bytes of the input
+    ins = q("insert into users x")
+    pad = q("select * from t") * 8
+    stream = use + ins + pad
+    # each request handed the input from its start to the end, as proxylib does
+    offs = np.array([0, len(use)], np.uint64)
+    lens = np.array([len(stream), len(stream) - len(use)], np.uint32)
+    arena = np.frombuffer(stream, np.uint8).copy()
+    v, r, c = pol.classify(conns, arena, offs, lens, np.zeros(2, np.uint32))
+    assert c.tolist() == [len(use), len(ins)]
+    assert v.tolist()[1] == 1  # keyspace "x\x04\x00...": the table still ends in "users"
