@@ -10,10 +10,11 @@
 // that take the same decode path for about as long, and no longer waits on one
 // long produce request among short fetches (a wave runs as long as its longest
 // lane, and divergent paths run one after the other).  The class comes from
-// the request's length alone: this kernel reads no request bytes (round 3 read
-// each Kafka request's api key and each memcached request's first byte, one
-// HBM line per request, 5 of its 7 GB per cfg5 launch); the memcached kernel
-// splits text from binary itself, from bytes it reads anyway.  One block owns
+// the request's length, and only where the length cannot tell a fetch from a
+// produce from the api key: round 3 read each Kafka request's api key and each
+// memcached request's first byte, one HBM line per request, 5 of its 7 GB per
+// cfg5 launch; the memcached kernel now splits text from binary itself, from
+// bytes it reads anyway.  One block owns
 // 2048 consecutive requests (8 per lane, protocol kept in registers between
 // the count and the write pass) and takes its slot range with one atomic per
 // protocol.
@@ -43,10 +44,15 @@ static_assert(kKafkaClasses + 4 <= 31, "counts[31] holds the compressed-Kafka co
 // and partitions a hundred or two, a produce carries its messages); a request
 // in the "wrong" class only shares a wave with a different path: every class
 // takes every kind, so this is scheduling, not semantics.
-__device__ __forceinline__ uint8_t kafka_class(uint32_t len) {
+// Lengths in [kKafkaAmbLo, kKafkaAmbHi) are where a fetch of many partitions
+// and a produce of one small message overlap: there (only there) the api key
+// (bytes 4-5) is read.  kind: that key, 0xFFFF when not read.
+constexpr uint32_t kKafkaAmbLo = 147, kKafkaAmbHi = 256;
+__device__ __forceinline__ uint8_t kafka_class(uint32_t len, uint32_t kind) {
     if (kKafkaClasses == 1) return 0;
     if (len < 67) return 1;   // no message set
-    if (len < 211) return 0;  // fetch
+    if (len < kKafkaAmbLo) return 0;  // fetch
+    if (len < kKafkaAmbHi && kind != 0) return kind == 1 ? 0 : 1;
     return len < 384 ? 2 : len < 640 ? 3 : len < 896 ? 4 : len < 1280 ? 5 : len < 2048 ? 6 : 7;  // produce
 }
 }  // namespace
@@ -103,6 +109,14 @@ __global__ __launch_bounds__(kBlock) void partition_kernel(Batch B, uint32_t *__
             len[r] = B.lens[idx];
         }
     }
+    uint32_t kd[kPer];  // Kafka api key where the length does not settle the class
+#pragma unroll
+    for (int r = 0; r < kPer; r++) {
+        kd[r] = 0xFFFFu;
+        if ((pw[r] & 0xFF) == PROTO_KAFKA && len[r] >= kKafkaAmbLo && len[r] < kKafkaAmbHi &&
+            l7_in_arena(off[r], len[r], B.arena_len))
+            kd[r] = (uint32_t)B.arena[off[r] + 4] << 8 | B.arena[off[r] + 5];
+    }
 #pragma unroll
     for (int r = 0; r < kPer; r++) {
         const uint64_t idx = start + (uint64_t)r * kBlock + threadIdx.x;
@@ -110,7 +124,7 @@ __global__ __launch_bounds__(kBlock) void partition_kernel(Batch B, uint32_t *__
         if (idx < n) {
             const uint32_t proto = pw[r] & 0xFF;
             if (proto == PROTO_KAFKA) {
-                cls = 1 + kafka_class(l7_in_arena(off[r], len[r], B.arena_len) ? len[r] : 0);
+                cls = 1 + kafka_class(l7_in_arena(off[r], len[r], B.arena_len) ? len[r] : 0, kd[r]);
             }
             else if (proto == PROTO_MEMCACHE) {
                 cls = 1 + kMcText;  // one list: the memcached kernel splits it by parser itself
