@@ -80,8 +80,8 @@ __global__ __launch_bounds__(kBlock) void partition_kernel(Batch B, uint32_t *__
     uint8_t p[kPer];  // class + 1, 0 = none
     uint32_t cnt[kClasses] = {};
     // The rows' loads go out phase by phase (connection ids, connections,
-    // Kafka offsets / lengths), so a block waits three memory latencies, not
-    // three per row.
+    // Kafka lengths, offsets, api keys), so a block waits five memory
+    // latencies, not five per row.
     uint32_t ci[kPer], pw[kPer];
 #pragma unroll
     for (int r = 0; r < kPer; r++) {
@@ -96,25 +96,26 @@ __global__ __launch_bounds__(kBlock) void partition_kernel(Batch B, uint32_t *__
             pw[r] = (uint32_t)c.proto | (uint32_t)c.flags << 8;
         }
     }
-    uint64_t off[kPer];
+    // Kafka: the length; the offset only where the api key is read (the
+    // classes are scheduling: the Kafka kernel checks every request's bytes
+    // against the arena itself)
     uint32_t len[kPer];
 #pragma unroll
     for (int r = 0; r < kPer; r++) {
         const uint64_t idx = start + (uint64_t)r * kBlock + threadIdx.x;
-        const uint32_t proto = pw[r] & 0xFF;
-        off[r] = 0;
-        len[r] = 0;
-        if (proto == PROTO_KAFKA) {
-            off[r] = B.offs[idx];
-            len[r] = B.lens[idx];
-        }
+        len[r] = (pw[r] & 0xFF) == PROTO_KAFKA ? B.lens[idx] : 0;
+    }
+    uint64_t off[kPer];
+#pragma unroll
+    for (int r = 0; r < kPer; r++) {
+        const uint64_t idx = start + (uint64_t)r * kBlock + threadIdx.x;
+        off[r] = (pw[r] & 0xFF) == PROTO_KAFKA && len[r] >= kKafkaAmbLo && len[r] < kKafkaAmbHi ? B.offs[idx] : ~0ull;
     }
     uint32_t kd[kPer];  // Kafka api key where the length does not settle the class
 #pragma unroll
     for (int r = 0; r < kPer; r++) {
         kd[r] = 0xFFFFu;
-        if ((pw[r] & 0xFF) == PROTO_KAFKA && len[r] >= kKafkaAmbLo && len[r] < kKafkaAmbHi &&
-            l7_in_arena(off[r], len[r], B.arena_len))
+        if (off[r] != ~0ull && l7_in_arena(off[r], len[r], B.arena_len))
             kd[r] = (uint32_t)B.arena[off[r] + 4] << 8 | B.arena[off[r] + 5];
     }
 #pragma unroll
@@ -124,7 +125,7 @@ __global__ __launch_bounds__(kBlock) void partition_kernel(Batch B, uint32_t *__
         if (idx < n) {
             const uint32_t proto = pw[r] & 0xFF;
             if (proto == PROTO_KAFKA) {
-                cls = 1 + kafka_class(l7_in_arena(off[r], len[r], B.arena_len) ? len[r] : 0, kd[r]);
+                cls = 1 + kafka_class(len[r], kd[r]);
             }
             else if (proto == PROTO_MEMCACHE) {
                 cls = 1 + kMcText;  // one list: the memcached kernel splits it by parser itself
