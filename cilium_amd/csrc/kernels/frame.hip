@@ -33,9 +33,26 @@ constexpr int kBlock = 128;
 struct Stream {
     const uint8_t *b;  // stream start
     uint64_t n;        // stream bytes
+    uint64_t blk;      // the 16-byte block held in w (~0: none)
+    uint4 w;
 };
 
-__device__ __forceinline__ uint32_t sbyte(const Stream &S, uint64_t i) { return S.b[i]; }
+// byte i of the stream, through a one-block cache: a lane scanning a line
+// issues one 16-byte load per block instead of one (dependent) load per byte
+__device__ __forceinline__ uint32_t sbyte(Stream &S, uint64_t i) {
+    const uint64_t a = (uint64_t)S.b + i, base = a & ~15ull;
+    if (base != S.blk) {
+        S.w = gload16(base);
+        S.blk = base;
+    }
+    const uint32_t k = (uint32_t)(a & 15);
+    const uint32_t d = k < 8 ? (k < 4 ? S.w.x : S.w.y) : (k < 12 ? S.w.z : S.w.w);
+    return (d >> (8 * (k & 3))) & 0xFF;
+}
+
+// byte i straight from memory (short lines: the memcached token scan, where
+// the block cache's compare and select cost more than the L1 hit they save)
+__device__ __forceinline__ uint32_t dbyte(const Stream &S, uint64_t i) { return S.b[i]; }
 
 __device__ __forceinline__ uint32_t eq16(uint4 w, uint32_t c) {  // bit k: byte k of w == c
     const uint32_t cc = c * 0x01010101u;
@@ -48,29 +65,37 @@ __device__ __forceinline__ uint32_t eq16(uint4 w, uint32_t c) {  // bit k: byte 
 }
 
 // first i in [from, S.n) with b[i] == '\r' and b[i + 1] == '\n' (S.n: none),
-// 16 bytes a step
-__device__ uint64_t find_crlf(const Stream &S, uint64_t from) {
+// 64 bytes (four 16-byte loads in flight) a step
+__device__ uint64_t find_crlf(Stream &S, uint64_t from) {
     if (from >= S.n) return S.n;
     const uint64_t a = (uint64_t)S.b + from;
     uint64_t base = a & ~15ull;
     const uint64_t end = (uint64_t)S.b + S.n;
     uint32_t skip = (uint32_t)(a - base);
-    uint32_t prev_cr = 0;  // the last chunk ended in '\r'
-    for (; base < end; base += 16) {
-        const uint4 w = gload16(base);
-        uint32_t valid = end - base >= 16 ? 0xFFFFu : (1u << (uint32_t)(end - base)) - 1u;
-        valid &= 0xFFFFu << skip;
-        skip = 0;
-        const uint32_t cr = eq16(w, '\r') & valid, lf = eq16(w, '\n') & valid;
-        const uint32_t hit = ((cr << 1) | prev_cr) & lf;  // LF right after a CR
-        if (hit) return base - (uint64_t)S.b + __builtin_ctz(hit) - 1;
-        prev_cr = (cr >> 15) & 1;
+    uint32_t prev_cr = 0;  // the last block ended in '\r'
+    for (; base < end; base += 64) {
+        uint4 w[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            if (base + 16 * k < end) w[k] = gload16(base + 16 * k);
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint64_t bk = base + 16 * k;
+            if (bk >= end) break;
+            uint32_t valid = end - bk >= 16 ? 0xFFFFu : (1u << (uint32_t)(end - bk)) - 1u;
+            valid &= 0xFFFFu << skip;
+            skip = 0;
+            const uint32_t cr = eq16(w[k], '\r') & valid, lf = eq16(w[k], '\n') & valid;
+            const uint32_t hit = ((cr << 1) | prev_cr) & lf;  // LF right after a CR
+            if (hit) return bk - (uint64_t)S.b + __builtin_ctz(hit) - 1;
+            prev_cr = (cr >> 15) & 1;
+        }
     }
     return S.n;
 }
 
 // NextKafka: [size int32 BE][size bytes]; size <= 0 or past the stream: stop
-__device__ uint64_t next_kafka(const Stream &S, uint64_t p) {
+__device__ uint64_t next_kafka(Stream &S, uint64_t p) {
     if (S.n - p < 4) return 0;
     const int32_t size = (int32_t)(sbyte(S, p) << 24 | sbyte(S, p + 1) << 16 | sbyte(S, p + 2) << 8 | sbyte(S, p + 3));
     if (size <= 0 || (uint64_t)size + 4 > S.n - p) return 0;
@@ -78,7 +103,7 @@ __device__ uint64_t next_kafka(const Stream &S, uint64_t p) {
 }
 
 // NextMcBinary: 24-byte header, total body length at bytes 8..11
-__device__ uint64_t next_mc_binary(const Stream &S, uint64_t p) {
+__device__ uint64_t next_mc_binary(Stream &S, uint64_t p) {
     if (S.n - p < 24) return 0;
     const uint64_t body = sbyte(S, p + 8) << 24 | sbyte(S, p + 9) << 16 | sbyte(S, p + 10) << 8 | sbyte(S, p + 11);
     return body + 24 <= S.n - p ? p + 24 + body : 0;
@@ -86,14 +111,14 @@ __device__ uint64_t next_mc_binary(const Stream &S, uint64_t p) {
 
 // bytes.Fields' separators (unicode.IsSpace) at s[i], as shim.cc SpaceLen:
 // the width of the space rune there, 0 for none
-__device__ uint32_t space_len(const Stream &S, uint64_t i, uint64_t n) {
-    const uint32_t c = sbyte(S, i);
+__device__ uint32_t space_len(Stream &S, uint64_t i, uint64_t n) {
+    const uint32_t c = dbyte(S, i);
     if (c == ' ' || (c >= 0x09 && c <= 0x0D)) return 1;
     if (c < 0xC2 || c > 0xE3 || i + 1 >= n) return 0;
-    const uint32_t c1 = sbyte(S, i + 1);
+    const uint32_t c1 = dbyte(S, i + 1);
     if (c == 0xC2) return (c1 == 0x85 || c1 == 0xA0) ? 2 : 0;
     if (i + 2 >= n) return 0;
-    const uint32_t c2 = sbyte(S, i + 2);
+    const uint32_t c2 = dbyte(S, i + 2);
     if (c == 0xE1) return (c1 == 0x9A && c2 == 0x80) ? 3 : 0;
     if (c == 0xE2 && c1 == 0x80) return ((c2 >= 0x80 && c2 <= 0x8A) || c2 == 0xA8 || c2 == 0xA9 || c2 == 0xAF) ? 3 : 0;
     if (c == 0xE2 && c1 == 0x81) return c2 == 0x9F ? 3 : 0;
@@ -103,7 +128,7 @@ __device__ uint32_t space_len(const Stream &S, uint64_t i, uint64_t n) {
 
 // NextMcText: the line to "\r\n"; set / add / replace / append / prepend / cas
 // also carry <bytes> + "\r\n" of data (tokens[4], a non-negative decimal)
-__device__ uint64_t next_mc_text(const Stream &S, uint64_t p) {
+__device__ uint64_t next_mc_text(Stream &S, uint64_t p) {
     const uint64_t lf = find_crlf(S, p);
     if (lf >= S.n) return 0;
     // tokens 0 and 4 of the line [p, lf)
@@ -142,7 +167,7 @@ __device__ uint64_t next_mc_text(const Stream &S, uint64_t p) {
         auto is = [&](const char *w, uint64_t wl) {
             if (k != wl) return false;
             for (uint64_t j = 0; j < wl; j++)
-                if (sbyte(S, t0 + j) != (uint32_t)(uint8_t)w[j]) return false;
+                if (dbyte(S, t0 + j) != (uint32_t)(uint8_t)w[j]) return false;
             return true;
         };
         storage = is("set", 3) || is("add", 3) || is("replace", 7) || is("append", 6) || is("prepend", 7) || is("cas", 3);
@@ -152,14 +177,14 @@ __device__ uint64_t next_mc_text(const Stream &S, uint64_t p) {
         // strtoll(tokens[4]) with the whole token consumed, >= 0
         uint64_t i = t4;
         bool neg = false;
-        if (i < t4e && (sbyte(S, i) == '+' || sbyte(S, i) == '-')) {
-            neg = sbyte(S, i) == '-';
+        if (i < t4e && (dbyte(S, i) == '+' || dbyte(S, i) == '-')) {
+            neg = dbyte(S, i) == '-';
             i++;
         }
         if (i >= t4e) return 0;
         uint64_t v = 0;
         for (; i < t4e; i++) {
-            const uint32_t d = sbyte(S, i) - '0';
+            const uint32_t d = dbyte(S, i) - '0';
             if (d > 9) return 0;
             v = v * 10 + d;
             if (v > (1ull << 40)) return 0;  // (strtoll saturates; no such frame fits a stream)
@@ -171,7 +196,7 @@ __device__ uint64_t next_mc_text(const Stream &S, uint64_t p) {
 }
 
 // NextLine (r2d2): to "\r\n"
-__device__ uint64_t next_line(const Stream &S, uint64_t p) {
+__device__ uint64_t next_line(Stream &S, uint64_t p) {
     const uint64_t lf = find_crlf(S, p);
     return lf >= S.n ? 0 : lf + 2;
 }
@@ -181,7 +206,7 @@ __device__ __forceinline__ uint32_t lower(uint32_t c) { return c - 'A' < 26u ? c
 // NextHttp: the head to "\r\n\r\n" plus Content-Length (strtoull of the value);
 // a Transfer-Encoding header stops the walk (chunked bodies are framed by the
 // classifier)
-__device__ uint64_t next_http(const Stream &S, uint64_t p) {
+__device__ uint64_t next_http(Stream &S, uint64_t p) {
     uint64_t ls = find_crlf(S, p);
     if (ls >= S.n) return 0;
     ls += 2;
@@ -228,7 +253,7 @@ __device__ uint64_t next_http(const Stream &S, uint64_t p) {
 }
 
 // cassandra: 9-byte header, body length at bytes 5..8
-__device__ uint64_t next_cassandra(const Stream &S, uint64_t p) {
+__device__ uint64_t next_cassandra(Stream &S, uint64_t p) {
     if (S.n - p < 9) return 0;
     const uint64_t fl = 9 + (uint64_t)(sbyte(S, p + 5) << 24 | sbyte(S, p + 6) << 16 | sbyte(S, p + 7) << 8 | sbyte(S, p + 8));
     return fl <= S.n - p ? p + fl : 0;
@@ -258,7 +283,7 @@ __global__ __launch_bounds__(kBlock) void frame_streams_kernel(const uint8_t *__
         uint32_t k = 0;
         if (l7_in_arena(so, sl, arena_len) && sl > 0 && ci < nconns) {
             const DevConn c = conns[ci];
-            const Stream S{arena + so, sl};
+            Stream S{arena + so, sl, ~0ull, make_uint4(0, 0, 0, 0)};
             uint32_t mode = c.flags & 3;  // memcached: the connection's parser, else the first byte's
             if (c.proto == PROTO_MEMCACHE && mode == 0) mode = sbyte(S, 0) >= 0x80 ? 2 : 1;
             for (uint64_t p = 0; p < S.n && k < max_frames;) {
