@@ -106,3 +106,25 @@ def test_connection_outside_image_compiles_locally():
     c.set_connections(w.conns)
     assert b.tables_compiled > 0
     assert np.array_equal(np.array(sorted(b.stats().items())), np.array(sorted(c.stats().items())))
+
+
+def test_large_nfa_tables_travel():
+    """Rule sets with large NFAs (sparse follow rows, past 1,024 positions) ship
+    in the exported image like any other table: the importer compiles nothing
+    and installs byte-identical tables."""
+    import sys
+    import cilium_amd
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import numpy as np
+    import test_gpu_large_nfa as L
+    from test_gpu_http import wl_from_reqs
+    pol = L._policy(L.PATS[1])
+    w = wl_from_reqs([b"x"] * 4, pol, L.CONNS, np.arange(4, dtype=np.uint32))
+    a = cilium_amd.Engine(-1)
+    a.update_policy(pol)
+    a.set_connections(w.conns)
+    assert a.stats()["http_nfas"] == 1 and a.stats()["nfa_pool_bytes"] > 100_000
+    b = cilium_amd.Engine(-1)
+    b.import_tables(a.export_tables())
+    b.set_connections(w.conns)
+    assert b.tables_compiled == 0 and b.tables_digest == a.tables_digest
