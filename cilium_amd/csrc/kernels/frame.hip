@@ -64,8 +64,12 @@ __device__ __forceinline__ uint32_t eq16(uint4 w, uint32_t c) {  // bit k: byte 
     return nib(e(w.x)) | nib(e(w.y)) << 4 | nib(e(w.z)) << 8 | nib(e(w.w)) << 12;
 }
 
+// 16-byte loads in flight per step of the CRLF scan (1M HTTP requests in 16k
+// streams: 4 -> 7.6 ms, 8 -> 6.9, 16 -> 6.7; memcached text 9.1, 8.6, 8.7)
+constexpr int kScan = 8;
+
 // first i in [from, S.n) with b[i] == '\r' and b[i + 1] == '\n' (S.n: none),
-// 64 bytes (four 16-byte loads in flight) a step
+// 16 * kScan bytes a step
 __device__ uint64_t find_crlf(Stream &S, uint64_t from) {
     if (from >= S.n) return S.n;
     const uint64_t a = (uint64_t)S.b + from;
@@ -73,13 +77,13 @@ __device__ uint64_t find_crlf(Stream &S, uint64_t from) {
     const uint64_t end = (uint64_t)S.b + S.n;
     uint32_t skip = (uint32_t)(a - base);
     uint32_t prev_cr = 0;  // the last block ended in '\r'
-    for (; base < end; base += 64) {
-        uint4 w[4];
+    for (; base < end; base += 16 * kScan) {
+        uint4 w[kScan];
 #pragma unroll
-        for (int k = 0; k < 4; k++)
+        for (int k = 0; k < kScan; k++)
             if (base + 16 * k < end) w[k] = gload16(base + 16 * k);
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
+        for (int k = 0; k < kScan; k++) {
             const uint64_t bk = base + 16 * k;
             if (bk >= end) break;
             uint32_t valid = end - bk >= 16 ? 0xFFFFu : (1u << (uint32_t)(end - bk)) - 1u;
