@@ -272,8 +272,12 @@ __device__ __forceinline__ void text_fast(const Image &I, Keys<kCh> &K, const ui
     const uint32_t end = a0 + len;  // request bytes are chunk positions [a0, end)
     bool in_tok = false, key_tok = false, prev_cr = false;
     uint32_t kstart = 0, carry = 0;  // carry: bytes of this chunk that end a space rune begun in the last one
+    // the next chunk's load is in flight while this one is scanned (a request
+    // read in place over PCIe -- a one-request call -- pays each load's latency)
+    uint4 wn = gload16(base);  // global, not flat (gmem.h)
     for (uint32_t cb = 0; cb < end; cb += 16) {
-        const uint4 w = gload16(base + cb);  // global, not flat (gmem.h)
+        const uint4 w = wn;
+        if (cb + 16 < end) wn = gload16(base + cb + 16);
         uint32_t valid = end >= cb + 16 ? 0xFFFFu : (1u << (end - cb)) - 1u;
         if (cb == 0) valid &= 0xFFFFu << a0;
         uint32_t S = ascii_space_mask(w) | carry;
@@ -378,7 +382,11 @@ __device__ __forceinline__ void mc_one(const Batch &B, const McTables &T, const 
     const uint32_t *__restrict__ conn_ids = B.conn_ids;
     const DevConn *__restrict__ conns = B.conns;
     {
+        // the request's connection, offset and length in one round trip (for
+        // a one-request call they come over PCIe)
         const uint32_t ci = conn_ids[idx];
+        const uint64_t off = B.offs[idx];
+        const uint32_t len = B.lens[idx];
         const DevConn conn = ci < nconns ? conns[ci] : DevConn{-1, PROTO_NONE, 0, 0xFFFF};
         if (conn.proto != PROTO_MEMCACHE || conn.ruleset < 0 || (uint32_t)conn.ruleset >= T.nrulesets) {
             if (answer_other && (!L7_PROTO_OWNED(conn.proto) || conn.proto == PROTO_MEMCACHE)) {  // no parser: UNSUPPORTED
@@ -400,8 +408,6 @@ __device__ __forceinline__ void mc_one(const Batch &B, const McTables &T, const 
         I.nnfa = hdr32(I, MC_OFF(nnfa));
         I.nfa_pool = T.nfa_pool;
         I.nfa_scratch = kNfa ? l7_nfa_lane_scratch(T.nfa_scratch, T.nfa_lane_words) : nullptr;
-        const uint64_t off = B.offs[idx];
-        const uint32_t len = B.lens[idx];
         const uint8_t *b = B.arena + off;
         uint8_t verdict = V_PARSE_ERROR;
         int32_t rule = -1;
