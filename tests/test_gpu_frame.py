@@ -223,3 +223,13 @@ def test_frame_streams_match_the_scan_and_the_oracle(engine, oracle, proto):
     assert frames > n * 2  # several frames per stream
     if proto in ("http", "kafka"):  # well-formed generated requests: the frames are the requests
         assert whole >= n * 3 // 4, (whole, n)
+
+
+@pytest.mark.parametrize("proto", ["http", "kafka"])
+def test_frame_streams_max_frames(engine, oracle, proto):
+    """More frames than slots: the first max_frames are emitted (the last one
+    handed the rest of its stream), as the restatement stops there too."""
+    w = {"http": lambda: gen.http_workload(2, 2000, nconns=32),
+         "kafka": lambda: gen.kafka_workload(2000, nconns=32)}[proto]()
+    n, whole, frames = _run(engine, oracle, w, max_frames=4)
+    assert frames == 4 * n and whole == n
