@@ -100,14 +100,18 @@ int main() {
     }
     gate.unlock();
     l7g_batcher_flush(slow);
+    // a request larger than a lane (the slot's bytes / 8) never fits: refused at once
+    std::vector<uint8_t> huge(4u << 20, 'h');
+    const int huge_rc = l7g_batcher_submit(slow, huge.data(), (uint32_t)huge.size(), 0,
+                                           [](void *, uint8_t, int32_t, uint32_t) {}, nullptr);
     const int slow_answered = slow_calls.load();
     l7g_batcher_destroy(slow);
     l7g_engine_destroy(e);
     printf("{\"calls\": %llu, \"after_flush\": %llu, \"expected\": %d, \"bad\": %d, \"flush_rc\": %d, "
            "\"reentrant_flush_rc\": %d, \"launches\": %llu, \"queued\": %d, \"refused\": %d, \"rejected\": %d, "
-           "\"slow_answered\": %d, \"large_calls\": %llu, \"large_expected\": %d}\n",
+           "\"slow_answered\": %d, \"large_calls\": %llu, \"large_expected\": %d, \"huge_rc\": %d}\n",
            (unsigned long long)g_calls.load(), (unsigned long long)after_flush, T * N, g_bad.load(), frc,
            g_flush_rc.load(), (unsigned long long)launches, queued, refused, rejected.load(), slow_answered,
-           (unsigned long long)large_calls, T * N2);
+           (unsigned long long)large_calls, T * N2, huge_rc);
     return 0;
 }
