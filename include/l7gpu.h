@@ -233,8 +233,8 @@ typedef struct l7g_batcher l7g_batcher;
 l7g_batcher *l7g_batcher_create(l7g_engine *e, uint32_t max_requests, uint32_t max_wait_us);
 /* 0 = queued; -1 = the batcher is shutting down; -2 = backpressure: both
  * flushers are busy and the open slot is full, or the request is larger than
- * a slot (the callback is not called; the caller decides the request itself
- * or retries). */
+ * one of a slot's eight lanes (max(2 x max_requests, 1024) x 256 bytes) (the
+ * callback is not called; the caller decides the request itself or retries). */
 int l7g_batcher_submit(l7g_batcher *b, const uint8_t *req, uint32_t len, uint32_t conn, l7g_done_fn done, void *ctx);
 /* Flushes now and returns once every request submitted before the call has
  * had its callback (0); -1 when called from a callback. */
