@@ -252,6 +252,7 @@ struct l7g_batcher {
                 continue;
             }
             Slot &s = slots[i];
+            const uint64_t gen = s.gen;  // (read now: once the slot is FREE, a Seal may reopen it under a new gen)
             const int64_t t0 = now_ns();
             const uint32_t n = Gather(s, rv, &seg);
             v.resize(n);
@@ -262,7 +263,7 @@ struct l7g_batcher {
             const int64_t t2 = now_ns();
             {  // callbacks in the order the slots were opened
                 std::unique_lock<std::mutex> lk(mu);
-                done_cv.wait(lk, [&] { return delivered + 1 == s.gen; });
+                done_cv.wait(lk, [&] { return delivered + 1 == gen; });
             }
             const int64_t t3 = now_ns();
             for (uint32_t k = 0; k < n; k++) {
@@ -279,7 +280,7 @@ struct l7g_batcher {
             }
             {
                 std::lock_guard<std::mutex> g(mu);
-                delivered = s.gen;
+                delivered = gen;
                 completed += n;
                 launches++;
             }
