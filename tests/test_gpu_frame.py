@@ -160,11 +160,16 @@ def _streams(w, rng, cut_every=5):
     return conns, streams, bounds
 
 
-def _run(engine, oracle, w, max_frames=64):
+def _run(engine, oracle, w, max_frames=64, extra=()):
+    """extra: (connection, stream) pairs appended to the generated streams."""
     rng = np.random.default_rng(7)
     engine.update_policy(w.policy)
     engine.set_connections(w.conns)
     conns, streams, bounds = _streams(w, rng)
+    for c, st in extra:
+        conns.append(c)
+        streams.append(st)
+        bounds.append([0])
     arena = np.frombuffer(b"".join(streams), np.uint8).copy()
     s_off = np.cumsum([0] + [len(s) for s in streams[:-1]]).astype(np.uint64)
     s_len = np.array([len(s) for s in streams], np.uint32)
@@ -192,8 +197,10 @@ def _run(engine, oracle, w, max_frames=64):
     whole = 0
     sel = []
     for s in range(n):
-        proto = int(w.conns["proto"][conns[s]])
-        want = _frames(streams[s], proto, modes[conns[s]], max_frames)
+        if conns[s] >= len(w.conns):  # unknown connection: one slot, the whole stream
+            want = [0]
+        else:
+            want = _frames(streams[s], int(w.conns["proto"][conns[s]]), modes[conns[s]], max_frames)
         got = [int(x) - int(s_off[s]) for x in f_off[s * max_frames:s * max_frames + nfr[s]]]
         assert got == want, (s, proto, got[:8], want[:8])
         assert all(int(x) == len(streams[s]) - g for x, g in zip(f_len[s * max_frames:], got))
@@ -233,3 +240,20 @@ def test_frame_streams_max_frames(engine, oracle, proto):
          "kafka": lambda: gen.kafka_workload(2000, nconns=32)}[proto]()
     n, whole, frames = _run(engine, oracle, w, max_frames=4)
     assert frames == 4 * n and whole == n
+
+
+def test_frame_streams_edges(engine, oracle):
+    """Empty streams (no frame), a stream on an unknown connection (one slot,
+    answered as the classifier answers an unknown connection), a stream shorter
+    than a Kafka size prefix and one whose size prefix overruns it (one frame
+    each, handed the whole stream), next to ordinary streams; and no streams."""
+    w = gen.kafka_workload(500, nconns=16)
+    unknown = len(w.conns) + 5
+    extra = [(0, b""), (1, b"\x00\x00\x00"), (2, b"\x00\x00\x10\x00" + b"x" * 40), (unknown, b"GET / HTTP/1.1\r\n\r\n"),
+             (unknown, b""), (3, b"")]
+    n, whole, frames = _run(engine, oracle, w, max_frames=8, extra=extra)
+    assert frames >= n - 3
+    z = torch.zeros(1, dtype=torch.int64, device="cuda")
+    engine.classify_streams_device(z.data_ptr(), 0, z.data_ptr(), z.data_ptr(), z.data_ptr(), 0, 8, z.data_ptr(),
+                                   z.data_ptr(), z.data_ptr(), z.data_ptr(), z.data_ptr(), z.data_ptr(), z.data_ptr())
+    torch.cuda.synchronize()
