@@ -16,14 +16,7 @@ namespace {
 
 constexpr uint32_t kMaxParseBuf = 6553500;
 constexpr int kCrcSlices = 8;
-#ifndef L7G_KAFKA_CRCSTREAMS  // independent CRC chains per 64-byte batch (1, 2 or 4)
-#define L7G_KAFKA_CRCSTREAMS 1
-#endif
-// Shift tables after the 8 slicing tables: Zn[j][b] = T_{n-1-j}[b], so that
-// crc(v, n zero bytes) = Zn[0][v & 0xFF] ^ ... ^ Zn[3][v >> 24] (the register
-// state is linear: crc(c, A || B) = crc(crc(c, A), 0^|B|) ^ crc(0, B)).
-constexpr int kCrcZ32 = 8 * 256, kCrcZ48 = 12 * 256, kCrcZ16 = 16 * 256;
-constexpr int kCrcTables = L7G_KAFKA_CRCSTREAMS == 1 ? 8 : L7G_KAFKA_CRCSTREAMS == 2 ? 12 : 20;
+constexpr int kCrcTables = 8;  // slicing-by-8: T_k[b] = the register after byte b and k zero bytes
 // The tables of one workgroup: thread t < 256 fills entry t of each.
 __device__ __forceinline__ void crc_tables_init(uint32_t *tab, uint32_t t) {
     if (t < 256) {
@@ -34,12 +27,9 @@ __device__ __forceinline__ void crc_tables_init(uint32_t *tab, uint32_t t) {
     __syncthreads();
     if (t < 256) {
         uint32_t v = tab[t];
-        for (int k = 1; k < (kCrcTables == 8 ? 8 : kCrcTables == 12 ? 32 : 48); k++) {
+        for (int k = 1; k < kCrcTables; k++) {
             v = (v >> 8) ^ tab[v & 0xFF];  // T_k[t]
-            if (k < 8) tab[k * 256 + t] = v;
-            if (kCrcTables >= 12 && k >= 28 && k < 32) tab[kCrcZ32 + (31 - k) * 256 + t] = v;
-            if (kCrcTables >= 20 && k >= 44) tab[kCrcZ48 + (47 - k) * 256 + t] = v;
-            if (kCrcTables >= 20 && k >= 12 && k < 16) tab[kCrcZ16 + (15 - k) * 256 + t] = v;
+            tab[k * 256 + t] = v;
         }
     }
     __syncthreads();
@@ -48,9 +38,6 @@ __device__ __forceinline__ uint32_t crc_slice8(const uint32_t *tab, uint32_t lo,
     return tab[7 * 256 + (lo & 0xFF)] ^ tab[6 * 256 + ((lo >> 8) & 0xFF)] ^ tab[5 * 256 + ((lo >> 16) & 0xFF)] ^
            tab[4 * 256 + (lo >> 24)] ^ tab[3 * 256 + (hi & 0xFF)] ^ tab[2 * 256 + ((hi >> 8) & 0xFF)] ^
            tab[1 * 256 + ((hi >> 16) & 0xFF)] ^ tab[hi >> 24];
-}
-__device__ __forceinline__ uint32_t crc_shift(const uint32_t *z, uint32_t v) {
-    return z[v & 0xFF] ^ z[256 + ((v >> 8) & 0xFF)] ^ z[512 + ((v >> 16) & 0xFF)] ^ z[768 + (v >> 24)];
 }
 constexpr uint32_t kInf = 0xFFFFFFFFu;
 
@@ -321,36 +308,12 @@ __device__ __forceinline__ uint32_t crc_batch(const uint32_t *tab, uint8_t *stag
                  : "v"(la)
                  : "memory");
     if (next) crc_stage(stage, next);
-#if L7G_KAFKA_CRCSTREAMS == 1
 #pragma unroll
     for (int j = 0; j < 8; j++) {
         const uint4 x = j < 2 ? v0 : j < 4 ? v1 : j < 6 ? v2 : v3;
         const uint32_t lo = ((j & 1) ? x.z : x.x) ^ c, hi = (j & 1) ? x.w : x.y;
         c = crc_slice8(tab, lo, hi);
     }
-#elif L7G_KAFKA_CRCSTREAMS == 2
-    // two independent chains (bytes 0-31 from c, bytes 32-63 from 0), joined
-    // by the 32-zero-byte shift: 5 dependent lookup rounds, not 8
-    uint32_t ca = c, cb = 0;
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-        const uint4 xa = j < 2 ? v0 : v1, xb = j < 2 ? v2 : v3;
-        ca = crc_slice8(tab, ((j & 1) ? xa.z : xa.x) ^ ca, (j & 1) ? xa.w : xa.y);
-        cb = crc_slice8(tab, ((j & 1) ? xb.z : xb.x) ^ cb, (j & 1) ? xb.w : xb.y);
-    }
-    c = crc_shift(tab + kCrcZ32, ca) ^ cb;
-#else
-    // four chains of 16 bytes, joined by the 48/32/16-zero-byte shifts: 3 rounds
-    uint32_t c0 = c, c1 = 0, c2 = 0, c3 = 0;
-#pragma unroll
-    for (int j = 0; j < 2; j++) {
-        c0 = crc_slice8(tab, (j ? v0.z : v0.x) ^ c0, j ? v0.w : v0.y);
-        c1 = crc_slice8(tab, (j ? v1.z : v1.x) ^ c1, j ? v1.w : v1.y);
-        c2 = crc_slice8(tab, (j ? v2.z : v2.x) ^ c2, j ? v2.w : v2.y);
-        c3 = crc_slice8(tab, (j ? v3.z : v3.x) ^ c3, j ? v3.w : v3.y);
-    }
-    c = crc_shift(tab + kCrcZ48, c0) ^ crc_shift(tab + kCrcZ32, c1) ^ crc_shift(tab + kCrcZ16, c2) ^ c3;
-#endif
     return c;
 }
 // the rest (fewer than 64 bytes, from i, 16-byte aligned) from the cursor's

@@ -24,7 +24,15 @@ def main():
     names = sys.argv[2:] or ["prod"]
     wl = os.environ.get("EXP_WORKLOAD", "cfg3")
     t0 = time.time()
-    w = gen.kafka_workload(n) if wl == "cfg3" else gen.mixed_workload(n)
+    if wl.startswith("cfg3"):
+        w = gen.kafka_workload(n)
+        if wl != "cfg3":  # cfg3produce / cfg3fetch / cfg3other: one kind's requests of the cfg3 stream
+            kinds = np.array([int(w.arena[int(o) + 4]) << 8 | int(w.arena[int(o) + 5]) for o in w.offsets])
+            want = {"cfg3produce": kinds == 0, "cfg3fetch": kinds == 1, "cfg3other": kinds > 1}[wl]
+            w = gen.select(w, np.nonzero(want)[0], wl)
+            n = w.n
+    else:
+        w = gen.mixed_workload(n)
     print(f"{wl}: {n} requests, {w.arena.nbytes / 1e6:.1f} MB, generated in {time.time() - t0:.1f}s", flush=True)
     ref = refpy.classify_workload(w, 16)
     dev = torch.device("cuda", 0)
@@ -32,6 +40,10 @@ def main():
          (w.arena, w.offsets.view(np.int64), w.lengths.view(np.int32), w.conn_ids.view(np.int32))]
     outs = [torch.empty(n, dtype=t, device=dev) for t in (torch.uint8, torch.int32, torch.int32)]
     s = torch.cuda.current_stream()
+    # algorithmic bytes of the Kafka kernel: the Kafka requests' bytes + 25 per
+    # Kafka request (not the whole mixed workload's)
+    kb = gen.protocol_bytes(w)["kafka"]
+    gb = (kb["payload"] + 25 * kb["requests"]) / 1e9
     for name in names:
         path = os.path.join(ROOT, "cilium_amd", "libl7gpu.so" if name == "prod" else f"libl7gpu_{name}.so")
         eng = Engine(0, lib_path=path)
@@ -49,18 +61,17 @@ def main():
         got = (outs[0].cpu().numpy(), outs[1].cpu().numpy(), outs[2].cpu().numpy().view(np.uint32))
         mism = int(((got[0] != ref[0]) | (got[1] != ref[1]) | (got[2] != ref[2])).sum())
         med = {k: float(np.median([m[k] for m in ms])) for k in ms[0] if ms[0][k] > 0}
-        gb = (w.lengths.astype(np.int64).sum() + 25 * n) / 1e9
         kms = med.get("kafka", 0.0)
         print(f"{name:12s} " + " ".join(f"{k}={v:.3f}ms" for k, v in med.items()) +
               (f"  kafka {gb / (kms / 1e3):.0f} GB/s frac {gb / (kms / 1e3) / 8000:.3f}" if kms else "") +
               f"  mismatches={mism}", flush=True)
         ph = eng.kafka_phase_times()
         if ph is not None:
-            tot = float(ph[:5].sum()) or 1.0
+            tot = float(ph[:6].sum()) or 1.0
             print("   phases: " + " ".join(f"{k}={ph[i] / tot:.3f}" for i, k in
-                                           enumerate(["frame", "walk", "crc", "topics", "out"])) +
-                  f"  rounds/tile={ph[5] / max(ph[7], 1):.1f} refills/tile={ph[6] / max(ph[7], 1):.1f}"
-                  f" cycles/tile={tot / max(ph[7], 1):.0f}", flush=True)
+                                           enumerate(["setup", "walk", "-", "crc", "-", "redo+out"])) +
+                  f"  groups={ph[6] / 13:.0f} redone-lanes={ph[7] / 13:.0f}"
+                  f" cycles/group={tot / max(ph[6], 1):.0f}", flush=True)
         eng.close()
 
 
