@@ -54,6 +54,7 @@ constexpr uint64_t kSealed = 1ull << 63;
 constexpr uint64_t kBytesMask = (1ull << 40) - 1;
 constexpr uint64_t kOne = 1ull << 40;
 constexpr uint32_t kMinSlotRequests = 1024;
+constexpr uint32_t kMaxBatchRequests = 1u << 16;  // max_requests cap (slots of 2 x 64 Ki requests)
 constexpr uint64_t kSlotBytesPerRequest = 2048;
 constexpr int kSubmitTries = 1000;
 constexpr uint32_t kPackMaxRequests = 256;     // a batch this small is packed and read in place
@@ -80,7 +81,7 @@ struct alignas(64) Lane {
 };
 
 struct Slot {
-    uint8_t *mem = nullptr;  // pinned; plain malloc when there is no device (a host-only engine)
+    uint8_t *mem = nullptr;  // pinned; plain malloc only for a host-only engine (no device to copy to)
     bool pinned = false;
     uint64_t *off = nullptr;  // [cap_n], then len [cap_n], conn [cap_n]: lane l owns entries [l * ln, (l + 1) * ln)
     uint32_t *len = nullptr, *conn = nullptr;
@@ -179,7 +180,7 @@ struct l7g_batcher {
             total += cnt[l];
             bytes += used[l];
             width = std::max(width, used[l]);
-            if (used[l]) rows = l + 1;
+            if (used[l] || cnt[l]) rows = l + 1;  // (a lane of zero-length requests still needs its row in range)
         }
         const bool pack = total <= kPackMaxRequests && bytes <= kPackMaxBytes;
         width = (width + 15) & ~(uint64_t)15;  // (rows start 16-byte aligned on the device too)
@@ -305,7 +306,8 @@ l7g_batcher *l7g_batcher_create(l7g_engine *e, uint32_t max_requests, uint32_t m
     if (!e) return nullptr;
     auto *b = new l7g_batcher();
     b->e = e;
-    b->max_n = std::min<uint32_t>(max_requests ? max_requests : 1, 1u << 20);
+    // (capped so that the four pinned slots stay within what a host can pin: 4 x 128 Ki x 2 KiB = 1 GiB)
+    b->max_n = std::min<uint32_t>(max_requests ? max_requests : 1, kMaxBatchRequests);
     b->max_wait = std::chrono::microseconds(max_wait_us);
     const uint32_t cap_n = (std::max<uint32_t>(2 * b->max_n, kMinSlotRequests) + kLanes - 1) / kLanes * kLanes;
     const uint64_t cap_bytes = (uint64_t)cap_n * kSlotBytesPerRequest;
@@ -314,7 +316,10 @@ l7g_batcher *l7g_batcher_create(l7g_engine *e, uint32_t max_requests, uint32_t m
     for (auto &s : b->slots) {
         s.mem = (uint8_t *)l7g_pinned_alloc(total);
         s.pinned = s.mem != nullptr;
-        if (!s.mem) s.mem = (uint8_t *)malloc(total);
+        // the device path reads a small batch in place (zero copy) and copies a
+        // large one with a 2-D copy: both need pinned memory, so an engine with
+        // a device gets no batcher rather than one that answers UNSUPPORTED
+        if (!s.mem && !l7g_engine_has_device(e)) s.mem = (uint8_t *)malloc(total);
         if (!s.mem) {
             FreeSlots(b);
             delete b;
@@ -345,12 +350,19 @@ int l7g_batcher_submit(l7g_batcher *b, const uint8_t *req, uint32_t len, uint32_
     int tries = 0;
     for (;;) {
         Slot &s = b->slots[b->open_idx.load()];
-        // this thread's lane first, then the ones after it (never back: a
-        // thread's requests stay in submission order when the lanes are closed up)
-        int l = t_last.slot == &s && t_last.gen == s.gen ? std::max(t_last.lane, t_lane) : t_lane;
+        // this thread's lane first, then the ones after it.  A thread that
+        // already has entries in this slot never goes back (its requests stay
+        // in submission order when the lanes are closed up); one with none in
+        // it yet wraps round to the lanes before its own, so a lone submitter
+        // can fill the whole slot whichever lane is its home.
+        const bool fresh = !(t_last.slot == &s && t_last.gen == s.gen);
+        const int l0 = fresh ? t_lane : t_last.lane;
+        const int nl = fresh ? kLanes : kLanes - l0;
+        int l = l0;
         uint64_t rv = 0;
         bool sealed = false, got = false;
-        for (; l < kLanes; l++) {
+        for (int step = 0; step < nl; step++) {
+            l = (l0 + step) % kLanes;
             Lane &ln = s.lane[l];
             const uint64_t cur = ln.resv.load(std::memory_order_relaxed);
             if (cur & kSealed) {

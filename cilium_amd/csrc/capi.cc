@@ -1132,6 +1132,8 @@ int l7g_host_reserve(l7g_engine *e, uint32_t n, uint64_t arena_len) {
     return (int)rc;
 }
 
+int l7g_engine_has_device(const l7g_engine *e) { return e && e->device >= 0 ? 1 : 0; }
+
 void *l7g_pinned_alloc(size_t bytes) {
     void *p = nullptr;
     return hipHostMalloc(&p, bytes, hipHostMallocDefault) == hipSuccess ? p : nullptr;

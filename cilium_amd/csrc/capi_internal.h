@@ -41,4 +41,5 @@ int l7g_host_run_pinned(l7g_engine *e, uint32_t n, const uint64_t *off, size_t s
 // over arena_len bytes now, so that no such call reallocates them.
 int l7g_host_reserve(l7g_engine *e, uint32_t n, uint64_t arena_len);
 void *l7g_pinned_alloc(size_t bytes);  // hipHostMalloc (NULL on failure)
+int l7g_engine_has_device(const l7g_engine *e);  // 1: the engine launches on a GPU; 0: host-only (tables only)
 void l7g_pinned_free(void *p);

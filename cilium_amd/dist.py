@@ -41,10 +41,14 @@ def broadcast_policy(policy, dist, src=0, device=None):
 
 
 def _broadcast_bytes(b, dist, src, device):
+    """b (read on src only) on every rank; b is None on src -> None everywhere
+    (the length word carries -1 and no payload follows)."""
     import torch
     rank = dist.get_rank()
-    n = torch.tensor([len(b) if rank == src else 0], dtype=torch.int64, device=device)
+    n = torch.tensor([(-1 if b is None else len(b)) if rank == src else 0], dtype=torch.int64, device=device)
     dist.broadcast(n, src)
+    if int(n.item()) < 0:
+        return None
     buf = torch.empty(int(n.item()), dtype=torch.uint8, device=device)
     if rank == src:
         buf.copy_(torch.frombuffer(bytearray(b), dtype=torch.uint8))
@@ -57,18 +61,29 @@ def broadcast_tables(engine, dist, src=0, device=None, policy=None, conns=None):
     both read on `src` only) and broadcasts its compiled tables; every other
     rank installs them into `engine` without compiling.  Returns the image
     bytes.  Over RCCL (backend "nccl", device = the rank's GPU) on the box,
-    gloo on CPU in the tests."""
+    gloo on CPU in the tests.
+
+    A policy `src` refuses (PolicyError: the NPDS NACK) still completes the
+    collective: `src` broadcasts "no image", every rank keeps the version it
+    has (as the reference keeps the previous policy on a NACK,
+    proxylib/proxylib/instance.go:168-219), the other ranks return None and
+    `src` re-raises."""
     rank = dist.get_rank()
+    err = None
+    image = None
     if rank == src:
-        if policy is not None:
-            engine.update_policy(policy)
-        if conns is not None:
-            engine.set_connections(conns)
-        image = engine.export_tables()
-    else:
-        image = None
+        try:
+            if policy is not None:
+                engine.update_policy(policy)
+            if conns is not None:
+                engine.set_connections(conns)
+            image = engine.export_tables()
+        except Exception as e:  # noqa: BLE001 -- re-raised below, after the collective
+            err, image = e, None
     image = _broadcast_bytes(image, dist, src, device)
-    if rank != src:
+    if err is not None:
+        raise err
+    if rank != src and image is not None:
         engine.import_tables(image)
     return image
 

@@ -215,8 +215,8 @@ int l7g_stats(l7g_engine *e, l7g_stats_t *out);
  * (envoy/cilium_l7policy.cc:127-182), which would return StopIteration and
  * resume (continueDecoding / sendLocalReply) from the callback.  Submitters
  * copy their request straight into the open batch slot (pinned host memory in
- * the layout the device copy reads; a compare-and-swap reserves the place, no
- * lock).  Two flusher threads each seal the open slot once max_requests are in
+ * the layout the device copy reads; a fetch-and-add on one of the slot's eight
+ * lane words reserves the place, no lock).  Two flusher threads each seal the open slot once max_requests are in
  * it, its first request has waited max_wait_us, or a flush is asked for
  * (under load a batch can hold up to twice max_requests: requests keep coming
  * while the slot is sealed), classify it in place with one launch on their own
@@ -229,7 +229,9 @@ int l7g_stats(l7g_engine *e, l7g_stats_t *out);
 typedef void (*l7g_done_fn)(void *ctx, uint8_t verdict, int32_t rule, uint32_t consumed);
 typedef struct l7g_batcher l7g_batcher;
 /* Slots hold max(2 x max_requests, 1024) requests and 2 KiB of request bytes
- * per request each; four slots are allocated (pinned) up front. */
+ * per request each; four slots are allocated (pinned) up front.  max_requests
+ * is capped at 65536 (4 x 256 MiB pinned).  NULL when the engine has a device
+ * and the slots cannot be pinned (the device path needs pinned slots). */
 l7g_batcher *l7g_batcher_create(l7g_engine *e, uint32_t max_requests, uint32_t max_wait_us);
 /* 0 = queued; -1 = the batcher is shutting down; -2 = backpressure: both
  * flushers are busy and the open slot is full, or the request is larger than

@@ -73,6 +73,56 @@ def test_tables_broadcast(world):
             assert compiled == 0, (rank, compiled)  # installed, not compiled
 
 
+def _nack_worker(rank, world, port, q):
+    import sys
+    import torch.distributed as dist
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import cilium_amd
+        from cilium_amd import dist as l7dist
+        w = _workload()
+        eng = cilium_amd.Engine(-1)
+        l7dist.broadcast_tables(eng, dist, policy=w.policy if rank == 0 else None,
+                                conns=w.conns if rank == 0 else None)
+        before = eng.tables_digest
+        # rank 0 is handed a policy it must refuse (not even JSON): a NACK
+        bad = "{not a policy"
+        raised = None
+        try:
+            got = l7dist.broadcast_tables(eng, dist, policy=bad if rank == 0 else None)
+        except cilium_amd.PolicyError as e:
+            raised, got = type(e).__name__, None
+        # the collective completed on every rank, and a later broadcast still works
+        again = l7dist.broadcast_tables(eng, dist, policy=w.policy if rank == 0 else None,
+                                        conns=w.conns if rank == 0 else None)
+        q.put((rank, raised, got is None, before == eng.tables_digest, again is not None))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_tables_broadcast_nack_does_not_hang():
+    """rank 0 refusing a policy must not leave the other ranks in
+    the broadcast; every rank keeps its tables, rank 0 re-raises."""
+    world = 3
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_nack_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=250) for _ in range(world))
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    for rank, raised, got_none, kept, again in res:
+        assert raised == ("PolicyError" if rank == 0 else None), (rank, raised)
+        assert got_none and kept and again, (rank, got_none, kept, again)
+
+
 def test_import_refuses_corrupt_image():
     import cilium_amd
     w = _workload()

@@ -48,3 +48,20 @@ def test_batcher_kafka_matches_sync():
     w = gen.kafka_workload(6000)
     d = _run(w, 1024, 200)
     assert d["n"] == 6000 and d["mismatches"] == 0 and d["calls_not_once"] == 0, d
+
+
+def test_batcher_zero_length_and_lone_thread():
+    """zero-length requests in a large (row-copied) batch must get
+    what the synchronous call gives (INCOMPLETE, not UNSUPPORTED from an
+    offset past the copied rows), and a single submitting thread must be able
+    to fill more than its own lane of a slot."""
+    w = gen.kafka_workload(6000)
+    reqs = [bytes(w.arena[int(o):int(o) + int(n)]) for o, n in zip(w.offsets, w.lengths)]
+    reqs = [b"" if i % 50 == 7 else q for i, q in enumerate(reqs)]
+    arena, offs, lens = gen.pack(reqs)
+    w2 = gen.Workload("kafka+empty", arena, offs, lens, w.conn_ids, w.conns, w.policy, {})
+    for threads in (8, 1):
+        d = _run(w2, 4096, 2000, threads=threads)
+        assert d["n"] == 6000 and d["mismatches"] == 0 and d["calls_not_once"] == 0, (threads, d)
+        if threads == 1:
+            assert d["max_batch"] > 4096 // 8, d  # more than one lane's worth from one thread
