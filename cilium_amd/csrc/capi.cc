@@ -58,6 +58,11 @@ hipError_t LaunchFrameStreams(const uint8_t *arena, uint64_t arena_len, const ui
                               uint32_t *nframes, hipStream_t stream);
 hipError_t HttpPhaseTimes(uint64_t *out, bool reset);
 hipError_t KafkaPhaseTimes(uint64_t *out, bool reset);
+hipError_t LaunchHttpGroup(const Batch &B, const HttpTables &T, const uint32_t *sel, const uint32_t *sel_count,
+                           uint32_t n, bool answer_other, uint32_t *ctl, uint32_t *hist, uint32_t *cursor,
+                           uint32_t *segs, uint32_t *gsel, uint32_t *gbig, hipStream_t stream);
+hipError_t LaunchHttpGrouped(const Batch &B, const HttpTables &T, const uint32_t *gsel, const uint32_t *segs,
+                             const uint32_t *gbig, uint32_t *ctl, bool any_big, hipStream_t stream);
 }  // namespace l7
 
 using namespace l7;
@@ -82,6 +87,10 @@ struct StreamScratch {
     size_t use_cap = 0;
     // work counters of unpartitioned batches (HTTP tile counters), allocated on first use
     uint32_t *d_work = nullptr;
+    // HTTP requests grouped by rule set (kernels/http_group.hip), grow-only:
+    // [ctl(8) | hist(R) | cursor(R) | segments(3 x (n / kGroupSegEntries + R + 1)) | grouped list(n) | big-image list(n)]
+    uint32_t *d_grp = nullptr;
+    size_t grp_cap = 0;
     // large NFAs' state sets: a lane's 2 W words for each lane of a launch (grow-only)
     uint64_t *d_bignfa = nullptr;
     size_t bignfa_bytes = 0;
@@ -91,6 +100,7 @@ struct StreamScratch {
     uint64_t last_use = 0;
     ~StreamScratch() {
         if (d_bignfa) hipFree(d_bignfa);
+        if (d_grp) hipFree(d_grp);
         if (d_sel) hipFree(d_sel);
         if (d_nfa) hipFree(d_nfa);
         if (d_hist) hipFree(d_hist);
@@ -107,6 +117,8 @@ constexpr size_t kZeroCopyMaxBytes = 256 * 1024;
 // batches below this size skip the protocol split when one classifier can walk them alone
 constexpr uint32_t kPartitionMin = 4096;
 constexpr uint32_t kHostScanMax = 4096;
+// batches from this size with HTTP requests on more than one rule set take the grouped path
+constexpr uint32_t kGroupMin = 1u << 16;
 constexpr size_t kNfaScratchBytes = 256ull << 20;  // large NFAs: state-set scratch per stream (lanes in flight)  // host calls up to this size check their connections for cold rule sets
 
 // l7g_classify_host's per-thread staging: its own stream, device arena and
@@ -157,6 +169,7 @@ struct l7g_engine {
     bool tables_dirty = true, conns_dirty = true;
     bool has_http = false, has_kafka = false, has_mc = false, has_r2 = false, has_cs = false;
     int32_t hot_ruleset = -1;  // HTTP rule set staged in LDS (most connections)
+    bool any_big_image = false;  // some HTTP rule set's image exceeds kGroupImageBytes
     // l7g_classify_host contexts, one per calling thread (guarded by hmu)
     std::mutex hmu;
     std::map<std::thread::id, std::unique_ptr<HostCtx>> hctx;
@@ -313,6 +326,9 @@ void PickHot(l7g_engine *e) {
     e->any_cold = false;
     for (size_t i = 0; i < e->attrs.size(); i++)
         if (e->attrs[i].proto == PROTO_HTTP && e->conns[i].ruleset != e->hot_ruleset) e->any_cold = true;
+    e->any_big_image = false;
+    for (size_t r = 0; r < uses.size(); r++)
+        if (uses[r] && e->hc->image().rulesets[r].image_len > kGroupImageBytes) e->any_big_image = true;
 }
 
 size_t TableRulesets(const l7g_engine *e) {
@@ -829,9 +845,34 @@ static int Classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, con
         if (rc == hipSuccess) rc = hipMemsetAsync(S->d_work, 0, 2 * sizeof(uint32_t), s);
         tile_ctr = S->d_work;
     }
-    if (rc == hipSuccess && run[1])
+    // many rule sets in use: the HTTP requests sorted by rule set, so that each
+    // workgroup stages one image per segment (kernels/http_group.hip)
+    const bool grouped = run[1] && any_cold && n >= kGroupMin && ht.nrulesets >= 2 &&
+                         ht.nrulesets <= kMaxGroupRulesets;
+    if (rc == hipSuccess && grouped) {
+        const size_t R = ht.nrulesets, segw = 3 * ((size_t)n / kGroupSegEntries + R + 1);
+        const size_t need = 8 + 2 * R + segw + 2 * (size_t)n;
+        if (need > S->grp_cap) {
+            if (S->d_grp) {
+                if (S->launched) rc = hipEventSynchronize(S->done_ev);
+                hipFree(S->d_grp);
+                S->d_grp = nullptr;
+                S->grp_cap = 0;
+            }
+            if (rc == hipSuccess) rc = hipMalloc(&S->d_grp, need * sizeof(uint32_t));
+            if (rc == hipSuccess) S->grp_cap = need;
+        }
+        uint32_t *ctl = S->d_grp, *hist = ctl + 8, *cursor = hist + R, *segs = cursor + R, *gsel = segs + segw,
+                 *gbig = gsel + n;
+        if (rc == hipSuccess) rc = hipMemsetAsync(ctl, 0, (8 + R) * sizeof(uint32_t), s);
+        if (rc == hipSuccess)
+            rc = LaunchHttpGroup(B, ht, sel_h, cnt ? cnt + L7_KAFKA_CLASSES + 2 : nullptr, n, !partitioned, ctl, hist,
+                                 cursor, segs, gsel, gbig, s);
+        if (rc == hipSuccess) rc = LaunchHttpGrouped(B, ht, gsel, segs, gbig, ctl, e->any_big_image, s);
+    } else if (rc == hipSuccess && run[1]) {
         rc = LaunchHttpClassify(B, ht, sel_h, cnt ? cnt + L7_KAFKA_CLASSES + 2 : nullptr, any_cold, !partitioned,
                                 tile_ctr, s);
+    }
     mark(2);
     uint32_t *zcount = cnt ? cnt + 31 : nullptr;
     if (rc == hipSuccess && run[2])

@@ -77,6 +77,13 @@ L7_HD inline bool l7_in_arena(uint64_t off, uint32_t len, uint64_t arena_len) {
 constexpr int kChunksPerPass = 4;       // chunk accumulators the kernel keeps in registers
 constexpr int kDfasPerPass = 1;         // DFAs per slot walked in one framing pass
 constexpr uint32_t kLdsImageBytes = 32 * 1024;  // LDS budget for the hot rule-set image
+// Requests grouped by rule set (kernels/http_group.hip): at most this many HTTP
+// rule sets (one LDS histogram bin each), runs cut into segments of at most
+// kGroupSegEntries entries, images up to kGroupImageBytes staged (the grouped
+// kernel keeps two control words after them).
+constexpr uint32_t kMaxGroupRulesets = 4096;
+constexpr uint32_t kGroupSegEntries = 1024;
+constexpr uint32_t kGroupImageBytes = kLdsImageBytes - 16;
 
 // Header-name recognition: every image carries a small DFA over the
 // lower-cased name bytes that spells out the names the framer must know

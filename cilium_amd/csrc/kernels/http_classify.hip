@@ -1531,6 +1531,83 @@ __global__ __launch_bounds__(kBlock) void http_classify_kernel(Batch B, HttpTabl
     }
 }
 
+
+// Requests grouped by rule set (http_group.hip): a workgroup takes one segment
+// of the grouped list at a time (all of it on one rule set), stages that rule
+// set's image in LDS, and its waves take the segment's tiles of 64 entries
+// from a counter in LDS; the image-in-LDS framer runs them (a tile never mixes
+// rule sets, so image-derived values are wave-uniform as in the hot kernel).
+// ctl: [0] segments, [1] the segment counter (zeroed by the launcher).
+__global__ __launch_bounds__(kBlock) void http_grouped_kernel(Batch B, HttpTables T, const uint32_t *__restrict__ gsel,
+                                                              const uint32_t *__restrict__ segs,
+                                                              uint32_t *__restrict__ ctl) {
+    const uint8_t *__restrict__ arena = B.arena;
+    const uint32_t n = B.n;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63, wave = tid >> 6;
+    uint8_t *s_img = lds + kOffImg;
+    uint32_t *s_ctl = reinterpret_cast<uint32_t *>(lds + kOffImg + kGroupImageBytes);  // segment, tile counter
+    const Out O{B.verdict, B.rule, B.consumed, T.nfa_bits};
+    uint8_t *wave_lds = lds + wave * kWaveLds;
+    const uint32_t nsegs = ctl[0];
+    for (;;) {
+        if (tid == 0) {
+            s_ctl[0] = atomicAdd(&ctl[1], 1u);
+            s_ctl[1] = 0;
+        }
+        __syncthreads();
+        const uint32_t sg = s_ctl[0];
+        if (sg >= nsegs) break;
+        const uint32_t rs = segs[3 * sg], e0 = segs[3 * sg + 1], cnt = segs[3 * sg + 2];
+        {
+            const DevRuleset r = T.rulesets[rs];
+            const uint4 *src = (const uint4 *)(T.images + r.image_off);
+            const uint32_t n16 = (r.image_len + 15) / 16;
+            constexpr uint32_t kIters = (kGroupImageBytes / 16 + kBlock - 1) / kBlock;
+            uint4 t[kIters];
+#pragma unroll
+            for (uint32_t k = 0; k < kIters; k++)
+                if (tid + k * kBlock < n16) t[k] = src[tid + k * kBlock];
+#pragma unroll
+            for (uint32_t k = 0; k < kIters; k++)
+                if (tid + k * kBlock < n16) ((uint4 *)s_img)[tid + k * kBlock] = t[k];
+        }
+        __syncthreads();
+        for (;;) {
+            uint32_t tile = 0;
+            if (lane == 0) tile = atomicAdd(&s_ctl[1], 1u);
+            tile = (uint32_t)__builtin_amdgcn_readfirstlane((int)tile);
+            if (tile * 64 >= cnt) break;
+            Lane L;
+            const uint32_t slot = tile * 64 + lane;
+            L.idx = slot < cnt ? gsel[e0 + slot] : n;
+            L.done = true;
+            L.owed = false;
+            L.verdict = V_UNSUPPORTED;
+            L.rule = -1;
+            L.consumed = 0;
+            L.mode = M_DONE;
+            L.base = 0;
+            L.a0 = L.pa = L.w = L.lena = 0;
+            if (L.idx < n) {  // (every grouped entry is an HTTP request on rule set rs)
+                L.owed = true;
+                const uint64_t off = B.offs[L.idx];
+                const uint32_t len = B.lens[L.idx];
+                if (l7_in_arena(off, len, B.arena_len)) {  // else out of contract: answered UNSUPPORTED
+                    const uint64_t a = (uint64_t)(arena + off);
+                    L.base = a & ~(uint64_t)15;
+                    L.a0 = (uint32_t)(a & 15);
+                    L.lena = len > 0xFFFFFF00u ? 0xFFFFFF00u + L.a0 : L.a0 + len;
+                    L.done = false;
+                }
+            }
+            run_tile<true>(L, s_img, wave_lds, lane, O);
+        }
+        __syncthreads();  // every wave is done with the image before the next segment's
+    }
+}
+
 // Host-side launcher (called from the C-ABI): persistent grids of one
 // 512-thread workgroup per CU; the hot-rule-set kernel, then (only if some
 // HTTP connection uses another rule set) the general one.
@@ -1556,6 +1633,28 @@ hipError_t LaunchHttpClassify(const Batch &B, const HttpTables &T, const uint32_
     if (!hot || any_cold)
         hipLaunchKernelGGL(http_classify_kernel<false>, dim3(blocks), dim3(kBlock), 0, stream, B, T, sel, sel_count, other,
                            tile_ctr ? tile_ctr + 1 : nullptr);
+    return hipGetLastError();
+}
+
+// The grouped list (LaunchHttpGroup's outputs): the grouped kernel over the
+// segments, then the general kernel over the entries on rule sets whose image
+// exceeds the LDS budget (gbig, ctl[2] of them; ctl[3] its tile counter).
+hipError_t LaunchHttpGrouped(const Batch &B, const HttpTables &T, const uint32_t *gsel, const uint32_t *segs,
+                             const uint32_t *gbig, uint32_t *ctl, bool any_big, hipStream_t stream) {
+    if (B.n == 0) return hipSuccess;
+    static int num_cus = 0;
+    if (num_cus == 0) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&num_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || num_cus <= 0)
+            num_cus = 256;
+    }
+    const uint32_t ntiles = (B.n + 63) / 64;
+    const uint32_t blocks = min((ntiles + kWaves - 1) / kWaves, (uint32_t)num_cus);
+    hipLaunchKernelGGL(http_grouped_kernel, dim3(blocks), dim3(kBlock), 0, stream, B, T, gsel, segs, ctl);
+    if (any_big)
+        hipLaunchKernelGGL(http_classify_kernel<false>, dim3(blocks), dim3(kBlock), 0, stream, B, T, gbig, ctl + 2, 0u,
+                           ctl + 3);
     return hipGetLastError();
 }
 
