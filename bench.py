@@ -34,6 +34,13 @@ Besides the device-resident rate (`value`) the line reports:
                   shard in 8 chunks on 2 streams (PCIe-inclusive; never `value`);
   * cpu_baseline -- the oracle (C restatement) on the host: all cores the
                   process may use, and one core, with nproc and the CPU model;
+  * streams    -- the same unique requests regrouped into connection streams
+                  (each connection's requests in order, cut into runs of 64:
+                  what one proxylib OnData hands over) and decided through
+                  l7g_classify_streams: device framing (a wave per HTTP /
+                  memcached-text stream, a lane per Kafka / binary one) then
+                  classification of every frame slot; frame-only ms, total ms,
+                  bytes the framers read, parity of every frame vs the oracle;
   * latency    -- per-request latency of the drop-in paths (p50/p90/p99 us):
                   one request per l7g_classify_host call (the Envoy adapter's
                   Allowed()), requests through the asynchronous batcher
@@ -190,6 +197,84 @@ def e2e_pipeline(torch, eng, w, dev, nchunks=8, reps=3):
     return float(np.median(ts)), moved, (h_v.numpy().copy(), h_r.numpy().copy(), h_c.numpy().view(np.uint32).copy())
 
 
+def streams_leg(torch, eng, gen, refpy, w, dev, threads, run=64, reps=10):
+    """w's requests regrouped into connection streams (each connection's
+    requests in order, cut into runs of `run`), framed and classified on the
+    device by l7g_classify_streams; every frame's verdict / rule / consumed
+    checked against the oracle on the same frame."""
+    order = np.argsort(w.conn_ids, kind="stable")
+    cid = w.conn_ids[order]
+    offs = w.offsets[order].astype(np.int64)
+    lens = w.lengths[order].astype(np.int64)
+    cuts = np.flatnonzero(np.diff(cid)) + 1
+    bounds = []
+    for a, b in zip(np.r_[0, cuts], np.r_[cuts, len(cid)]):
+        bounds.extend((k, min(k + run, b)) for k in range(a, b, run))
+    buf = np.ascontiguousarray(w.arena)
+    pieces, s_len, s_conn = [], [], []
+    for a, b in bounds:
+        pieces.extend(buf[offs[k]:offs[k] + lens[k]] for k in range(a, b))
+        s_len.append(int(lens[a:b].sum()))
+        s_conn.append(int(cid[a]))
+    arena = np.concatenate(pieces)
+    s_len = np.array(s_len, np.uint32)
+    s_off = np.r_[0, np.cumsum(s_len[:-1], dtype=np.int64)].astype(np.uint64)
+    s_conn = np.array(s_conn, np.uint32)
+    ns, mf = len(bounds), run
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    d_arena, d_soff, d_slen, d_sconn = T(arena), T(s_off.view(np.int64)), T(s_len.view(np.int32)), T(s_conn.view(np.int32))
+    slots = ns * mf
+    fo = torch.zeros(slots, dtype=torch.int64, device=dev)
+    fl = torch.zeros(slots, dtype=torch.int32, device=dev)
+    fc = torch.zeros(slots, dtype=torch.int32, device=dev)
+    nf = torch.zeros(ns, dtype=torch.int32, device=dev)
+    v = torch.zeros(slots, dtype=torch.uint8, device=dev)
+    r = torch.zeros(slots, dtype=torch.int32, device=dev)
+    c = torch.zeros(slots, dtype=torch.int32, device=dev)
+    args = [d_arena.data_ptr(), arena.nbytes, d_soff.data_ptr(), d_slen.data_ptr(), d_sconn.data_ptr(), ns, mf,
+            fo.data_ptr(), fl.data_ptr(), fc.data_ptr(), nf.data_ptr()]
+    st = torch.cuda.current_stream()
+
+    def timeit(f):
+        f()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(reps):
+            f()
+        e1.record(st)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps
+
+    t_frame = timeit(lambda: eng.classify_streams_device(*args, stream=st.cuda_stream))
+    t_all = timeit(lambda: eng.classify_streams_device(*args, v.data_ptr(), r.data_ptr(), c.data_ptr(),
+                                                       stream=st.cuda_stream))
+    nfr = nf.cpu().numpy()
+    sel = np.concatenate([np.arange(s * mf, s * mf + nfr[s]) for s in range(ns)])
+    fo_h = fo.cpu().numpy().view(np.uint64)[sel]
+    fl_h = fl.cpu().numpy().view(np.uint32)[sel]
+    fc_h = fc.cpu().numpy().view(np.uint32)[sel]
+    ref = refpy.Policy(w.policy).classify(w.conns, arena, fo_h, fl_h, fc_h, threads)
+    got = (v.cpu().numpy()[sel], r.cpu().numpy()[sel], c.cpu().numpy().view(np.uint32)[sel])
+    mism = int(((got[0] != ref[0]) | (got[1] != ref[1]) | (got[2] != ref[2])).sum())
+    # bytes the framers read: every byte of an HTTP / memcached-text / r2d2
+    # stream (windows; bodies framed by length are not read), 16 B per frame of
+    # a Kafka / memcached-binary / cassandra stream (the size field's chunk)
+    proto = w.conns["proto"][s_conn]
+    flags = w.conns["flags"][s_conn] & 3
+    first = arena[s_off.astype(np.int64)]
+    text = (proto == gen.PROTO_HTTP) | (proto == gen.PROTO_R2D2) | (
+        (proto == gen.PROTO_MEMCACHE) & ((flags == 1) | ((flags == 0) & (first < 0x80))))
+    read = int(s_len[text].astype(np.int64).sum()) + 16 * int(nfr[~text].sum())
+    return {"streams": ns, "requests_per_stream_max": mf, "stream_bytes": int(arena.nbytes),
+            "frames": int(nfr.sum()), "requests": w.n, "frame_ms": round(t_frame, 4),
+            "frame_and_classify_ms": round(t_all, 4), "framer_bytes_read": read,
+            "framer_read_gbps": round(read / (t_frame / 1e3) / 1e9, 1),
+            "verdicts_per_s": round(int(nfr.sum()) / (t_all / 1e3), 1), "mismatches": mism,
+            "note": "each connection's requests in order, cut into runs of 64 (one OnData buffer each); "
+                    "l7g_classify_streams: framing, then every frame slot classified"}
+
+
 def latency_leg(gen, refpy, iters=2000):
     """Drop-in path latency (rank 0, N = 1): tests/native/bin/latency_main on
     cfg2's HTTP requests and memcached text requests, and the oracle deciding
@@ -243,6 +328,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-latency", action="store_true")
+    ap.add_argument("--no-streams", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0, help="oracle threads (0 = every usable core)")
     ap.add_argument("--profile-steps", type=int, default=3, help="extra steps with per-kernel HIP events")
     args = ap.parse_args()
@@ -424,6 +510,12 @@ def main():
     latency = None
     if rank == 0 and world == 1 and not args.no_latency:
         latency = latency_leg(gen, refpy)
+    streams = None
+    if rank == 0 and world == 1 and not args.no_streams:
+        try:
+            streams = streams_leg(torch, eng, gen, refpy, w, dev, threads)
+        except Exception as e:  # the streams leg never fails the bench line
+            streams = {"error": repr(e)}
 
     if rank != 0:
         if dist is not None:
@@ -499,6 +591,7 @@ def main():
                                   "storage command's data block is framed by length and never read), which lowers "
                                   "its frac against the len_i + 25 definition",
         "latency": latency,
+        "streams": streams,
         "e2e": None if e2e is None else {
             "verdicts_per_s": round(e2e["requests"] / e2e["s"], 1), "ms_per_pass": round(e2e["s"] * 1e3, 3),
             "requests_per_pass": e2e["requests"], "pcie_gbps": round(e2e["bytes"] / e2e["s"] / 1e9, 2),

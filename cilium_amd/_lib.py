@@ -38,7 +38,7 @@ EXPORTS = (
     "l7g_engine_create", "l7g_engine_destroy", "l7g_policy_update", "l7g_policy_index",
     "l7g_policy_nrules", "l7g_conns_set", "l7g_conn_update", "l7g_classify", "l7g_classify_host", "l7g_stats",
     "l7g_debug_regex", "l7g_debug_phase_times", "l7g_profile_enable", "l7g_profile_last",
-    "l7g_debug_kafka_phase_times", "l7g_kafka_deny_response", "l7g_debug_regex_nfa", "l7g_policy_update_proto", "l7g_kafka_corr_create", "l7g_kafka_corr_destroy",
+    "l7g_debug_kafka_phase_times", "l7g_debug_frame_phase_times", "l7g_kafka_deny_response", "l7g_debug_regex_nfa", "l7g_policy_update_proto", "l7g_kafka_corr_create", "l7g_kafka_corr_destroy",
     "l7g_kafka_corr_requests", "l7g_kafka_corr_responses", "l7g_kafka_corr_gc", "l7g_kafka_corr_size",
     "l7g_flow_stats_enable", "l7g_flow_stats",
     "l7g_tables_export", "l7g_tables_import", "l7g_tables_compiled", "l7g_tables_digest",
@@ -97,6 +97,7 @@ def load(path=None):
     lib.l7g_debug_regex_nfa.argtypes = [cp, sz, C.c_int, cp, sz, cp, sz]
     lib.l7g_debug_phase_times.argtypes = [vp, vp, C.c_int]
     lib.l7g_debug_kafka_phase_times.argtypes = [vp, vp, C.c_int]
+    lib.l7g_debug_frame_phase_times.argtypes = [vp, vp, C.c_int]
     lib.l7g_kafka_corr_create.restype = vp
     lib.l7g_kafka_corr_destroy.argtypes = [vp]
     lib.l7g_kafka_corr_requests.argtypes = [vp, vp, vp, vp, C.c_uint32, vp]

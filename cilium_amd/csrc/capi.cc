@@ -58,6 +58,7 @@ hipError_t LaunchFrameStreams(const uint8_t *arena, uint64_t arena_len, const ui
                               uint32_t *nframes, hipStream_t stream);
 hipError_t HttpPhaseTimes(uint64_t *out, bool reset);
 hipError_t KafkaPhaseTimes(uint64_t *out, bool reset);
+hipError_t FramePhaseTimes(uint64_t *out, bool reset);
 hipError_t LaunchHttpGroup(const Batch &B, const HttpTables &T, const uint32_t *sel, const uint32_t *sel_count,
                            uint32_t n, bool answer_other, uint32_t *ctl, uint32_t *hist, uint32_t *cursor,
                            uint32_t *segs, uint32_t *gsel, uint32_t *gbig, hipStream_t stream);
@@ -1295,6 +1296,12 @@ int l7g_debug_phase_times(l7g_engine *e, uint64_t *out8, int reset) {
     if (!e || e->device < 0) return (int)hipErrorNoDevice;
     hipSetDevice(e->device);
     return (int)HttpPhaseTimes(out8, reset != 0);
+}
+
+int l7g_debug_frame_phase_times(l7g_engine *e, uint64_t *out8, int reset) {
+    if (!e || e->device < 0) return (int)hipErrorNoDevice;
+    hipSetDevice(e->device);
+    return (int)FramePhaseTimes(out8, reset != 0);
 }
 
 int l7g_debug_kafka_phase_times(l7g_engine *e, uint64_t *out8, int reset) {

@@ -167,6 +167,13 @@ class Engine:
             return None
         return out
 
+    def frame_phase_times(self, reset=True):
+        """Per-phase cycle totals of the text-stream framer (-DL7G_FRAME_PHASES build only), or None."""
+        out = np.zeros(8, np.uint64)
+        if self._lib.l7g_debug_frame_phase_times(self._h, out.ctypes.data, 1 if reset else 0) != 0:
+            return None
+        return out
+
     def phase_times(self, reset=True):
         """Per-phase cycle totals of the HTTP kernel (timing build only), or None."""
         out = np.zeros(8, np.uint64)

@@ -286,6 +286,8 @@ int l7g_debug_phase_times(l7g_engine *e, uint64_t *out8, int reset);
  * 1 walk, 2 CRC pass, 3 topic lookups, 4 verdict + output, 5 walk rounds,
  * 6 window refills, 7 tiles). */
 int l7g_debug_kafka_phase_times(l7g_engine *e, uint64_t *out8, int reset);
+/* Per-phase cycle totals of the text-stream framer (-DL7G_FRAME_PHASES builds only; else an error). */
+int l7g_debug_frame_phase_times(l7g_engine *e, uint64_t *out8, int reset);
 
 /* Kafka correlation-ID rewriting of the in-agent Kafka proxy's forwarding
  * path (pkg/kafka/correlation_cache.go:97-213; one cache per client

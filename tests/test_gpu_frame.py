@@ -257,3 +257,47 @@ def test_frame_streams_edges(engine, oracle):
     engine.classify_streams_device(z.data_ptr(), 0, z.data_ptr(), z.data_ptr(), z.data_ptr(), 0, 8, z.data_ptr(),
                                    z.data_ptr(), z.data_ptr(), z.data_ptr(), z.data_ptr(), z.data_ptr(), z.data_ptr())
     torch.cuda.synchronize()
+
+
+def _http_body_requests(n, seed):
+    """Requests whose framing needs the head's content-length / transfer-encoding
+    lines: bodies by Content-Length (any case, signs, spaces, overflow), TE
+    lines, and long pad headers before and after them so that their line
+    starts fall anywhere in the wave framer's 1 KiB windows, window edges
+    included."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        pad1 = b"a" * int(rng.integers(0, 2400))
+        pad2 = b"b" * int(rng.integers(0, 1200))
+        body = b"x" * int(rng.integers(0, 300))
+        k = int(rng.integers(0, 9))
+        name = [b"Content-Length", b"content-length", b"CONTENT-LENGTH", b"Content-Lengthx", b"Content-Length "][
+            int(rng.integers(0, 5))]
+        val = [b"%d" % len(body), b" %d" % len(body), b"+%d" % len(body), b"-1", b"99999999999999999999999",
+               b"\t%d" % len(body), b"%dzz" % len(body), b""][int(rng.integers(0, 8))]
+        hdrs = [b"Host: h%d" % i, b"X-Pad: " + pad1]
+        if k < 6:
+            hdrs.insert(int(rng.integers(0, len(hdrs) + 1)), name + b":" + val)
+        if k == 6:
+            hdrs.insert(int(rng.integers(0, len(hdrs) + 1)), [b"Transfer-Encoding: chunked", b"transfer-encoding:x",
+                                                              b"Transfer-Encodingx: 1"][int(rng.integers(0, 3))])
+        if k == 7:  # two content-length lines: the last one counts
+            hdrs += [b"Content-Length: 3", b"X-B: " + pad2, b"Content-Length: %d" % len(body)]
+        out.append(b"POST /p HTTP/1.1\r\n" + b"\r\n".join(hdrs) + b"\r\n\r\n" + body)
+    return out
+
+
+def test_frame_streams_http_heads_and_bodies(engine, oracle):
+    """The wave-per-stream HTTP framer on heads whose content-length and
+    transfer-encoding lines decide the frames, the adversarial requests and the
+    chunked ones, against the scan restatement and the oracle's verdicts."""
+    reqs = _http_body_requests(1500, 21) + gen.http_adversarial(800, 22) + gen.http_chunked(300, 23)
+    rng = np.random.default_rng(24)
+    reqs = [reqs[i] for i in rng.permutation(len(reqs))]
+    arena, offs, lens = gen.pack(reqs)
+    base = gen.http_workload(2, 10, nconns=48)
+    w = gen.Workload("http-bodies", arena, offs, lens, rng.integers(0, 48, len(reqs)).astype(np.uint32), base.conns,
+                     base.policy, {})
+    n, whole, frames = _run(engine, oracle, w, max_frames=96)
+    assert frames > n * 3

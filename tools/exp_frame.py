@@ -30,7 +30,8 @@ def main():
     s_len = np.array([int(offs[e - 1]) + int(lens[e - 1]) - int(offs[b]) for b, e in zip(first, ends)], np.uint32)
     per = ends - first
     mf = int(per.max())
-    eng = Engine(0)
+    lib = os.environ.get("L7G_LIB")
+    eng = Engine(0, lib_path=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "cilium_amd", f"libl7gpu_{lib}.so")) if lib else Engine(0)
     eng.update_policy(w.policy)
     eng.set_connections(w.conns)
     dev = torch.device("cuda", 0)
@@ -61,7 +62,12 @@ def main():
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) / steps
 
+    eng.frame_phase_times(True)
     t_frame = timeit(lambda: eng.classify_streams_device(*args, stream=s.cuda_stream))
+    ph = eng.frame_phase_times(True)
+    if ph is not None and ph[4]:
+        print(f"  text framer per stream: {ph[1] / ph[4]:.0f} cycles, window loads {ph[2] / ph[4]:.1f} "
+              f"({ph[0] / max(ph[2], 1):.0f} cycles each, {ph[0] / max(ph[1], 1):.2f} of the time), frames {ph[3] / ph[4]:.1f}")
     t_both = timeit(lambda: eng.classify_streams_device(*args, v.data_ptr(), r.data_ptr(), c.data_ptr(),
                                                         stream=s.cuda_stream))
     got = int(nf.sum().item())
