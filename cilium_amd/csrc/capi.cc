@@ -58,6 +58,16 @@ hipError_t LaunchFrameStreams(const uint8_t *arena, uint64_t arena_len, const ui
                               uint32_t *nframes, hipStream_t stream);
 hipError_t HttpPhaseTimes(uint64_t *out, bool reset);
 hipError_t KafkaPhaseTimes(uint64_t *out, bool reset);
+struct CopyPiece {
+    const uint8_t *src;
+    uint8_t *dst;
+    uint64_t bytes;
+};
+struct CopyIn {
+    CopyPiece p[4];
+    int n;
+};
+hipError_t LaunchCopyIn(const CopyIn &c, hipStream_t stream);
 hipError_t FramePhaseTimes(uint64_t *out, bool reset);
 hipError_t LaunchHttpGroup(const Batch &B, const HttpTables &T, const uint32_t *sel, const uint32_t *sel_count,
                            uint32_t n, bool answer_other, uint32_t *ctl, uint32_t *hist, uint32_t *cursor,
@@ -134,6 +144,8 @@ struct HostCtx {
     uint8_t *dev = nullptr;        // device: [inputs | outputs]
     uint8_t *pin_in = nullptr;     // pinned host staging of the inputs
     uint8_t *pin_out = nullptr;    // pinned host staging of the outputs
+    uint8_t *pin_in_dev = nullptr;   // their device addresses (zero-copy; looked up once)
+    uint8_t *pin_out_dev = nullptr;
     size_t in_cap = 0, out_cap = 0;
     ~HostCtx() {
         if (s) hipStreamSynchronize(s);
@@ -737,13 +749,32 @@ static int Classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, con
     // and the text / binary lists the memcached kernel's)
     // (a small memcached-only batch gains nothing from converged waves: its one
     // kernel walks the batch itself, one launch fewer on the latency path)
-    const bool partitioned = nproto > 1 || e->has_kafka || (e->has_mc && n >= kPartitionMin);
+    bool partitioned = nproto > 1 || e->has_kafka || (e->has_mc && n >= kPartitionMin);
     bool any_cold = e->any_cold;
-    if (any_cold && host_conn && n <= kHostScanMax) {
+    // which kernels run: a small call whose connections the host can read (the
+    // synchronous drop-ins: one Allowed(), one OnData) launches only the kernel
+    // of the one protocol its requests use, unpartitioned, where it answers the
+    // requests no parser owns too -- no partition pass, no counter memset, no
+    // launch of the other protocols' kernels on an empty list
+    bool run_http = e->has_http || nproto == 0, run_kafka = e->has_kafka, run_mc = e->has_mc;
+    bool run_r2 = e->has_r2, run_cs = e->has_cs;
+    if (host_conn && n <= kHostScanMax) {
         any_cold = false;
-        for (uint32_t i = 0; i < n && !any_cold; i++) {
+        uint32_t seen = 0;  // bit per parser
+        for (uint32_t i = 0; i < n; i++) {
             const uint32_t ci = host_conn[i];
-            any_cold = ci < e->conns.size() && e->attrs[ci].proto == PROTO_HTTP && e->conns[ci].ruleset != e->hot_ruleset;
+            if (ci >= e->conns.size()) continue;
+            const uint32_t pr = e->attrs[ci].proto;
+            if (pr < 32) seen |= 1u << pr;
+            any_cold = any_cold || (pr == PROTO_HTTP && e->conns[ci].ruleset != e->hot_ruleset);
+        }
+        any_cold = any_cold && e->any_cold;
+        const uint32_t owned = seen & ((1u << PROTO_HTTP) | (1u << PROTO_KAFKA) | (1u << PROTO_MEMCACHE) |
+                                       (1u << PROTO_R2D2) | (1u << PROTO_CASSANDRA));
+        if (owned == (1u << PROTO_HTTP) && e->has_http) {
+            partitioned = run_kafka = run_mc = run_r2 = run_cs = false;
+        } else if (owned == (1u << PROTO_MEMCACHE) && e->has_mc) {
+            partitioned = run_http = run_kafka = run_r2 = run_cs = false;
         }
     }
     StreamScratch *S = nullptr;
@@ -779,7 +810,7 @@ static int Classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, con
     }
     // rule sets with NFA-fallback matchers: the pre-pass writes one u64 per request
     HttpTables ht = e->ht;
-    const bool nfa = e->ht.nfa_pool != nullptr && (e->has_http || nproto == 0);
+    const bool nfa = e->ht.nfa_pool != nullptr && run_http;
     if (nfa && rc == hipSuccess) {
         if (n > S->nfa_cap) {
             if (S->d_nfa) {
@@ -831,7 +862,7 @@ static int Classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, con
     auto mark = [&](int k) {
         if (prof && rc == hipSuccess) rc = hipEventRecord(e->prof_ev[k], s);
     };
-    const bool run[4] = {partitioned, e->has_http || nproto == 0, e->has_kafka, e->has_mc};
+    const bool run[4] = {partitioned, run_http, run_kafka, run_mc};
     for (int k = 0; k < 4; k++) e->prof_ran[k] = run[k];
     mark(0);
     if (rc == hipSuccess && run[0]) rc = LaunchPartition(B, sel_k, sel_m, sel_h, cnt, s);
@@ -891,9 +922,9 @@ static int Classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, con
         rc = LaunchMemcacheClassify(B, mt, sel_m, sel_h, cnt ? cnt + L7_KAFKA_CLASSES : nullptr, !partitioned, big_lanes,
                                     s);
     // r2d2 (proxylib's example line protocol): one lane per request over the whole batch
-    if (rc == hipSuccess && e->has_r2) rc = LaunchR2d2Classify(B, rt, !partitioned, big_lanes, s);
+    if (rc == hipSuccess && run_r2) rc = LaunchR2d2Classify(B, rt, !partitioned, big_lanes, s);
     // cassandra (proxylib): the batch's USE requests, then one lane per request
-    if (rc == hipSuccess && e->has_cs) {
+    if (rc == hipSuccess && run_cs) {
         const size_t need = CassandraScratchBytes(n);
         if (need == 0) rc = hipErrorInvalidValue;
         if (rc == hipSuccess && need > S->use_cap) {
@@ -1009,13 +1040,15 @@ static hipError_t HostGrow(HostCtx *H, uint32_t n, uint64_t arena_len) {
     if (H->dev) hipFree(H->dev);
     if (H->pin_in) hipHostFree(H->pin_in);
     if (H->pin_out) hipHostFree(H->pin_out);
-    H->dev = H->pin_in = H->pin_out = nullptr;
+    H->dev = H->pin_in = H->pin_out = H->pin_in_dev = H->pin_out_dev = nullptr;
     H->in_cap = std::max(need_in + need_in / 4, (size_t)1 << 16);  // (some slack: batches vary)
     H->out_cap = std::max(need_out + need_out / 4, (size_t)1 << 14);
     hipError_t rc;
     if ((rc = hipMalloc(&H->dev, H->in_cap + H->out_cap)) != hipSuccess) { H->in_cap = H->out_cap = 0; return rc; }
     if ((rc = hipHostMalloc(&H->pin_in, H->in_cap, hipHostMallocDefault)) != hipSuccess ||
-        (rc = hipHostMalloc(&H->pin_out, H->out_cap, hipHostMallocDefault)) != hipSuccess) {
+        (rc = hipHostMalloc(&H->pin_out, H->out_cap, hipHostMallocDefault)) != hipSuccess ||
+        (rc = hipHostGetDevicePointer((void **)&H->pin_in_dev, H->pin_in, 0)) != hipSuccess ||
+        (rc = hipHostGetDevicePointer((void **)&H->pin_out_dev, H->pin_out, 0)) != hipSuccess) {
         H->in_cap = H->out_cap = 0;
         return rc;
     }
@@ -1056,17 +1089,49 @@ static hipError_t HostRun(l7g_engine *e, HostCtx *H, uint32_t n, uint64_t arena_
     const uint8_t *d_a;
     uint8_t *d_out = H->dev + H->in_cap;
     if (zc) {
-        void *dp = nullptr;
-        auto dev_ptr = [&](const void *h) -> const uint8_t * {
-            if (rc == hipSuccess) rc = hipHostGetDevicePointer(&dp, const_cast<void *>(h), 0);
-            return (const uint8_t *)dp;
-        };
-        d_o = (const uint64_t *)dev_ptr(in.off);
-        d_l = (const uint32_t *)dev_ptr(in.len);
-        d_c = (const uint32_t *)dev_ptr(in.conn);
-        d_a = in.nseg ? dev_ptr(in.seg[0].p) : (const uint8_t *)d_o;
-        d_out = (uint8_t *)dev_ptr(H->pin_out);
-        if (rc != hipSuccess) return rc;
+        // The inputs are copied into HBM by one kernel (one PCIe round trip per
+        // 64 KiB, every load in flight before the first store) and classified
+        // there: read in place, every dependent read of a framer was a PCIe round
+        // trip.  The verdicts are still written to the pinned memory in place.
+        d_out = H->pin_out_dev;
+        uint8_t *d_in = H->dev;
+        CopyIn ci{};
+        const size_t a_at = in.nseg ? (size_t)((const uint8_t *)in.seg[0].p - H->pin_in) : 0;
+        if (in.off == (const uint64_t *)H->pin_in && in.len == (const uint32_t *)(H->pin_in + nn * 8) &&
+            in.conn == (const uint32_t *)(H->pin_in + nn * 12) && a_at <= a_off && a_at % 16 == 0) {
+            // the thread's staging ([off | len | conn | arena at a_off]): one piece
+            ci.p[0] = {H->pin_in_dev, d_in, (uint64_t)(a_off + arena_len)};
+            ci.n = 1;
+            d_o = (const uint64_t *)d_in;
+            d_l = (const uint32_t *)(d_in + nn * 8);
+            d_c = (const uint32_t *)(d_in + nn * 12);
+            d_a = d_in + a_at;
+        } else {
+            // a batcher slot: four pieces into [off | len | conn | arena], the arrays
+            // nn4 entries long so each starts 16-byte aligned (a_off, a multiple of
+            // 256 at least 16 nn, is at least 16 nn4)
+            void *dp = nullptr;
+            auto dev_ptr = [&](const void *h) -> const uint8_t * {
+                if (rc == hipSuccess) rc = hipHostGetDevicePointer(&dp, const_cast<void *>(h), 0);
+                return (const uint8_t *)dp;
+            };
+            const uint8_t *h_o = dev_ptr(in.off), *h_l = dev_ptr(in.len), *h_c = dev_ptr(in.conn);
+            const uint8_t *h_a = in.nseg ? dev_ptr(in.seg[0].p) : h_o;
+            if (rc != hipSuccess) return rc;
+            auto al16 = [](const void *p) { return ((uintptr_t)p & 15) == 0; };
+            if (!(al16(h_o) && al16(h_l) && al16(h_c) && al16(h_a))) return hipErrorInvalidValue;  // (slots are)
+            const size_t nn4 = (nn + 3) & ~(size_t)3;
+            ci.p[0] = {h_o, d_in, (uint64_t)nn * 8};
+            ci.p[1] = {h_l, d_in + nn4 * 8, (uint64_t)nn * 4};
+            ci.p[2] = {h_c, d_in + nn4 * 12, (uint64_t)nn * 4};
+            ci.p[3] = {h_a, d_in + a_off, in.nseg ? arena_len : 0};
+            ci.n = 4;
+            d_o = (const uint64_t *)d_in;
+            d_l = (const uint32_t *)(d_in + nn4 * 8);
+            d_c = (const uint32_t *)(d_in + nn4 * 12);
+            d_a = in.nseg ? d_in + a_off : d_in;
+        }
+        rc = LaunchCopyIn(ci, s);
     } else {
         uint8_t *d_in = H->dev;
         const bool staging = in.off == (const uint64_t *)H->pin_in;

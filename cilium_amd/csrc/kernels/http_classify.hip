@@ -55,30 +55,9 @@ namespace l7 {
 
 namespace {
 
-#ifndef L7G_HTTP_WAVES  // experiment knobs (tools/exp_http.py builds); defaults are the product's
-#define L7G_HTTP_WAVES 8
-#endif
-#ifndef L7G_HTTP_WIN
-#define L7G_HTTP_WIN 256
-#endif
-#ifndef L7G_HTTP_VMAP  // lane-mode tile map streamed through VGPRs, head windows DMA'd meanwhile
-#define L7G_HTTP_VMAP 1
-#endif
-#ifndef L7G_HTTP_MAPDEPTH  // 64-byte-per-lane map steps in flight (VGPR mode)
-#define L7G_HTTP_MAPDEPTH 3
-#endif
-#ifndef L7G_HTTP_LPR  // lanes per request in the lane-mode map (4: 64-byte steps, 8: 128-byte steps)
-#define L7G_HTTP_LPR 8
-#endif
-#ifndef L7G_HTTP_FASTLINE  // header lines 16 bytes at a time (fast_line, the skip's LF check)
-#define L7G_HTTP_FASTLINE 1
-#endif
-#ifndef L7G_HTTP_DYN  // tiles after the first from a per-launch counter (0: static stride; 1: taken at the tile's start; 2: at its end)
-#define L7G_HTTP_DYN 2
-#endif
-constexpr int kWaves = L7G_HTTP_WAVES;
+constexpr int kWaves = 8;
 constexpr int kBlock = 64 * kWaves;
-constexpr uint32_t kWin = L7G_HTTP_WIN;        // bytes per lane window
+constexpr uint32_t kWin = 256;                 // bytes per lane window
 constexpr uint32_t kWinChunks = kWin / 16;
 constexpr uint32_t kWaveLds = 64 * kWin;       // 16 KiB per wave
 constexpr uint32_t kOffImg = kWaves * kWaveLds;
@@ -630,7 +609,7 @@ __device__ __forceinline__ void parse_window(const Img<kLds> &I, Lane &L, Cursor
     }
     // ---- header lines
     while (L.mode >= M_LINE && L.mode < M_DONE && L.pa < lim) {
-        if (L7G_HTTP_FASTLINE && L.mode == M_LINE && L.pa + 16 <= lim) fast_line(I, L, C, nfa_bits);
+        if (L.mode == M_LINE && L.pa + 16 <= lim) fast_line(I, L, C, nfa_bits);
         if (L.mode == M_LINE) {
             if (C.at(L.pa) == '\r') {
                 L.pa++;
@@ -720,7 +699,7 @@ __device__ __forceinline__ void parse_window(const Img<kLds> &I, Lane &L, Cursor
                     c1 = c2;
                     k = k1;
                 }
-                if (L7G_HTTP_FASTLINE && L.pa + 1 < lim) nx = c1 | 0x100;
+                if (L.pa + 1 < lim) nx = c1 | 0x100;
             }
             if (L.pa < lim && !((c < 0x20 && c != '\t') || c == 0x7F)) {  // absorbing: skip to the value's end
                 L.pa = find_stop<1>(C, L.pa, lim);
@@ -791,7 +770,7 @@ __device__ __forceinline__ void parse_window(const Img<kLds> &I, Lane &L, Cursor
                     const uint32_t c = byte_of(w, p & 15);
                     if (c != '\t') {
                         stop = c | 0x100;
-                        if (L7G_HTTP_FASTLINE && p + 1 < cend && p + 1 < lim) next = byte_of(w, (p + 1) & 15) | 0x100;
+                        if (p + 1 < cend && p + 1 < lim) next = byte_of(w, (p + 1) & 15) | 0x100;
                         break;
                     }
                     L.pa++;
@@ -949,24 +928,26 @@ __device__ __forceinline__ uint64_t window_packed(Lane &L) {
 // ---------------------------------------------------------------- value-stop map of a tile
 // A value nobody constrains ends at its first "value stop" byte (< 0x20 other
 // than HT, or DEL: CR normally, anything else is an error).  Before its first
-// window the wave streams its tile's bytes through its window area, and each
-// lane keeps, for its own request, one bit per 16-byte chunk -- "holds a value
-// stop" -- in registers.  Lane l streams request l: a step moves 64 bytes per
-// lane as four 16-byte LDS-DMA loads (the four 1 KiB blocks of a 4 KiB ring
-// slot; lane l's bytes at 16 l of each block), kMapSlots steps in flight.  So
-// every 16-byte chunk of a request is read once, whatever lies between the
-// tile's requests (packed streams, the HTTP list of a mixed batch, scattered
-// offsets), and a lane searches only its own bits.  (The loads are issued four
-// lanes per request -- a load instruction covers 16 requests' 64-byte runs, not
-// 64 single lines: 2.42 -> 2.18 ms on 4M mixed-stream HTTP requests -- and a
-// ballot hands each lane its request's four bits.)  A long value is then
-// skipped by finding the lane's first marked chunk at or after L.pa and
-// reading only that chunk and the next.  Chunks past the mapped range
-// (kMapChunks, 3 KiB) continue window by window.
+// window the wave streams its tile's bytes, and each lane keeps, for its own
+// request, one bit per 16-byte chunk -- "holds a value stop" -- in registers.
+// A step moves 128 bytes of every request of the tile into VGPRs: load q of
+// step j covers requests 8q..8q+7, lane l reading chunk 8j + (l & 7) of
+// request 8q + (l >> 3), so one load instruction touches 8 full lines; a
+// ballot per load hands each lane its request's eight bits; three steps are in
+// flight.  (Four lanes per request and 64-byte steps: 2.42 -> 2.18 ms on 4M
+// mixed-stream HTTP requests against one line per lane; eight lanes and VGPRs
+// instead of an LDS ring went further, DESIGN.md.)  So every 16-byte chunk of
+// a request is read once, whatever lies between the tile's requests (packed
+// streams, the HTTP list of a mixed batch, scattered offsets), and a lane
+// searches only its own bits.  A long value is then skipped by finding the
+// lane's first marked chunk at or after L.pa and reading only that chunk and
+// the next.  Chunks past the mapped range (kMapChunks, 3 KiB) continue window
+// by window.  The head windows' DMA is issued before the map, into the window
+// area, so it overlaps the map's stream.
 //
-// The bits enter a per-lane shift register four at a time (one step), so
-// after smax steps (the tile's longest request) chunk c sits at bit
-// c + T.off with T.off = kMapChunks - 4 smax, the same for every lane.
+// The bits enter a per-lane shift register eight at a time (one step), so
+// after smax8 steps (the tile's longest request) chunk c sits at bit
+// c + T.off with T.off = kMapChunks - 8 smax8, the same for every lane.
 //
 // Packed tiles (the 64 requests side by side, their span at most 9/8 of their
 // own chunks) take the span mode instead: the span streams as coalesced 1 KiB
@@ -979,9 +960,6 @@ __device__ __forceinline__ uint64_t window_packed(Lane &L) {
 // 4M requests) since no foreign byte is read.
 constexpr uint32_t kMapWords = 6;
 constexpr uint32_t kMapChunks = kMapWords * 32;             // chunks mapped per request
-constexpr uint32_t kStepBytes = 64 * 64;                    // one step: 64 lanes x 64 bytes
-constexpr int kMapSlots = (int)(kWaveLds / kStepBytes);     // steps in flight
-static_assert(kMapSlots >= 2, "map ring");
 constexpr int kRing = (int)(kWaveLds / 1024);               // span mode: 1 KiB pieces in flight
 constexpr uint64_t kSpanChunksMax = 256 * 64;               // span mode: at most 256 KiB
 
@@ -1104,38 +1082,16 @@ __device__ __forceinline__ bool build_tile_map(TileMap &T, Lane &L, uint32_t lan
     T.off = kMapChunks - 4 * smax;
     T.from = 4 * kSkipSteps;
     if (smax <= kSkipSteps) return false;  // every request fits its head window
-    // lanes with nothing (more) to load still issue theirs, at a chunk of the
-    // tile, so every step is four loads and vmcnt counts stay exact
-    // four lanes per request: load q of step j covers requests 16q..16q+15,
-    // lane l reading chunk 4j + (l & 3) of request 16q + (l >> 2), so one load
-    // instruction touches 16 requests' 64-byte runs instead of 64 lines
-    const uint32_t sub = lane & 3, grp = lane >> 2;
-    // the four requests this lane loads for (fixed for the tile): fetched once,
-    // not per step (the compiler waits on each ds_bpermute where it is used)
-    uint64_t qb[4];
-    uint32_t qn[4];
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-        qb[q] = (uint64_t)__shfl((unsigned long long)L.base, 16 * q + (int)grp);
-        qn[q] = (uint32_t)__shfl((int)nch, 16 * q + (int)grp);
-    }
-#define MAP_ISSUE(s, j)                                                                                        \
-    do {                                                                                                       \
-        _Pragma("unroll") for (int q_ = 0; q_ < 4; q_++) {                                                     \
-            const uint64_t b_ = qb[q_];                                                                        \
-            const uint32_t n_ = qn[q_];                                                                        \
-            const uint32_t c_ = 4 * (uint32_t)(j) + sub;                                                       \
-            const uint64_t a_ = c_ < n_ ? b_ + ((uint64_t)c_ << 4) : dummy;                                    \
-            __builtin_amdgcn_global_load_lds((const void *)a_,                                                \
-                                             (__attribute__((address_space(3))) void *)(wave_lds + (s) * kStepBytes + q_ * 1024), \
-                                             16, 0, 0);                                                        \
-        }                                                                                                      \
-    } while (0)
-#if L7G_HTTP_VMAP && L7G_HTTP_LPR == 8
-#undef MAP_ISSUE
-    // As below with eight lanes per request: a step is 128 bytes (a whole
-    // line) per request, load q covers requests 8q..8q+7, so every load
-    // instruction touches 8 full lines.
+    // Lanes with nothing (more) to load still issue theirs, at a chunk of the
+    // tile, so every step is eight loads and vmcnt counts stay exact.  Eight
+    // lanes per request: a step is 128 bytes (a whole line) per request, load q
+    // of step j covers requests 8q..8q+7, lane l reading chunk 8j + (l & 7) of
+    // request 8q + (l >> 3), so every load instruction touches 8 full lines.
+    // The head windows go into the window area now (the map does not use it),
+    // so their DMA overlaps the map stream; the map's steps land in VGPRs,
+    // kMapDepth of them in flight.  Loads and waits are written out (inline
+    // asm): the compiler's own wait placement drains every load at the loop
+    // head (vmcnt(0)), which leaves one memory latency per kMapDepth steps.
     {
         dma_windows_issue(wave_lds, window_packed(L), lane);
         const uint32_t smax8 = (smax + 1) >> 1, skip8 = kWin / 128;
@@ -1148,7 +1104,7 @@ __device__ __forceinline__ bool build_tile_map(TileMap &T, Lane &L, uint32_t lan
             qb8[q] = (uint64_t)__shfl((unsigned long long)L.base, 8 * q + (int)grp8);
             qn8[q] = (uint32_t)__shfl((int)nch, 8 * q + (int)grp8);
         }
-        constexpr int kMapDepth = L7G_HTTP_MAPDEPTH;
+        constexpr int kMapDepth = 3;  // 128-byte-per-lane steps in flight
         gm_u32x4 buf[kMapDepth][8];
 #define MAP_LOAD8(s, j)                                                                                        \
     do {                                                                                                       \
@@ -1190,92 +1146,6 @@ __device__ __forceinline__ bool build_tile_map(TileMap &T, Lane &L, uint32_t lan
         wait_vmcnt<0>();
         return true;
     }
-#elif L7G_HTTP_VMAP
-#undef MAP_ISSUE
-    // The head windows go into the window area now (the map does not use it),
-    // so their DMA overlaps the map stream; the map's 64-byte steps land in
-    // VGPRs, kMapDepth of them in flight (the LDS ring held four).
-    dma_windows_issue(wave_lds, window_packed(L), lane);
-    constexpr int kMapDepth = L7G_HTTP_MAPDEPTH;
-    gm_u32x4 buf[kMapDepth][4];
-    // Loads and waits are written out (inline asm): the compiler's own wait
-    // placement drains every load at the loop head (vmcnt(0)), which leaves
-    // one memory latency per kMapDepth steps.  Slot s is waited for with the
-    // 4 (kMapDepth - 1) loads of the later slots still in flight (vmcnt
-    // retires in issue order; the window DMA above was issued first).
-#define MAP_LOAD(s, j)                                                                                         \
-    do {                                                                                                       \
-        _Pragma("unroll") for (int q_ = 0; q_ < 4; q_++) {                                                     \
-            const uint32_t c_ = 4 * (uint32_t)(j) + sub;                                                       \
-            const uint64_t a_ = c_ < qn[q_] ? qb[q_] + ((uint64_t)c_ << 4) : dummy;                            \
-            asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(buf[s][q_]) : "v"(a_) : "memory");           \
-        }                                                                                                      \
-    } while (0)
-#pragma unroll
-    for (int s = 0; s < kMapDepth; s++) MAP_LOAD(s, kSkipSteps + (uint32_t)s);
-    for (uint32_t j0 = kSkipSteps; j0 < smax; j0 += kMapDepth) {
-#pragma unroll
-        for (int s = 0; s < kMapDepth; s++) {
-            const uint32_t j = j0 + s;
-            asm volatile("s_waitcnt vmcnt(%4)"
-                         : "+v"(buf[s][0]), "+v"(buf[s][1]), "+v"(buf[s][2]), "+v"(buf[s][3])
-                         : "n"(4 * (kMapDepth - 1)));
-            // block q, bit l: request 16q + (l >> 2), chunk 4j + (l & 3)
-            const uint64_t M0 = __ballot(stop_any(u4(buf[s][0])) != 0), M1 = __ballot(stop_any(u4(buf[s][1])) != 0);
-            const uint64_t M2 = __ballot(stop_any(u4(buf[s][2])) != 0), M3 = __ballot(stop_any(u4(buf[s][3])) != 0);
-            MAP_LOAD(s, j + kMapDepth);
-            if (j < smax) {
-                const uint32_t qo = lane >> 4;
-                const uint64_t Mq = qo == 0 ? M0 : qo == 1 ? M1 : qo == 2 ? M2 : M3;
-                uint32_t nb = (uint32_t)(Mq >> (4 * (lane & 15))) & 0xFu;
-                if (4 * j >= nch) nb = 0;
-#pragma unroll
-                for (int q = 0; q < (int)kMapWords - 1; q++) T.m[q] = __builtin_amdgcn_alignbit(T.m[q + 1], T.m[q], 4);
-                T.m[kMapWords - 1] = (T.m[kMapWords - 1] >> 4) | (nb << 28);
-            }
-        }
-    }
-#undef MAP_LOAD
-    wait_vmcnt<0>();
-    return true;
-#else
-#pragma unroll
-    for (int s = 0; s < kMapSlots; s++) MAP_ISSUE(s, kSkipSteps + (uint32_t)s);
-    for (uint32_t j0 = kSkipSteps; j0 < smax; j0 += kMapSlots) {
-#pragma unroll
-        for (int s = 0; s < kMapSlots; s++) {
-            const uint32_t j = j0 + s;
-            wait_vmcnt<4 * (kMapSlots - 1)>();
-            if (j < smax) {
-                // inline asm: a plain LDS read here would make hipcc drain every
-                // in-flight LDS-DMA first (vmcnt(0)), serialising the ring
-                uint4 v0, v1, v2, v3;
-                const uint32_t la = (uint32_t)(uintptr_t)(wave_lds + s * kStepBytes + 16 * lane);
-                asm volatile("ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:1024\n\t"
-                             "ds_read_b128 %2, %4 offset:2048\n\tds_read_b128 %3, %4 offset:3072\n\t"
-                             "s_waitcnt lgkmcnt(0)"
-                             : "=v"(v0), "=v"(v1), "=v"(v2), "=v"(v3)
-                             : "v"(la)
-                             : "memory");
-                // block q, bit l: request 16q + (l >> 2), chunk 4j + (l & 3)
-                const uint64_t M0 = __ballot(stop_any(v0) != 0), M1 = __ballot(stop_any(v1) != 0);
-                const uint64_t M2 = __ballot(stop_any(v2) != 0), M3 = __ballot(stop_any(v3) != 0);
-                const uint32_t qo = lane >> 4;
-                const uint64_t Mq = qo == 0 ? M0 : qo == 1 ? M1 : qo == 2 ? M2 : M3;
-                uint32_t nb = (uint32_t)(Mq >> (4 * (lane & 15))) & 0xFu;
-                if (4 * j >= nch) nb = 0;
-                // shift the register right by 4, the new bits in at the top
-#pragma unroll
-                for (int q = 0; q < (int)kMapWords - 1; q++) T.m[q] = __builtin_amdgcn_alignbit(T.m[q + 1], T.m[q], 4);
-                T.m[kMapWords - 1] = (T.m[kMapWords - 1] >> 4) | (nb << 28);
-            }
-            MAP_ISSUE(s, j + kMapSlots);
-        }
-    }
-    wait_vmcnt<0>();
-#undef MAP_ISSUE
-    return false;
-#endif
 }
 
 // Lanes with L.scan set: skip the rest of the value with the lane's map.
@@ -1371,7 +1241,7 @@ __device__ __forceinline__ void emit(const Lane &L, const Out &O) {
 }
 
 // All rounds of one tile.
-template <bool kLds>
+template <bool kLds, bool kFlush = true>
 __device__ __forceinline__ void run_tile(Lane &L, const uint8_t *img, uint8_t *wave_lds, uint32_t lane, const Out &O) {
     const Img<kLds> I{img};
     L.scan = false;
@@ -1417,7 +1287,7 @@ __device__ __forceinline__ void run_tile(Lane &L, const uint8_t *img, uint8_t *w
     }
     PH_MARK(3);
     PH_COUNT(6, 1);
-    PH_FLUSH(lane);
+    if (kFlush) PH_FLUSH(lane);
 }
 
 }  // namespace
@@ -1444,6 +1314,9 @@ __global__ __launch_bounds__(kBlock) void http_classify_kernel(Batch B, HttpTabl
     const int32_t hot = T.hot_ruleset;
     const bool hot_ok = hot >= 0 && (uint32_t)hot < T.nrulesets && T.rulesets[hot].image_len <= kLdsImageBytes;
     if (kHot && !hot_ok) return;
+#ifdef L7G_PHASE_TIMING
+    const uint64_t ph_k0 = __builtin_amdgcn_s_memtime();
+#endif
     // stage the hot rule set's image
     if (kHot) {
         const DevRuleset r = T.rulesets[hot];
@@ -1461,6 +1334,9 @@ __global__ __launch_bounds__(kBlock) void http_classify_kernel(Batch B, HttpTabl
             if (tid + k * kBlock < n16) ((uint4 *)s_img)[tid + k * kBlock] = t[k];
     }
     __syncthreads();
+#ifdef L7G_PHASE_TIMING
+    if (tid == 0) atomicAdd(&g_phase[7], (unsigned long long)(__builtin_amdgcn_s_memtime() - ph_k0));
+#endif
 
     const Out O{B.verdict, B.rule, B.consumed, T.nfa_bits};
     uint8_t *wave_lds = lds + wave * kWaveLds;
@@ -1472,17 +1348,7 @@ __global__ __launch_bounds__(kBlock) void http_classify_kernel(Batch B, HttpTabl
     // fixed stride.
     const uint32_t stride = gridDim.x * kWaves;
     for (uint32_t tile = blockIdx.x * kWaves + wave, next; tile < ntiles; tile = next) {
-#if L7G_HTTP_DYN == 1
-        if (tile_ctr) {
-            uint32_t t = 0;
-            if (lane == 0) t = atomicAdd(tile_ctr, 1u);
-            next = stride + __builtin_amdgcn_readfirstlane(t);
-        } else {
-            next = tile + stride;
-        }
-#else
         next = tile + stride;
-#endif
         Lane L;
         const uint32_t slot = tile * 64 + lane;
         L.idx = sel ? (slot < m ? sel[slot] : n) : slot;
@@ -1520,14 +1386,18 @@ __global__ __launch_bounds__(kBlock) void http_classify_kernel(Batch B, HttpTabl
                 }
             }
         }
+#ifdef L7G_LAT_REPEAT  // experiment: the tile twice, the second time with warm caches (phases: second only)
+        {
+            Lane L2 = L;
+            run_tile<kHot, false>(L2, img, wave_lds, lane, O);
+        }
+#endif
         run_tile<kHot>(L, img, wave_lds, lane, O);
-#if L7G_HTTP_DYN == 2
-        if (tile_ctr) {
+        if (tile_ctr) {  // taken at the tile's end: a wave asks for work only when it is free
             uint32_t t = 0;
             if (lane == 0) t = atomicAdd(tile_ctr, 1u);
             next = stride + __builtin_amdgcn_readfirstlane(t);
         }
-#endif
     }
 }
 

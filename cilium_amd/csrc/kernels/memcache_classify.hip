@@ -34,18 +34,13 @@ namespace {
 
 constexpr int kBlock = 256;
 // key DFAs walked per pass over the line (more DFAs: more passes)
-#ifndef L7G_MC_DFAS
-#define L7G_MC_DFAS 1
-#endif
-constexpr int kMcPassDfas = L7G_MC_DFAS < kMcMaxDfas ? L7G_MC_DFAS : kMcMaxDfas;
+constexpr int kMcPassDfas = 1;
 constexpr uint32_t kMcLdsImages = 32 * 1024;  // LDS budget for the staged rule-set images
 constexpr int kMcWaves = kBlock / 64;
 constexpr int kMcSortPer = 4;                          // list entries per lane per chunk (1: 4.33 ms, 2: 3.82, 4: 3.25, 8: 3.26, 16: 4.41 on cfg5)
 constexpr uint32_t kMcWaveChunk = 64 * kMcSortPer;     // entries a wave orders by parser at a time
-// waves per SIMD the common kernel is built for (experiments: -DL7G_MC_WAVES=N)
-#ifndef L7G_MC_WAVES
-#define L7G_MC_WAVES 5
-#endif
+// waves per SIMD the common kernel is built for (below)
+constexpr int kMcWavesPerSimd = 5;
 
 // 16-byte aligned register window over one request (the arena is readable up
 // to the 16-byte boundary after its last byte; see include/l7gpu.h).
@@ -641,7 +636,7 @@ __device__ __forceinline__ void mc_classify(Batch B, McTables T, const uint32_t 
     }
 }
 
-// The common kernel is built for L7G_MC_WAVES waves per SIMD (7; 2.4M
+// The common kernel is built for kMcWavesPerSimd waves per SIMD (round 3 on 2.4M
 // mixed-stream memcached requests: 4 waves (100 VGPRs, no spill) 0.91 ms,
 // 6 waves 0.79-0.82, 7 waves 0.79, 8 waves 0.84 -- the spills grow);
 // the NFA variant keeps its registers.
@@ -649,7 +644,7 @@ __device__ __forceinline__ void mc_classify(Batch B, McTables T, const uint32_t 
 // has at most 64 rules: 6 fewer registers per lane than the 4-chunk build).
 // (the 4-chunk build holds 6 more registers: 4 waves per SIMD, where it does not spill)
 template <int kCh>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kCh == 1 ? L7G_MC_WAVES : 4, 8))) void memcache_classify_kernel(Batch B, McTables T,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kCh == 1 ? kMcWavesPerSimd : 4, 8))) void memcache_classify_kernel(Batch B, McTables T,
                                                                                   const uint32_t *__restrict__ sel,
                                                                                   const uint32_t *__restrict__ sel2,
                                                                                   const uint32_t *__restrict__ sel_count,
