@@ -598,11 +598,17 @@ static int SwapIn(l7g_engine *e, std::unique_ptr<PolicySet> ps, std::unique_ptr<
 
 // ---- compiled tables across ranks (engine/serial.h)
 constexpr uint64_t kTablesMagic = 0x3154473754L;  // "T7G1"
+// format and struct-layout tag: an image from a build with another layout of
+// the device records is refused (it would be read at the wrong offsets)
+constexpr uint64_t kTablesAbi = 2ull << 56 | (uint64_t)sizeof(DevRuleset) << 48 | (uint64_t)sizeof(DevNfa) << 36 |
+                                (uint64_t)sizeof(ImgHeader) << 24 | (uint64_t)sizeof(DevKafkaRuleset) << 12 |
+                                (uint64_t)sizeof(McImgHeader);
 
 int l7g_tables_export(l7g_engine *e, uint8_t *buf, size_t cap, size_t *len) {
     std::lock_guard<std::mutex> g(e->mu);
     Ser s;
     s.u64(kTablesMagic);
+    s.u64(kTablesAbi);
     s.u64((uint64_t)e->policy_form);
     s.u64((uint64_t)e->policy_px);
     s.str(e->policy_src);
@@ -621,6 +627,7 @@ int l7g_tables_import(l7g_engine *e, const uint8_t *buf, size_t len, char *err, 
     std::lock_guard<std::mutex> g(e->mu);
     Des d(buf, len);
     if (d.u64() != kTablesMagic) { set_err(err, errlen, "not an l7g_tables_export image"); return -1; }
+    if (d.u64() != kTablesAbi) { set_err(err, errlen, "tables image from a build with another table layout"); return -1; }
     const int form = (int)d.u64(), px = (int)d.u64();
     const std::string src = d.str();
     if (!d.ok) { set_err(err, errlen, "truncated tables image"); return -1; }
@@ -635,7 +642,7 @@ int l7g_tables_import(l7g_engine *e, const uint8_t *buf, size_t len, char *err, 
     auto r2 = std::make_unique<R2Compiler>(ps.get());
     auto cs = std::make_unique<CassCompiler>(ps.get());
     if (!hc->Load(d) || !kc->Load(d) || !mc->Load(d) || !r2->Load(d) || !cs->Load(d) || d.p != d.end) {
-        set_err(err, errlen, "corrupt tables image");
+        set_err(err, errlen, "corrupt or inconsistent tables image");
         return -1;
     }
     const int rc = SwapIn(e, std::move(ps), std::move(hc), std::move(kc), std::move(mc), std::move(r2), std::move(cs),

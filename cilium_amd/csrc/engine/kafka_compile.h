@@ -56,7 +56,15 @@ public:
         d.vec(img_.strings); img_.topic_mask = (uint32_t)d.u64(); img_.client_mask = (uint32_t)d.u64();
         img_.ntopics = d.u64();
         d.umap(topic_id_); d.umap(client_id_); d.cache(cache_);
-        return d.ok;
+        // the kernels probe the hash tables with the masks and read rules by index
+        auto table_ok = [](const std::vector<DevStrSlot> &t, uint32_t mask) {
+            return !t.empty() && (uint64_t)mask + 1 == t.size() && (t.size() & (t.size() - 1)) == 0;
+        };
+        if (!d.ok || !table_ok(img_.topic_hash, img_.topic_mask) || !table_ok(img_.client_hash, img_.client_mask))
+            return false;
+        for (const auto &r : img_.rulesets)
+            if ((uint64_t)r.rule_first + r.nrules > img_.rules.size()) return false;
+        return true;
     }
     size_t compiled = 0;  // rule sets compiled (not taken from the cache) since construction
 

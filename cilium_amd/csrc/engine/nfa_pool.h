@@ -100,4 +100,33 @@ inline uint32_t NfaPoolMaxWords(const std::vector<uint8_t> &pool, const Map &off
     return w;
 }
 
+// An imported tables image (engine/serial.h) is trusted only as far as these
+// checks go: every pattern's DevNfa lies inside the pool, 16-byte aligned,
+// with its tables inside the pool too; every rule set's image lies inside the
+// image bytes.  A well-framed but inconsistent image is refused instead of
+// sending the host or the kernels out of bounds.
+template <class Map>
+inline bool NfaOffsetsValid(const std::vector<uint8_t> &pool, const Map &offsets) {
+    const uint64_t size = pool.size();
+    auto in = [&](uint64_t off, uint64_t bytes) { return off % 16 == 0 && off <= size && bytes <= size - off; };
+    for (const auto &kv : offsets) {
+        const uint64_t off = kv.second;
+        if (!in(off, sizeof(DevNfa))) return false;
+        DevNfa d;
+        memcpy(&d, pool.data() + off, sizeof d);
+        const uint64_t W = d.W, K = d.K, niv = d.nivl;
+        if (W == 0 || W > (1u << 16) || K == 0 || K > 64 || niv > (1u << 24)) return false;
+        if (!in(d.ivl_off, niv * 4) || !in(d.b_off, niv * W * 8) || !in(d.acc_off, K * W * 8) ||
+            !in(d.ascii_off, 128 * 2) || !in(d.t_off, W > (uint64_t)kNfaMaxWords ? sizeof(DevNfaSparse) : K * 8 * W * 256 * W * 8))
+            return false;
+    }
+    return true;
+}
+template <class R>
+inline bool RulesetImagesValid(const std::vector<R> &rulesets, const std::vector<uint8_t> &images) {
+    for (const auto &r : rulesets)
+        if ((uint64_t)r.image_off + r.image_len > images.size()) return false;
+    return true;
+}
+
 }  // namespace l7

@@ -139,6 +139,34 @@ def test_import_refuses_corrupt_image():
     assert b.tables_digest == a.tables_digest and b.tables_compiled == 0
 
 
+def test_import_refuses_inconsistent_image():
+    """a well-framed image whose layout tag or offsets do not fit
+    this build is refused (not read out of bounds)."""
+    import struct
+    import cilium_amd
+    w = _workload()
+    a = cilium_amd.Engine(-1)
+    a.update_policy(w.policy)
+    a.set_connections(w.conns)
+    img = bytearray(a.export_tables())
+    b = cilium_amd.Engine(-1)
+    other_abi = bytearray(img)
+    other_abi[8] ^= 1  # [magic | layout tag | form | px | policy source | HTTP rule sets ...]
+    with pytest.raises(cilium_amd.PolicyError, match="layout"):
+        b.import_tables(bytes(other_abi))
+    (srclen,) = struct.unpack_from("<Q", img, 32)
+    at = 40 + srclen
+    (nrs,) = struct.unpack_from("<Q", img, at)
+    assert nrs >= 1
+    bad = bytearray(img)
+    struct.pack_into("<I", bad, at + 8 + 4, 0xFFFFFFF0)  # rule set 0's image_len
+    with pytest.raises(cilium_amd.PolicyError, match="inconsistent"):
+        b.import_tables(bytes(bad))
+    b.import_tables(bytes(img))
+    b.set_connections(w.conns)
+    assert b.tables_digest == a.tables_digest
+
+
 def test_connection_outside_image_compiles_locally():
     """A rank whose connections need a rule set the exporter never compiled
     compiles just that one (same tables as compiling everything locally)."""
