@@ -21,6 +21,7 @@
 #include "engine/mc_compile.h"
 #include "engine/nfa_pool.h"
 #include "engine/r2_compile.h"
+#include "kernels/copy_in_types.h"
 #include "policy/npds_proto.h"
 #include "policy/policy.h"
 #include "regex/nfa_walk.h"
@@ -28,7 +29,8 @@
 
 namespace l7 {
 hipError_t LaunchHttpClassify(const Batch &B, const HttpTables &T, const uint32_t *sel, const uint32_t *sel_count,
-                              bool any_cold, bool answer_other, uint32_t *tile_ctr, hipStream_t stream);
+                              bool any_cold, bool answer_other, uint32_t *tile_ctr, bool latency, const CopyIn *ci,
+                              hipStream_t stream);
 hipError_t LaunchKafkaClassify(const Batch &B, const KafkaTables &T, const uint32_t *sel, const uint32_t *sel_count,
                                bool answer_other, uint32_t *zlist, uint32_t *zcount, uint32_t *work,
                                hipStream_t stream);
@@ -38,7 +40,7 @@ uint32_t KafkaInflateBlocks();
 uint32_t KafkaInflateRegionBytes();
 hipError_t LaunchMemcacheClassify(const Batch &B, const McTables &T, const uint32_t *sel, const uint32_t *sel2,
                                   const uint32_t *sel_count, bool answer_other, uint32_t scratch_lanes,
-                                  hipStream_t stream);
+                                  hipStream_t stream, const CopyIn *ci = nullptr);
 hipError_t LaunchR2d2Classify(const Batch &B, const R2Tables &T, bool answer_other, uint32_t scratch_lanes,
                               hipStream_t stream);
 size_t CassandraScratchBytes(uint32_t n);
@@ -58,15 +60,6 @@ hipError_t LaunchFrameStreams(const uint8_t *arena, uint64_t arena_len, const ui
                               uint32_t *nframes, hipStream_t stream);
 hipError_t HttpPhaseTimes(uint64_t *out, bool reset);
 hipError_t KafkaPhaseTimes(uint64_t *out, bool reset);
-struct CopyPiece {
-    const uint8_t *src;
-    uint8_t *dst;
-    uint64_t bytes;
-};
-struct CopyIn {
-    CopyPiece p[4];
-    int n;
-};
 hipError_t LaunchCopyIn(const CopyIn &c, hipStream_t stream);
 hipError_t FramePhaseTimes(uint64_t *out, bool reset);
 hipError_t LaunchHttpGroup(const Batch &B, const HttpTables &T, const uint32_t *sel, const uint32_t *sel_count,
@@ -128,6 +121,9 @@ constexpr size_t kZeroCopyMaxBytes = 256 * 1024;
 // batches below this size skip the protocol split when one classifier can walk them alone
 constexpr uint32_t kPartitionMin = 4096;
 constexpr uint32_t kHostScanMax = 4096;
+// at most this many requests: the HTTP requests are framed one per wave, their
+// lines side by side (http_latency_kernel), not one per lane
+constexpr uint32_t kLatencyMax = 64;
 // batches from this size with HTTP requests on more than one rule set take the grouped path
 constexpr uint32_t kGroupMin = 1u << 16;
 constexpr size_t kNfaScratchBytes = 256ull << 20;  // large NFAs: state-set scratch per stream (lanes in flight)  // host calls up to this size check their connections for cold rule sets
@@ -721,9 +717,12 @@ int l7g_conn_update(l7g_engine *e, uint32_t index, const l7g_conn_t *conn, char 
 // l7g_classify; host_conn: the connection indices in host memory as well
 // (l7g_classify_host's calls), so that a small call whose requests all use the
 // hot HTTP rule set skips the general HTTP kernel's launch
+// pre: the call's inputs still to be copied from pinned host memory to where
+// arena / off / len / conn point (HostRun); done by the first kernel when the
+// call is one workgroup of one classifier, else by copy_in_kernel first.
 static int Classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const uint64_t *off, const uint32_t *len,
                     const uint32_t *conn, uint32_t n, uint8_t *verdict, int32_t *rule, uint32_t *consumed,
-                    uint64_t *counters, void *stream, const uint32_t *host_conn) {
+                    uint64_t *counters, void *stream, const uint32_t *host_conn, const CopyIn *pre = nullptr) {
     std::lock_guard<std::mutex> g(e->mu);
     if (e->device < 0) return (int)hipErrorNoDevice;
     hipError_t rc = hipSetDevice(e->device);
@@ -869,6 +868,14 @@ static int Classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, con
     auto mark = [&](int k) {
         if (prof && rc == hipSuccess) rc = hipEventRecord(e->prof_ev[k], s);
     };
+    // the copy of a small call's inputs: inside the one kernel that reads them
+    // when that kernel is one workgroup (HTTP: one request per wave, at most 8;
+    // memcached: at most 64 requests, one wave), else a launch of its own
+    const bool only_http = run_http && !partitioned && !run_kafka && !run_mc && !run_r2 && !run_cs;
+    const bool only_mc = run_mc && !partitioned && !run_http && !run_kafka && !run_r2 && !run_cs;
+    const CopyIn *fuse_http = pre && only_http && !nfa && n <= 8 ? pre : nullptr;
+    const CopyIn *fuse_mc = pre && only_mc && n <= 64 ? pre : nullptr;
+    if (pre && !fuse_http && !fuse_mc && rc == hipSuccess) rc = LaunchCopyIn(*pre, s);
     const bool run[4] = {partitioned, run_http, run_kafka, run_mc};
     for (int k = 0; k < 4; k++) e->prof_ran[k] = run[k];
     mark(0);
@@ -910,7 +917,7 @@ static int Classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, con
         if (rc == hipSuccess) rc = LaunchHttpGrouped(B, ht, gsel, segs, gbig, ctl, e->any_big_image, s);
     } else if (rc == hipSuccess && run[1]) {
         rc = LaunchHttpClassify(B, ht, sel_h, cnt ? cnt + L7_KAFKA_CLASSES + 2 : nullptr, any_cold, !partitioned,
-                                tile_ctr, s);
+                                tile_ctr, n <= kLatencyMax, fuse_http, s);
     }
     mark(2);
     uint32_t *zcount = cnt ? cnt + 31 : nullptr;
@@ -927,7 +934,7 @@ static int Classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, con
     mark(3);
     if (rc == hipSuccess && run[3])
         rc = LaunchMemcacheClassify(B, mt, sel_m, sel_h, cnt ? cnt + L7_KAFKA_CLASSES : nullptr, !partitioned, big_lanes,
-                                    s);
+                                    s, fuse_mc);
     // r2d2 (proxylib's example line protocol): one lane per request over the whole batch
     if (rc == hipSuccess && run_r2) rc = LaunchR2d2Classify(B, rt, !partitioned, big_lanes, s);
     // cassandra (proxylib): the batch's USE requests, then one lane per request
@@ -1095,11 +1102,13 @@ static hipError_t HostRun(l7g_engine *e, HostCtx *H, uint32_t n, uint64_t arena_
     const uint32_t *d_l, *d_c;
     const uint8_t *d_a;
     uint8_t *d_out = H->dev + H->in_cap;
+    CopyIn pre{};  // zero-copy: the inputs' copy into HBM, done by the call's first kernel
     if (zc) {
-        // The inputs are copied into HBM by one kernel (one PCIe round trip per
-        // 64 KiB, every load in flight before the first store) and classified
-        // there: read in place, every dependent read of a framer was a PCIe round
-        // trip.  The verdicts are still written to the pinned memory in place.
+        // The inputs are copied into HBM (one PCIe round trip per 64 KiB, every
+        // load in flight before the first store: by the call's first kernel when
+        // it is one workgroup, else by copy_in_kernel) and classified there: read
+        // in place, every dependent read of a framer was a PCIe round trip.  The
+        // verdicts are still written to the pinned memory in place.
         d_out = H->pin_out_dev;
         uint8_t *d_in = H->dev;
         CopyIn ci{};
@@ -1138,7 +1147,7 @@ static hipError_t HostRun(l7g_engine *e, HostCtx *H, uint32_t n, uint64_t arena_
             d_c = (const uint32_t *)(d_in + nn4 * 12);
             d_a = in.nseg ? d_in + a_off : d_in;
         }
-        rc = LaunchCopyIn(ci, s);
+        pre = ci;
     } else {
         uint8_t *d_in = H->dev;
         const bool staging = in.off == (const uint64_t *)H->pin_in;
@@ -1174,7 +1183,8 @@ static hipError_t HostRun(l7g_engine *e, HostCtx *H, uint32_t n, uint64_t arena_
     int32_t *d_r = (int32_t *)(d_out + ((nn + 3) & ~(size_t)3));
     uint32_t *d_cons = (uint32_t *)(d_out + ((nn + 3) & ~(size_t)3) + nn * 4);
     if (rc == hipSuccess)
-        rc = (hipError_t)Classify(e, d_a, arena_len, d_o, d_l, d_c, n, d_v, d_r, d_cons, nullptr, s, in.conn);
+        rc = (hipError_t)Classify(e, d_a, arena_len, d_o, d_l, d_c, n, d_v, d_r, d_cons, nullptr, s, in.conn,
+                                  pre.n ? &pre : nullptr);
     const size_t out_bytes = ((nn + 3) & ~(size_t)3) + nn * 8;
     if (rc == hipSuccess && n && !zc) rc = hipMemcpyAsync(H->pin_out, d_out, out_bytes, hipMemcpyDeviceToHost, s);
     if (rc == hipSuccess) rc = hipStreamSynchronize(s);
@@ -1364,10 +1374,10 @@ int l7g_profile_last(l7g_engine *e, float out_ms[4]) {
     return (int)rc;
 }
 
-int l7g_debug_phase_times(l7g_engine *e, uint64_t *out8, int reset) {
+int l7g_debug_phase_times(l7g_engine *e, uint64_t *out16, int reset) {
     if (!e || e->device < 0) return (int)hipErrorNoDevice;
     hipSetDevice(e->device);
-    return (int)HttpPhaseTimes(out8, reset != 0);
+    return (int)HttpPhaseTimes(out16, reset != 0);
 }
 
 int l7g_debug_frame_phase_times(l7g_engine *e, uint64_t *out8, int reset) {

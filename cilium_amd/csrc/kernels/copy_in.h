@@ -1,0 +1,38 @@
+// The copy of a small call's inputs done by the call's first kernel when that
+// kernel is a single workgroup (a one-request Allowed(), one OnData): every
+// thread's loads before its stores, then a fence and a barrier, so the
+// workgroup's waves read the copy -- one launch fewer than copy_in_kernel.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "copy_in_types.h"
+#include "gmem.h"
+
+namespace l7 {
+
+__device__ __forceinline__ void copy_in_block(const CopyIn &c) {
+    if (c.n == 0) return;
+    constexpr int kPer = 4;
+    for (int k = 0; k < c.n; k++) {
+        const uint64_t units = (c.p[k].bytes + 15) / 16;
+        const uint4 *s = reinterpret_cast<const uint4 *>(c.p[k].src);
+        uint4 *d = reinterpret_cast<uint4 *>(c.p[k].dst);
+        for (uint64_t u0 = 0; u0 < units; u0 += (uint64_t)blockDim.x * kPer) {
+            uint4 v[kPer];
+#pragma unroll
+            for (int j = 0; j < kPer; j++) {
+                const uint64_t u = u0 + (uint64_t)j * blockDim.x + threadIdx.x;
+                if (u < units) v[j] = gload16((uint64_t)(uintptr_t)(s + u));
+            }
+#pragma unroll
+            for (int j = 0; j < kPer; j++) {
+                const uint64_t u = u0 + (uint64_t)j * blockDim.x + threadIdx.x;
+                if (u < units) d[u] = v[j];
+            }
+        }
+    }
+    __threadfence();
+    __syncthreads();
+}
+
+}  // namespace l7

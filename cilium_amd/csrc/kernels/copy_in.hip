@@ -12,19 +12,10 @@
 
 #include <stdint.h>
 
+#include "copy_in_types.h"
 #include "gmem.h"
 
 namespace l7 {
-
-struct CopyPiece {
-    const uint8_t *src;  // 16-byte aligned, readable to the next multiple of 16
-    uint8_t *dst;        // 16-byte aligned
-    uint64_t bytes;
-};
-struct CopyIn {
-    CopyPiece p[4];
-    int n;
-};
 
 namespace {
 constexpr int kBlock = 1024;

@@ -45,11 +45,13 @@
 #include <cstddef>
 
 #include "../device_tables.h"
+#include "copy_in.h"
 #include "gmem.h"
 
 // OCKL's DPP wave reductions (64-bit forms are not declared by hip_runtime.h)
 extern "C" __device__ __attribute__((const)) unsigned long long __ockl_wfred_min_u64(unsigned long long);
 extern "C" __device__ __attribute__((const)) unsigned long long __ockl_wfred_max_u64(unsigned long long);
+extern "C" __device__ __attribute__((const)) unsigned long long __ockl_wfred_and_u64(unsigned long long);
 
 namespace l7 {
 
@@ -76,7 +78,7 @@ __device__ __forceinline__ uint32_t win_swizzle(uint32_t t) {
 // libl7gpu_timing.so, used by tools/exp_http.py).  Slots: 0 dma, 1 parse,
 // 2 tile map + skips, 3 emit/other, 4 rounds, 5 skips, 6 tiles.
 #ifdef L7G_PHASE_TIMING
-__device__ unsigned long long g_phase[8];
+__device__ unsigned long long g_phase[16];
 #define PH_DECL uint64_t ph_t = __builtin_amdgcn_s_memtime(); uint64_t ph_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #define PH_MARK(slot) do { const uint64_t ph_n = __builtin_amdgcn_s_memtime(); ph_acc[slot] += ph_n - ph_t; ph_t = ph_n; } while (0)
 #define PH_COUNT(slot, v) (ph_acc[slot] += (v))
@@ -86,6 +88,16 @@ __device__ unsigned long long g_phase[8];
 #define PH_MARK(slot) do {} while (0)
 #define PH_COUNT(slot, v) do {} while (0)
 #define PH_FLUSH(lane) do {} while (0)
+#endif
+// latency path: cycles of a section, added to g_phase[slot] by lane 0
+#ifdef L7G_PHASE_TIMING
+#define LAT_T0 uint64_t lat_t = __builtin_amdgcn_s_memtime();
+#define LAT_T(slot) do { const uint64_t lat_n = __builtin_amdgcn_s_memtime(); if ((threadIdx.x & 63) == 0) atomicAdd(&g_phase[slot], (unsigned long long)(lat_n - lat_t)); lat_t = lat_n; } while (0)
+#define LAT_N(slot) do { if ((threadIdx.x & 63) == 0) atomicAdd(&g_phase[slot], 1ull); } while (0)
+#else
+#define LAT_T0
+#define LAT_T(slot) do {} while (0)
+#define LAT_N(slot) do {} while (0)
 #endif
 
 enum : uint32_t {
@@ -1241,12 +1253,15 @@ __device__ __forceinline__ void emit(const Lane &L, const Out &O) {
 }
 
 // All rounds of one tile.
-template <bool kLds, bool kFlush = true>
-__device__ __forceinline__ void run_tile(Lane &L, const uint8_t *img, uint8_t *wave_lds, uint32_t lane, const Out &O) {
+// kInit = false: the lanes' framing state is set up by the caller (latency path).
+// pre: the tile's map, already built (latency path); null: built here.
+template <bool kLds, bool kFlush = true, bool kInit = true>
+__device__ __forceinline__ void run_tile(Lane &L, const uint8_t *img, uint8_t *wave_lds, uint32_t lane, const Out &O,
+                                         const TileMap *pre = nullptr) {
     const Img<kLds> I{img};
     L.scan = false;
     L.tail = false;
-    if (!L.done) {
+    if (kInit && !L.done) {
         L.cg = 0;
         L.dg = 0;
         acc_init(I, L);
@@ -1255,7 +1270,9 @@ __device__ __forceinline__ void run_tile(Lane &L, const uint8_t *img, uint8_t *w
     }
     PH_DECL
     TileMap TM;
-    bool loaded = build_tile_map(TM, L, lane, wave_lds);  // true: the first windows are in
+    bool loaded = false;  // true: the first windows are in
+    if (pre) TM = *pre;
+    else loaded = build_tile_map(TM, L, lane, wave_lds);
     PH_MARK(2);
     Cursor C;
     C.slot = wave_lds + lane * kWin;
@@ -1288,6 +1305,236 @@ __device__ __forceinline__ void run_tile(Lane &L, const uint8_t *img, uint8_t *w
     PH_MARK(3);
     PH_COUNT(6, 1);
     if (kFlush) PH_FLUSH(lane);
+}
+
+
+// ---------------------------------------------------------------- latency path
+// bit i (0..15) set iff byte i of the chunk is CR
+__device__ __forceinline__ uint32_t cr_mask(uint4 w) {
+    auto eq = [](uint32_t x) {
+        const uint32_t t = x ^ 0x0D0D0D0Du;
+        return ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;
+    };
+    return nib(eq(w.x)) | nib(eq(w.y)) << 4 | nib(eq(w.z)) << 8 | nib(eq(w.w)) << 12;
+}
+
+constexpr uint32_t kLatLines = 63;  // header lines one wave frames side by side (lane k: line k)
+
+// One request per wave, for the small calls of the synchronous drop-ins (one
+// Allowed(), a few requests): the tile kernel's one lane walks a request's
+// lines one after the other, every byte a chain of dependent LDS reads (a
+// 1.1 KB cfg2 request: ~43k cycles of framing on one lane, the same with
+// warm caches).  Here the request's lines are framed side by side.
+//
+// Every line of a request ends at its first CR: the method, target, name and
+// value walks all stop there, and anything but LF after it is an error.  So
+// the wave first finds the CRs (a ballot scan, 1 KiB per step, up to the
+// empty line that ends the header block), then lane k runs the ordinary
+// framer over line k alone -- lane 0 the request line from the request's
+// start, lane k >= 1 from line k's first byte in M_LINE, each with L.lena at
+// its line's end (its CR + 2) -- and what the lines leave behind is merged
+// the way the sequential walk accumulates it: any error makes the request
+// PARSE_ERROR; a slot counts at its first occurrence only (the lowest line),
+// and its masks AND into the rule accumulators, which start at the init masks
+// on lane 0 and at all ones on the other lanes; two Content-Length lines are
+// an error and the first one's value counts; a chunked Transfer-Encoding line
+// makes the body chunked.  (A repeated slot's value is walked by its DFA where
+// the sequential framer skips it: both stop at the same bytes and fail on the
+// same ones, and the walk's masks are dropped.)  Lane 0 then ends the header
+// block as the framer does (headers_done on the merged state) and, when the
+// answer needs more -- a chunked body, another framing pass of a large rule
+// set -- carries on sequentially from there.  A header block of more than
+// kLatLines lines is framed sequentially from the start by lane 0.
+// All lanes enter with the same L (the request; done = false, owed = true).
+template <bool kLds>
+__device__ __forceinline__ void lat_request(const Lane &L, const uint8_t *img, uint8_t *wave_lds, uint32_t lane,
+                                            const Out &O) {
+    const Img<kLds> I{img};
+    const uint32_t a0 = L.a0, lena = L.lena;
+    if (lena == a0) {  // nothing yet
+        if (lane == 0) {
+            Lane W = L;
+            finish(W, V_INCOMPLETE);
+            emit(W, O);
+        }
+        return;
+    }
+    LAT_T0
+    // ---- the CRs, in order, until the empty line (crpos: kLatLines + 2 entries)
+    const uint32_t nch = (lena + 15) >> 4;
+    uint32_t *crpos = reinterpret_cast<uint32_t *>(wave_lds);
+    const uint64_t below = (1ull << lane) - 1;
+    uint32_t ncr = 0;
+    int hend = -1;     // index of the empty line that ends the header block
+    bool all = false;  // every byte scanned
+    // The scan also yields the tile map run_tile would stream (span mode: every
+    // lane's request has this base, so chunk c is bit c): the value-stop bits of
+    // the first kMapChunks chunks, one ballot per 64.
+    TileMap TM;
+#pragma unroll
+    for (int q = 0; q < (int)kMapWords; q++) TM.m[q] = 0;
+    TM.off = 0;
+    TM.from = 0;
+    // crpos[r]: the r-th CR's position | kLfKnown (the byte after it was in the
+    // scan's registers) | kLfYes (and it is LF)
+    constexpr uint32_t kLfKnown = 1u << 31, kLfYes = 1u << 30, kPos = kLfYes - 1;
+    for (uint32_t c0 = 0;; c0 += 64) {
+        const uint32_t c = c0 + lane;
+        uint32_t m = 0;
+        uint4 w = make_uint4(0, 0, 0, 0);
+        if (c < nch) {
+            w = gload16(L.base + 16ull * c);
+            m = cr_mask(w);
+            const uint32_t p0 = 16 * c;
+            if (p0 < a0) m &= 0xFFFFu << (a0 - p0);
+            if (p0 + 16 > lena) m &= (1u << (lena - p0)) - 1u;
+        }
+        const uint64_t sb = __ballot(c < nch && stop_any(w) != 0);
+        if (c0 < kMapChunks) {
+#pragma unroll
+            for (int q = 0; q < (int)kMapWords; q += 2)
+                if ((uint32_t)q == c0 / 32) {
+                    TM.m[q] = (uint32_t)sb;
+                    TM.m[q + 1] = (uint32_t)(sb >> 32);
+                }
+        }
+        const uint32_t nb0 = (uint32_t)__shfl_down((int)(w.x & 0xFF), 1);  // the next chunk's first byte
+        const uint32_t cnt = (uint32_t)__builtin_popcount(m);
+        uint32_t ex = 0;  // exclusive prefix of cnt over the lanes (cnt <= 16: five ballots)
+#pragma unroll
+        for (int b = 0; b < 5; b++) ex += (uint32_t)__popcll(__ballot((cnt >> b) & 1) & below) << b;
+        const uint32_t tot = (uint32_t)__builtin_amdgcn_readfirstlane((int)__ockl_wfred_add_u32(cnt));
+        for (uint32_t r = ncr + ex; m; m &= m - 1, r++) {
+            const uint32_t b = (uint32_t)__builtin_ctz(m);
+            const bool known = b < 15 || (lane < 63 && c + 1 < nch);
+            const uint32_t nx = b < 15 ? byte_of(w, b + 1) : nb0;
+            if (r < kLatLines + 2) crpos[r] = (16 * c + b) | (known ? kLfKnown : 0u) | (known && nx == '\n' ? kLfYes : 0u);
+        }
+        ncr += tot;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint32_t have = min(ncr, kLatLines + 1);
+        const uint64_t eb =
+            __ballot(lane >= 1 && lane < have && (crpos[lane] & kPos) == (crpos[lane - 1] & kPos) + 2);
+        if (eb) {
+            hend = (int)__builtin_ctzll(eb);
+            break;
+        }
+        if (c0 + 64 >= nch) {
+            all = true;
+            break;
+        }
+        if (ncr > kLatLines) break;
+    }
+    LAT_T(9);
+    if (!(hend > 0 || (all && ncr <= kLatLines))) {  // too many lines: sequentially, lane 0
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        Lane W = L;
+        if (lane != 0) {
+            W.done = true;
+            W.owed = false;
+            W.base = 0;
+            W.a0 = W.pa = W.lena = 0;
+        }
+        run_tile<kLds>(W, img, wave_lds, lane, O);
+        return;
+    }
+    // ---- lane k: line k
+    uint32_t nl;
+    if (hend > 0) {
+        nl = (uint32_t)hend;
+    } else {
+        const uint32_t sp = ncr ? (crpos[ncr - 1] & kPos) + 2 : a0;  // an unterminated last line
+        nl = ncr + (sp < lena ? 1u : 0u);
+    }
+    uint32_t start = a0, cr = 0;
+    const bool has_cr = lane < nl && lane < ncr;
+    if (lane < nl && lane > 0) start = (crpos[lane - 1] & kPos) + 2;
+    if (has_cr) cr = crpos[lane] & kPos;
+    const uint32_t lend = has_cr ? min(cr + 2, lena) : lena;
+    // (a line that would start at the request's end follows "\r\r" there: the
+    // line before it fails on its LF, and this one has no byte to frame)
+    const bool act = lane < nl && start < lend;
+    const uint32_t cr_end_w = hend > 0 ? crpos[hend] : 0u, cr_end = cr_end_w & kPos;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // crpos read: the window area is the lanes' again
+    __builtin_amdgcn_wave_barrier();
+    const bool complete = has_cr && cr + 2 <= lena;
+    Lane W = L;
+    W.owed = false;
+    W.cg = 0;
+    W.dg = 0;
+    acc_init(I, W);
+    frame_reset(I, W);
+    if (act) {
+        W.lena = lend;
+        if (lane > 0) {
+#pragma unroll
+            for (int c = 0; c < kChunksPerPass; c++) W.acc[c] = ~0ull;
+            W.pa = W.mark = start;
+            W.mode = M_LINE;
+            W.st = 0;
+            W.dcls = W.dtrans = W.dmask = W.dncls = W.dabs = 0;
+            W.slot = kNoSlot;
+        }
+    } else {
+        W.done = true;
+        W.base = 0;
+        W.a0 = W.pa = W.lena = 0;
+    }
+    run_tile<kLds, true, false>(W, img, wave_lds, lane, O, &TM);
+    LAT_T(10);
+    // ---- merge (a line that reached its end finished INCOMPLETE there)
+    const bool bad = act && W.verdict == V_PARSE_ERROR;
+    const bool inc = act && !bad && !complete;
+    const uint64_t clb = __ballot(act && W.have_cl);
+    const bool err = __ballot(bad) != 0 || __popcll(clb) > 1;
+    const bool any_inc = __ballot(inc) != 0;
+    const uint64_t cl = clb ? (uint64_t)__shfl((unsigned long long)W.cl, (int)__builtin_ctzll(clb)) : 0ull;
+    const bool chunked = __ballot(act && W.chunked) != 0;
+    const uint32_t pres = act ? W.present : 0u;
+    bool keep = act;
+#pragma unroll
+    for (int sl = 0; sl < 16; sl++) {
+        const bool mine = lane >= 1 && act && pres == (1u << sl);
+        const uint64_t mk = __ballot(mine);
+        if (mine && lane != (uint32_t)__builtin_ctzll(mk)) keep = false;
+    }
+    const uint32_t present = __ockl_wfred_or_u32(keep ? pres : 0u);
+    uint64_t acc[kChunksPerPass];
+#pragma unroll
+    for (int c = 0; c < kChunksPerPass; c++) acc[c] = __ockl_wfred_and_u64(keep ? W.acc[c] : ~0ull);
+    if (lane != 0) {
+        W.done = true;
+        W.owed = false;
+        W.base = 0;
+        W.a0 = W.pa = W.lena = 0;
+    } else {
+        W.done = false;
+        W.owed = true;
+        W.scan = W.tail = false;
+        W.lena = lena;
+        if (err) {
+            finish(W, V_PARSE_ERROR);
+        } else if (hend <= 0 || any_inc || cr_end + 1 >= lena) {
+            finish(W, V_INCOMPLETE);
+        } else if ((cr_end_w & kLfKnown) ? !(cr_end_w & kLfYes) : *(const uint8_t *)(L.base + cr_end + 1) != '\n') {
+            finish(W, V_PARSE_ERROR);
+        } else {
+            W.pa = cr_end + 2;
+            W.mode = M_LINE;
+            W.present = present;
+#pragma unroll
+            for (int c = 0; c < kChunksPerPass; c++) W.acc[c] = acc[c];
+            W.have_cl = clb != 0;
+            W.cl = cl;
+            W.chunked = chunked;
+            headers_done(I, W, O.nfa_bits);
+        }
+    }
+    if (__ballot(lane == 0 && !W.done)) run_tile<kLds, true, false>(W, img, wave_lds, lane, O);  // body / next pass
+    else if (lane == 0) emit(W, O);
+    LAT_T(11);
 }
 
 }  // namespace
@@ -1386,12 +1633,6 @@ __global__ __launch_bounds__(kBlock) void http_classify_kernel(Batch B, HttpTabl
                 }
             }
         }
-#ifdef L7G_LAT_REPEAT  // experiment: the tile twice, the second time with warm caches (phases: second only)
-        {
-            Lane L2 = L;
-            run_tile<kHot, false>(L2, img, wave_lds, lane, O);
-        }
-#endif
         run_tile<kHot>(L, img, wave_lds, lane, O);
         if (tile_ctr) {  // taken at the tile's end: a wave asks for work only when it is free
             uint32_t t = 0;
@@ -1401,6 +1642,90 @@ __global__ __launch_bounds__(kBlock) void http_classify_kernel(Batch B, HttpTabl
     }
 }
 
+
+// One request per wave (lat_request above) for small calls; the image
+// staging, the request's checks and the answers for entries no parser owns are
+// the tile kernel's.
+template <bool kHot>
+// ci: the call's inputs to copy first (a one-workgroup launch), or none.
+__global__ __launch_bounds__(kBlock) void http_latency_kernel(Batch B, HttpTables T, const uint32_t *__restrict__ sel,
+                                                              const uint32_t *__restrict__ sel_count,
+                                                              uint32_t answer_other, CopyIn ci) {
+    const uint8_t *__restrict__ arena = B.arena;
+    const uint32_t n = B.n, nconns = B.nconns;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63, wave = tid >> 6;
+    uint8_t *s_img = lds + kOffImg;
+#ifdef L7G_PHASE_TIMING
+    const uint64_t ph_k0 = __builtin_amdgcn_s_memtime();
+#endif
+    copy_in_block(ci);
+    const int32_t hot = T.hot_ruleset;
+    const bool hot_ok = hot >= 0 && (uint32_t)hot < T.nrulesets && T.rulesets[hot].image_len <= kLdsImageBytes;
+    if (kHot && !hot_ok) return;
+    if (kHot) {
+        const DevRuleset r = T.rulesets[hot];
+        const uint4 *src = (const uint4 *)(T.images + r.image_off);
+        const uint32_t n16 = (r.image_len + 15) / 16;
+        constexpr uint32_t kIters = (kLdsImageBytes / 16 + kBlock - 1) / kBlock;
+        uint4 t[kIters];
+#pragma unroll
+        for (uint32_t k = 0; k < kIters; k++)
+            if (tid + k * kBlock < n16) t[k] = src[tid + k * kBlock];
+#pragma unroll
+        for (uint32_t k = 0; k < kIters; k++)
+            if (tid + k * kBlock < n16) ((uint4 *)s_img)[tid + k * kBlock] = t[k];
+    }
+    __syncthreads();
+#ifdef L7G_PHASE_TIMING
+    if (tid == 0) atomicAdd(&g_phase[7], (unsigned long long)(__builtin_amdgcn_s_memtime() - ph_k0));
+#endif
+    const Out O{B.verdict, B.rule, B.consumed, T.nfa_bits};
+    uint8_t *wave_lds = lds + wave * kWaveLds;
+    const uint32_t m = sel ? *sel_count : n;
+    for (uint32_t r = blockIdx.x * kWaves + wave; r < m; r += gridDim.x * kWaves) {
+        LAT_T0
+        Lane L;
+        L.idx = sel ? sel[r] : r;
+        L.done = true;
+        L.owed = false;
+        L.verdict = V_UNSUPPORTED;
+        L.rule = -1;
+        L.consumed = 0;
+        L.mode = M_DONE;
+        L.base = 0;
+        L.a0 = L.pa = L.w = L.lena = 0;
+        const uint8_t *img = kHot ? s_img : nullptr;
+        if (L.idx < n) {
+            const uint32_t ci = B.conn_ids[L.idx];
+            const DevConn conn = ci < nconns ? B.conns[ci] : DevConn{-1, PROTO_NONE, 0, 0xFFFF};
+            const bool mine = !L7_PROTO_OWNED(conn.proto) || conn.proto == PROTO_HTTP;
+            const bool http = mine && conn.proto == PROTO_HTTP && conn.ruleset >= 0 && (uint32_t)conn.ruleset < T.nrulesets;
+            const bool is_hot = http && hot_ok && conn.ruleset == hot;
+            if (mine && !http && answer_other && (kHot || !hot_ok)) L.owed = true;
+            if (http && is_hot == kHot) {
+                const uint64_t off = B.offs[L.idx];
+                const uint32_t len = B.lens[L.idx];
+                if (!l7_in_arena(off, len, B.arena_len)) {
+                    L.owed = true;
+                } else {
+                    const uint64_t a = (uint64_t)(arena + off);
+                    L.base = a & ~(uint64_t)15;
+                    L.a0 = (uint32_t)(a & 15);
+                    L.lena = len > 0xFFFFFF00u ? 0xFFFFFF00u + L.a0 : L.a0 + len;
+                    if (!kHot) img = T.images + T.rulesets[conn.ruleset].image_off;
+                    L.done = false;
+                    L.owed = true;
+                }
+            }
+        }
+        LAT_T(8);
+        LAT_N(12);
+        if (!L.done) lat_request<kHot>(L, img, wave_lds, lane, O);
+        else if (L.owed && lane == 0) emit(L, O);
+    }
+}
 
 // Requests grouped by rule set (http_group.hip): a workgroup takes one segment
 // of the grouped list at a time (all of it on one rule set), stages that rule
@@ -1481,8 +1806,11 @@ __global__ __launch_bounds__(kBlock) void http_grouped_kernel(Batch B, HttpTable
 // Host-side launcher (called from the C-ABI): persistent grids of one
 // 512-thread workgroup per CU; the hot-rule-set kernel, then (only if some
 // HTTP connection uses another rule set) the general one.
+// latency: a small call, one request per wave (http_latency_kernel)
+// (ci: latency only, with one workgroup: copied by the first kernel launched)
 hipError_t LaunchHttpClassify(const Batch &B, const HttpTables &T, const uint32_t *sel, const uint32_t *sel_count,
-                              bool any_cold, bool answer_other, uint32_t *tile_ctr, hipStream_t stream) {
+                              bool any_cold, bool answer_other, uint32_t *tile_ctr, bool latency, const CopyIn *ci,
+                              hipStream_t stream) {
     if (B.n == 0) return hipSuccess;
     static int num_cus = 0;
     if (num_cus == 0) {
@@ -1491,11 +1819,26 @@ hipError_t LaunchHttpClassify(const Batch &B, const HttpTables &T, const uint32_
             hipDeviceGetAttribute(&num_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || num_cus <= 0)
             num_cus = 256;
     }
+    const bool hot = T.hot_ruleset >= 0;
+    const uint32_t other = answer_other ? 1u : 0u;
+    if (latency) {
+        const uint32_t lblocks = min((B.n + kWaves - 1) / kWaves, (uint32_t)num_cus);
+        if (ci && lblocks != 1) return hipErrorInvalidValue;
+        CopyIn first = ci ? *ci : CopyIn{};
+        if (hot) {
+            hipLaunchKernelGGL(http_latency_kernel<true>, dim3(lblocks), dim3(kBlock), 0, stream, B, T, sel, sel_count,
+                               other, first);
+            first = CopyIn{};
+        }
+        if (!hot || any_cold)
+            hipLaunchKernelGGL(http_latency_kernel<false>, dim3(lblocks), dim3(kBlock), 0, stream, B, T, sel, sel_count,
+                               other, first);
+        return hipGetLastError();
+    }
+    if (ci) return hipErrorInvalidValue;
     const uint32_t ntiles = (B.n + 63) / 64;
     uint32_t blocks = (ntiles + kWaves - 1) / kWaves;
     blocks = min(blocks, (uint32_t)num_cus);
-    const bool hot = T.hot_ruleset >= 0;
-    const uint32_t other = answer_other ? 1u : 0u;
     // tile_ctr: two zeroed counters (hot, general launch) or null (fixed stride)
     if (hot)
         hipLaunchKernelGGL(http_classify_kernel<true>, dim3(blocks), dim3(kBlock), 0, stream, B, T, sel, sel_count, other,
@@ -1530,9 +1873,9 @@ hipError_t LaunchHttpGrouped(const Batch &B, const HttpTables &T, const uint32_t
 
 #ifdef L7G_PHASE_TIMING
 hipError_t HttpPhaseTimes(uint64_t *out, bool reset) {
-    hipError_t rc = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), sizeof(unsigned long long) * 8);
+    hipError_t rc = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), sizeof(unsigned long long) * 16);
     if (rc == hipSuccess && reset) {
-        static const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        static const unsigned long long z[16] = {};
         rc = hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof z);
     }
     return rc;

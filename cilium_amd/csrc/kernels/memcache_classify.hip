@@ -26,6 +26,7 @@
 #include "../device_tables.h"
 #include "../engine/mc_groups.h"
 #include "../regex/nfa_walk.h"
+#include "copy_in.h"
 #include "gmem.h"
 
 namespace l7 {
@@ -610,7 +611,8 @@ __device__ __forceinline__ void mc_loop(Batch B, McTables T, const uint8_t *imag
 template <bool kNfa, int kCh>
 __device__ __forceinline__ void mc_classify(Batch B, McTables T, const uint32_t *__restrict__ sel,
                                             const uint32_t *__restrict__ sel2, const uint32_t *__restrict__ sel_count,
-                                            uint32_t answer_other) {
+                                            uint32_t answer_other, const CopyIn &ci) {
+    copy_in_block(ci);  // (a one-workgroup call's inputs, when the host asks)
     // The rule-set images (command / opcode masks, key DFAs) are read once per
     // key byte in a dependent chain: when they all fit, every workgroup stages
     // them in LDS (dynamic shared memory sized by the launcher) and walks them
@@ -648,35 +650,37 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kCh == 1
                                                                                   const uint32_t *__restrict__ sel,
                                                                                   const uint32_t *__restrict__ sel2,
                                                                                   const uint32_t *__restrict__ sel_count,
-                                                                                  uint32_t answer_other) {
-    mc_classify<false, kCh>(B, T, sel, sel2, sel_count, answer_other);
+                                                                                  uint32_t answer_other, CopyIn ci) {
+    mc_classify<false, kCh>(B, T, sel, sel2, sel_count, answer_other, ci);
 }
 __global__ __launch_bounds__(kBlock) void memcache_classify_nfa_kernel(Batch B, McTables T,
                                                                        const uint32_t *__restrict__ sel,
                                                                        const uint32_t *__restrict__ sel2,
                                                                        const uint32_t *__restrict__ sel_count,
-                                                                       uint32_t answer_other) {
-    mc_classify<true, kMcMaxChunks>(B, T, sel, sel2, sel_count, answer_other);
+                                                                       uint32_t answer_other, CopyIn ci) {
+    mc_classify<true, kMcMaxChunks>(B, T, sel, sel2, sel_count, answer_other, ci);
 }
 
 // scratch_lanes: lanes T.nfa_scratch holds (when it is set)
 hipError_t LaunchMemcacheClassify(const Batch &B, const McTables &T, const uint32_t *sel, const uint32_t *sel2,
                                   const uint32_t *sel_count, bool answer_other, uint32_t scratch_lanes,
-                                  hipStream_t stream) {
+                                  hipStream_t stream, const CopyIn *ci) {
     if (B.n == 0) return hipSuccess;
     uint32_t blocks = (B.n + kBlock - 1) / kBlock;
     if (blocks > 8192) blocks = 8192;
     if (T.nfa_scratch) blocks = max(1u, min(blocks, scratch_lanes / kBlock));  // (grid-stride loop)
+    if (ci && blocks != 1) return hipErrorInvalidValue;  // (the copy is one workgroup's)
+    const CopyIn c = ci ? *ci : CopyIn{};
     const size_t lds = T.images_len && T.images_len <= kMcLdsImages ? ((T.images_len + 15) & ~15u) : 0;
     if (T.nfa_pool)
         hipLaunchKernelGGL(memcache_classify_nfa_kernel, dim3(blocks), dim3(kBlock), lds, stream, B, T, sel, sel2, sel_count,
-                           answer_other ? 1u : 0u);
+                           answer_other ? 1u : 0u, c);
     else if (T.max_chunks <= 1)
         hipLaunchKernelGGL(memcache_classify_kernel<1>, dim3(blocks), dim3(kBlock), lds, stream, B, T, sel, sel2, sel_count,
-                           answer_other ? 1u : 0u);
+                           answer_other ? 1u : 0u, c);
     else
         hipLaunchKernelGGL(memcache_classify_kernel<kMcMaxChunks>, dim3(blocks), dim3(kBlock), lds, stream, B, T, sel, sel2,
-                           sel_count, answer_other ? 1u : 0u);
+                           sel_count, answer_other ? 1u : 0u, c);
     return hipGetLastError();
 }
 

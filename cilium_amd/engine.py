@@ -175,8 +175,9 @@ class Engine:
         return out
 
     def phase_times(self, reset=True):
-        """Per-phase cycle totals of the HTTP kernel (timing build only), or None."""
-        out = np.zeros(8, np.uint64)
+        """Per-phase cycle totals of the HTTP kernels (timing build only; 16 slots,
+        include/l7gpu.h), or None."""
+        out = np.zeros(16, np.uint64)
         if self._lib.l7g_debug_phase_times(self._h, out.ctypes.data, 1 if reset else 0) != 0:
             return None
         return out

@@ -276,12 +276,14 @@ int l7g_flow_stats_enable(l7g_engine *e, int on);
 int l7g_flow_stats(l7g_engine *e, l7g_flow_stat_t *out, uint32_t cap, uint32_t *n, int reset);
 int l7g_profile_last(l7g_engine *e, float out_ms[4]);
 
-/* Profiling hook: per-phase cycle totals of the HTTP kernel (slots: 0 window
- * DMA, 1 parse, 2 long-value scan, 3 other, 4 rounds, 5 scanned values,
- * 6 tiles), summed over waves since the last reset.  Only the timing build
- * (libl7gpu_timing.so, -DL7G_PHASE_TIMING) records them; the product build
- * returns hipErrorNotSupported. */
-int l7g_debug_phase_times(l7g_engine *e, uint64_t *out8, int reset);
+/* Profiling hook: per-phase cycle totals of the HTTP kernels, 16 slots (0
+ * window DMA, 1 parse, 2 long-value scan, 3 other, 4 rounds, 5 scanned values,
+ * 6 tiles, 7 rule-set image staging; latency kernel: 8 request fetch, 9 CR
+ * scan, 10 lines framed, 11 merge + end of the header block, 12 requests),
+ * summed over waves since the last reset.  Only a timing build
+ * (-DL7G_PHASE_TIMING) records them; the product build returns
+ * hipErrorNotSupported. */
+int l7g_debug_phase_times(l7g_engine *e, uint64_t *out16, int reset);
 /* The same for the Kafka kernel (-DL7G_KX_TIMING builds; slots: 0 framing,
  * 1 walk, 2 CRC pass, 3 topic lookups, 4 verdict + output, 5 walk rounds,
  * 6 window refills, 7 tiles). */

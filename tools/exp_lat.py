@@ -52,6 +52,9 @@ def main():
             m = np.mean(phs[5:], axis=0)
             line += (f" | cycles: stage {m[7]:.0f} map/emit {m[2]:.0f} dma {m[0]:.0f} parse {m[1]:.0f} other {m[3]:.0f}"
                      f" rounds {m[4]:.1f} scans {m[5]:.1f}")
+            if m[12]:  # latency kernel (one request per wave)
+                line += (f" | latency kernel: fetch {m[8]:.0f} CR scan {m[9]:.0f} lines {m[10]:.0f}"
+                         f" merge+end {m[11]:.0f}")
         print(line, flush=True)
 
 

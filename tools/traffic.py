@@ -18,8 +18,10 @@ import json
 import os
 import sys
 
-STAGES = {"http_classify_kernel": "http_classify_kernel", "kafka_classify_kernel": "kafka_classify_kernel",
-          "memcache_classify_kernel": "memcache_classify_kernel", "partition_kernel": "partition_kernel"}
+STAGES = {"http_classify_kernel": "http_classify_kernel", "http_grouped_kernel": "http_grouped_kernel",
+          "http_group_count_kernel": "http_group_count_kernel", "http_group_scatter_kernel": "http_group_scatter_kernel",
+          "kafka_classify_kernel": "kafka_classify_kernel", "memcache_classify_kernel": "memcache_classify_kernel",
+          "partition_kernel": "partition_kernel"}
 
 
 def per_name(root, counter):
