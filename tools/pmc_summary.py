@@ -8,7 +8,7 @@ import sys
 
 def summarize(root, pattern="http_classify"):
     out = {}
-    for f in sorted(glob.glob(f"{root}/pmc*/pmc_counter_collection.csv")):
+    for f in sorted(set(glob.glob(f"{root}/**/pmc_counter_collection.csv", recursive=True))):
         agg = collections.defaultdict(float)
         for r in csv.DictReader(open(f)):
             if pattern not in r["Kernel_Name"]:
