@@ -13,7 +13,9 @@ namespace l7 {
 __device__ __forceinline__ void copy_in_block(const CopyIn &c) {
     if (c.n == 0) return;
     constexpr int kPer = 4;
-    for (int k = 0; k < c.n; k++) {
+#pragma unroll
+    for (int k = 0; k < 4; k++) {  // (unrolled: an indexed kernel argument would live in scratch)
+        if (k >= c.n) break;
         const uint64_t units = (c.p[k].bytes + 15) / 16;
         const uint4 *s = reinterpret_cast<const uint4 *>(c.p[k].src);
         uint4 *d = reinterpret_cast<uint4 *>(c.p[k].dst);

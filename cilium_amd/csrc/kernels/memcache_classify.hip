@@ -371,19 +371,11 @@ __device__ __forceinline__ void text_fast(const Image &I, Keys<kCh> &K, const ui
 // kLds: `images` is the workgroup's LDS copy.  The two cases are separate
 // instantiations so that every image read compiles to a ds_read (LDS) or a
 // global_load: one pointer that may be either makes them all flat loads.
+// mc_body: the request's offset, length and connection already in hand.
 template <bool kNfa, bool kLds, int kCh>
-__device__ __forceinline__ void mc_one(const Batch &B, const McTables &T, const uint8_t *images, uint32_t idx,
-                                       uint32_t answer_other) {
-    const uint32_t nconns = B.nconns;
-    const uint32_t *__restrict__ conn_ids = B.conn_ids;
-    const DevConn *__restrict__ conns = B.conns;
+__device__ __forceinline__ void mc_body(const Batch &B, const McTables &T, const uint8_t *images, uint32_t idx,
+                                        uint64_t off, uint32_t len, DevConn conn, uint32_t answer_other) {
     {
-        // the request's connection, offset and length in one round trip (for
-        // a one-request call they come over PCIe)
-        const uint32_t ci = conn_ids[idx];
-        const uint64_t off = B.offs[idx];
-        const uint32_t len = B.lens[idx];
-        const DevConn conn = ci < nconns ? conns[ci] : DevConn{-1, PROTO_NONE, 0, 0xFFFF};
         if (conn.proto != PROTO_MEMCACHE || conn.ruleset < 0 || (uint32_t)conn.ruleset >= T.nrulesets) {
             if (answer_other && (!L7_PROTO_OWNED(conn.proto) || conn.proto == PROTO_MEMCACHE)) {  // no parser: UNSUPPORTED
                 B.verdict[idx] = V_UNSUPPORTED;
@@ -502,6 +494,18 @@ __device__ __forceinline__ void mc_one(const Batch &B, const McTables &T, const 
     }
 }
 
+template <bool kNfa, bool kLds, int kCh>
+__device__ __forceinline__ void mc_one(const Batch &B, const McTables &T, const uint8_t *images, uint32_t idx,
+                                       uint32_t answer_other) {
+    // the request's connection, offset and length in one round trip (for a
+    // one-request call they come over PCIe), then its connection
+    const uint32_t ci = B.conn_ids[idx];
+    const uint64_t off = B.offs[idx];
+    const uint32_t len = B.lens[idx];
+    const DevConn conn = ci < B.nconns ? B.conns[ci] : DevConn{-1, PROTO_NONE, 0, 0xFFFF};
+    mc_body<kNfa, kLds, kCh>(B, T, images, idx, off, len, conn, answer_other);
+}
+
 // The parser each of a lane's kMcSortPer entries takes (memcached/parser.go:
 // 186-202: the connection's, else the one its first byte picks), and text
 // retrievals (get / gets / gat / gats) apart from the other commands, whose
@@ -509,21 +513,27 @@ __device__ __forceinline__ void mc_one(const Batch &B, const McTables &T, const 
 // binary, 3 everything else, 4 no entry.  The loads go out phase by phase
 // (connection ids, connections, offsets / lengths, first bytes) so the lane
 // waits four memory latencies, not four per entry.
+// Also returned, for the classifying lane (no second fetch): the entry's
+// offset, length and connection (rsf: rule set << 12 | flags << 10 | offset
+// bits 32..41; ~0u: kind 3, or a field that does not fit, and the
+// classifying lane reads them itself).
 __device__ __forceinline__ void mc_kinds(const Batch &B, const McTables &T, const uint32_t (&ix)[kMcSortPer],
-                                         uint32_t (&kd)[kMcSortPer]) {
-    uint32_t ci[kMcSortPer], fl[kMcSortPer], ln[kMcSortPer];
-    uint64_t of[kMcSortPer];
+                                         uint32_t (&kd)[kMcSortPer], uint64_t (&of)[kMcSortPer],
+                                         uint32_t (&ln)[kMcSortPer], uint32_t (&rsf)[kMcSortPer]) {
+    uint32_t ci[kMcSortPer], fl[kMcSortPer];
 #pragma unroll
     for (int r = 0; r < kMcSortPer; r++) ci[r] = ix[r] != ~0u ? B.conn_ids[ix[r]] : ~0u;
 #pragma unroll
     for (int r = 0; r < kMcSortPer; r++) {
         kd[r] = ix[r] == ~0u ? 4 : 3;
         fl[r] = 0;
+        rsf[r] = ~0u;
         if (ci[r] < B.nconns) {
             const DevConn c = B.conns[ci[r]];
             if (c.proto == PROTO_MEMCACHE && c.ruleset >= 0 && (uint32_t)c.ruleset < T.nrulesets) {
                 kd[r] = 0;
                 fl[r] = c.flags;
+                rsf[r] = c.ruleset < (1 << 20) ? (uint32_t)c.ruleset << 12 | (c.flags & 3u) << 10 : ~0u;
             }
         }
     }
@@ -534,7 +544,12 @@ __device__ __forceinline__ void mc_kinds(const Batch &B, const McTables &T, cons
         if (kd[r] == 0) {
             of[r] = B.offs[ix[r]];
             ln[r] = B.lens[ix[r]];
-            if (ln[r] == 0 || !l7_in_arena(of[r], ln[r], B.arena_len)) kd[r] = 3;
+            if (ln[r] == 0 || !l7_in_arena(of[r], ln[r], B.arena_len)) {
+                kd[r] = 3;
+                rsf[r] = ~0u;
+            } else if (rsf[r] != ~0u) {
+                rsf[r] = of[r] >> 42 ? ~0u : rsf[r] | (uint32_t)(of[r] >> 32);  // (offsets past 4 TiB: fetched again)
+            }
         }
     }
 #pragma unroll
@@ -553,18 +568,20 @@ __device__ __forceinline__ void mc_kinds(const Batch &B, const McTables &T, cons
 // reads next anyway), orders them by parser in its own LDS slice (stable:
 // list order within a parser), then classifies them in that order, so the
 // wave mostly runs one parser's path instead of text and binary one after the
-// other.  Waves never wait for each other (no workgroup barrier).
+// other.  The slice holds each entry's index, length, offset and connection
+// (16 bytes), so the classifying lane starts from the rule set and the
+// request's bytes instead of fetching the entry's metadata a second time.
+// Waves never wait for each other (no workgroup barrier).
 template <bool kNfa, bool kLds, int kCh>
 __device__ __forceinline__ void mc_loop(Batch B, McTables T, const uint8_t *images, const uint32_t *__restrict__ sel,
                                         const uint32_t *__restrict__ sel2, const uint32_t *__restrict__ sel_count,
-                                        uint32_t answer_other) {
+                                        uint32_t answer_other, uint4 *ent) {
     const uint32_t n = B.n;
     // sel: sel_count[0] entries from sel's start, sel_count[1] from its end,
     // sel_count[3] from sel2's end (n slots each); null: all n
     const uint32_t ma = sel ? sel_count[0] : n;
     const uint32_t mb = sel ? ma + sel_count[3] : n;
     const uint32_t m = sel ? mb + sel_count[1] : n;
-    __shared__ uint32_t s_idx[kMcWaves][kMcWaveChunk];  // a wave's entries in parser order
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if (m <= 64) {  // one wave's worth (a proxylib OnData): nothing to order, and the
                     // first bytes would be one more round trip (zero-copy: over PCIe)
@@ -575,16 +592,17 @@ __device__ __forceinline__ void mc_loop(Batch B, McTables T, const uint8_t *imag
         return;
     }
     const uint64_t below = (1ull << lane) - 1;
-    uint32_t *slot = s_idx[wave];
+    uint4 *slot = ent + wave * kMcWaveChunk;
     for (uint32_t base = (blockIdx.x * kMcWaves + wave) * kMcWaveChunk; base < m;
          base += gridDim.x * kMcWaves * kMcWaveChunk) {
-        uint32_t ix[kMcSortPer], kd[kMcSortPer];
+        uint32_t ix[kMcSortPer], kd[kMcSortPer], ln[kMcSortPer], rsf[kMcSortPer];
+        uint64_t of[kMcSortPer];
 #pragma unroll
         for (int r = 0; r < kMcSortPer; r++) {
             const uint32_t i = base + r * 64 + lane;
             ix[r] = i >= m ? ~0u : !sel ? i : i < ma ? sel[i] : i < mb ? sel2[n - 1 - (i - ma)] : sel[n - 1 - (i - mb)];
         }
-        mc_kinds(B, T, ix, kd);
+        mc_kinds(B, T, ix, kd, of, ln, rsf);
         uint32_t lo[4] = {0, 0, 0, 0};  // exclusive offsets, parser-major
 #pragma unroll
         for (int r = 0; r < kMcSortPer; r++)
@@ -595,7 +613,7 @@ __device__ __forceinline__ void mc_loop(Batch B, McTables T, const uint8_t *imag
 #pragma unroll
             for (int k = 0; k < 4; k++) {
                 const uint64_t mk = __ballot(kd[r] == (uint32_t)k);
-                if (kd[r] == (uint32_t)k) slot[lo[k] + __popcll(mk & below)] = ix[r];
+                if (kd[r] == (uint32_t)k) slot[lo[k] + __popcll(mk & below)] = make_uint4(ix[r], ln[r], (uint32_t)of[r], rsf[r]);
                 lo[k] += __popcll(mk);
             }
         }
@@ -603,7 +621,16 @@ __device__ __forceinline__ void mc_loop(Batch B, McTables T, const uint8_t *imag
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        for (uint32_t k = lane; k < total; k += 64) mc_one<kNfa, kLds, kCh>(B, T, images, slot[k], answer_other);
+        for (uint32_t k = lane; k < total; k += 64) {
+            const uint4 e = slot[k];  // {index, length, offset low, offset high 10 bits | rule set << 12 | flags << 10}
+            if (e.w == ~0u) {
+                mc_one<kNfa, kLds, kCh>(B, T, images, e.x, answer_other);
+            } else {
+                const DevConn conn{(int32_t)(e.w >> 12), PROTO_MEMCACHE, (uint8_t)((e.w >> 10) & 3u), 0xFFFF};
+                mc_body<kNfa, kLds, kCh>(B, T, images, e.x, (uint64_t)(e.w & 0x3FFu) << 32 | e.z, e.y, conn,
+                                         answer_other);
+            }
+        }
         __builtin_amdgcn_wave_barrier();  // (the slice is rewritten by the next chunk)
     }
 }
@@ -618,6 +645,7 @@ __device__ __forceinline__ void mc_classify(Batch B, McTables T, const uint32_t 
     // them in LDS (dynamic shared memory sized by the launcher) and walks them
     // there instead of through L1/L2.
     extern __shared__ __attribute__((aligned(16))) uint8_t mc_lds[];
+    __shared__ uint4 s_ent[kMcWaves][kMcWaveChunk];  // each wave's entries in parser order, with their fields
     if (T.images_len && T.images_len <= kMcLdsImages) {
         const uint32_t n16 = (T.images_len + 15) / 16;
         // every load issued before the first store: one memory round trip per
@@ -632,9 +660,9 @@ __device__ __forceinline__ void mc_classify(Batch B, McTables T, const uint32_t 
         for (uint32_t k = 0; k < kIters; k++)
             if (threadIdx.x + k * kBlock < n16) ((uint4 *)mc_lds)[threadIdx.x + k * kBlock] = t[k];
         __syncthreads();
-        mc_loop<kNfa, true, kCh>(B, T, mc_lds, sel, sel2, sel_count, answer_other);
+        mc_loop<kNfa, true, kCh>(B, T, mc_lds, sel, sel2, sel_count, answer_other, &s_ent[0][0]);
     } else {
-        mc_loop<kNfa, false, kCh>(B, T, T.images, sel, sel2, sel_count, answer_other);
+        mc_loop<kNfa, false, kCh>(B, T, T.images, sel, sel2, sel_count, answer_other, &s_ent[0][0]);
     }
 }
 

@@ -31,6 +31,8 @@ def main():
             want = {"cfg3produce": kinds == 0, "cfg3fetch": kinds == 1, "cfg3other": kinds > 1}[wl]
             w = gen.select(w, np.nonzero(want)[0], wl)
             n = w.n
+    elif wl == "mc":  # memcached alone (cfg5's memcached stream)
+        w = gen.memcache_workload(n)
     else:
         w = gen.mixed_workload(n)
     print(f"{wl}: {n} requests, {w.arena.nbytes / 1e6:.1f} MB, generated in {time.time() - t0:.1f}s", flush=True)
