@@ -82,7 +82,10 @@ constexpr uint32_t kLdsImageBytes = 32 * 1024;  // LDS budget for the hot rule-s
 // kGroupSegEntries entries, images up to kGroupImageBytes staged (the grouped
 // kernel keeps two control words after them).
 constexpr uint32_t kMaxGroupRulesets = 4096;
-constexpr uint32_t kGroupSegEntries = 1024;
+// (a workgroup waits at a barrier between segments while the next image is
+// staged: cfg4 5.46 / 5.21 / 5.28 / 5.63 ms at 2048 / 4096 / 8192 / 16384
+// entries, 5.66 at 1024; profiles/r5/ab5g_group_segment.log)
+constexpr uint32_t kGroupSegEntries = 4096;
 constexpr uint32_t kGroupImageBytes = kLdsImageBytes - 16;
 
 // Header-name recognition: every image carries a small DFA over the
