@@ -15,9 +15,9 @@
 // memcached request's first byte, one HBM line per request, 5 of its 7 GB per
 // cfg5 launch; the memcached kernel now splits text from binary itself, from
 // bytes it reads anyway.  One block owns
-// 2048 consecutive requests (8 per lane, protocol kept in registers between
+// 4096 consecutive requests (8 per lane, protocol kept in registers between
 // the count and the write pass) and takes its slot range with one atomic per
-// protocol.
+// list.
 #include <hip/hip_runtime.h>
 
 #include "../device_tables.h"
@@ -25,8 +25,12 @@
 namespace l7 {
 
 namespace {
-constexpr int kBlock = 256;
-constexpr int kPer = 8;  // rows (of 256 requests) per workgroup
+// 512 threads x 8 rows: a workgroup's 4096 requests keep stream order in every
+// list, so a Kafka wave's 64 entries lie closer together than with 2048
+// (cfg5: partition 0.69 -> 0.65 ms and Kafka 16.69 -> 16.49 ms; 16 rows of 256:
+// partition 0.79; 1024 threads: 0.97; profiles/r5/ab5h_partition_block.log)
+constexpr int kBlock = 512;
+constexpr int kPer = 8;  // rows (of kBlock requests) per workgroup
 constexpr int kWaves = kBlock / 64;
 // list classes: 0..kKafkaClasses-1 Kafka by kind / length, then memcached
 // text, memcached binary, then HTTP
