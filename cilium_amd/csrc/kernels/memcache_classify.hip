@@ -41,6 +41,8 @@ constexpr int kMcWaves = kBlock / 64;
 constexpr int kMcSortPer = 4;                          // list entries per lane per chunk (1: 4.33 ms, 2: 3.82, 4: 3.25, 8: 3.26, 16: 4.41 on cfg5)
 constexpr uint32_t kMcWaveChunk = 64 * kMcSortPer;     // entries a wave orders by parser at a time
 // waves per SIMD the common kernel is built for (below)
+// (round 5, with the entry fields in LDS: 4 / 5 / 6 waves -> cfg5 memcached 3.55 /
+// 3.27 / 3.24 ms, the mixed 4M stream 0.242 / 0.257 / 0.275 ms; profiles/r5/ab5i_*)
 constexpr int kMcWavesPerSimd = 5;
 
 // 16-byte aligned register window over one request (the arena is readable up
