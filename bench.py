@@ -405,15 +405,20 @@ def main():
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
 
     def step(i=None):
-        step_counters.zero_()
+        # The counters kernel adds into the array it is given: one GPU accumulates
+        # straight into the job's totals; with N GPUs each step's counters are
+        # all-reduced first (the one collective on the data path).
+        if dist is not None:
+            step_counters.zero_()
         if i is not None:
             ev[i][0].record(stream)
-        eng.classify_device(*ptrs, n, *outs, counters_ptr=step_counters.data_ptr(), stream=stream.cuda_stream)
+        eng.classify_device(*ptrs, n, *outs, counters_ptr=(step_counters if dist is not None else totals).data_ptr(),
+                            stream=stream.cuda_stream)
         if i is not None:
             ev[i][1].record(stream)
         if dist is not None:
             l7dist.allreduce_counters(step_counters, dist)  # RCCL over xGMI: per-rule hit counters
-        totals.add_(step_counters)
+            totals.add_(step_counters)
 
     for _ in range(args.warmup):
         step()
