@@ -3,6 +3,8 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cstring>
 #include <map>
 #include <thread>
@@ -142,12 +144,16 @@ struct HostCtx {
     uint8_t *pin_out = nullptr;    // pinned host staging of the outputs
     uint8_t *pin_in_dev = nullptr;   // their device addresses (zero-copy; looked up once)
     uint8_t *pin_out_dev = nullptr;
+    uint32_t *pin_done = nullptr;     // pinned word the call's last kernel stores its sequence number to
+    uint32_t *pin_done_dev = nullptr;
+    uint32_t seq = 0;
     size_t in_cap = 0, out_cap = 0;
     ~HostCtx() {
         if (s) hipStreamSynchronize(s);
         if (dev) hipFree(dev);
         if (pin_in) hipHostFree(pin_in);
         if (pin_out) hipHostFree(pin_out);
+        if (pin_done) hipHostFree(pin_done);
         if (s) hipStreamDestroy(s);
     }
 };
@@ -722,7 +728,8 @@ int l7g_conn_update(l7g_engine *e, uint32_t index, const l7g_conn_t *conn, char 
 // call is one workgroup of one classifier, else by copy_in_kernel first.
 static int Classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const uint64_t *off, const uint32_t *len,
                     const uint32_t *conn, uint32_t n, uint8_t *verdict, int32_t *rule, uint32_t *consumed,
-                    uint64_t *counters, void *stream, const uint32_t *host_conn, const CopyIn *pre = nullptr) {
+                    uint64_t *counters, void *stream, const uint32_t *host_conn, const CopyIn *pre = nullptr,
+                    bool *signaled = nullptr) {
     std::lock_guard<std::mutex> g(e->mu);
     if (e->device < 0) return (int)hipErrorNoDevice;
     hipError_t rc = hipSetDevice(e->device);
@@ -875,7 +882,22 @@ static int Classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, con
     const bool only_mc = run_mc && !partitioned && !run_http && !run_kafka && !run_r2 && !run_cs;
     const CopyIn *fuse_http = pre && only_http && !nfa && n <= 8 ? pre : nullptr;
     const CopyIn *fuse_mc = pre && only_mc && n <= 64 ? pre : nullptr;
-    if (pre && !fuse_http && !fuse_mc && rc == hipSuccess) rc = LaunchCopyIn(*pre, s);
+    if (pre && !fuse_http && !fuse_mc && rc == hipSuccess) {
+        CopyIn c = *pre;
+        c.done = nullptr;  // (the classifiers that follow end the call)
+        rc = LaunchCopyIn(c, s);
+    }
+    // the one-workgroup kernel that ends the call stores the done word (and no
+    // counters or proxy statistics follow it)
+    const bool signal = (fuse_http || fuse_mc) && pre->done && !counters && !(e->flow_stats && !e->skey_list.empty());
+    CopyIn fused_c{};
+    if (fuse_http || fuse_mc) {
+        fused_c = *pre;
+        if (!signal) fused_c.done = nullptr;
+    }
+    if (fuse_http) fuse_http = &fused_c;
+    if (fuse_mc) fuse_mc = &fused_c;
+    if (signaled) *signaled = signal;
     const bool run[4] = {partitioned, run_http, run_kafka, run_mc};
     for (int k = 0; k < 4; k++) e->prof_ran[k] = run[k];
     mark(0);
@@ -1050,7 +1072,9 @@ static hipError_t HostGrow(HostCtx *H, uint32_t n, uint64_t arena_len) {
     const size_t need_in = HostArenaOff(n) + arena_len + 64;
     const size_t need_out = nn * 9 + 64;
     if (need_in <= H->in_cap && need_out <= H->out_cap) return hipSuccess;
-    // (the previous call of this thread synchronised its stream: the staging is free)
+    // (the previous call of this thread has its answers; its kernels may still be
+    // retiring after storing the done word)
+    if (H->s) hipStreamSynchronize(H->s);
     if (H->dev) hipFree(H->dev);
     if (H->pin_in) hipHostFree(H->pin_in);
     if (H->pin_out) hipHostFree(H->pin_out);
@@ -1065,6 +1089,12 @@ static hipError_t HostGrow(HostCtx *H, uint32_t n, uint64_t arena_len) {
         (rc = hipHostGetDevicePointer((void **)&H->pin_out_dev, H->pin_out, 0)) != hipSuccess) {
         H->in_cap = H->out_cap = 0;
         return rc;
+    }
+    if (!H->pin_done) {
+        if ((rc = hipHostMalloc((void **)&H->pin_done, 64, hipHostMallocDefault)) != hipSuccess) return rc;
+        *(volatile uint32_t *)H->pin_done = 0;
+        H->seq = 0;
+        if ((rc = hipHostGetDevicePointer((void **)&H->pin_done_dev, H->pin_done, 0)) != hipSuccess) return rc;
     }
     return hipSuccess;
 }
@@ -1148,6 +1178,8 @@ static hipError_t HostRun(l7g_engine *e, HostCtx *H, uint32_t n, uint64_t arena_
             d_a = in.nseg ? d_in + a_off : d_in;
         }
         pre = ci;
+        pre.done = H->pin_done_dev;
+        pre.seq = ++H->seq ? H->seq : ++H->seq;  // (never 0, the word's initial value)
     } else {
         uint8_t *d_in = H->dev;
         const bool staging = in.off == (const uint64_t *)H->pin_in;
@@ -1182,12 +1214,30 @@ static hipError_t HostRun(l7g_engine *e, HostCtx *H, uint32_t n, uint64_t arena_
     uint8_t *d_v = d_out;
     int32_t *d_r = (int32_t *)(d_out + ((nn + 3) & ~(size_t)3));
     uint32_t *d_cons = (uint32_t *)(d_out + ((nn + 3) & ~(size_t)3) + nn * 4);
+    bool signaled = false;
     if (rc == hipSuccess)
         rc = (hipError_t)Classify(e, d_a, arena_len, d_o, d_l, d_c, n, d_v, d_r, d_cons, nullptr, s, in.conn,
-                                  pre.n ? &pre : nullptr);
+                                  pre.n ? &pre : nullptr, &signaled);
     const size_t out_bytes = ((nn + 3) & ~(size_t)3) + nn * 8;
     if (rc == hipSuccess && n && !zc) rc = hipMemcpyAsync(H->pin_out, d_out, out_bytes, hipMemcpyDeviceToHost, s);
-    if (rc == hipSuccess) rc = hipStreamSynchronize(s);
+    // One workgroup answered the call: its done word says the answers are in
+    // pinned memory (a spin on that word is some microseconds shorter than the
+    // stream's completion signal); past 2 ms, or otherwise, wait on the stream,
+    // which also reports a kernel's failure.
+    bool done = false;
+    if (rc == hipSuccess && signaled) {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (uint32_t k = 0;; k++) {
+            if (*(volatile uint32_t *)H->pin_done == pre.seq) {
+                done = true;
+                break;
+            }
+            if ((k & 255) == 255 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) break;
+            __builtin_ia32_pause();
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);
+    }
+    if (rc == hipSuccess && !done) rc = hipStreamSynchronize(s);
     if (rc == hipSuccess && n) {
         const uint8_t *po = H->pin_out;
         memcpy(verdict, po, n);

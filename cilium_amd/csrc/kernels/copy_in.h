@@ -37,4 +37,15 @@ __device__ __forceinline__ void copy_in_block(const CopyIn &c) {
     __syncthreads();
 }
 
+// The call's last kernel, one workgroup: every output stored, then seq to
+// the host's done word (system scope, vector store); all threads call it.
+__device__ __forceinline__ void signal_done_block(const CopyIn &c) {
+    if (c.done == nullptr) return;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence_system();
+        __hip_atomic_store(c.done, c.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 }  // namespace l7

@@ -15,6 +15,11 @@ struct CopyPiece {
 struct CopyIn {
     CopyPiece p[4];
     int n;  // pieces (0: nothing to copy)
+    // with done: the kernel that ends the call (one workgroup) stores seq there
+    // (pinned host memory) after its outputs, and the host waits on that word
+    // instead of on the stream
+    uint32_t *done;
+    uint32_t seq;
 };
 
 }  // namespace l7

@@ -1678,7 +1678,10 @@ __global__ __launch_bounds__(kBlock) void http_latency_kernel(Batch B, HttpTable
     copy_in_block(ci);
     const int32_t hot = T.hot_ruleset;
     const bool hot_ok = hot >= 0 && (uint32_t)hot < T.nrulesets && T.rulesets[hot].image_len <= kLdsImageBytes;
-    if (kHot && !hot_ok) return;
+    if (kHot && !hot_ok) {
+        signal_done_block(ci);
+        return;
+    }
     if (kHot) {
         const DevRuleset r = T.rulesets[hot];
         const uint4 *src = (const uint4 *)(T.images + r.image_off);
@@ -1740,6 +1743,7 @@ __global__ __launch_bounds__(kBlock) void http_latency_kernel(Batch B, HttpTable
         if (!L.done) lat_request<kHot>(L, img, wave_lds, lane, O);
         else if (L.owed && lane == 0) emit(L, O);
     }
+    signal_done_block(ci);
 }
 
 // Requests grouped by rule set (http_group.hip): a workgroup takes one segment
@@ -1839,13 +1843,17 @@ hipError_t LaunchHttpClassify(const Batch &B, const HttpTables &T, const uint32_
     if (latency) {
         const uint32_t lblocks = min((B.n + kWaves - 1) / kWaves, (uint32_t)num_cus);
         if (ci && lblocks != 1) return hipErrorInvalidValue;
+        // the copy in the first kernel, the done word from the last
+        const bool gen = !hot || any_cold;
         CopyIn first = ci ? *ci : CopyIn{};
         if (hot) {
+            CopyIn k = first;
+            if (gen) k.done = nullptr;
             hipLaunchKernelGGL(http_latency_kernel<true>, dim3(lblocks), dim3(kBlock), 0, stream, B, T, sel, sel_count,
-                               other, first);
-            first = CopyIn{};
+                               other, k);
+            first.n = 0;
         }
-        if (!hot || any_cold)
+        if (gen)
             hipLaunchKernelGGL(http_latency_kernel<false>, dim3(lblocks), dim3(kBlock), 0, stream, B, T, sel, sel_count,
                                other, first);
         return hipGetLastError();

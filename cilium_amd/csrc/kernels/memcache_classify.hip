@@ -666,6 +666,7 @@ __device__ __forceinline__ void mc_classify(Batch B, McTables T, const uint32_t 
     } else {
         mc_loop<kNfa, false, kCh>(B, T, T.images, sel, sel2, sel_count, answer_other, &s_ent[0][0]);
     }
+    signal_done_block(ci);
 }
 
 // The common kernel is built for kMcWavesPerSimd waves per SIMD (round 3 on 2.4M
