@@ -697,8 +697,10 @@ hipError_t LaunchMemcacheClassify(const Batch &B, const McTables &T, const uint3
                                   const uint32_t *sel_count, bool answer_other, uint32_t scratch_lanes,
                                   hipStream_t stream, const CopyIn *ci) {
     if (B.n == 0) return hipSuccess;
+    // (cfg5, 20M entries: caps of 2048 / 4096 / 8192 / 16384 / 32768 / 131072
+    // workgroups -> 3.62 / 3.39 / 3.26 / 3.21 / 3.25 / 3.72 ms; profiles/r5/ab5l_*)
     uint32_t blocks = (B.n + kBlock - 1) / kBlock;
-    if (blocks > 8192) blocks = 8192;
+    if (blocks > 16384) blocks = 16384;
     if (T.nfa_scratch) blocks = max(1u, min(blocks, scratch_lanes / kBlock));  // (grid-stride loop)
     if (ci && blocks != 1) return hipErrorInvalidValue;  // (the copy is one workgroup's)
     const CopyIn c = ci ? *ci : CopyIn{};
