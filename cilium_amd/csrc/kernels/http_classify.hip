@@ -1867,15 +1867,20 @@ hipError_t LaunchHttpClassify(const Batch &B, const HttpTables &T, const uint32_
     // they are quick (short requests: 4M 34-byte requests 0.74 ms, taken four at
     // a time 0.36 ms), and cost a longer tail when they are not (cfg2's 1.1 KB
     // requests: 1.59 vs 1.63 ms), so a batch of short requests takes four.
-    const bool grab4 = B.arena_len / B.n < 512;
+    // A wave with many tiles to run (a long batch: cfg5's 50M HTTP requests are
+    // ~380 tiles per wave) also takes two per atomic: the tail grows by half a
+    // tile, the counter's queue shrinks (cfg5 HTTP 16.94 -> 16.87 ms, profiles/r5/ab5e_work_grab.log).
+    const uint32_t per_wave = ntiles / (blocks * kWaves);
+    const uint32_t grab = B.arena_len / B.n < 512 ? 4u : per_wave >= 64 ? 2u : 1u;
     using Kern = void (*)(Batch, HttpTables, const uint32_t *, const uint32_t *, uint32_t, uint32_t *);
-    const Kern kHot1 = http_classify_kernel<true, 1>, kHot4 = http_classify_kernel<true, 4>;
-    const Kern kGen1 = http_classify_kernel<false, 1>, kGen4 = http_classify_kernel<false, 4>;
+    const Kern kHot = grab == 4 ? http_classify_kernel<true, 4> : grab == 2 ? http_classify_kernel<true, 2>
+                                                                         : http_classify_kernel<true, 1>;
+    const Kern kGen = grab == 4 ? http_classify_kernel<false, 4> : grab == 2 ? http_classify_kernel<false, 2>
+                                                                          : http_classify_kernel<false, 1>;
     if (hot)
-        hipLaunchKernelGGL(grab4 ? kHot4 : kHot1, dim3(blocks), dim3(kBlock), 0, stream, B, T, sel, sel_count, other,
-                           tile_ctr);
+        hipLaunchKernelGGL(kHot, dim3(blocks), dim3(kBlock), 0, stream, B, T, sel, sel_count, other, tile_ctr);
     if (!hot || any_cold)
-        hipLaunchKernelGGL(grab4 ? kGen4 : kGen1, dim3(blocks), dim3(kBlock), 0, stream, B, T, sel, sel_count, other,
+        hipLaunchKernelGGL(kGen, dim3(blocks), dim3(kBlock), 0, stream, B, T, sel, sel_count, other,
                            tile_ctr ? tile_ctr + 1 : nullptr);
     return hipGetLastError();
 }
