@@ -343,6 +343,8 @@ l7g_batcher *l7g_batcher_create(l7g_engine *e, uint32_t max_requests, uint32_t m
     return b;
 }
 
+uint32_t l7g_batcher_max_requests(const l7g_batcher *b) { return b ? b->max_n : 0; }
+
 int l7g_batcher_submit(l7g_batcher *b, const uint8_t *req, uint32_t len, uint32_t conn, l7g_done_fn done, void *ctx) {
     if (b->stop.load(std::memory_order_relaxed)) return -1;  // (a submit racing destroy is the caller's error)
     if (len > b->slots[0].lb) return -2;                       // never fits a lane

@@ -58,7 +58,8 @@ public:
         d.vec(img_.rulesets); d.vec(img_.images); d.vec(img_.nfa_pool);
         d.cache(cache_); d.smap(nfa_cache_);
         img_.chunks = d.u64(); img_.dfas = d.u64(); img_.dfa_states = d.u64(); img_.nfas = d.u64();
-        return d.ok && NfaOffsetsValid(img_.nfa_pool, nfa_cache_) && RulesetImagesValid(img_.rulesets, img_.images);
+        return d.ok && NfaOffsetsValid(img_.nfa_pool, nfa_cache_) && RulesetImagesValid(img_.rulesets, img_.images) &&
+               ImageNfaRefsValid<ImgHeader>(img_.rulesets, img_.images, nfa_cache_, 16);
     }
     size_t compiled = 0;  // rule sets compiled (not taken from the cache) since construction
 

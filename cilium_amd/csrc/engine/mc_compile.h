@@ -53,7 +53,8 @@ public:
         d.cache(cache_); d.smap(nfa_cache_);
         img_.rules = d.u64(); img_.dfas = d.u64(); img_.dfa_states = d.u64(); img_.nfas = d.u64();
         img_.max_chunks = d.u64();
-        return d.ok && NfaOffsetsValid(img_.nfa_pool, nfa_cache_) && RulesetImagesValid(img_.rulesets, img_.images);
+        return d.ok && NfaOffsetsValid(img_.nfa_pool, nfa_cache_) && RulesetImagesValid(img_.rulesets, img_.images) &&
+               ImageNfaRefsValid<McImgHeader>(img_.rulesets, img_.images, nfa_cache_, 8);
     }
     size_t compiled = 0;  // rule sets compiled (not taken from the cache) since construction
 

@@ -119,6 +119,27 @@ inline bool NfaOffsetsValid(const std::vector<uint8_t> &pool, const Map &offsets
         if (!in(d.ivl_off, niv * 4) || !in(d.b_off, niv * W * 8) || !in(d.acc_off, K * W * 8) ||
             !in(d.ascii_off, 128 * 2) || !in(d.t_off, W > (uint64_t)kNfaMaxWords ? sizeof(DevNfaSparse) : K * 8 * W * 256 * W * 8))
             return false;
+        if (W > (uint64_t)kNfaMaxWords) {
+            // the sparse rows (nfa_walk.h nfa_big_step): every position's row
+            // index, each row's pair range and every pair inside the pool
+            const uint64_t m = d.m;
+            if (m == 0 || m > W * 64) return false;
+            DevNfaSparse sp;
+            memcpy(&sp, pool.data() + d.t_off, sizeof sp);
+            if (!in(sp.row_of_off, K * m * 4) || !in(sp.row_ptr_off, 4)) return false;
+            const uint32_t *row_of = (const uint32_t *)(pool.data() + sp.row_of_off);
+            uint64_t rows = 0;
+            for (uint64_t i = 0; i < K * m; i++) rows = std::max(rows, (uint64_t)row_of[i] + 1);
+            if (!in(sp.row_ptr_off, (rows + 1) * 4)) return false;
+            const uint32_t *row_ptr = (const uint32_t *)(pool.data() + sp.row_ptr_off);
+            for (uint64_t r = 0; r < rows; r++)
+                if (row_ptr[r] > row_ptr[r + 1]) return false;
+            const uint64_t pairs = row_ptr[rows];
+            if (!in(sp.pair_w_off, pairs * 4) || !in(sp.pair_m_off, pairs * 8)) return false;
+            const uint32_t *pair_w = (const uint32_t *)(pool.data() + sp.pair_w_off);
+            for (uint64_t q = 0; q < pairs; q++)
+                if (pair_w[q] >= W) return false;
+        }
     }
     return true;
 }
@@ -126,6 +147,33 @@ template <class R>
 inline bool RulesetImagesValid(const std::vector<R> &rulesets, const std::vector<uint8_t> &images) {
     for (const auto &r : rulesets)
         if ((uint64_t)r.image_off + r.image_len > images.size()) return false;
+    return true;
+}
+// The NFA references a rule-set image holds (header Hdr at the image's
+// offset 0: nchunks, nnfa, nfa_off -> DevNfaRef[nnfa]): the reference table
+// and each mask row inside the image, each NFA offset one the pool's checked
+// map holds (mask rows: HTTP u64[2][nchunks], the others u64[nchunks]).
+// Checked after RulesetImagesValid.
+template <class Hdr, class R, class Map>
+inline bool ImageNfaRefsValid(const std::vector<R> &rulesets, const std::vector<uint8_t> &images, const Map &offsets,
+                              uint64_t mask_bytes_per_chunk) {
+    for (const auto &r : rulesets) {
+        if (r.image_len < sizeof(Hdr)) return false;
+        Hdr h;
+        memcpy(&h, images.data() + r.image_off, sizeof h);
+        const uint64_t nnfa = h.nnfa;
+        if (nnfa == 0) continue;
+        if ((uint64_t)h.nfa_off + nnfa * sizeof(DevNfaRef) > r.image_len) return false;
+        for (uint64_t k = 0; k < nnfa; k++) {
+            DevNfaRef ref;
+            memcpy(&ref, images.data() + r.image_off + h.nfa_off + k * sizeof(DevNfaRef), sizeof ref);
+            if ((uint64_t)ref.mask_off + mask_bytes_per_chunk * h.nchunks > r.image_len) return false;
+            bool known = false;
+            for (const auto &kv : offsets)
+                if ((uint64_t)kv.second == ref.nfa) { known = true; break; }
+            if (!known) return false;
+        }
+    }
     return true;
 }
 

@@ -43,7 +43,8 @@ public:
         d.vec(img_.rulesets); d.vec(img_.images); d.vec(img_.nfa_pool);
         d.cache(cache_); d.smap(nfa_cache_);
         img_.rules = d.u64(); img_.dfas = d.u64(); img_.nfas = d.u64();
-        return d.ok && NfaOffsetsValid(img_.nfa_pool, nfa_cache_) && RulesetImagesValid(img_.rulesets, img_.images);
+        return d.ok && NfaOffsetsValid(img_.nfa_pool, nfa_cache_) && RulesetImagesValid(img_.rulesets, img_.images) &&
+               ImageNfaRefsValid<R2ImgHeader>(img_.rulesets, img_.images, nfa_cache_, 8);
     }
     size_t compiled = 0;  // rule sets compiled (not taken from the cache) since construction
 

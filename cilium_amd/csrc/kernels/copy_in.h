@@ -41,6 +41,10 @@ __device__ __forceinline__ void copy_in_block(const CopyIn &c) {
 // the host's done word (system scope, vector store); all threads call it.
 __device__ __forceinline__ void signal_done_block(const CopyIn &c) {
     if (c.done == nullptr) return;
+    // every thread fences its own stores (answers in pinned host memory on the
+    // zero-copy path) at system scope before the barrier, so all waves'
+    // answers are visible to the host before thread 0's release of the word
+    __threadfence_system();
     __syncthreads();
     if (threadIdx.x == 0) {
         __threadfence_system();

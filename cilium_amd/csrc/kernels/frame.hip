@@ -409,7 +409,12 @@ __device__ __forceinline__ uint4 twin_chunk(const TWin &W, uint64_t wa) {
     if (ca + 16 > (uint64_t)W.A && ca < (uint64_t)W.A + W.n) w = gload16(ca);
     return w;
 }
-constexpr uint32_t kNextWin = kWinBytes - 32;  // where an HTTP scan goes on (kHttpSure)
+// An HTTP scan trusts a window's first kHttpSure bytes (the masks of its last
+// two chunks need bytes past it) and goes on in a window one chunk before that
+// point, so that a header line starting at the first bytes it has not trusted
+// has the CRLF before it (and its line-start bit) inside the new window.
+constexpr uint32_t kHttpSure = kWinBytes - 32;
+constexpr uint32_t kNextWin = kHttpSure - 16;  // where an HTTP scan's next window starts
 // load the window at address wa
 __device__ __forceinline__ void twin_load(TWin &W, uint64_t wa) {
     FPH(const uint64_t t0_ = __builtin_amdgcn_s_memtime();)
@@ -477,8 +482,10 @@ __device__ __forceinline__ uint32_t tword(TWin &W, uint64_t x) {
 // between stops the walk, and the last content-length line start gives the
 // body length.  The masks of a window's last 32 bytes need bytes past it, so a
 // window vouches for its first 992 bytes (all of them when it holds the
-// stream's end) and the scan goes on in the next window from there.
-constexpr uint32_t kHttpSure = kNextWin;
+// stream's end) and the scan goes on from there in the window that starts one
+// chunk earlier (kNextWin): lane 0's line starts take no carry from a previous
+// chunk, so a line starting at byte 992 or 993 is seen only with the CRLF
+// before it in the same window.
 // bits of lanes [c0, c1] (c0 <= c1 < 64)
 __device__ __forceinline__ uint64_t lanes_between(uint32_t c0, uint32_t c1) {
     const uint64_t hi = c1 >= 63 ? ~0ull : (2ull << c1) - 1;
@@ -541,6 +548,7 @@ __device__ __forceinline__ uint64_t tnext_http(TWin &W, uint64_t p) {
         }
         if (W.wa + kWinBytes >= (uint64_t)W.A + W.n) return 0;  // no "\r\n\r\n": incomplete
         x = s_end - (uint64_t)W.A;
+        twin_load(W, W.wa + kNextWin);  // (s_end - 16: the scan goes on at its byte 16)
     }
     uint64_t cl = 0;
     if (last_cl != ~0ull) {  // strtoull: leading spaces, optional sign, digits

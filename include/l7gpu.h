@@ -233,6 +233,9 @@ typedef struct l7g_batcher l7g_batcher;
  * is capped at 65536 (4 x 256 MiB pinned).  NULL when the engine has a device
  * and the slots cannot be pinned (the device path needs pinned slots). */
 l7g_batcher *l7g_batcher_create(l7g_engine *e, uint32_t max_requests, uint32_t max_wait_us);
+/* The batch size the batcher flushes at: max_requests as created, or 65536
+ * when create capped it (a caller that asked for more learns it here). */
+uint32_t l7g_batcher_max_requests(const l7g_batcher *b);
 /* 0 = queued; -1 = the batcher is shutting down; -2 = backpressure: both
  * flushers are busy and the open slot is full, or the request is larger than
  * one of a slot's eight lanes (max(2 x max_requests, 1024) x 256 bytes) (the

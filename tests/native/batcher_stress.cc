@@ -105,13 +105,19 @@ int main() {
     const int huge_rc = l7g_batcher_submit(slow, huge.data(), (uint32_t)huge.size(), 0,
                                            [](void *, uint8_t, int32_t, uint32_t) {}, nullptr);
     const int slow_answered = slow_calls.load();
+    const uint32_t slow_max = l7g_batcher_max_requests(slow);
     l7g_batcher_destroy(slow);
+    // a batch size past the cap is reduced, and the caller can read what it got
+    l7g_batcher *big = l7g_batcher_create(e, 1u << 20, 50);
+    const uint32_t big_max = big ? l7g_batcher_max_requests(big) : 0;
+    if (big) l7g_batcher_destroy(big);
     l7g_engine_destroy(e);
     printf("{\"calls\": %llu, \"after_flush\": %llu, \"expected\": %d, \"bad\": %d, \"flush_rc\": %d, "
            "\"reentrant_flush_rc\": %d, \"launches\": %llu, \"queued\": %d, \"refused\": %d, \"rejected\": %d, "
-           "\"slow_answered\": %d, \"large_calls\": %llu, \"large_expected\": %d, \"huge_rc\": %d}\n",
+           "\"slow_answered\": %d, \"large_calls\": %llu, \"large_expected\": %d, \"huge_rc\": %d, "
+           "\"slow_max\": %u, \"big_max\": %u}\n",
            (unsigned long long)g_calls.load(), (unsigned long long)after_flush, T * N, g_bad.load(), frc,
            g_flush_rc.load(), (unsigned long long)launches, queued, refused, rejected.load(), slow_answered,
-           (unsigned long long)large_calls, T * N2, huge_rc);
+           (unsigned long long)large_calls, T * N2, huge_rc, slow_max, big_max);
     return 0;
 }

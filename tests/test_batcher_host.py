@@ -24,6 +24,7 @@ def test_batcher_threads_order_flush_backpressure():
     assert d["launches"] < d["expected"] // 8, d  # batched, not one launch per request
     assert d["large_calls"] == d["large_expected"], d  # byte-full slots (holes closed up): every callback once
     assert d["huge_rc"] == -2, d  # larger than a lane: refused
+    assert d["slow_max"] == 4 and d["big_max"] == 65536, d  # the effective batch size, capped
     # both flushers blocked in callbacks: at most two sealed batches and one full open slot are taken
     assert d["refused"] > 0 and d["queued"] + d["refused"] == 5000, d
     assert 1024 <= d["queued"] <= 3 * 1024 and d["slow_answered"] == d["queued"], d

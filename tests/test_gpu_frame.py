@@ -3,21 +3,27 @@ l7g_classify_streams, kernels/frame.hip) on the GPU.
 
 Each protocol's generated requests are grouped by connection and concatenated
 into one stream per connection (some cut short), the way a proxy receives
-them.  The device walk must find exactly the frame starts the restatement below
-finds -- the parsers' framing as csrc/proxylib/shim.cc scans it on the host
-(Kafka's BE int32 size prefix, vendor/github.com/optiopay/kafka/proto/
-messages.go:124-165; memcached text lines + storage data blocks and binary
-headers, proxylib/memcached/{text,binary}/parser.go; HTTP head +
-Content-Length; r2d2 lines; cassandra 9-byte headers) -- and, for generated
-well-formed requests, exactly the request boundaries.  l7g_classify_streams'
-verdicts, rule ids and consumed lengths for every frame equal the oracle's on
-the same frames."""
+them.  The frame starts are checked against the oracle's sequential walk: the
+proxylib op loop (proxylib/proxylib/connection.go:118-174) hands the parser
+the stream from the last frame's end, and the next frame starts where the
+oracle's PASS / DROP length (`consumed`) ends it -- Kafka's BE int32 size
+prefix (vendor/github.com/optiopay/kafka/proto/messages.go:124-165), memcached
+text lines + storage data blocks and binary headers
+(proxylib/memcached/{text,binary}/parser.go), HTTP heads + bodies, r2d2 lines,
+cassandra headers.  For Kafka and memcached the oracle is the only reference.
+For HTTP, r2d2 and cassandra the frames must also equal the restatement below
+of the device walk's contract (the parsers' framing as csrc/proxylib/shim.cc
+scans it: stop at a Transfer-Encoding head, frame malformed heads by their
+"\r\n\r\n"), and, for generated well-formed requests, the request
+boundaries.  l7g_classify_streams' verdicts, rule ids and consumed lengths for
+every frame equal the oracle's on the same frames."""
 import numpy as np
 import pytest
 import torch
 
 from cilium_amd import gen
-from cilium_amd._lib import PROTO_CASSANDRA, PROTO_HTTP, PROTO_KAFKA, PROTO_MEMCACHE, PROTO_R2D2
+from cilium_amd._lib import (ALLOW, DENY, INCOMPLETE, PARSE_ERROR, PROTO_CASSANDRA, PROTO_HTTP, PROTO_KAFKA,
+                             PROTO_MEMCACHE, PROTO_R2D2)
 
 pytestmark = pytest.mark.gpu
 
@@ -141,15 +147,78 @@ def _frames(d, proto, mode, max_frames):
     return out
 
 
+def _oracle_walk(ref, conns, streams, conn_of, max_frames):
+    """The oracle's sequential framing of each stream: frame k + 1 starts
+    where the oracle's PASS / DROP of frame k (handed the stream from frame
+    k's start, as OnData hands the parser its unconsumed input) ends it; the
+    walk stops at the first frame the oracle does not pass or drop
+    (INCOMPLETE: MORE; PARSE_ERROR: the connection is closed) or at
+    max_frames.  Returns per stream the frame starts and the last frame's
+    verdict.  All streams advance together, one oracle batch per frame index."""
+    arena = np.frombuffer(b"".join(streams), np.uint8).copy()
+    base = np.cumsum([0] + [len(s) for s in streams[:-1]]).astype(np.int64)
+    # one connection per stream: memcached's parser is chosen by the first byte
+    # the connection carries and kept for its lifetime
+    # (proxylib/memcached/parser.go:186-199), so the later OnData calls see it
+    # locked, as the connection's flags would hold it
+    nc = len(conns)
+    conns = np.concatenate([conns, np.zeros(len(streams), conns.dtype)])
+    for s, st in enumerate(streams):
+        c = conn_of[s]
+        if c < nc:
+            conns[nc + s] = conns[c]
+            if int(conns[c]["proto"]) == PROTO_MEMCACHE and int(conns[c]["flags"]) & 3 == 0 and st:
+                conns[nc + s]["flags"] = (int(conns[c]["flags"]) & ~3) | (2 if st[0] >= 0x80 else 1)
+    conn_of = [nc + s if conn_of[s] < nc else conn_of[s] + len(streams) for s in range(len(streams))]
+    pos = [0] * len(streams)
+    starts = [[] for _ in streams]
+    last = [None] * len(streams)
+    live = [s for s in range(len(streams)) if len(streams[s]) > 0]
+    while live:
+        off = np.array([base[s] + pos[s] for s in live], np.uint64)
+        ln = np.array([len(streams[s]) - pos[s] for s in live], np.uint32)
+        cid = np.array([conn_of[s] for s in live], np.uint32)
+        v, _, c = ref.classify(conns, arena, off, ln, cid, 8)
+        nxt = []
+        for k, s in enumerate(live):
+            starts[s].append(pos[s])
+            last[s] = int(v[k])
+            if int(v[k]) in (ALLOW, DENY) and 0 < int(c[k]) < len(streams[s]) - pos[s] and \
+                    len(starts[s]) < max_frames:
+                pos[s] += int(c[k])
+                nxt.append(s)
+        live = nxt
+    return starts, last
+
+
+def _check_against_oracle_walk(got, want, last, proto, stream, max_frames):
+    """The device's frames against the oracle's walk.  They agree on every
+    frame both have.  The device may propose frames past one the oracle
+    rejects (it frames by length and delimiters only; the caller discards
+    them, as proxylib closes the connection), and stops early only where a
+    length cannot be read ahead of parsing: a chunked HTTP body (the frame is
+    handed the rest of the stream; the classifier frames it)."""
+    k = min(len(got), len(want))
+    assert got[:k] == want[:k], (proto, got[:8], want[:8])
+    if len(got) > len(want):
+        assert last == PARSE_ERROR, (proto, len(got), len(want), last)
+    elif len(got) < len(want):
+        assert proto == PROTO_HTTP and b"transfer-encoding" in stream[got[-1]:].lower(), (proto, got[-3:], want[:len(got) + 1])
+
+
 def _streams(w, rng, cut_every=5):
     """One stream per connection: its requests in order; every cut_every-th
     stream cut short at a random point."""
     reqs = [bytes(w.arena[int(o):int(o) + int(n)]) for o, n in zip(w.offsets, w.lengths)]
     by = {}
     for q, c in zip(reqs, w.conn_ids):
-        by.setdefault(int(c), []).append(q)
+        # a memcached connection carries one wire format (its first byte picks
+        # the parser for good): the generator's text and binary requests of one
+        # connection go to two streams
+        mc = int(c) < len(w.conns) and int(w.conns["proto"][int(c)]) == PROTO_MEMCACHE and len(q) > 0
+        by.setdefault((int(c), mc and q[0] >= 0x80), []).append(q)
     conns, streams, bounds = [], [], []
-    for k, (c, qs) in enumerate(sorted(by.items())):
+    for k, ((c, _), qs) in enumerate(sorted(by.items())):
         s = b"".join(qs)
         b = list(np.cumsum([0] + [len(q) for q in qs[:-1]]))
         if k % cut_every == 3 and len(s) > 2:
@@ -160,18 +229,29 @@ def _streams(w, rng, cut_every=5):
     return conns, streams, bounds
 
 
-def _run(engine, oracle, w, max_frames=64, extra=()):
-    """extra: (connection, stream) pairs appended to the generated streams."""
+def _run(engine, oracle, w, max_frames=64, extra=(), streams=None, align=1):
+    """extra: (connection, stream) pairs appended to the generated streams;
+    streams: (connections, streams, request boundaries) instead of the
+    generated ones; align: each stream starts at an arena offset that is a
+    multiple of it (the device walk's windows then start at stream offset 0)."""
     rng = np.random.default_rng(7)
     engine.update_policy(w.policy)
     engine.set_connections(w.conns)
-    conns, streams, bounds = _streams(w, rng)
+    conns, streams, bounds = _streams(w, rng) if streams is None else streams
     for c, st in extra:
         conns.append(c)
         streams.append(st)
         bounds.append([0])
-    arena = np.frombuffer(b"".join(streams), np.uint8).copy()
-    s_off = np.cumsum([0] + [len(s) for s in streams[:-1]]).astype(np.uint64)
+    s_off = np.zeros(len(streams), np.uint64)
+    parts, at = [], 0
+    for k, st in enumerate(streams):
+        pad = (-at) % align
+        parts.append(b"\0" * pad)
+        at += pad
+        s_off[k] = at
+        parts.append(st)
+        at += len(st)
+    arena = np.frombuffer(b"".join(parts) + b"\0", np.uint8).copy()
     s_len = np.array([len(s) for s in streams], np.uint32)
     s_conn = np.array(conns, np.uint32)
     n = len(streams)
@@ -194,15 +274,20 @@ def _run(engine, oracle, w, max_frames=64, extra=()):
         f_conn.cpu().numpy().view(np.uint32)
     nfr = nfr.cpu().numpy()
     modes = {i: int(w.conns["flags"][i]) & 3 for i in range(len(w.conns))}
+    ref = oracle.Policy(w.policy)
+    owalk, olast = _oracle_walk(ref, w.conns, streams, conns, max_frames)
     whole = 0
     sel = []
     for s in range(n):
-        if conns[s] >= len(w.conns):  # unknown connection: one slot, the whole stream
-            want = [0]
-        else:
-            want = _frames(streams[s], int(w.conns["proto"][conns[s]]), modes[conns[s]], max_frames)
         got = [int(x) - int(s_off[s]) for x in f_off[s * max_frames:s * max_frames + nfr[s]]]
-        assert got == want, (s, proto, got[:8], want[:8])
+        if conns[s] >= len(w.conns):  # unknown connection: one slot, the whole stream
+            assert got == [0], (s, got)
+        else:
+            proto = int(w.conns["proto"][conns[s]])
+            _check_against_oracle_walk(got, owalk[s], olast[s], proto, streams[s], max_frames)
+            if proto not in (PROTO_KAFKA, PROTO_MEMCACHE):  # the device walk's contract, restated
+                want = _frames(streams[s], proto, modes[conns[s]], max_frames)
+                assert got == want, (s, proto, got[:8], want[:8])
         assert all(int(x) == len(streams[s]) - g for x, g in zip(f_len[s * max_frames:], got))
         assert (f_conn[s * max_frames:s * max_frames + nfr[s]] == conns[s]).all()
         assert (f_len[s * max_frames + nfr[s]:(s + 1) * max_frames] == 0).all()
@@ -210,7 +295,7 @@ def _run(engine, oracle, w, max_frames=64, extra=()):
             whole += 1
         sel.extend(range(s * max_frames, s * max_frames + nfr[s]))
     sel = np.array(sel)
-    ref = oracle.Policy(w.policy).classify(w.conns, arena, f_off[sel], f_len[sel], f_conn[sel], 8)
+    ref = ref.classify(w.conns, arena, f_off[sel], f_len[sel], f_conn[sel], 8)
     assert (v.cpu().numpy()[sel] == ref[0]).all()
     assert (r.cpu().numpy()[sel] == ref[1]).all()
     assert (c.cpu().numpy().view(np.uint32)[sel] == ref[2]).all()
@@ -301,3 +386,33 @@ def test_frame_streams_http_heads_and_bodies(engine, oracle):
                      base.policy, {})
     n, whole, frames = _run(engine, oracle, w, max_frames=96)
     assert frames > n * 3
+
+
+def _edge_requests():
+    """HTTP heads whose Content-Length or Transfer-Encoding line starts at
+    exactly stream offset 990-995 or 1966-1971: the first bytes past what the
+    wave framer's first and second 1 KiB windows vouch for (a window vouches
+    for its first 992 bytes; the next starts 976 bytes on).  Each is followed
+    by a second request, so a missed length line frames the body as a request."""
+    out = []
+    line1 = b"POST /p HTTP/1.1\r\n"
+    for at in list(range(988, 998)) + list(range(1964, 1974)):
+        for hdr in (b"Content-Length: 7", b"content-length:7", b"Transfer-Encoding: chunked"):
+            pad = at - len(line1) - len(b"X-Pad: ") - 2
+            head = line1 + b"X-Pad: " + b"a" * pad + b"\r\n" + hdr + b"\r\nHost: h\r\n\r\n"
+            assert head.index(hdr) == at
+            body = b"7\r\nabcdefg\r\n0\r\n\r\n" if hdr.startswith(b"Transfer") else b"GET / H"
+            out.append(head + body + b"GET /public/x HTTP/1.1\r\nHost: h\r\n\r\n")
+    return out
+
+
+def test_frame_streams_http_length_line_at_window_edges(engine, oracle):
+    """a length line starting at byte 992 / 993 of a window
+    was missed.  Every stream starts 16-byte aligned, so its first window
+    starts at stream offset 0 and the lines fall on the window edges exactly."""
+    reqs = _edge_requests()
+    base = gen.http_workload(2, 10, nconns=4)
+    conns = [k % 4 for k in range(len(reqs))]
+    streams = (conns, list(reqs), [[0] for _ in reqs])
+    n, whole, frames = _run(engine, oracle, base, max_frames=4, streams=streams, align=16)
+    assert frames >= 2 * n - sum(1 for r in reqs if b"Transfer" in r)
