@@ -29,7 +29,29 @@ constexpr int kHistBlock = 1024;
 constexpr uint32_t kHistBins = 16384;  // u32 bins per LDS pass (64 KiB)
 constexpr uint32_t kHistBlocks = 256;  // workgroups (one per CU)
 
-// rule bins [lo, lo + nb) of this pass; verdict bins counted only when lo == 0
+// One rule bin per lane (key = bin index, ~0u = none) into the LDS bins.
+// Lanes hitting one bin in one ds_add serialise on it (a wave of allowed
+// requests of one hot rule is 64 adds to one address), so the lanes that share
+// the bin of the first lane with a key are added first as one count, twice
+// over; whatever keys remain go in as single adds.
+__device__ __forceinline__ void bin_add(uint32_t *bins, uint32_t key, uint32_t lane) {
+#pragma unroll
+    for (int round = 0; round < 2; round++) {
+        const uint64_t act = __ballot(key != ~0u);
+        if (!act) return;
+        const uint32_t lead = (uint32_t)__builtin_ctzll(act);
+        const uint32_t kl = (uint32_t)__builtin_amdgcn_readlane((int)key, (int)lead);
+        const uint64_t same = __ballot(key == kl);
+        if (lane == lead) atomicAdd(&bins[kl], (uint32_t)__popcll(same));
+        if (key == kl) key = ~0u;
+    }
+    if (key != ~0u) atomicAdd(&bins[key], 1u);
+}
+
+// rule bins [lo, lo + nb) of this pass; verdict bins counted only when lo == 0.
+// A thread takes 4 consecutive entries per step (one 16-byte load of rules, one
+// 4-byte load of verdicts), two steps' loads in flight.
+constexpr uint32_t kHistPer = 4;
 __global__ __launch_bounds__(kHistBlock) void histogram_kernel(const uint8_t *__restrict__ verdict,
                                                                const int32_t *__restrict__ rule, uint32_t n,
                                                                uint32_t lo, uint32_t nb, uint32_t *__restrict__ scratch,
@@ -37,19 +59,56 @@ __global__ __launch_bounds__(kHistBlock) void histogram_kernel(const uint8_t *__
     __shared__ uint32_t bins[kHistBins + 8];
     for (uint32_t i = threadIdx.x; i < nb + 8; i += kHistBlock) bins[i] = 0;
     __syncthreads();
-    const uint32_t per = (n + gridDim.x - 1) / gridDim.x;
-    const uint32_t b0 = blockIdx.x * per, b1 = min(n, b0 + per);
+    // slices of whole 4-entry groups (16-byte aligned rule loads)
+    const uint32_t ngroups = (n + kHistPer - 1) / kHistPer;
+    const uint32_t per = (ngroups + gridDim.x - 1) / gridDim.x;
+    const uint32_t g0 = blockIdx.x * per, g1 = min(ngroups, g0 + per);
     const uint32_t lane = threadIdx.x & 63;
     uint32_t vc[5] = {0, 0, 0, 0, 0};
-    for (uint32_t i0 = b0; i0 < b1; i0 += kHistBlock) {
-        const uint32_t i = i0 + threadIdx.x;
-        const bool in = i < b1;
-        const int32_t r = in ? rule[i] : -1;
-        if ((uint32_t)(r - (int32_t)lo) < nb) atomicAdd(&bins[r - lo], 1u);
-        if (lo == 0) {
-            const uint32_t v = in ? verdict[i] : 0xFF;
+    const bool aligned = ((uintptr_t)rule & 15) == 0;
+    for (uint32_t gb = g0; gb < g1; gb += 2 * kHistBlock) {
+        int4 rr[2];
+        uint32_t vv[2];
+        bool full[2];
 #pragma unroll
-            for (uint32_t k = 0; k < 5; k++) vc[k] += (uint32_t)__popcll(__ballot(v == k));
+        for (int u = 0; u < 2; u++) {
+            const uint32_t g = gb + u * kHistBlock + threadIdx.x;
+            const uint32_t i = g * kHistPer;
+            full[u] = g < g1 && i + kHistPer <= n;
+            rr[u] = make_int4(-1, -1, -1, -1);
+            vv[u] = 0xFFFFFFFFu;
+            if (full[u] && aligned) {
+                rr[u] = *reinterpret_cast<const int4 *>(rule + i);
+                vv[u] = (uint32_t)verdict[i] | (uint32_t)verdict[i + 1] << 8 | (uint32_t)verdict[i + 2] << 16 |
+                        (uint32_t)verdict[i + 3] << 24;
+            } else if (full[u]) {  // (rule[] not 16-byte aligned: four dword loads)
+                rr[u] = make_int4(rule[i], rule[i + 1], rule[i + 2], rule[i + 3]);
+                vv[u] = (uint32_t)verdict[i] | (uint32_t)verdict[i + 1] << 8 | (uint32_t)verdict[i + 2] << 16 |
+                        (uint32_t)verdict[i + 3] << 24;
+            } else if (g < g1) {  // the batch's last, partial group
+                int32_t t[4] = {-1, -1, -1, -1};
+                uint32_t v = 0xFFFFFFFFu;
+                for (uint32_t k = 0; k < kHistPer && i + k < n; k++) {
+                    t[k] = rule[i + k];
+                    v = (v & ~(0xFFu << (8 * k))) | (uint32_t)verdict[i + k] << (8 * k);
+                }
+                rr[u] = make_int4(t[0], t[1], t[2], t[3]);
+                vv[u] = v;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            const int32_t r4[4] = {rr[u].x, rr[u].y, rr[u].z, rr[u].w};
+#pragma unroll
+            for (int k = 0; k < (int)kHistPer; k++) {
+                const int32_t r = r4[k];
+                bin_add(bins, (uint32_t)(r - (int32_t)lo) < nb ? (uint32_t)(r - (int32_t)lo) : ~0u, lane);
+                if (lo == 0) {
+                    const uint32_t v = (vv[u] >> (8 * k)) & 0xFF;
+#pragma unroll
+                    for (uint32_t q = 0; q < 5; q++) vc[q] += (uint32_t)__popcll(__ballot(v == q));
+                }
+            }
         }
     }
     if (lo == 0 && lane == 0)

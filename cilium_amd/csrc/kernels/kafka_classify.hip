@@ -21,10 +21,9 @@
 // else takes the field-by-field loop from the same position, so the verdicts
 // are those of the reference's decoders either way.  (Round 5 also built and
 // measured two restructurings, both bit-exact and both slower on produce
-// requests: an LDS-staged walk with a segment-parallel CRC,
-// tools/experiments/kafka_staged_r5.hip, and this walk with the CRCs deferred
-// to a wave-cooperative pass, tools/experiments/kafka_deferred_r5.hip; their
-// numbers are in DESIGN.md.)
+// requests: an LDS-staged walk with a segment-parallel CRC, and this walk
+// with the CRCs deferred to a wave-cooperative pass; their sources are in git
+// history at commit e7ccfd8 and their numbers in DESIGN.md.)
 #include <hip/hip_runtime.h>
 
 #include "../device_tables.h"
@@ -35,6 +34,9 @@ namespace l7 {
 namespace {
 
 constexpr int kBlock = 256;  // threads per workgroup: the CRC tables are shared by its waves
+#ifndef L7G_KAFKA_PAD_LDS  // (A/B variants only: dynamic LDS that lowers the occupancy; TEMP)
+#define L7G_KAFKA_PAD_LDS 0
+#endif
 
 // 4 bytes at p as a little-endian word through the lane's chunk cursor
 __device__ __forceinline__ uint32_t le_load4(Cur &c, const uint8_t *p) {
@@ -562,8 +564,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
         uint32_t idx = i;
         if (sel) {
             // the length classes longest first: long produce requests start first, short ones fill the tail
-            uint32_t c = kCls - 1, j = i;
-            while (c > 0 && j >= kc[c]) { j -= kc[c]; c--; }
+            // (unrolled over constant indices: a loop indexing kc[] kept it in scratch, a chain of
+            // dependent scratch loads per entry)
+            uint32_t c = 0, j = i;
+            bool hit = false;
+#pragma unroll
+            for (int k = kCls - 1; k > 0; k--) {
+                if (!hit) {
+                    if (j >= kc[k]) j -= kc[k];
+                    else { c = (uint32_t)k; hit = true; }
+                }
+            }
             idx = sel[(size_t)c * n + j];
         }
         const uint32_t ci = B.conn_ids[idx];
@@ -627,7 +638,7 @@ hipError_t LaunchKafkaClassify(const Batch &B, const KafkaTables &T, const uint3
         int dev = 0, cus = 0, per_cu = 0;
         if (hipGetDevice(&dev) == hipSuccess &&
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kafka_classify_kernel, kBlock, 0) == hipSuccess &&
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kafka_classify_kernel, kBlock, L7G_KAFKA_PAD_LDS) == hipSuccess &&
             cus > 0 && per_cu > 0)
             resident = cus * per_cu;
         else
@@ -635,7 +646,7 @@ hipError_t LaunchKafkaClassify(const Batch &B, const KafkaTables &T, const uint3
     }
     if (!work) blocks = blocks > 8192 ? 8192 : blocks;  // grid-stride beyond this
     else if (blocks > (uint32_t)resident) blocks = (uint32_t)resident;
-    hipLaunchKernelGGL(kafka_classify_kernel, dim3(blocks), dim3(kBlock), 0, stream, B, T, sel, sel_count,
+    hipLaunchKernelGGL(kafka_classify_kernel, dim3(blocks), dim3(kBlock), L7G_KAFKA_PAD_LDS, stream, B, T, sel, sel_count,
                        answer_other ? 1u : 0u, zlist, zcount, work);
     return hipGetLastError();
 }
