@@ -36,11 +36,12 @@ def test_mixed_batch_beside_http(engine, oracle):
     nr = engine.nrules
     streams = [torch.cuda.current_stream(), torch.cuda.Stream()]
     outs = []
+    torch.cuda.synchronize()  # the inputs are on the device before either stream reads them
     for call in range(4):
         s = streams[call % 2]
-        o = [torch.full((w.n,), 7, dtype=t, device=dev) for t in (torch.uint8, torch.int32, torch.int32)]
-        cnt = torch.zeros(nr + 8, dtype=torch.int64, device=dev)
-        with torch.cuda.stream(s):
+        with torch.cuda.stream(s):  # (the outputs' fills are ordered before the call on its stream)
+            o = [torch.full((w.n,), 7, dtype=t, device=dev) for t in (torch.uint8, torch.int32, torch.int32)]
+            cnt = torch.zeros(nr + 8, dtype=torch.int64, device=dev)
             engine.classify_device(d_arena.data_ptr(), d_arena.numel(), d_off.data_ptr(), d_len.data_ptr(),
                                    d_cid.data_ptr(), w.n, *[t.data_ptr() for t in o], counters_ptr=cnt.data_ptr(),
                                    stream=s.cuda_stream)
