@@ -104,16 +104,7 @@ struct StreamScratch {
     hipEvent_t done_ev = nullptr;
     bool launched = false;
     uint64_t last_use = 0;
-    // a large mixed batch runs its Kafka and memcached kernels on a second
-    // stream beside the HTTP kernel (fork after partition_kernel, join before
-    // the counters); created with the first such call
-    hipStream_t side = nullptr;
-    hipEvent_t fork_ev = nullptr, join_ev = nullptr;
     ~StreamScratch() {
-        if (side) hipStreamSynchronize(side);
-        if (fork_ev) hipEventDestroy(fork_ev);
-        if (join_ev) hipEventDestroy(join_ev);
-        if (side) hipStreamDestroy(side);
         if (d_bignfa) hipFree(d_bignfa);
         if (d_grp) hipFree(d_grp);
         if (d_sel) hipFree(d_sel);
@@ -137,8 +128,6 @@ constexpr uint32_t kHostScanMax = 4096;
 constexpr uint32_t kLatencyMax = 64;
 // batches from this size with HTTP requests on more than one rule set take the grouped path
 constexpr uint32_t kGroupMin = 1u << 16;
-// mixed batches from this size run the Kafka / memcached kernels beside the HTTP kernel
-constexpr uint32_t kOverlapMin = 1u << 20;
 constexpr size_t kNfaScratchBytes = 256ull << 20;  // large NFAs: state-set scratch per stream (lanes in flight)  // host calls up to this size check their connections for cold rule sets
 
 // l7g_classify_host's per-thread staging: its own stream, device arena and
@@ -914,31 +903,6 @@ static int Classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, con
     mark(0);
     if (rc == hipSuccess && run[0]) rc = LaunchPartition(B, sel_k, sel_m, sel_h, cnt, s);
     mark(1);
-    // Kafka and memcached beside HTTP: a large mixed batch's classifiers are
-    // independent once the partition lists exist (each request is answered by
-    // its own protocol's kernel: pkg/proxy/kafka.go:313-359 and
-    // envoy/cilium_l7policy.cc:127-182 are separate per-request paths), and
-    // each kernel is latency-bound with a tail where CUs idle; on two streams
-    // one kernel's workgroups fill the CUs the other's tail leaves.  Not with
-    // large-NFA scratch (one per call, shared by the launches) or when
-    // profiling (per-kernel events need them one after another).
-    hipStream_t ks = s;  // the Kafka / memcached stream
-#ifdef L7G_NO_OVERLAP  // (A/B variant only; TEMP)
-    const bool overlap = false;
-#else
-    const bool overlap = partitioned && run[1] && (run[2] || run[3]) && !prof && big_lanes == 0 &&
-                         n >= kOverlapMin && !pre;
-#endif
-    if (overlap && rc == hipSuccess) {
-        if (!S->side) {
-            rc = hipStreamCreateWithFlags(&S->side, hipStreamNonBlocking);
-            if (rc == hipSuccess) rc = hipEventCreateWithFlags(&S->fork_ev, hipEventDisableTiming);
-            if (rc == hipSuccess) rc = hipEventCreateWithFlags(&S->join_ev, hipEventDisableTiming);
-        }
-        if (rc == hipSuccess) rc = hipEventRecord(S->fork_ev, s);
-        if (rc == hipSuccess) rc = hipStreamWaitEvent(S->side, S->fork_ev, 0);
-        if (rc == hipSuccess) ks = S->side;
-    }
     if (rc == hipSuccess && run[1] && nfa) rc = LaunchHttpNfa(B, ht, big_lanes, s);
     // tile counters: in the partition counts (zeroed above), or, for a large
     // unpartitioned batch, two words zeroed here (a small batch keeps the fixed
@@ -980,23 +944,19 @@ static int Classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, con
     mark(2);
     uint32_t *zcount = cnt ? cnt + 31 : nullptr;
     if (rc == hipSuccess && run[2])
-        rc = LaunchKafkaClassify(B, e->kt, sel_k, cnt, !partitioned, sel_z, zcount, cnt ? cnt + 26 : nullptr, ks);
+        rc = LaunchKafkaClassify(B, e->kt, sel_k, cnt, !partitioned, sel_z, zcount, cnt ? cnt + 26 : nullptr, s);
     // requests with gzip / snappy messages: decoded, their sets read, failures answered
     if (rc == hipSuccess && run[2] && sel_z) {
         // the engine's one decode region: after the previous inflate launch on any stream
-        if (e->zreg_used) rc = hipStreamWaitEvent(ks, e->zreg_ev, 0);
-        if (rc == hipSuccess) rc = LaunchKafkaInflate(B, sel_z, zcount, e->d_zreg, ks);
-        if (rc == hipSuccess) rc = hipEventRecord(e->zreg_ev, ks);
+        if (e->zreg_used) rc = hipStreamWaitEvent(s, e->zreg_ev, 0);
+        if (rc == hipSuccess) rc = LaunchKafkaInflate(B, sel_z, zcount, e->d_zreg, s);
+        if (rc == hipSuccess) rc = hipEventRecord(e->zreg_ev, s);
         if (rc == hipSuccess) e->zreg_used = true;
     }
     mark(3);
     if (rc == hipSuccess && run[3])
         rc = LaunchMemcacheClassify(B, mt, sel_m, sel_h, cnt ? cnt + L7_KAFKA_CLASSES : nullptr, !partitioned, big_lanes,
-                                    ks, fuse_mc);
-    if (ks != s && rc == hipSuccess) {  // join: everything after reads every classifier's outputs
-        rc = hipEventRecord(S->join_ev, ks);
-        if (rc == hipSuccess) rc = hipStreamWaitEvent(s, S->join_ev, 0);
-    }
+                                    s, fuse_mc);
     // r2d2 (proxylib's example line protocol): one lane per request over the whole batch
     if (rc == hipSuccess && run_r2) rc = LaunchR2d2Classify(B, rt, !partitioned, big_lanes, s);
     // cassandra (proxylib): the batch's USE requests, then one lane per request

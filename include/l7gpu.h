@@ -162,10 +162,7 @@ int l7g_conn_update(l7g_engine *e, uint32_t index, const l7g_conn_t *conn, char 
  * batches of 2^18 or more requests 4 words (tile counters); scratch is kept per stream (up to
  * 16 streams, then handed over least recently used first), so calls on
  * different streams run concurrently and calls on one stream are ordered by
- * it.  A batch of 2^20 or more requests with HTTP and Kafka or memcached
- * requests runs its Kafka and memcached kernels on a second, library-owned
- * stream forked from `stream` after the protocol split and joined back to it
- * before the counters, so the call is still ordered on `stream` alone.  With Kafka rules the engine also holds ONE 1 GiB decode region for
+ * it.  With Kafka rules the engine also holds ONE 1 GiB decode region for
  * compressed message sets, allocated with the first Kafka batch and shared by
  * all streams: the decode kernels of calls on different streams run one after
  * the other (each waits for the previous one's completion event).  Returns 0

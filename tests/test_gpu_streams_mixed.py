@@ -1,9 +1,10 @@
-"""A large mixed batch runs its Kafka and memcached kernels on a second
-stream beside the HTTP kernel (capi.cc Classify: fork after partition_kernel,
-join before the counters).  Every verdict, rule id and consumed length of such
-a batch -- and the per-rule counters the join orders after all three
-classifiers -- must equal the oracle's; calls in a row on one stream, and on
-two caller streams, must not see each other's lists."""
+"""Large mixed batches (past 2^20 requests, every classifier, the partition
+lists and work counters in use) on two caller streams, four calls in flight:
+every verdict, rule id and consumed length, and the per-rule counters, equal
+the oracle's -- calls in a row on one stream, and calls on two streams, do not
+see each other's lists or counters.  (Round 6 also ran the Kafka and memcached
+kernels of such a batch on a second stream beside the HTTP kernel: cfg5 37.45
+vs 37.44 ms one after the other, not kept; profiles/r6/ab6b_*.)"""
 import numpy as np
 import pytest
 import torch
@@ -20,10 +21,10 @@ def _tiled(w, n):
 
 
 @pytest.mark.timeout(600)
-def test_mixed_batch_beside_http(engine, oracle):
+def test_large_mixed_batches_on_two_streams(engine, oracle):
     u = gen.mixed_workload(200_000)
     ref_u = oracle.classify_workload(u, 8)
-    w = _tiled(u, (1 << 20) + 4321)  # past kOverlapMin
+    w = _tiled(u, (1 << 20) + 4321)
     k = -(-w.n // u.n)
     ref = tuple(np.concatenate([r] * k)[:w.n] for r in ref_u)
     engine.update_policy(w.policy)
