@@ -57,6 +57,9 @@ namespace l7 {
 
 namespace {
 
+// (Round 6: 16 waves with 128-byte windows, 128 VGPRs, 4 waves per SIMD:
+// 22.8 ms on cfg5 against 17.0 -- the spills and twice the window rounds cost
+// more than the occupancy gains; 12 waves 23.2 ms; profiles/r6/ab6d_*.)
 constexpr int kWaves = 8;
 constexpr int kBlock = 64 * kWaves;
 constexpr uint32_t kWin = 256;                 // bytes per lane window

@@ -34,9 +34,7 @@ namespace l7 {
 namespace {
 
 constexpr int kBlock = 256;  // threads per workgroup: the CRC tables are shared by its waves
-#ifndef L7G_KAFKA_PAD_LDS  // (A/B variants only: dynamic LDS that lowers the occupancy; TEMP)
-#define L7G_KAFKA_PAD_LDS 0
-#endif
+
 
 // 4 bytes at p as a little-endian word through the lane's chunk cursor
 __device__ __forceinline__ uint32_t le_load4(Cur &c, const uint8_t *p) {
@@ -638,7 +636,7 @@ hipError_t LaunchKafkaClassify(const Batch &B, const KafkaTables &T, const uint3
         int dev = 0, cus = 0, per_cu = 0;
         if (hipGetDevice(&dev) == hipSuccess &&
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kafka_classify_kernel, kBlock, L7G_KAFKA_PAD_LDS) == hipSuccess &&
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kafka_classify_kernel, kBlock, 0) == hipSuccess &&
             cus > 0 && per_cu > 0)
             resident = cus * per_cu;
         else
@@ -646,7 +644,7 @@ hipError_t LaunchKafkaClassify(const Batch &B, const KafkaTables &T, const uint3
     }
     if (!work) blocks = blocks > 8192 ? 8192 : blocks;  // grid-stride beyond this
     else if (blocks > (uint32_t)resident) blocks = (uint32_t)resident;
-    hipLaunchKernelGGL(kafka_classify_kernel, dim3(blocks), dim3(kBlock), L7G_KAFKA_PAD_LDS, stream, B, T, sel, sel_count,
+    hipLaunchKernelGGL(kafka_classify_kernel, dim3(blocks), dim3(kBlock), 0, stream, B, T, sel, sel_count,
                        answer_other ? 1u : 0u, zlist, zcount, work);
     return hipGetLastError();
 }

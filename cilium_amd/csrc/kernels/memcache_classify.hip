@@ -43,10 +43,7 @@ constexpr uint32_t kMcWaveChunk = 64 * kMcSortPer;     // entries a wave orders 
 // waves per SIMD the common kernel is built for (below)
 // (round 5, with the entry fields in LDS: 4 / 5 / 6 waves -> cfg5 memcached 3.55 /
 // 3.27 / 3.24 ms, the mixed 4M stream 0.242 / 0.257 / 0.275 ms; profiles/r5/ab5i_*)
-#ifndef L7G_MC_WAVES  // (A/B variants only; TEMP)
-#define L7G_MC_WAVES 5
-#endif
-constexpr int kMcWavesPerSimd = L7G_MC_WAVES;
+constexpr int kMcWavesPerSimd = 5;
 
 // 16-byte aligned register window over one request (the arena is readable up
 // to the 16-byte boundary after its last byte; see include/l7gpu.h).
