@@ -42,7 +42,7 @@ EXPORTS = (
     "l7g_kafka_corr_requests", "l7g_kafka_corr_responses", "l7g_kafka_corr_gc", "l7g_kafka_corr_size",
     "l7g_flow_stats_enable", "l7g_flow_stats",
     "l7g_tables_export", "l7g_tables_import", "l7g_tables_compiled", "l7g_tables_digest",
-    "l7g_frame_streams", "l7g_classify_streams",
+    "l7g_frame_streams", "l7g_classify_streams", "l7g_service_enable", "l7g_service_stats",
 )
 
 
@@ -92,6 +92,9 @@ def load(path=None):
     lib.l7g_classify_streams.argtypes = [vp, vp, C.c_uint64, vp, vp, vp, C.c_uint32, C.c_uint32, vp, vp, vp, vp, vp, vp,
                                          vp, vp, vp]
     lib.l7g_classify_host.argtypes = [vp, vp, C.c_uint64, vp, vp, vp, C.c_uint32, vp, vp, vp]
+    lib.l7g_service_enable.argtypes = [vp, C.c_int]
+    lib.l7g_service_stats.argtypes = [vp, C.POINTER(C.c_uint64)]
+    lib.l7g_service_stats.restype = None
     lib.l7g_stats.argtypes = [vp, C.POINTER(Stats)]
     lib.l7g_debug_regex.argtypes = [cp, sz, C.c_int, cp, sz, cp, sz]
     lib.l7g_debug_regex_nfa.argtypes = [cp, sz, C.c_int, cp, sz, cp, sz]

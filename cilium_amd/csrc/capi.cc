@@ -24,6 +24,7 @@
 #include "engine/nfa_pool.h"
 #include "engine/r2_compile.h"
 #include "kernels/copy_in_types.h"
+#include "kernels/service_types.h"
 #include "policy/npds_proto.h"
 #include "policy/policy.h"
 #include "regex/nfa_walk.h"
@@ -69,6 +70,10 @@ hipError_t LaunchHttpGroup(const Batch &B, const HttpTables &T, const uint32_t *
                            uint32_t *segs, uint32_t *gsel, uint32_t *gbig, hipStream_t stream);
 hipError_t LaunchHttpGrouped(const Batch &B, const HttpTables &T, const uint32_t *gsel, const uint32_t *segs,
                              const uint32_t *gbig, uint32_t *ctl, bool any_big, hipStream_t stream);
+hipError_t LaunchHttpService(SvcBox *box, const SvcStatic &S, const HttpTables &T, uint32_t seen0, uint64_t idle,
+                             hipStream_t stream);
+hipError_t LaunchMemcacheService(SvcBox *box, const SvcStatic &S, const McTables &T, uint32_t seen0, uint64_t idle,
+                                 hipStream_t stream);
 }  // namespace l7
 
 using namespace l7;
@@ -158,8 +163,43 @@ struct HostCtx {
     }
 };
 
+// ---- resident services (kernels/service.h): the synchronous drop-in calls
+// (one Allowed(), one OnData) posted to a polling workgroup instead of launched
+constexpr uint32_t kSvcHttpMax = 8;    // HTTP requests per call (one per wave of the workgroup)
+constexpr uint32_t kSvcMcMax = 64;     // memcached requests per call (one wave)
+constexpr size_t kSvcInBytes = SvcArenaOff(kSvcMcMax) + kZeroCopyMaxBytes + 64;
+constexpr size_t kSvcOutBytes = kSvcMcMax * 9 + 64;
+// a service leaves after this many shader-clock cycles without a call (~50 ms at 2.4 GHz)
+constexpr uint64_t kSvcIdleCycles = 120000000ull;
+struct Service {
+    std::mutex mu;  // one call at a time, held from its posting to its answers
+    hipStream_t s = nullptr;
+    SvcBox *box = nullptr, *box_dev = nullptr;  // pinned, coherent
+    uint8_t *pin_in = nullptr, *pin_in_dev = nullptr, *pin_out = nullptr, *pin_out_dev = nullptr;
+    uint8_t *dev_in = nullptr;
+    uint32_t seq = 0;
+    bool launched = false;  // a workgroup may be serving (launched, not yet seen leaving)
+    // its launch arguments: the tables and connections it serves with
+    HttpTables ht{};
+    McTables mt{};
+    const DevConn *conns = nullptr;
+    uint32_t nconns = 0;
+    uint64_t calls = 0, launches = 0;
+    ~Service() {
+        if (s) hipStreamSynchronize(s);
+        if (dev_in) hipFree(dev_in);
+        if (pin_in) hipHostFree(pin_in);
+        if (pin_out) hipHostFree(pin_out);
+        if (box) hipHostFree(box);
+        if (s) hipStreamDestroy(s);
+    }
+};
+
 struct l7g_engine {
     int device = 0;
+    // [0] HTTP, [1] memcached (l7g_service_enable; L7G_SERVICE=0 turns them off)
+    Service svc[2];
+    bool svc_on = true;
     std::mutex mu;
     std::unique_ptr<PolicySet> ps;
     std::unique_ptr<HttpCompiler> hc;
@@ -215,8 +255,34 @@ struct l7g_engine {
     bool prof_ran[4] = {};
 };
 
-// Waits for the kernels of every stream's last call.  Caller holds e->mu.
+// Stops a service's workgroup and waits for it to leave (v.mu held): its
+// launch arguments (tables, connections) are about to change, or the engine
+// goes away.
+static hipError_t ServiceStop(Service &v) {
+    if (!v.launched) return hipSuccess;
+    __atomic_store_n(&v.box->stop, 1u, __ATOMIC_SEQ_CST);
+    v.launched = false;
+    return hipStreamSynchronize(v.s);  // (it leaves at its next poll; a fault is reported here)
+}
+static void StopServices(l7g_engine *e) {
+    for (Service &v : e->svc) {
+        std::lock_guard<std::mutex> g(v.mu);  // (waits for a call in flight)
+        ServiceStop(v);
+    }
+}
+// A launch that wants every CU (a persistent grid) asks the services to leave
+// without waiting; the next synchronous call starts them again.
+static void ReleaseServiceCUs(l7g_engine *e) {
+    for (Service &v : e->svc)
+        if (v.box && __atomic_load_n(&v.box->state, __ATOMIC_ACQUIRE) != kSvcStopped)
+            __atomic_store_n(&v.box->stop, 1u, __ATOMIC_SEQ_CST);
+}
+
+// Waits for the kernels of every stream's last call, and stops the services
+// (their launch arguments are what the caller is about to rewrite).  Caller
+// holds e->mu.
 static hipError_t WaitLastClassify(l7g_engine *e) {
+    StopServices(e);
     hipError_t rc = hipSuccess;
     for (auto &kv : e->scr)
         if (kv.second->launched) {
@@ -495,6 +561,10 @@ l7g_engine *l7g_engine_create(int device, char *err, size_t errlen) {
     if ((rc = hipSetDevice(device)) != hipSuccess) { set_err(err, errlen, hipGetErrorString(rc)); return nullptr; }
     auto *e = new l7g_engine();
     e->device = device;
+    {
+        const char *v = getenv("L7G_SERVICE");
+        e->svc_on = !(v && v[0] == '0');
+    }
     e->ps = std::make_unique<PolicySet>();
     e->hc = std::make_unique<HttpCompiler>(e->ps.get());
     e->kc = std::make_unique<KafkaCompiler>(e->ps.get());
@@ -508,6 +578,7 @@ void l7g_engine_destroy(l7g_engine *e) {
     if (!e) return;
     if (e->device < 0) { delete e; return; }
     hipSetDevice(e->device);
+    StopServices(e);
     hipDeviceSynchronize();
     if (e->d_blob) hipFree(e->d_blob);
     if (e->d_conns) hipFree(e->d_conns);
@@ -790,6 +861,7 @@ static int Classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, con
             partitioned = run_http = run_kafka = run_r2 = run_cs = false;
         }
     }
+    if (n >= kPartitionMin) ReleaseServiceCUs(e);  // (persistent grids: every CU)
     StreamScratch *S = nullptr;
     if ((rc = GetScratch(e, s, &S)) != hipSuccess) return (int)rc;
     uint32_t *sel_k = nullptr, *sel_m = nullptr, *sel_h = nullptr, *sel_z = nullptr, *cnt = nullptr;
@@ -1110,11 +1182,168 @@ struct HostIn {
     int nseg;  // the arena is these pieces, concatenated
 };
 
+// The service's box, staging and stream (v.mu held), on its first call.
+static hipError_t ServiceAlloc(Service &v) {
+    if (v.s) return hipSuccess;
+    hipError_t rc;
+    void *p = nullptr;
+    if ((rc = hipHostMalloc(&p, sizeof(SvcBox), hipHostMallocCoherent)) != hipSuccess) return rc;
+    v.box = (SvcBox *)p;
+    memset(v.box, 0, sizeof(SvcBox));
+    if ((rc = hipHostGetDevicePointer((void **)&v.box_dev, v.box, 0)) != hipSuccess ||
+        (rc = hipHostMalloc((void **)&v.pin_in, kSvcInBytes, hipHostMallocDefault)) != hipSuccess ||
+        (rc = hipHostMalloc((void **)&v.pin_out, kSvcOutBytes, hipHostMallocDefault)) != hipSuccess ||
+        (rc = hipHostGetDevicePointer((void **)&v.pin_in_dev, v.pin_in, 0)) != hipSuccess ||
+        (rc = hipHostGetDevicePointer((void **)&v.pin_out_dev, v.pin_out, 0)) != hipSuccess ||
+        (rc = hipMalloc((void **)&v.dev_in, kSvcInBytes)) != hipSuccess)
+        return rc;
+    return hipStreamCreateWithFlags(&v.s, hipStreamNonBlocking);  // (last: v.s marks a complete allocation)
+}
+
+// Posts a call to service v (e->mu and v.mu held; the inputs are in
+// v.pin_in): the job's words, then req_seq, then the state read that decides
+// whether a workgroup must be launched (a new service, one that has left, or
+// one whose launch arguments are stale).
+static hipError_t ServicePost(l7g_engine *e, Service &v, int kind, uint32_t n, uint64_t arena_len, uint32_t flags,
+                              uint32_t *seq_out) {
+    hipError_t rc = hipSuccess;
+    const uint32_t nconns = (uint32_t)e->conns.size();
+    const bool same = kind == 0 ? memcmp(&v.ht, &e->ht, sizeof v.ht) == 0 : memcmp(&v.mt, &e->mt, sizeof v.mt) == 0;
+    if (v.launched && !(same && v.conns == e->d_conns && v.nconns == nconns) && (rc = ServiceStop(v)) != hipSuccess)
+        return rc;
+    SvcBox *b = v.box;
+    __atomic_store_n(&b->n, n, __ATOMIC_RELAXED);
+    __atomic_store_n(&b->arena_len, (uint32_t)arena_len, __ATOMIC_RELAXED);
+    __atomic_store_n(&b->flags, flags, __ATOMIC_RELAXED);
+    __atomic_store_n(&b->stop, 0u, __ATOMIC_RELAXED);
+    uint32_t seq = ++v.seq;
+    if (!seq) seq = ++v.seq;  // (never 0: the done word's initial value)
+    __atomic_store_n(&b->req_seq, seq, __ATOMIC_SEQ_CST);  // (after the inputs and the job's words)
+    // the workgroup's exit handshake writes EXITING, fences, reads req_seq:
+    // either it sees this call, or this read sees it leaving
+    uint32_t st = __atomic_load_n(&b->state, __ATOMIC_SEQ_CST);
+    bool start = !v.launched;
+    if (v.launched && st != kSvcRunning) {
+        const auto t0 = std::chrono::steady_clock::now();
+        while ((st = __atomic_load_n(&b->state, __ATOMIC_SEQ_CST)) == kSvcExiting &&
+               std::chrono::steady_clock::now() - t0 < std::chrono::seconds(1))
+            __builtin_ia32_pause();
+        start = st != kSvcRunning;
+        if (start && (rc = hipStreamSynchronize(v.s)) != hipSuccess) return rc;  // (the old workgroup has left)
+    }
+    if (start) {
+        __atomic_store_n(&b->state, (uint32_t)kSvcRunning, __ATOMIC_SEQ_CST);
+        const SvcStatic S{v.pin_in_dev, v.dev_in, v.pin_out_dev, e->d_conns, nconns, 0};
+        rc = kind == 0 ? LaunchHttpService(v.box_dev, S, e->ht, seq - 1, kSvcIdleCycles, v.s)
+                       : LaunchMemcacheService(v.box_dev, S, e->mt, seq - 1, kSvcIdleCycles, v.s);
+        if (rc != hipSuccess) return rc;
+        v.ht = e->ht;
+        v.mt = e->mt;
+        v.conns = e->d_conns;
+        v.nconns = nconns;
+        v.launched = true;
+        v.launches++;
+    }
+    v.calls++;
+    *seq_out = seq;
+    return hipSuccess;
+}
+
+// A synchronous call a service can take: the HTTP (at most kSvcHttpMax) or the
+// memcached (at most kSvcMcMax) requests of one small call whose inputs lie in
+// one piece of pinned memory, with the selection Classify makes for such a
+// call (only that protocol's kernel, unpartitioned, answering the requests no
+// parser owns) and nothing else to run (no NFA-fallback matchers, no proxy
+// statistics).  Returns false when the call takes the launched path; true
+// when it was answered (or failed: *rc_out).
+static bool ServiceTry(l7g_engine *e, uint32_t n, uint64_t arena_len, const HostIn &in, uint8_t *verdict,
+                       int32_t *rule, uint32_t *consumed, hipError_t *rc_out) {
+    if (!e->svc_on || n == 0 || n > kSvcMcMax || arena_len > kZeroCopyMaxBytes) return false;
+    if (!(in.nseg == 0 || (in.nseg == 1 && in.seg[0].rows <= 1 && in.seg[0].width == arena_len))) return false;
+    if (in.nseg == 0 && arena_len) return false;
+    Service *v = nullptr;
+    uint32_t seq = 0;
+    {
+        std::lock_guard<std::mutex> g(e->mu);
+        if (e->device < 0 || hipSetDevice(e->device) != hipSuccess || Upload(e) != hipSuccess) return false;
+        if (e->flow_stats && !e->skey_list.empty()) return false;
+        uint32_t seen = 0;
+        bool any_cold = false;
+        for (uint32_t i = 0; i < n; i++) {
+            const uint32_t ci = in.conn[i];
+            if (ci >= e->conns.size()) continue;
+            const uint32_t pr = e->attrs[ci].proto;
+            if (pr < 32) seen |= 1u << pr;
+            any_cold = any_cold || (pr == PROTO_HTTP && e->conns[ci].ruleset != e->hot_ruleset);
+        }
+        any_cold = any_cold && e->any_cold;
+        const uint32_t owned = seen & ((1u << PROTO_HTTP) | (1u << PROTO_KAFKA) | (1u << PROTO_MEMCACHE) |
+                                       (1u << PROTO_R2D2) | (1u << PROTO_CASSANDRA));
+        int kind = -1;
+        uint32_t flags = kSvcAnswerOther;
+        if (owned == (1u << PROTO_HTTP) && e->has_http && n <= kSvcHttpMax && !e->ht.nfa_pool) {
+            kind = 0;
+            const bool hot = e->ht.hot_ruleset >= 0;
+            flags |= (hot ? kSvcHttpHot : 0u) | (!hot || any_cold ? kSvcHttpGeneral : 0u);
+        } else if (owned == (1u << PROTO_MEMCACHE) && e->has_mc && !e->mt.nfa_pool) {
+            kind = 1;
+        }
+        if (kind < 0) return false;
+        v = &e->svc[kind];
+        if (!v->mu.try_lock()) return false;  // (another thread's call is in the service: launch this one)
+        // the inputs, in the service's layout (service_types.h)
+        const uint32_t nn = n;
+        const size_t a_off = SvcArenaOff(n);
+        hipError_t rc = ServiceAlloc(*v);
+        if (rc == hipSuccess) {
+            memcpy(v->pin_in, in.off, (size_t)nn * 8);
+            memcpy(v->pin_in + (size_t)nn * 8, in.len, (size_t)nn * 4);
+            memcpy(v->pin_in + (size_t)nn * 12, in.conn, (size_t)nn * 4);
+            if (arena_len) memcpy(v->pin_in + a_off, in.seg[0].p, arena_len);
+            rc = ServicePost(e, *v, kind, n, arena_len, flags, &seq);
+        }
+        if (rc != hipSuccess) {
+            v->mu.unlock();
+            *rc_out = rc;
+            return true;
+        }
+    }
+    // the answers: the done word, then pinned memory (no stream wait: a fault
+    // shows as a done word that never comes, and the service's stream reports it)
+    hipError_t rc = hipSuccess;
+    bool done = false;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t k = 0;; k++) {
+        if (__atomic_load_n(&v->box->done, __ATOMIC_ACQUIRE) == seq) {
+            done = true;
+            break;
+        }
+        if ((k & 255) == 255 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(1000)) break;
+        __builtin_ia32_pause();
+    }
+    if (!done) {  // (v->mu held: the service's own fields only, no engine lock)
+        rc = hipStreamQuery(v->s);
+        if (rc == hipSuccess || rc == hipErrorNotReady) rc = hipErrorLaunchTimeOut;
+        const hipError_t r2 = ServiceStop(*v);
+        if (rc == hipErrorLaunchTimeOut && r2 != hipSuccess) rc = r2;
+    } else {
+        const uint32_t nn = n;
+        const uint8_t *po = v->pin_out;
+        memcpy(verdict, po, n);
+        memcpy(rule, po + ((nn + 3) & ~3u), (size_t)n * 4);
+        memcpy(consumed, po + ((nn + 3) & ~3u) + (size_t)nn * 4, (size_t)n * 4);
+    }
+    v->mu.unlock();
+    *rc_out = rc;
+    return true;
+}
+
 // classify a call whose inputs are in pinned host memory, wait for it, copy
 // the answers out
 static hipError_t HostRun(l7g_engine *e, HostCtx *H, uint32_t n, uint64_t arena_len, const HostIn &in,
                           uint8_t *verdict, int32_t *rule, uint32_t *consumed) {
     hipError_t rc = hipSuccess;
+    if (ServiceTry(e, n, arena_len, in, verdict, rule, consumed, &rc)) return rc;
     const size_t nn = std::max<uint32_t>(n, 1);
     const size_t a_off = HostArenaOff(n);
     // A small call (the Envoy adapter's Allowed(), one OnData, a light batch)
@@ -1307,6 +1536,24 @@ int l7g_host_reserve(l7g_engine *e, uint32_t n, uint64_t arena_len) {
 }
 
 int l7g_engine_has_device(const l7g_engine *e) { return e && e->device >= 0 ? 1 : 0; }
+
+extern "C" {
+int l7g_service_enable(l7g_engine *e, int on) {
+    if (!e) return 0;
+    std::lock_guard<std::mutex> g(e->mu);
+    const int was = e->svc_on ? 1 : 0;
+    e->svc_on = on != 0;
+    if (!e->svc_on && e->device >= 0) StopServices(e);
+    return was;
+}
+void l7g_service_stats(l7g_engine *e, uint64_t out[4]) {
+    for (int k = 0; k < 2; k++) {
+        std::lock_guard<std::mutex> g(e->svc[k].mu);
+        out[2 * k] = e->svc[k].calls;
+        out[2 * k + 1] = e->svc[k].launches;
+    }
+}
+}  // extern "C"
 
 void *l7g_pinned_alloc(size_t bytes) {
     void *p = nullptr;

@@ -47,6 +47,7 @@
 #include "../device_tables.h"
 #include "copy_in.h"
 #include "gmem.h"
+#include "service.h"
 
 // OCKL's DPP wave reductions (64-bit forms are not declared by hip_runtime.h)
 extern "C" __device__ __attribute__((const)) unsigned long long __ockl_wfred_min_u64(unsigned long long);
@@ -1663,29 +1664,24 @@ __global__ __launch_bounds__(kBlock) void http_classify_kernel(Batch B, HttpTabl
 
 // One request per wave (lat_request above) for small calls; the image
 // staging, the request's checks and the answers for entries no parser owns are
-// the tile kernel's.
+// the tile kernel's.  stage: copy the hot rule set's image into LDS (the
+// resident service stages it once for its lifetime).  Ends with a barrier.
 template <bool kHot>
-// ci: the call's inputs to copy first (a one-workgroup launch), or none.
-__global__ __launch_bounds__(kBlock) void http_latency_kernel(Batch B, HttpTables T, const uint32_t *__restrict__ sel,
-                                                              const uint32_t *__restrict__ sel_count,
-                                                              uint32_t answer_other, CopyIn ci) {
+__device__ __forceinline__ void lat_body(const Batch &B, const HttpTables &T, const uint32_t *__restrict__ sel,
+                                         const uint32_t *__restrict__ sel_count, uint32_t answer_other, uint8_t *lds,
+                                         bool stage) {
     const uint8_t *__restrict__ arena = B.arena;
     const uint32_t n = B.n, nconns = B.nconns;
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63, wave = tid >> 6;
     uint8_t *s_img = lds + kOffImg;
 #ifdef L7G_PHASE_TIMING
     const uint64_t ph_k0 = __builtin_amdgcn_s_memtime();
 #endif
-    copy_in_block(ci);
     const int32_t hot = T.hot_ruleset;
     const bool hot_ok = hot >= 0 && (uint32_t)hot < T.nrulesets && T.rulesets[hot].image_len <= kLdsImageBytes;
-    if (kHot && !hot_ok) {
-        signal_done_block(ci);
-        return;
-    }
-    if (kHot) {
+    if (kHot && !hot_ok) return;
+    if (kHot && stage) {
         const DevRuleset r = T.rulesets[hot];
         const uint4 *src = (const uint4 *)(T.images + r.image_off);
         const uint32_t n16 = (r.image_len + 15) / 16;
@@ -1746,7 +1742,55 @@ __global__ __launch_bounds__(kBlock) void http_latency_kernel(Batch B, HttpTable
         if (!L.done) lat_request<kHot>(L, img, wave_lds, lane, O);
         else if (L.owed && lane == 0) emit(L, O);
     }
+    __syncthreads();
+}
+
+template <bool kHot>
+// ci: the call's inputs to copy first (a one-workgroup launch), or none.
+__global__ __launch_bounds__(kBlock) void http_latency_kernel(Batch B, HttpTables T, const uint32_t *__restrict__ sel,
+                                                              const uint32_t *__restrict__ sel_count,
+                                                              uint32_t answer_other, CopyIn ci) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
+    copy_in_block(ci);
+    lat_body<kHot>(B, T, sel, sel_count, answer_other, lds, true);
     signal_done_block(ci);
+}
+
+// The resident service (kernels/service.h): one workgroup serves the
+// synchronous HTTP calls (one Envoy Allowed(), a few requests) the host posts
+// to the box, each as the launched path would run it -- the inputs copied
+// into HBM, the hot pass and / or the general pass of lat_body, the answers to
+// pinned memory, then the done word -- with the hot rule set's image staged
+// in LDS once for the service's lifetime.  The box's first word holds the
+// poll's result (wave 0's window area: free between calls).
+__global__ __launch_bounds__(kBlock) void http_service_kernel(SvcBox *box, SvcStatic S, HttpTables T, uint32_t seen0,
+                                                              uint64_t idle) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
+    uint32_t *word = reinterpret_cast<uint32_t *>(lds);
+    uint32_t seen = seen0;
+    uint64_t t_last = __builtin_amdgcn_s_memtime();
+    bool staged = false;
+    if (threadIdx.x == 0) svc_store(&box->state, kSvcRunning);
+    for (;;) {
+        const SvcCall c = svc_next(box, seen, t_last, idle, word);
+        if (!c.seq) break;
+        const Batch B = svc_batch(S, c);
+        const CopyIn ci = svc_copy(S, box, c);
+        copy_in_block(ci);
+        const uint32_t other = (c.flags & kSvcAnswerOther) ? 1u : 0u;
+        if (c.flags & kSvcHttpHot) {
+            lat_body<true>(B, T, nullptr, nullptr, other, lds, !staged);
+            staged = true;
+        }
+        if (c.flags & kSvcHttpGeneral) lat_body<false>(B, T, nullptr, nullptr, other, lds, false);
+        signal_done_block(ci);
+        __syncthreads();
+        t_last = __builtin_amdgcn_s_memtime();
+    }
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        svc_store(&box->state, kSvcStopped);
+    }
 }
 
 // Requests grouped by rule set (http_group.hip): a workgroup takes one segment
@@ -1907,6 +1951,14 @@ hipError_t LaunchHttpGrouped(const Batch &B, const HttpTables &T, const uint32_t
     if (any_big)
         hipLaunchKernelGGL(http_classify_kernel<false>, dim3(blocks), dim3(kBlock), 0, stream, B, T, gbig, ctl + 2, 0u,
                            ctl + 3);
+    return hipGetLastError();
+}
+
+// The HTTP service: one workgroup on `stream` until it leaves (idle cycles
+// without a call, or stop).
+hipError_t LaunchHttpService(SvcBox *box, const SvcStatic &S, const HttpTables &T, uint32_t seen0, uint64_t idle,
+                             hipStream_t stream) {
+    hipLaunchKernelGGL(http_service_kernel, dim3(1), dim3(kBlock), 0, stream, box, S, T, seen0, idle);
     return hipGetLastError();
 }
 

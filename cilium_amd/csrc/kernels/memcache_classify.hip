@@ -28,6 +28,7 @@
 #include "../regex/nfa_walk.h"
 #include "copy_in.h"
 #include "gmem.h"
+#include "service.h"
 
 namespace l7 {
 
@@ -637,36 +638,75 @@ __device__ __forceinline__ void mc_loop(Batch B, McTables T, const uint8_t *imag
     }
 }
 
+// The rule-set images (command / opcode masks, key DFAs) are read once per
+// key byte in a dependent chain: when they all fit, every workgroup stages
+// them in LDS and walks them there instead of through L1/L2.
+__device__ __forceinline__ void mc_stage_images(const McTables &T, uint8_t *lds) {
+    const uint32_t n16 = (T.images_len + 15) / 16;
+    // every load issued before the first store: one memory round trip per
+    // 32 KiB, not one per 4 KiB (a one-request launch waits on this)
+    constexpr uint32_t kIters = 8;  // kMcLdsImages / (16 * kBlock)
+    static_assert(kIters * 16 * kBlock == kMcLdsImages, "staging rounds");
+    uint4 t[kIters];
+#pragma unroll
+    for (uint32_t k = 0; k < kIters; k++)
+        if (threadIdx.x + k * kBlock < n16) t[k] = ((const uint4 *)T.images)[threadIdx.x + k * kBlock];
+#pragma unroll
+    for (uint32_t k = 0; k < kIters; k++)
+        if (threadIdx.x + k * kBlock < n16) ((uint4 *)lds)[threadIdx.x + k * kBlock] = t[k];
+    __syncthreads();
+}
+__device__ __forceinline__ bool mc_images_fit(const McTables &T) { return T.images_len && T.images_len <= kMcLdsImages; }
+
 template <bool kNfa, int kCh>
 __device__ __forceinline__ void mc_classify(Batch B, McTables T, const uint32_t *__restrict__ sel,
                                             const uint32_t *__restrict__ sel2, const uint32_t *__restrict__ sel_count,
                                             uint32_t answer_other, const CopyIn &ci) {
     copy_in_block(ci);  // (a one-workgroup call's inputs, when the host asks)
-    // The rule-set images (command / opcode masks, key DFAs) are read once per
-    // key byte in a dependent chain: when they all fit, every workgroup stages
-    // them in LDS (dynamic shared memory sized by the launcher) and walks them
-    // there instead of through L1/L2.
     extern __shared__ __attribute__((aligned(16))) uint8_t mc_lds[];
     __shared__ uint4 s_ent[kMcWaves][kMcWaveChunk];  // each wave's entries in parser order, with their fields
-    if (T.images_len && T.images_len <= kMcLdsImages) {
-        const uint32_t n16 = (T.images_len + 15) / 16;
-        // every load issued before the first store: one memory round trip per
-        // 32 KiB, not one per 4 KiB (a one-request launch waits on this)
-        constexpr uint32_t kIters = 8;  // kMcLdsImages / (16 * kBlock)
-        static_assert(kIters * 16 * kBlock == kMcLdsImages, "staging rounds");
-        uint4 t[kIters];
-#pragma unroll
-        for (uint32_t k = 0; k < kIters; k++)
-            if (threadIdx.x + k * kBlock < n16) t[k] = ((const uint4 *)T.images)[threadIdx.x + k * kBlock];
-#pragma unroll
-        for (uint32_t k = 0; k < kIters; k++)
-            if (threadIdx.x + k * kBlock < n16) ((uint4 *)mc_lds)[threadIdx.x + k * kBlock] = t[k];
-        __syncthreads();
+    if (mc_images_fit(T)) {
+        mc_stage_images(T, mc_lds);
         mc_loop<kNfa, true, kCh>(B, T, mc_lds, sel, sel2, sel_count, answer_other, &s_ent[0][0]);
     } else {
         mc_loop<kNfa, false, kCh>(B, T, T.images, sel, sel2, sel_count, answer_other, &s_ent[0][0]);
     }
     signal_done_block(ci);
+}
+
+// The resident service (kernels/service.h) for the synchronous memcached calls
+// (one proxylib OnData): each posted call's inputs copied into HBM, mc_loop
+// over them (at most 64 requests: one wave, no parser ordering), the answers
+// to pinned memory, then the done word; the images staged in LDS once for
+// the service's lifetime.
+template <int kCh>
+__global__ __launch_bounds__(kBlock) void memcache_service_kernel(SvcBox *box, SvcStatic S, McTables T, uint32_t seen0,
+                                                                  uint64_t idle) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kMcLdsImages];
+    __shared__ uint4 s_ent[kMcWaves][kMcWaveChunk];
+    uint32_t *word = reinterpret_cast<uint32_t *>(&s_ent[0][0]);  // (the entries' slice: unused between calls)
+    uint32_t seen = seen0;
+    uint64_t t_last = __builtin_amdgcn_s_memtime();
+    const bool fit = mc_images_fit(T);
+    if (fit) mc_stage_images(T, lds);
+    if (threadIdx.x == 0) svc_store(&box->state, kSvcRunning);
+    for (;;) {
+        const SvcCall c = svc_next(box, seen, t_last, idle, word);
+        if (!c.seq) break;
+        const Batch B = svc_batch(S, c);
+        const CopyIn ci = svc_copy(S, box, c);
+        copy_in_block(ci);
+        const uint32_t other = (c.flags & kSvcAnswerOther) ? 1u : 0u;
+        if (fit) mc_loop<false, true, kCh>(B, T, lds, nullptr, nullptr, nullptr, other, &s_ent[0][0]);
+        else mc_loop<false, false, kCh>(B, T, T.images, nullptr, nullptr, nullptr, other, &s_ent[0][0]);
+        signal_done_block(ci);
+        __syncthreads();
+        t_last = __builtin_amdgcn_s_memtime();
+    }
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        svc_store(&box->state, kSvcStopped);
+    }
 }
 
 // The common kernel is built for kMcWavesPerSimd waves per SIMD (round 3 on 2.4M
@@ -714,6 +754,19 @@ hipError_t LaunchMemcacheClassify(const Batch &B, const McTables &T, const uint3
     else
         hipLaunchKernelGGL(memcache_classify_kernel<kMcMaxChunks>, dim3(blocks), dim3(kBlock), lds, stream, B, T, sel, sel2,
                            sel_count, answer_other ? 1u : 0u, c);
+    return hipGetLastError();
+}
+
+// The memcached service: one workgroup on `stream` until it leaves (idle
+// cycles without a call, or stop).  Calls of at most 64 requests (one wave).
+hipError_t LaunchMemcacheService(SvcBox *box, const SvcStatic &S, const McTables &T, uint32_t seen0, uint64_t idle,
+                                 hipStream_t stream) {
+    if (T.nfa_pool) return hipErrorInvalidValue;  // (NFA key matchers: the launched path)
+    if (T.max_chunks <= 1)
+        hipLaunchKernelGGL(memcache_service_kernel<1>, dim3(1), dim3(kBlock), 0, stream, box, S, T, seen0, idle);
+    else
+        hipLaunchKernelGGL(memcache_service_kernel<kMcMaxChunks>, dim3(1), dim3(kBlock), 0, stream, box, S, T, seen0,
+                           idle);
     return hipGetLastError();
 }
 

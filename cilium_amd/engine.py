@@ -201,6 +201,17 @@ class Engine:
         return {(x.policy, x.proto, x.port, x.ingress): (x.received, x.forwarded, x.denied, x.error)
                 for x in arr[:n.value]}
 
+    def service(self, on=None):
+        """Resident services (l7g_service_enable): with on given, enable (True)
+        or stop and disable (False); returns the previous setting and the
+        counts {http_calls, http_launches, mc_calls, mc_launches}."""
+        prev = None
+        if on is not None:
+            prev = bool(self._lib.l7g_service_enable(self._h, 1 if on else 0))
+        out = (C.c_uint64 * 4)()
+        self._lib.l7g_service_stats(self._h, out)
+        return prev, dict(zip(("http_calls", "http_launches", "mc_calls", "mc_launches"), list(out)))
+
     def stats(self):
         s = _lib.Stats()
         self._lib.l7g_stats(self._h, C.byref(s))

@@ -210,6 +210,22 @@ int l7g_classify_host(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, c
 
 int l7g_stats(l7g_engine *e, l7g_stats_t *out);
 
+/* Resident services: the synchronous drop-in calls of l7g_classify_host (and
+ * so the Envoy adapter's Allowed() and proxylib's OnData) whose requests are
+ * all HTTP (at most 8) or all memcached (at most 64) are posted to one polling
+ * workgroup per protocol instead of launched: no launch and no completion
+ * signal per call.  A service starts with the first such call, stays while
+ * calls keep coming and leaves after ~50 ms without one, when a batch of
+ * 4096 or more requests wants every CU, or before a policy or connection
+ * update.  Answers are those of the launched path (the same device code); a
+ * kernel fault is reported by the call that was waiting.  On by default
+ * (L7G_SERVICE=0 at engine creation turns it off).  Returns the previous
+ * setting. */
+int l7g_service_enable(l7g_engine *e, int on);
+/* [0] HTTP calls served, [1] HTTP workgroup launches, [2] memcached calls,
+ * [3] memcached launches. */
+void l7g_service_stats(l7g_engine *e, uint64_t out[4]);
+
 /* Asynchronous batching for callers that decide one request at a time on an
  * event loop -- Envoy's cilium.l7policy decodeHeaders
  * (envoy/cilium_l7policy.cc:127-182), which would return StopIteration and
