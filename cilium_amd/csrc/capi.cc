@@ -1212,10 +1212,11 @@ static hipError_t ServicePost(l7g_engine *e, Service &v, int kind, uint32_t n, u
     if (v.launched && !(same && v.conns == e->d_conns && v.nconns == nconns) && (rc = ServiceStop(v)) != hipSuccess)
         return rc;
     SvcBox *b = v.box;
-    __atomic_store_n(&b->n, n, __ATOMIC_RELAXED);
+    __atomic_store_n(&b->n, n, __ATOMIC_RELAXED);  // (the line's other words: stored before req_seq)
     __atomic_store_n(&b->arena_len, (uint32_t)arena_len, __ATOMIC_RELAXED);
     __atomic_store_n(&b->flags, flags, __ATOMIC_RELAXED);
     __atomic_store_n(&b->stop, 0u, __ATOMIC_RELAXED);
+    std::atomic_thread_fence(std::memory_order_release);
     uint32_t seq = ++v.seq;
     if (!seq) seq = ++v.seq;  // (never 0: the done word's initial value)
     __atomic_store_n(&b->req_seq, seq, __ATOMIC_SEQ_CST);  // (after the inputs and the job's words)

@@ -27,6 +27,13 @@ __device__ __forceinline__ void svc_store(uint32_t *p, uint32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// the box's first 16 bytes, read past every cache (system scope: sc0 sc1)
+__device__ __forceinline__ uint4 svc_load_head(const SvcBox *box) {
+    uint4 v;
+    asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(box) : "memory");
+    return v;
+}
+
 struct SvcCall {
     uint32_t seq, n, arena_len, flags;
 };
@@ -36,30 +43,27 @@ struct SvcCall {
 __device__ __forceinline__ SvcCall svc_next(SvcBox *box, uint32_t &seen, uint64_t &t_last, uint64_t idle,
                                             uint32_t *word) {
     if (threadIdx.x == 0) {
-        uint32_t q = 0;
+        uint4 h = make_uint4(0, 0, 0, 0);
         for (;;) {
-            q = svc_load(&box->req_seq);
-            if (q != seen) break;
+            h = svc_load_head(box);
+            if (h.x != seen) break;
             if (svc_load(&box->stop) || __builtin_amdgcn_s_memtime() - t_last > idle) {
                 svc_store(&box->state, kSvcExiting);
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
-                q = svc_load(&box->req_seq);
-                if (q != seen) {
+                h = svc_load_head(box);
+                if (h.x != seen) {
                     svc_store(&box->state, kSvcRunning);
                     break;
                 }
-                q = 0;  // leave (the caller stores STOPPED)
+                h.x = 0;  // leave (the caller stores STOPPED)
                 break;
             }
-            __builtin_amdgcn_s_sleep(4);
+            __builtin_amdgcn_s_sleep(1);
         }
-        word[0] = q;
-        if (q) {  // the job's words: written by the host before req_seq
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-            word[1] = svc_load(&box->n);
-            word[2] = svc_load(&box->arena_len);
-            word[3] = svc_load(&box->flags);
-        }
+        word[0] = h.x;
+        word[1] = h.y;
+        word[2] = h.z;
+        word[3] = h.w;
     }
     __syncthreads();
     SvcCall c;

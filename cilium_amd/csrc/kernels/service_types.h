@@ -40,11 +40,13 @@ enum : uint32_t {
 };
 
 struct SvcBox {
+    // one 16-byte read per poll brings a new req_seq with its job's words (the
+    // host writes them first; a read of one line returns them as of one moment)
     uint32_t req_seq;    // host: the last job posted (served when it differs from the last one seen)
+    uint32_t n, arena_len, flags;  // host: the job
     uint32_t stop;       // host: exit at the next poll (a throughput launch wants every CU; an update)
     uint32_t state;      // kernel: kSvcRunning / kSvcExiting / kSvcStopped
     uint32_t done;       // kernel: req_seq of the last job answered (after its answers)
-    uint32_t n, arena_len, flags;  // host: the job (written before req_seq)
     uint32_t pad[9];
 };
 static_assert(sizeof(SvcBox) == 64, "one line");

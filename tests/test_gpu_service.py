@@ -55,8 +55,10 @@ def test_service_calls_match_the_launched_path_and_the_oracle(engine, oracle):
     _, s0 = engine.service()
     _check(engine, ref, w, http + mc)
     _, s1 = engine.service()
-    assert s1["http_calls"] - s0["http_calls"] == len(http)
-    assert s1["mc_calls"] - s0["mc_calls"] == len(mc)
+    # (a call whose one request is on an unknown connection uses no parser: launched)
+    served = lambda calls: sum(1 for _, c in calls if (c < len(w.conns)).any())  # noqa: E731
+    assert s1["http_calls"] - s0["http_calls"] == served(http)
+    assert s1["mc_calls"] - s0["mc_calls"] == served(mc)
     assert s1["http_launches"] - s0["http_launches"] <= 2 and s1["mc_launches"] - s0["mc_launches"] <= 2
     # the launched path on the same calls
     engine.service(False)

@@ -1,5 +1,5 @@
 """HBM traffic per l7g_classify call from rocprofv3 FETCH_SIZE / WRITE_SIZE
-passes (separate runs, tools/run_traffic.sh) -> profiles/traffic_<workload>.json,
+passes (separate runs, tools/run_r6_pmc.sh) -> profiles/traffic_<workload>.json,
 which bench.py reports as roofline.traffic for the dominant kernel.
 
 Per kernel name (template instantiations apart) the counters are averaged
@@ -55,8 +55,11 @@ def main():
                           "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
                           "hbm_bytes_per_launch": rd + wr}
     out = {"workload": wl, "note": note,
-           "source": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE, separate passes (tools/run_traffic.sh)",
-           "correction": "gfx950 FETCH_SIZE x2 (16-byte-per-lane reads), WRITE_SIZE as reported; KiB -> bytes",
+           "source": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE, separate passes (tools/run_r6_pmc.sh)",
+           "correction": ("gfx950 FETCH_SIZE x2: one TCC_EA0_RDREQ per 128-byte line read, counted as 64 B -- "
+                          "calibrated for these kernels' access shapes on known reads of cfg5's requests "
+                          "(wave-coalesced, one lane per request in 16- and 64-byte steps: "
+                          "profiles/r6/kafka_traffic_calibration_pmc.txt); WRITE_SIZE as reported; KiB -> bytes"),
            "kernels": kernels}
     if len(kernels) == 1:
         out["hbm_bytes_per_launch"] = next(iter(kernels.values()))["hbm_bytes_per_launch"]
