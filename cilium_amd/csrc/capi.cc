@@ -1342,9 +1342,9 @@ static bool ServiceTry(l7g_engine *e, uint32_t n, uint64_t arena_len, const Host
 // classify a call whose inputs are in pinned host memory, wait for it, copy
 // the answers out
 static hipError_t HostRun(l7g_engine *e, HostCtx *H, uint32_t n, uint64_t arena_len, const HostIn &in,
-                          uint8_t *verdict, int32_t *rule, uint32_t *consumed) {
+                          uint8_t *verdict, int32_t *rule, uint32_t *consumed, bool try_service = true) {
     hipError_t rc = hipSuccess;
-    if (ServiceTry(e, n, arena_len, in, verdict, rule, consumed, &rc)) return rc;
+    if (try_service && ServiceTry(e, n, arena_len, in, verdict, rule, consumed, &rc)) return rc;
     const size_t nn = std::max<uint32_t>(n, 1);
     const size_t a_off = HostArenaOff(n);
     // A small call (the Envoy adapter's Allowed(), one OnData, a light batch)
@@ -1493,7 +1493,8 @@ int l7g_host_stage(l7g_engine *e, uint32_t n, uint64_t arena_len, uint8_t **aren
     return 0;
 }
 
-int l7g_host_run(l7g_engine *e, uint32_t n, uint64_t arena_len, uint8_t *verdict, int32_t *rule, uint32_t *consumed) {
+static int HostRunStaged(l7g_engine *e, uint32_t n, uint64_t arena_len, uint8_t *verdict, int32_t *rule,
+                         uint32_t *consumed, bool try_service) {
     if (e->device < 0) return (int)hipErrorNoDevice;
     hipError_t rc = hipSetDevice(e->device);
     HostCtx *H = nullptr;
@@ -1503,11 +1504,14 @@ int l7g_host_run(l7g_engine *e, uint32_t n, uint64_t arena_len, uint8_t *verdict
         const l7g_host_seg seg{H->pin_in + HostArenaOff(n), arena_len, arena_len, 1};
         const HostIn in{(const uint64_t *)H->pin_in, (const uint32_t *)(H->pin_in + nn * 8),
                         (const uint32_t *)(H->pin_in + nn * 12), nn, &seg, 1};
-        rc = HostRun(e, H, n, arena_len, in, verdict, rule, consumed);
+        rc = HostRun(e, H, n, arena_len, in, verdict, rule, consumed, try_service);
     }
     return (int)rc;
 }
 
+int l7g_host_run(l7g_engine *e, uint32_t n, uint64_t arena_len, uint8_t *verdict, int32_t *rule, uint32_t *consumed) {
+    return HostRunStaged(e, n, arena_len, verdict, rule, consumed, true);
+}
 int l7g_host_run_pinned(l7g_engine *e, uint32_t n, const uint64_t *off, size_t stride, const l7g_host_seg *seg,
                         int nseg, uint8_t *verdict, int32_t *rule, uint32_t *consumed) {
     if (e->device < 0) return (int)hipErrorNoDevice;
@@ -1568,6 +1572,12 @@ extern "C" {
 
 int l7g_classify_host(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, const uint64_t *off, const uint32_t *len,
                       const uint32_t *conn, uint32_t n, uint8_t *verdict, int32_t *rule, uint32_t *consumed) {
+    {  // a call a service takes goes from the caller's buffers straight into the service's staging
+        const l7g_host_seg seg{arena, arena_len, arena_len, 1};
+        const HostIn in{off, len, conn, 0, &seg, 1};
+        hipError_t rc = hipSuccess;
+        if (e->device >= 0 && ServiceTry(e, n, arena_len, in, verdict, rule, consumed, &rc)) return (int)rc;
+    }
     uint8_t *pa;
     uint64_t *po;
     uint32_t *pl, *pc;
@@ -1579,7 +1589,7 @@ int l7g_classify_host(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, c
         memcpy(pc, conn, (size_t)n * 4);
     }
     if (arena_len) memcpy(pa, arena, arena_len);
-    return l7g_host_run(e, n, arena_len, verdict, rule, consumed);
+    return HostRunStaged(e, n, arena_len, verdict, rule, consumed, false);
 }
 
 int l7g_stats(l7g_engine *e, l7g_stats_t *out) {
