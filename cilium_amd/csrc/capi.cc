@@ -36,7 +36,7 @@ hipError_t LaunchHttpClassify(const Batch &B, const HttpTables &T, const uint32_
                               hipStream_t stream);
 hipError_t LaunchKafkaClassify(const Batch &B, const KafkaTables &T, const uint32_t *sel, const uint32_t *sel_count,
                                bool answer_other, uint32_t *zlist, uint32_t *zcount, uint32_t *work,
-                               hipStream_t stream);
+                               hipStream_t stream, int leave_per_cu = 0);
 hipError_t LaunchKafkaInflate(const Batch &B, const uint32_t *zlist, const uint32_t *zcount, uint8_t *region,
                               hipStream_t stream);
 uint32_t KafkaInflateBlocks();
@@ -109,7 +109,14 @@ struct StreamScratch {
     hipEvent_t done_ev = nullptr;
     bool launched = false;
     uint64_t last_use = 0;
+    // the memcached kernel beside the Kafka kernel (large mixed batches)
+    hipStream_t side = nullptr;
+    hipEvent_t fork_ev = nullptr, join_ev = nullptr;
     ~StreamScratch() {
+        if (side) hipStreamSynchronize(side);
+        if (fork_ev) hipEventDestroy(fork_ev);
+        if (join_ev) hipEventDestroy(join_ev);
+        if (side) hipStreamDestroy(side);
         if (d_bignfa) hipFree(d_bignfa);
         if (d_grp) hipFree(d_grp);
         if (d_sel) hipFree(d_sel);
@@ -127,6 +134,7 @@ constexpr uint32_t kZeroCopyMaxRequests = 256;
 constexpr size_t kZeroCopyMaxBytes = 256 * 1024;
 // batches below this size skip the protocol split when one classifier can walk them alone
 constexpr uint32_t kPartitionMin = 4096;
+constexpr uint32_t kBesideMin = 1u << 20;  // memcached kernel beside Kafka from this batch size
 constexpr uint32_t kHostScanMax = 4096;
 // at most this many requests: the HTTP requests are framed one per wave, their
 // lines side by side (http_latency_kernel), not one per lane
@@ -175,6 +183,7 @@ struct Service {
     std::mutex mu;  // one call at a time, held from its posting to its answers
     hipStream_t s = nullptr;
     SvcBox *box = nullptr, *box_dev = nullptr;  // pinned, coherent
+    SvcBox *box_ready = nullptr;  // box, published once the service is allocated (read without mu)
     uint8_t *pin_in = nullptr, *pin_in_dev = nullptr, *pin_out = nullptr, *pin_out_dev = nullptr;
     uint8_t *dev_in = nullptr;
     uint32_t seq = 0;
@@ -273,9 +282,10 @@ static void StopServices(l7g_engine *e) {
 // A launch that wants every CU (a persistent grid) asks the services to leave
 // without waiting; the next synchronous call starts them again.
 static void ReleaseServiceCUs(l7g_engine *e) {
-    for (Service &v : e->svc)
-        if (v.box && __atomic_load_n(&v.box->state, __ATOMIC_ACQUIRE) != kSvcStopped)
-            __atomic_store_n(&v.box->stop, 1u, __ATOMIC_SEQ_CST);
+    for (Service &v : e->svc) {
+        SvcBox *b = __atomic_load_n(&v.box_ready, __ATOMIC_ACQUIRE);  // (set once; v.mu not taken here)
+        if (b && __atomic_load_n(&b->state, __ATOMIC_ACQUIRE) != kSvcStopped) __atomic_store_n(&b->stop, 1u, __ATOMIC_SEQ_CST);
+    }
 }
 
 // Waits for the kernels of every stream's last call, and stops the services
@@ -1014,9 +1024,27 @@ static int Classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, con
                                 tile_ctr, n <= kLatencyMax, fuse_http, s);
     }
     mark(2);
+    // a large partitioned batch with both Kafka and memcached requests: the
+    // memcached kernel runs on a side stream beside the Kafka kernel, which leaves
+    // one workgroup slot per CU for it (cfg5: 37.31 -> 36.44 ms per step,
+    // profiles/r6/ab6h_kafka_memcached_beside.txt)
+    const bool km = partitioned && run[2] && run[3] && !prof && big_lanes == 0 && n >= kBesideMin && !pre;
+    const int kafka_leave = km ? 1 : 0;
+    hipStream_t ms = s;
+    if (km && rc == hipSuccess) {
+        if (!S->side) {
+            rc = hipStreamCreateWithFlags(&S->side, hipStreamNonBlocking);
+            if (rc == hipSuccess) rc = hipEventCreateWithFlags(&S->fork_ev, hipEventDisableTiming);
+            if (rc == hipSuccess) rc = hipEventCreateWithFlags(&S->join_ev, hipEventDisableTiming);
+        }
+        if (rc == hipSuccess) rc = hipEventRecord(S->fork_ev, s);
+        if (rc == hipSuccess) rc = hipStreamWaitEvent(S->side, S->fork_ev, 0);
+        if (rc == hipSuccess) ms = S->side;
+    }
     uint32_t *zcount = cnt ? cnt + 31 : nullptr;
     if (rc == hipSuccess && run[2])
-        rc = LaunchKafkaClassify(B, e->kt, sel_k, cnt, !partitioned, sel_z, zcount, cnt ? cnt + 26 : nullptr, s);
+        rc = LaunchKafkaClassify(B, e->kt, sel_k, cnt, !partitioned, sel_z, zcount, cnt ? cnt + 26 : nullptr, s,
+                                 kafka_leave);
     // requests with gzip / snappy messages: decoded, their sets read, failures answered
     if (rc == hipSuccess && run[2] && sel_z) {
         // the engine's one decode region: after the previous inflate launch on any stream
@@ -1028,7 +1056,11 @@ static int Classify(l7g_engine *e, const uint8_t *arena, uint64_t arena_len, con
     mark(3);
     if (rc == hipSuccess && run[3])
         rc = LaunchMemcacheClassify(B, mt, sel_m, sel_h, cnt ? cnt + L7_KAFKA_CLASSES : nullptr, !partitioned, big_lanes,
-                                    s, fuse_mc);
+                                    ms, fuse_mc);
+    if (ms != s && rc == hipSuccess) {
+        rc = hipEventRecord(S->join_ev, ms);
+        if (rc == hipSuccess) rc = hipStreamWaitEvent(s, S->join_ev, 0);
+    }
     // r2d2 (proxylib's example line protocol): one lane per request over the whole batch
     if (rc == hipSuccess && run_r2) rc = LaunchR2d2Classify(B, rt, !partitioned, big_lanes, s);
     // cassandra (proxylib): the batch's USE requests, then one lane per request
@@ -1197,7 +1229,9 @@ static hipError_t ServiceAlloc(Service &v) {
         (rc = hipHostGetDevicePointer((void **)&v.pin_out_dev, v.pin_out, 0)) != hipSuccess ||
         (rc = hipMalloc((void **)&v.dev_in, kSvcInBytes)) != hipSuccess)
         return rc;
-    return hipStreamCreateWithFlags(&v.s, hipStreamNonBlocking);  // (last: v.s marks a complete allocation)
+    if ((rc = hipStreamCreateWithFlags(&v.s, hipStreamNonBlocking)) != hipSuccess) return rc;  // (v.s: allocated)
+    __atomic_store_n(&v.box_ready, v.box, __ATOMIC_RELEASE);
+    return hipSuccess;
 }
 
 // Posts a call to service v (e->mu and v.mu held; the inputs are in

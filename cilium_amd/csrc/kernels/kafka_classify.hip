@@ -625,25 +625,31 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
 
 hipError_t KafkaPhaseTimes(uint64_t *, bool) { return hipErrorNotSupported; }
 
+// leave_per_cu > 0 (persistent grid only): that many workgroup slots per CU left
+// free for a kernel running beside this one on another stream
 hipError_t LaunchKafkaClassify(const Batch &B, const KafkaTables &T, const uint32_t *sel, const uint32_t *sel_count,
                                bool answer_other, uint32_t *zlist, uint32_t *zcount, uint32_t *work,
-                               hipStream_t stream) {
+                               hipStream_t stream, int leave_per_cu) {
     if (B.n == 0) return hipSuccess;
     uint32_t blocks = (B.n + kBlock - 1) / kBlock;
     // persistent grid: as many workgroups as the CUs hold at once
-    static int resident = 0;
-    if (resident == 0) {
-        int dev = 0, cus = 0, per_cu = 0;
+    static int cus = 0, per_cu = 0;
+    if (cus == 0) {
+        int dev = 0, c = 0, p = 0;
         if (hipGetDevice(&dev) == hipSuccess &&
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kafka_classify_kernel, kBlock, 0) == hipSuccess &&
-            cus > 0 && per_cu > 0)
-            resident = cus * per_cu;
-        else
-            resident = 8192;
+            hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&p, kafka_classify_kernel, kBlock, 0) == hipSuccess && c > 0 &&
+            p > 0) {
+            per_cu = p;
+            cus = c;
+        } else {
+            per_cu = 32;
+            cus = 256;
+        }
     }
+    const int slots = leave_per_cu > 0 && per_cu > leave_per_cu ? per_cu - leave_per_cu : per_cu;
     if (!work) blocks = blocks > 8192 ? 8192 : blocks;  // grid-stride beyond this
-    else if (blocks > (uint32_t)resident) blocks = (uint32_t)resident;
+    else if (blocks > (uint32_t)(cus * slots)) blocks = (uint32_t)(cus * slots);
     hipLaunchKernelGGL(kafka_classify_kernel, dim3(blocks), dim3(kBlock), 0, stream, B, T, sel, sel_count,
                        answer_other ? 1u : 0u, zlist, zcount, work);
     return hipGetLastError();

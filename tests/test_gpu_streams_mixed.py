@@ -2,9 +2,9 @@
 lists and work counters in use) on two caller streams, four calls in flight:
 every verdict, rule id and consumed length, and the per-rule counters, equal
 the oracle's -- calls in a row on one stream, and calls on two streams, do not
-see each other's lists or counters.  (Round 6 also ran the Kafka and memcached
-kernels of such a batch on a second stream beside the HTTP kernel: cfg5 37.45
-vs 37.44 ms one after the other, not kept; profiles/r6/ab6b_*.)"""
+see each other's lists or counters.  At this size the memcached kernel runs on
+the scratch set's side stream beside the Kafka kernel (capi.cc kBesideMin), so
+the test also covers that fork / join with two caller streams in flight."""
 import numpy as np
 import pytest
 import torch
