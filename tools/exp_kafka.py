@@ -31,6 +31,23 @@ def main():
             want = {"cfg3produce": kinds == 0, "cfg3fetch": kinds == 1, "cfg3other": kinds > 1}[wl]
             w = gen.select(w, np.nonzero(want)[0], wl)
             n = w.n
+    elif wl in ("produni", "prodcnt"):  # produce requests of one fixed structure (divergence probe)
+        rng = np.random.default_rng(7)
+        topics = gen.kafka_topics()
+        reqs = []
+        for i in range(n):
+            tps = []
+            for t in range(2):
+                k = 2 if t == 0 else 3
+                ln = [288] * k if wl == "produni" else [int(rng.integers(64, 513)) for _ in range(k)]
+                msgs = [gen.k_message(rng.integers(0, 256, size=L, dtype=np.uint8).tobytes(),
+                                      key=None if i % 2 else b"k%d" % i, version=i % 3) for L in ln]
+                tps.append((topics[int(rng.integers(0, 1000))], [(0, msgs)]))
+            reqs.append(gen.k_produce(i % 3, i, "client-%02d" % (i % 16), tps))
+        arena, offs, lens = gen.pack(reqs)
+        conn_ids = rng.integers(0, 256, size=n).astype(np.uint32)
+        conns = gen.make_conns(256, 0, 9092, True, gen.PROTO_KAFKA, 2000 + np.arange(256))
+        w = gen.Workload(wl, arena, offs, lens, conn_ids, conns, gen.cfg3_policy())
     elif wl == "mc":  # memcached alone (cfg5's memcached stream)
         w = gen.memcache_workload(n)
     else:
