@@ -1541,6 +1541,282 @@ __device__ __forceinline__ void lat_request(const Lane &L, const uint8_t *img, u
     LAT_T(11);
 }
 
+// ---------------------------------------------------------------- latency path: well-formed heads
+// lat_request runs the general framer on each lane's line, and on one wave its
+// instruction path -- every mode of the resumable state machine, per byte --
+// is what a synchronous call waits for (cfg2's 1.1 KB request: ~38k cycles of
+// parse_window for six lines).  Most requests a proxy sees are well formed,
+// and for those the framer's outcome has a short closed form, computed here
+// with the bytes in LDS, the token boundaries from wave-wide masks, one lane
+// per header line and one lane per DFA walk:
+//
+//   the header block [a0, H) ends at the first empty line; in it, no byte is a
+//   CTL other than HT / CR / LF or DEL, every CR is followed by LF and every
+//   LF follows a CR; line 0 is  method SP target SP "HTTP/" DIGIT "." DIGIT
+//   with a method of 1..16 tchars and a target of >= 1 bytes (no SP: the
+//   second SP ends it); every other line is  name ":" value  with a name of
+//   1..15 [0-9A-Za-z-] (the image's name table: fast_line's lookup) and no
+//   Content-Length or Transfer-Encoding header (their framing stays with the
+//   framer); the rule set needs one framing pass (one DFA per slot, at most
+//   kChunksPerPass chunks, no NFA matchers); at most 62 header lines.
+//
+// Under those conditions the framer walks the method and the target through
+// their slot DFAs (the target until its state is absorbing), gives each
+// header line its name's slot at the slot's first occurrence when a rule
+// looks at it, walks that value from its first non-OWS byte through the
+// slot's DFA with the trailing OWS excluded (until absorbing outside OWS),
+// ANDs the end states' masks and the absent slots' masks into the init masks,
+// and answers the first rule left (else the terminal verdict) with consumed =
+// H - a0 (no Content-Length) -- which is what this computes.  Anything else,
+// or a request longer than 4 KiB, returns false and goes to lat_request
+// (envoy/cilium_l7policy.cc:127-182, envoy/cilium_network_policy.h:128-192).
+constexpr uint32_t kFastMaxChunks = 256;  // 4 KiB of request bytes in the wave's LDS area
+constexpr uint32_t kFastOffCr = kFastMaxChunks * 16, kFastOffLf = kFastOffCr + 2 * kFastMaxChunks;
+constexpr uint32_t kFastOffBad = kFastOffLf + 2 * kFastMaxChunks, kFastOffPos = kFastOffBad + 2 * kFastMaxChunks;
+static_assert(kFastOffPos + 4 * 64 <= kWaveLds, "fast path LDS layout");
+
+// bit i (0..15) set iff byte i of the chunk is b
+__device__ __forceinline__ uint32_t byte_mask(uint4 w, uint32_t b) {
+    const uint32_t bb = b * 0x01010101u;
+    auto eq = [bb](uint32_t x) {
+        const uint32_t t = x ^ bb;
+        return ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;
+    };
+    return nib(eq(w.x)) | nib(eq(w.y)) << 4 | nib(eq(w.z)) << 8 | nib(eq(w.w)) << 12;
+}
+// bytes the fast path refuses anywhere in a header block: < 0x20 other than
+// HT / CR / LF, or DEL
+__device__ __forceinline__ uint32_t fast_bad_mask(uint4 w) {
+    return stop_mask(w) & ~(byte_mask(w, '\t') | byte_mask(w, '\r') | byte_mask(w, '\n'));
+}
+
+template <bool kLds>
+__device__ __forceinline__ bool lat_fast(const Lane &L, const uint8_t *img, uint8_t *wave_lds, uint32_t lane,
+                                         const Out &O) {
+    const Img<kLds> I{img};
+    const uint32_t a0 = L.a0, lena = L.lena;
+    const uint32_t nch = (lena + 15) >> 4;
+    // the rule set: one framing pass, no NFA matchers, a name table
+    const uint32_t nchunks = HDR_U8(I, nchunks);
+    if (lena <= a0 || nch > kFastMaxChunks || HDR_U8(I, nnfa) != 0 || HDR_U8(I, max_slot_dfas) > 1 ||
+        nchunks > (uint32_t)kChunksPerPass || HDR_U8(I, ntab_bits) == 0)
+        return false;
+    uint16_t *crm = reinterpret_cast<uint16_t *>(wave_lds + kFastOffCr);
+    uint16_t *lfm = reinterpret_cast<uint16_t *>(wave_lds + kFastOffLf);
+    uint16_t *badm = reinterpret_cast<uint16_t *>(wave_lds + kFastOffBad);
+    uint32_t *crpos = reinterpret_cast<uint32_t *>(wave_lds + kFastOffPos);
+    const uint64_t below = (1ull << lane) - 1;
+    // ---- the request into LDS, its CR / LF / refused-byte masks, the first 64 CRs in order
+    uint32_t ncr = 0;
+    for (uint32_t c0 = 0; c0 < nch; c0 += 64) {
+        const uint32_t c = c0 + lane;
+        uint32_t m = 0;
+        if (c < nch) {
+            const uint4 w = gload16(L.base + 16ull * c);
+            *reinterpret_cast<uint4 *>(wave_lds + 16 * c) = w;
+            const uint32_t p0 = 16 * c;
+            uint32_t in = 0xFFFFu;  // bytes of [a0, lena)
+            if (p0 < a0) in &= 0xFFFFu << (a0 - p0);
+            if (p0 + 16 > lena) in &= (1u << (lena - p0)) - 1u;
+            m = byte_mask(w, '\r') & in;
+            crm[c] = (uint16_t)m;
+            lfm[c] = (uint16_t)(byte_mask(w, '\n') & in);
+            badm[c] = (uint16_t)(fast_bad_mask(w) & in);
+        }
+        const uint32_t cnt = (uint32_t)__builtin_popcount(m);
+        uint32_t ex = 0;
+#pragma unroll
+        for (int b = 0; b < 5; b++) ex += (uint32_t)__popcll(__ballot((cnt >> b) & 1) & below) << b;
+        for (uint32_t r = ncr + ex; m; m &= m - 1, r++)
+            if (r < 64) crpos[r] = 16 * c + (uint32_t)__builtin_ctz(m);
+        ncr += (uint32_t)__builtin_amdgcn_readfirstlane((int)__ockl_wfred_add_u32(cnt));
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // the empty line: the first CR two bytes after the one before it
+    const uint32_t have = min(ncr, 64u);
+    const uint32_t mycr = lane < have ? crpos[lane] : 0u;
+    const uint32_t prevcr = lane >= 1 && lane < have ? crpos[lane - 1] : 0u;
+    const uint64_t eb = __ballot(lane >= 1 && lane < have && mycr == prevcr + 2);
+    if (!eb) return false;
+    const uint32_t hend = (uint32_t)__builtin_ctzll(eb);  // lines 0 .. hend-1, then the empty line
+    if (hend > 62) return false;
+    const uint32_t H = (uint32_t)__shfl((int)mycr, (int)hend) + 2;  // end of the header block
+    if (H > lena) return false;
+    // ---- the block's bytes: nothing refused, CR and LF only as CRLF
+    bool bad = false;
+    for (uint32_t c = lane; 16 * c < H; c += 64) {
+        const uint32_t p0 = 16 * c;
+        uint32_t in = 0xFFFFu;
+        if (p0 < a0) in &= 0xFFFFu << (a0 - p0);
+        if (p0 + 16 > H) in &= (1u << (H - p0)) - 1u;
+        const uint32_t cr = crm[c], prev = c ? (uint32_t)crm[c - 1] >> 15 : 0u;
+        bad |= (badm[c] & in) != 0 || (lfm[c] & in) != (((cr << 1) | prev) & in);
+    }
+    if (__ballot(bad)) return false;
+    // ---- lane k: line k = [s, e), e its CR
+    const uint32_t s = lane == 0 ? a0 : prevcr + 2, e = mycr;
+    const bool line = lane < hend;
+    auto chunk = [&](uint32_t k) { return *reinterpret_cast<const uint4 *>(wave_lds + 16 * k); };
+    // the 16 bytes at p (p + 16 may pass the copy's end only inside its last chunk's area)
+    auto bytes16 = [&](uint32_t p) {
+        const uint32_t k0 = p >> 4, o = p & 15, i = o >> 2, sh = (o & 3) * 8;
+        const uint4 a = chunk(k0), b = k0 + 1 < kFastMaxChunks ? chunk(k0 + 1) : make_uint4(0, 0, 0, 0);
+        const uint32_t d0 = i == 0 ? a.x : i == 1 ? a.y : i == 2 ? a.z : a.w;
+        const uint32_t d1 = i == 0 ? a.y : i == 1 ? a.z : i == 2 ? a.w : b.x;
+        const uint32_t d2 = i == 0 ? a.z : i == 1 ? a.w : i == 2 ? b.x : b.y;
+        const uint32_t d3 = i == 0 ? a.w : i == 1 ? b.x : i == 2 ? b.y : b.z;
+        const uint32_t d4 = i == 0 ? b.x : i == 1 ? b.y : i == 2 ? b.z : b.w;
+        uint4 f;
+        f.x = (uint32_t)((((uint64_t)d1 << 32) | d0) >> sh);
+        f.y = (uint32_t)((((uint64_t)d2 << 32) | d1) >> sh);
+        f.z = (uint32_t)((((uint64_t)d3 << 32) | d2) >> sh);
+        f.w = (uint32_t)((((uint64_t)d4 << 32) | d3) >> sh);
+        return f;
+    };
+    auto byte_at = [&](uint32_t p) { return (uint32_t)wave_lds[p]; };
+    bool refuse = false;
+    // request line (lane 0): the two SPs, the method's tchars, the version
+    uint32_t sp1 = 0, sp2 = 0;
+    if (lane == 0) {
+        uint32_t nsp = 0;
+        for (uint32_t p = s & ~15u; p < e && nsp < 2; p += 16) {
+            uint32_t m = byte_mask(chunk(p >> 4), ' ');
+            if (p < s) m &= 0xFFFFu << (s - p);
+            if (p + 16 > e) m &= (1u << (e - p)) - 1u;
+            while (m && nsp < 2) {
+                const uint32_t q = p + (uint32_t)__builtin_ctz(m);
+                m &= m - 1;
+                if (nsp == 0) sp1 = q; else sp2 = q;
+                nsp++;
+            }
+        }
+        refuse = nsp < 2 || sp1 == s || sp1 - s > 16 || sp2 == sp1 + 1 || e - sp2 != 9;
+        for (uint32_t p = s & ~15u; p < e && !refuse; p += 16) {  // HT ends a target (then not SP: an error)
+            uint32_t m = byte_mask(chunk(p >> 4), '\t');
+            if (p < s) m &= 0xFFFFu << (s - p);
+            if (p + 16 > e) m &= (1u << (e - p)) - 1u;
+            refuse = m != 0;
+        }
+        if (!refuse) {
+            for (uint32_t p = s; p < sp1; p++) refuse |= !is_tchar(byte_at(p));
+            const uint4 v = bytes16(sp2 + 1);
+            refuse |= !(v.x == 0x50545448u && (v.y & 0x00FF00FFu) == 0x002E002Fu && ((v.y >> 8) & 0xFF) - '0' < 10u &&
+                        (v.y >> 24) - '0' < 10u);
+        }
+    }
+    // header lines (lanes 1 .. hend-1): the name's flags from the name table
+    uint32_t ninfo = 0, vs = 0;
+    if (line && lane > 0) {
+        const uint4 f = bytes16(s);
+        const uint32_t en = (uint32_t)__builtin_ctz(nonalnum_mask(f) | 0x10000u);
+        if (en == 0 || en == 16 || s + en >= e || byte_of(f, en) != ':') {
+            refuse = true;
+        } else {
+            auto keep = [en](uint32_t j) { return en >= 4 * j + 4 ? 0xFFFFFFFFu : en <= 4 * j ? 0u : (1u << (8 * (en - 4 * j))) - 1u; };
+            const uint32_t w0 = (f.x | 0x20202020u) & keep(0), w1 = (f.y | 0x20202020u) & keep(1);
+            const uint32_t w2 = (f.z | 0x20202020u) & keep(2), w3 = (f.w | 0x20202020u) & keep(3);
+            const uint32_t h = l7_name_hash(w0, w1, w2, w3, en, HDR_U32(I, ntab_mul), HDR_U8(I, ntab_bits));
+            const uint32_t ent = HDR_U32(I, ntab_off) + h * (uint32_t)sizeof(DevNameEnt);
+            const uint4 n = I.u128(ent);
+            const uint32_t meta = I.u32(ent + 16);
+            const bool hit = (meta & 0xFF) == en && n.x == w0 && n.y == w1 && n.z == w2 && n.w == w3;
+            ninfo = hit ? (meta >> 8) & 0xFF : 0u;
+            if (ninfo & (NI_CL | NI_TE)) refuse = true;  // body framing: the framer's
+            vs = s + en + 1;
+            while (vs < e && (byte_at(vs) == ' ' || byte_at(vs) == '\t')) vs++;  // OWS (M_OWS)
+        }
+    }
+    if (__ballot(refuse)) return false;
+    // slots: a header's at its first occurrence when some rule looks at it
+    const uint32_t ref = HDR_U32(I, ref_slots);
+    uint32_t slot = kNoSlot;
+    if (line && lane > 0) {
+        if (ninfo & NI_HOST) slot = SLOT_AUTHORITY;
+        else if (ninfo & NI_CUSTOM) slot = SLOT_CUSTOM0 + (ninfo & NI_CUSTOM) - 1;
+        if (slot != kNoSlot && !((ref >> slot) & 1)) slot = kNoSlot;
+    }
+#pragma unroll
+    for (uint32_t sl = SLOT_AUTHORITY; sl < (uint32_t)kNumSlots; sl++) {
+        const uint64_t mk = __ballot(slot == sl);
+        if (slot == sl && lane != (uint32_t)__builtin_ctzll(mk)) slot = kNoSlot;
+    }
+    // ---- the DFA walks: lane 0 the target, lane 63 the method, lane k its value
+    sp1 = (uint32_t)__shfl((int)sp1, 0);
+    sp2 = (uint32_t)__shfl((int)sp2, 0);
+    uint32_t wslot = slot, from = vs, to = e, kind = 2;  // kind: 0 method, 1 target, 2 value
+    if (lane == 0) { wslot = SLOT_PATH; from = sp1 + 1; to = sp2; kind = 1; }
+    if (lane == 63) { wslot = SLOT_METHOD; from = a0; to = sp1; kind = 0; }
+    uint64_t acc[kChunksPerPass];
+#pragma unroll
+    for (int c = 0; c < kChunksPerPass; c++) acc[c] = ~0ull;
+    const uint32_t nc = min(nchunks, (uint32_t)kChunksPerPass);
+    if (wslot != kNoSlot) {
+        const uint32_t lo = I.u8(offsetof(ImgHeader, slot_dfa) + wslot);
+        const uint32_t hi = I.u8(offsetof(ImgHeader, slot_dfa) + wslot + 1);
+        if (lo < hi) {
+            const uint32_t d = HDR_U32(I, dfa_off) + lo * sizeof(DevDfa);
+            const uint32_t dcls = I.u32(d + 0), dtrans = I.u32(d + 4), dmask = I.u32(d + 8);
+            const uint32_t nc_st = I.u32(d + 12), dncls = nc_st & 0xFFFF, dabs = I.u32(d + 16);
+            uint32_t st = nc_st >> 16, saved = 0;
+            bool in_ows = false;
+            uint32_t p = from;
+            // the framer's walks (parse_window M_METHOD / M_TARGET / M_VALUE): the
+            // byte after p and its class read while the transition on p is in flight
+            uint32_t c = p < to ? byte_at(p) : 0u;
+            uint32_t k = p < to ? I.u8(dcls + c) : 0u;
+            while (p < to && (kind == 0 || in_ows || (st != 0 && st < dabs))) {
+                const uint32_t c1 = p + 1 < to ? byte_at(p + 1) : 0u;
+                const uint32_t k1 = p + 1 < to ? I.u8(dcls + c1) : 0u;
+                if (kind == 2) {
+                    const bool ws = c == ' ' || c == '\t';
+                    if (ws && !in_ows) saved = st;
+                    in_ows = ws;
+                }
+                if (st) st = I.u16(dtrans + 2 * (st * dncls + k));
+                p++;
+                c = c1;
+                k = k1;
+            }
+            if (kind == 2 && p >= to && in_ows) st = saved;  // trailing OWS is not part of the value
+            const uint32_t base = dmask + 8 * (st * nchunks);
+#pragma unroll
+            for (int cc = 0; cc < kChunksPerPass; cc++)
+                if ((uint32_t)cc < nc) acc[cc] = I.u64(base + 8 * cc);
+        }
+    }
+    // ---- merge (headers_done on one pass)
+    const uint32_t present = __ockl_wfred_or_u32(lane > 0 && lane < 63 && slot != kNoSlot ? 1u << slot : 0u) |
+                             (1u << SLOT_METHOD) | (1u << SLOT_PATH);
+    uint64_t a[kChunksPerPass];
+#pragma unroll
+    for (int c = 0; c < kChunksPerPass; c++) a[c] = __ockl_wfred_and_u64(acc[c]);
+    if (lane == 0) {
+#pragma unroll
+        for (int c = 0; c < kChunksPerPass; c++)
+            a[c] &= (uint32_t)c < nchunks ? I.u64(HDR_U32(I, init_off) + 8 * c) : 0ull;
+        uint32_t missing = ref & 0xFFFF & ~present;
+        while (missing) {
+            const uint32_t sl = __builtin_ctz(missing);
+            missing &= missing - 1;
+#pragma unroll
+            for (int c = 0; c < kChunksPerPass; c++)
+                if ((uint32_t)c < nc) a[c] &= I.u64(HDR_U32(I, absent_off) + 8 * (sl * nchunks + c));
+        }
+        int32_t hit = -1;
+#pragma unroll
+        for (int c = kChunksPerPass - 1; c >= 0; c--)
+            if ((uint32_t)c < nc && a[c]) hit = (int32_t)(64 * c + (uint32_t)__builtin_ctzll(a[c]));
+        Lane W = L;
+        W.consumed = H - a0;
+        if (hit >= 0) finish(W, V_ALLOW, (int32_t)I.u32(HDR_U32(I, rule_off) + 4 * (uint32_t)hit));
+        else finish(W, (uint8_t)HDR_U8(I, terminal), -1);
+        emit(W, O);
+    }
+    return true;
+}
+
 }  // namespace
 
 // kHot = true : requests whose connection uses the hot rule set (image in LDS),
@@ -1739,8 +2015,11 @@ __device__ __forceinline__ void lat_body(const Batch &B, const HttpTables &T, co
         }
         LAT_T(8);
         LAT_N(12);
-        if (!L.done) lat_request<kHot>(L, img, wave_lds, lane, O);
-        else if (L.owed && lane == 0) emit(L, O);
+        if (!L.done) {
+            if (!lat_fast<kHot>(L, img, wave_lds, lane, O)) lat_request<kHot>(L, img, wave_lds, lane, O);
+        } else if (L.owed && lane == 0) {
+            emit(L, O);
+        }
     }
     __syncthreads();
 }
