@@ -1594,6 +1594,7 @@ template <bool kLds>
 __device__ __forceinline__ bool lat_fast(const Lane &L, const uint8_t *img, uint8_t *wave_lds, uint32_t lane,
                                          const Out &O) {
     const Img<kLds> I{img};
+    LAT_T0
     const uint32_t a0 = L.a0, lena = L.lena;
     const uint32_t nch = (lena + 15) >> 4;
     // the rule set: one framing pass, no NFA matchers, a name table
@@ -1634,6 +1635,7 @@ __device__ __forceinline__ bool lat_fast(const Lane &L, const uint8_t *img, uint
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    LAT_T(13);
     // the empty line: the first CR two bytes after the one before it
     const uint32_t have = min(ncr, 64u);
     const uint32_t mycr = lane < have ? crpos[lane] : 0u;
@@ -1677,34 +1679,31 @@ __device__ __forceinline__ bool lat_fast(const Lane &L, const uint8_t *img, uint
     };
     auto byte_at = [&](uint32_t p) { return (uint32_t)wave_lds[p]; };
     bool refuse = false;
-    // request line (lane 0): the two SPs, the method's tchars, the version
+    // request line (lane 0): exactly two SPs and no HT (HT ends a target, and
+    // not SP after it is an error), a method of 1..15 [0-9A-Za-z-], the version
     uint32_t sp1 = 0, sp2 = 0;
     if (lane == 0) {
         uint32_t nsp = 0;
-        for (uint32_t p = s & ~15u; p < e && nsp < 2; p += 16) {
-            uint32_t m = byte_mask(chunk(p >> 4), ' ');
-            if (p < s) m &= 0xFFFFu << (s - p);
-            if (p + 16 > e) m &= (1u << (e - p)) - 1u;
-            while (m && nsp < 2) {
-                const uint32_t q = p + (uint32_t)__builtin_ctz(m);
-                m &= m - 1;
-                if (nsp == 0) sp1 = q; else sp2 = q;
-                nsp++;
-            }
+        bool ht = false;
+        for (uint32_t p = s & ~15u; p < e; p += 16) {
+            const uint4 w = chunk(p >> 4);
+            uint32_t in = 0xFFFFu;
+            if (p < s) in &= 0xFFFFu << (s - p);
+            if (p + 16 > e) in &= (1u << (e - p)) - 1u;
+            uint32_t m = byte_mask(w, ' ') & in;
+            ht |= (byte_mask(w, '\t') & in) != 0;
+            const uint32_t q1 = p + (uint32_t)__builtin_ctz(m | 0x10000u);
+            const uint32_t m2 = m & (m - 1);
+            const uint32_t q2 = p + (uint32_t)__builtin_ctz(m2 | 0x10000u);
+            sp2 = nsp == 0 ? q2 : nsp == 1 ? q1 : sp2;
+            sp1 = nsp == 0 ? q1 : sp1;
+            nsp += (uint32_t)__builtin_popcount(m);
         }
-        refuse = nsp < 2 || sp1 == s || sp1 - s > 16 || sp2 == sp1 + 1 || e - sp2 != 9;
-        for (uint32_t p = s & ~15u; p < e && !refuse; p += 16) {  // HT ends a target (then not SP: an error)
-            uint32_t m = byte_mask(chunk(p >> 4), '\t');
-            if (p < s) m &= 0xFFFFu << (s - p);
-            if (p + 16 > e) m &= (1u << (e - p)) - 1u;
-            refuse = m != 0;
-        }
-        if (!refuse) {
-            for (uint32_t p = s; p < sp1; p++) refuse |= !is_tchar(byte_at(p));
-            const uint4 v = bytes16(sp2 + 1);
-            refuse |= !(v.x == 0x50545448u && (v.y & 0x00FF00FFu) == 0x002E002Fu && ((v.y >> 8) & 0xFF) - '0' < 10u &&
-                        (v.y >> 24) - '0' < 10u);
-        }
+        const uint4 f = bytes16(s), v = bytes16(sp2 + 1);
+        refuse = nsp != 2 || ht || sp1 == s || sp1 - s > 15 || sp2 == sp1 + 1 || e - sp2 != 9 ||
+                 (uint32_t)__builtin_ctz(nonalnum_mask(f) | 0x10000u) != sp1 - s ||
+                 !(v.x == 0x50545448u && (v.y & 0x00FF00FFu) == 0x002E002Fu && ((v.y >> 8) & 0xFF) - '0' < 10u &&
+                   (v.y >> 24) - '0' < 10u);
     }
     // header lines (lanes 1 .. hend-1): the name's flags from the name table
     uint32_t ninfo = 0, vs = 0;
@@ -1724,8 +1723,11 @@ __device__ __forceinline__ bool lat_fast(const Lane &L, const uint8_t *img, uint
             const bool hit = (meta & 0xFF) == en && n.x == w0 && n.y == w1 && n.z == w2 && n.w == w3;
             ninfo = hit ? (meta >> 8) & 0xFF : 0u;
             if (ninfo & (NI_CL | NI_TE)) refuse = true;  // body framing: the framer's
-            vs = s + en + 1;
-            while (vs < e && (byte_at(vs) == ' ' || byte_at(vs) == '\t')) vs++;  // OWS (M_OWS)
+            vs = s + en + 1;  // then past the OWS (M_OWS)
+            const uint32_t o = (uint32_t)__builtin_ctz((~ws_mask(bytes16(vs)) & 0xFFFFu) | 0x10000u);
+            vs += o;
+            if (o == 16)
+                while (vs < e && (byte_at(vs) == ' ' || byte_at(vs) == '\t')) vs++;
         }
     }
     if (__ballot(refuse)) return false;
@@ -1742,6 +1744,7 @@ __device__ __forceinline__ bool lat_fast(const Lane &L, const uint8_t *img, uint
         const uint64_t mk = __ballot(slot == sl);
         if (slot == sl && lane != (uint32_t)__builtin_ctzll(mk)) slot = kNoSlot;
     }
+    LAT_T(14);
     // ---- the DFA walks: lane 0 the target, lane 63 the method, lane k its value
     sp1 = (uint32_t)__shfl((int)sp1, 0);
     sp2 = (uint32_t)__shfl((int)sp2, 0);
@@ -1762,22 +1765,28 @@ __device__ __forceinline__ bool lat_fast(const Lane &L, const uint8_t *img, uint
             uint32_t st = nc_st >> 16, saved = 0;
             bool in_ows = false;
             uint32_t p = from;
-            // the framer's walks (parse_window M_METHOD / M_TARGET / M_VALUE): the
-            // byte after p and its class read while the transition on p is in flight
-            uint32_t c = p < to ? byte_at(p) : 0u;
-            uint32_t k = p < to ? I.u8(dcls + c) : 0u;
-            while (p < to && (kind == 0 || in_ows || (st != 0 && st < dabs))) {
-                const uint32_t c1 = p + 1 < to ? byte_at(p + 1) : 0u;
-                const uint32_t k1 = p + 1 < to ? I.u8(dcls + c1) : 0u;
-                if (kind == 2) {
-                    const bool ws = c == ' ' || c == '\t';
-                    if (ws && !in_ows) saved = st;
-                    in_ows = ws;
+            // the framer's walks (parse_window M_METHOD / M_TARGET / M_VALUE), 16
+            // bytes a step: their classes read together, then the transitions
+            bool go = p < to && (kind == 0 || (st != 0 && st < dabs));
+            while (go) {
+                const uint4 f = bytes16(p);
+                uint32_t k[16];
+#pragma unroll
+                for (uint32_t j = 0; j < 16; j++) k[j] = I.u8(dcls + byte_of(f, j));
+#pragma unroll
+                for (uint32_t j = 0; j < 16; j++) {
+                    if (go) {
+                        if (kind == 2) {
+                            const uint32_t c = byte_of(f, j);
+                            const bool ws = c == ' ' || c == '\t';
+                            if (ws && !in_ows) saved = st;
+                            in_ows = ws;
+                        }
+                        if (st) st = I.u16(dtrans + 2 * (st * dncls + k[j]));
+                        p++;
+                        go = p < to && (kind == 0 || in_ows || (st != 0 && st < dabs));
+                    }
                 }
-                if (st) st = I.u16(dtrans + 2 * (st * dncls + k));
-                p++;
-                c = c1;
-                k = k1;
             }
             if (kind == 2 && p >= to && in_ows) st = saved;  // trailing OWS is not part of the value
             const uint32_t base = dmask + 8 * (st * nchunks);
@@ -1786,6 +1795,7 @@ __device__ __forceinline__ bool lat_fast(const Lane &L, const uint8_t *img, uint
                 if ((uint32_t)cc < nc) acc[cc] = I.u64(base + 8 * cc);
         }
     }
+    LAT_T(15);
     // ---- merge (headers_done on one pass)
     const uint32_t present = __ockl_wfred_or_u32(lane > 0 && lane < 63 && slot != kNoSlot ? 1u << slot : 0u) |
                              (1u << SLOT_METHOD) | (1u << SLOT_PATH);
