@@ -1657,6 +1657,7 @@ __device__ __forceinline__ bool lat_fast(const Lane &L, const uint8_t *img, uint
         bad |= (badm[c] & in) != 0 || (lfm[c] & in) != (((cr << 1) | prev) & in);
     }
     if (__ballot(bad)) return false;
+    LAT_T(9);
     // ---- lane k: line k = [s, e), e its CR
     const uint32_t s = lane == 0 ? a0 : prevcr + 2, e = mycr;
     const bool line = lane < hend;
@@ -1731,6 +1732,7 @@ __device__ __forceinline__ bool lat_fast(const Lane &L, const uint8_t *img, uint
         }
     }
     if (__ballot(refuse)) return false;
+    LAT_T(10);
     // slots: a header's at its first occurrence when some rule looks at it
     const uint32_t ref = HDR_U32(I, ref_slots);
     uint32_t slot = kNoSlot;
@@ -1824,6 +1826,7 @@ __device__ __forceinline__ bool lat_fast(const Lane &L, const uint8_t *img, uint
         else finish(W, (uint8_t)HDR_U8(I, terminal), -1);
         emit(W, O);
     }
+    LAT_T(11);
     return true;
 }
 

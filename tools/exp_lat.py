@@ -53,8 +53,9 @@ def main():
             line += (f" | cycles: stage {m[7]:.0f} map/emit {m[2]:.0f} dma {m[0]:.0f} parse {m[1]:.0f} other {m[3]:.0f}"
                      f" rounds {m[4]:.1f} scans {m[5]:.1f}")
             if m[13]:  # well-formed-head shortcut (lat_fast): scan, lines, walks (merge+end under 11 when it declines)
-                line += f" | lat_fast: load+masks {m[13]:.0f} checks+lines {m[14]:.0f} walks {m[15]:.0f}"
-            if m[12]:  # latency kernel (one request per wave)
+                line += (f" | lat_fast: load+masks {m[13]:.0f} block checks {m[9]:.0f} line parse {m[10]:.0f}"
+                         f" slots {m[14]:.0f} walks {m[15]:.0f} merge {m[11]:.0f}")
+            elif m[12]:  # latency kernel (one request per wave)
                 line += (f" | latency kernel: fetch {m[8]:.0f} CR scan {m[9]:.0f} lines {m[10]:.0f}"
                          f" merge+end {m[11]:.0f}")
         print(line, flush=True)
