@@ -1,8 +1,10 @@
-# Round 6, call S (GPU box): lat_fast with 16-byte walk steps: the HTTP
-# latency / fast-path / service / Envoy tests, the phase split, and the bench's
-# latency leg against the previous library (old).
+# Latency A/B (GPU box): the HTTP latency / fast-path / service / Envoy GPU tests,
+# the phase split of one-request calls (tools/exp_lat.py with the timing build),
+# then the bench latency leg alternating product and cilium_amd/libl7gpu_old.so.
+# (Needs cilium_amd/libl7gpu_timing.so: python -m cilium_amd.build --timing, and the
+# library to compare against copied to cilium_amd/libl7gpu_old.so.)
 set -o pipefail
-O=gpurun_out/${TAG:-r6s}; mkdir -p $O $O/oldlib; export TMPDIR=/tmp
+O=gpurun_out/${TAG:-latab}; mkdir -p $O $O/oldlib; export TMPDIR=/tmp
 cp cilium_amd/libl7gpu_old.so $O/oldlib/libl7gpu.so
 timeout -k 10 400 python -u -m pytest tests/test_gpu_http_fast.py tests/test_gpu_http_latency.py tests/test_gpu_service.py tests/test_gpu_envoy_adapter.py tests/test_gpu_sync_path.py -m gpu -x -v --timeout 300 --timeout-method thread > $O/tests.log 2>&1; rc=$?
 tail -2 $O/tests.log; [ $rc -ne 0 ] && { grep -E "FAILED|Error|assert" $O/tests.log | head -30; exit 1; }
