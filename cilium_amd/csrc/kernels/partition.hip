@@ -14,7 +14,9 @@
 // produce from the api key: round 3 read each Kafka request's api key and each
 // memcached request's first byte, one HBM line per request, 5 of its 7 GB per
 // cfg5 launch; the memcached kernel now splits text from binary itself, from
-// bytes it reads anyway.  One block owns
+// bytes it reads anyway.  HTTP entries stay one list, but a block writes its
+// HTTP entries length class by length class (round 6), so the HTTP kernel's
+// tiles hold requests of about one length (http_class below).  One block owns
 // 4096 consecutive requests (8 per lane, protocol kept in registers between
 // the count and the write pass) and takes its slot range with one atomic per
 // list.
@@ -33,14 +35,27 @@ constexpr int kBlock = 512;
 constexpr int kPer = 8;  // rows (of kBlock requests) per workgroup
 constexpr int kWaves = kBlock / 64;
 // list classes: 0..kKafkaClasses-1 Kafka by kind / length, then memcached
-// text, memcached binary, then HTTP
+// text, memcached binary, other memcached text, then HTTP by length
+// (kHttpSub classes, one list).  counts[] keeps one word per list: the Kafka
+// classes, memcached retrievals, memcached binary, HTTP, other memcached text.
 constexpr int kKafkaClasses = L7_KAFKA_CLASSES;
-constexpr int kMcText = kKafkaClasses, kMcBinary = kKafkaClasses + 1, kHttp = kKafkaClasses + 2;
-constexpr int kMcText2 = kKafkaClasses + 3;  // text commands not starting with 'g' (storage, delete, ...)
-constexpr int kClasses = kKafkaClasses + 4;
+constexpr int kMcText = kKafkaClasses, kMcBinary = kKafkaClasses + 1;
+constexpr int kMcText2 = kKafkaClasses + 2;  // text commands not starting with 'g' (storage, delete, ...)
+constexpr int kHttp0 = kKafkaClasses + 3;    // HTTP by length class: kHttp0 .. kHttp0 + kHttpSub - 1
+constexpr int kHttpSub = 4;  // (2 classes: cfg5 36.23 ms, 8: 36.25, 4: 36.06-36.16, none: 36.52-36.60)
+constexpr int kClasses = kHttp0 + kHttpSub;
+constexpr int kCntHttp = kKafkaClasses + 2, kCntMcText2 = kKafkaClasses + 3;  // their counts[] words
+__device__ __forceinline__ int count_word(int c) { return c < kMcText2 ? c : c == kMcText2 ? kCntMcText2 : kCntHttp; }
 
 static_assert(kKafkaClasses == 1 || kKafkaClasses == 8, "length classes");
-static_assert(kKafkaClasses + 4 <= 31, "counts[31] holds the compressed-Kafka count");
+static_assert(kKafkaClasses + 4 <= 26, "counts[26..31] hold the work counters and the compressed-Kafka count");
+// HTTP length classes: within a workgroup's 4096 requests the HTTP entries are
+// written class by class (stream order within a class), so an HTTP tile of 64
+// entries mostly holds requests of about one length, and the kernel's
+// value-stop map, which steps as far as the tile's longest request, runs about
+// as long as its requests (cfg5: 256..2048-byte requests)
+// (cfg5 step, profiles/r6/ab6r_http_length_classes.txt)
+__device__ __forceinline__ int http_class(uint32_t len) { return len < 704 ? 0 : len < 1152 ? 1 : len < 1600 ? 2 : 3; }
 // Kafka list class: the decode path a lane takes is set by the request kind
 // and, for produce, by how many message bytes it hashes.  The length tells the
 // kinds apart well enough to schedule by (requests without message sets --
@@ -107,7 +122,7 @@ __global__ __launch_bounds__(kBlock) void partition_kernel(Batch B, uint32_t *__
 #pragma unroll
     for (int r = 0; r < kPer; r++) {
         const uint64_t idx = start + (uint64_t)r * kBlock + threadIdx.x;
-        len[r] = (pw[r] & 0xFF) == PROTO_KAFKA ? B.lens[idx] : 0;
+        len[r] = (pw[r] & 0xFF) == PROTO_KAFKA || (pw[r] & 0xFF) == PROTO_HTTP ? B.lens[idx] : 0;
     }
     uint64_t off[kPer];
 #pragma unroll
@@ -134,7 +149,7 @@ __global__ __launch_bounds__(kBlock) void partition_kernel(Batch B, uint32_t *__
             else if (proto == PROTO_MEMCACHE) {
                 cls = 1 + kMcText;  // one list: the memcached kernel splits it by parser itself
             }
-            else if (proto == PROTO_HTTP) cls = 1 + kHttp;
+            else if (proto == PROTO_HTTP) cls = 1 + kHttp0 + http_class(len[r]);
             else if (!L7_PROTO_OWNED(proto)) {  // (r2d2, cassandra: their kernels walk the whole batch)
                 B.verdict[idx] = V_UNSUPPORTED;
                 B.rule[idx] = -1;
@@ -148,16 +163,27 @@ __global__ __launch_bounds__(kBlock) void partition_kernel(Batch B, uint32_t *__
     if (lane == 0)
         for (int c = 0; c < kClasses; c++) s_off[wave][c] = cnt[c];
     __syncthreads();
-    if (threadIdx.x < kClasses) {
+    if (threadIdx.x < kHttp0) {
         const int c = threadIdx.x;
         uint32_t t = 0;
         for (int w = 0; w < kWaves; w++) t += s_off[w][c];
-        uint32_t b = t ? atomicAdd(&counts[c], t) : 0;
+        uint32_t b = t ? atomicAdd(&counts[count_word(c)], t) : 0;
         for (int w = 0; w < kWaves; w++) {
             const uint32_t a = s_off[w][c];
             s_off[w][c] = b;
             b += a;
         }
+    } else if (threadIdx.x == kHttp0) {  // the HTTP classes: one range of the list, class by class
+        uint32_t t = 0;
+        for (int c = kHttp0; c < kClasses; c++)
+            for (int w = 0; w < kWaves; w++) t += s_off[w][c];
+        uint32_t b = t ? atomicAdd(&counts[kCntHttp], t) : 0;
+        for (int c = kHttp0; c < kClasses; c++)
+            for (int w = 0; w < kWaves; w++) {
+                const uint32_t a = s_off[w][c];
+                s_off[w][c] = b;
+                b += a;
+            }
     }
     __syncthreads();
     uint32_t lo[kClasses];
@@ -174,15 +200,15 @@ __global__ __launch_bounds__(kBlock) void partition_kernel(Batch B, uint32_t *__
                 if (c < kKafkaClasses) sel_kafka[(size_t)c * n + pos] = idx;
                 else if (c == kMcText) sel_mc[pos] = idx;
                 else if (c == kMcBinary) sel_mc[n - 1 - pos] = idx;  // binary from the list's end
-                else if (c == kHttp) sel_http[pos] = idx;
-                else sel_http[n - 1 - pos] = idx;  // other text commands from the HTTP list's end
+                else if (c == kMcText2) sel_http[n - 1 - pos] = idx;  // other text commands from the HTTP list's end
+                else sel_http[pos] = idx;
             }
             lo[c] += __popcll(mk);
         }
     }
 }
 
-// counts[0..kClasses) must be zero on entry (the caller clears them on `stream`).
+// counts[0..kKafkaClasses + 4) must be zero on entry (the caller clears them on `stream`).
 hipError_t LaunchPartition(const Batch &B, uint32_t *sel_kafka, uint32_t *sel_mc, uint32_t *sel_http, uint32_t *counts,
                            hipStream_t stream) {
     if (B.n == 0) return hipSuccess;
