@@ -204,7 +204,11 @@ __device__ __forceinline__ int kd_message_set(R &r, uint32_t &pos, uint32_t end,
             } else {
                 if ((uint32_t)klen > msize || vo + (uint32_t)klen + 4 > at + msize) break;
                 vo += (uint32_t)klen;
+                // the cursor kept on byte at + 4's chunk, where the CRC starts
+                // (crc_head hashes its bytes without another round trip)
+                const Cur keep = r.cur;
                 vlen = (int32_t)r.be(vo, 4);
+                r.cur = keep;
             }
             if (vlen >= 1 && ((uint32_t)vlen > msize || vo + 4 + (uint32_t)vlen > at + msize)) break;
             // committed: the message is read whole
@@ -516,7 +520,7 @@ struct ExactHooks {
     }
     // CRC32-IEEE of the message bytes [pos, pos + n) against the stored value
     __device__ __forceinline__ bool msg(uint32_t pos, uint32_t n, uint32_t stored) {
-        return crc32_ieee_staged(crctab, r.cur, r.b + pos, n, stage) == stored;
+        return crc32_ieee_staged(crctab, r.cur, r.b + pos, n, stage, r.lastc) == stored;
     }
 };
 

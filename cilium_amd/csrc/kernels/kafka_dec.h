@@ -261,8 +261,9 @@ __device__ __forceinline__ uint32_t cur_word_at(const Cur &c, uint32_t k) {
 // memory latency per batch -- the second buffer costs LDS, not VGPRs.  (cfg3:
 // 0.929 -> 0.919 ms; holding the next batch in registers instead spills.)
 // Correct under any exec mask: each active lane stages and reads only its own
-// bytes, and a batch is waited for with vmcnt(0).  In pieces, so that the
-// message-set walk can interleave them (read_message_set in kafka_classify).
+// bytes, and a batch is waited for with vmcnt(0).  The last, short batch is
+// staged too (crc_last): its up to four chunks cost one round trip, where the
+// cursor took one per chunk (cfg5 Kafka 16.45 -> 16.10 ms).
 
 // bytes before the first 16-byte boundary (at most 15, one chunk) in 8-, 4-
 // and 1-byte steps; returns how many were hashed into c
@@ -289,15 +290,20 @@ __device__ __forceinline__ uint32_t crc_head(uint32_t tabaddr, Cur &cur, const u
     }
     return i;
 }
-// the 64 bytes at q (16-byte aligned) into the lane's staging slot
-__device__ __forceinline__ void crc_stage(uint8_t *stage, const uint8_t *q) {
+// the 64 bytes at q (16-byte aligned) into the lane's staging slot, chunks
+// past lastc (the request's last one) clamped to it: a message's last batch
+// is staged like the others and only its own bytes are read back
+__device__ __forceinline__ void crc_stage(uint8_t *stage, const uint8_t *q, uintptr_t lastc) {
 #pragma unroll
-    for (int k = 0; k < 4; k++)
-        __builtin_amdgcn_global_load_lds((const void *)(q + 16 * k),
+    for (int k = 0; k < 4; k++) {
+        const uintptr_t a = (uintptr_t)(q + 16 * k);
+        __builtin_amdgcn_global_load_lds((const void *)(k == 0 || a <= lastc ? a : lastc),
                                          (__attribute__((address_space(3))) void *)(stage + k * 1024), 16, 0, 0);
+    }
 }
 // one staged 64-byte batch hashed into c; the next one (if any) staged meanwhile
-__device__ __forceinline__ uint32_t crc_batch(const uint32_t *tab, uint8_t *stage, uint32_t c, const uint8_t *next) {
+__device__ __forceinline__ uint32_t crc_batch(const uint32_t *tab, uint8_t *stage, uint32_t c, const uint8_t *next,
+                                              uintptr_t lastc) {
     const uint32_t la = (uint32_t)(uintptr_t)(stage + 16 * (threadIdx.x & 63));
     uint4 v0, v1, v2, v3;
     asm volatile("s_waitcnt vmcnt(0)\n\t"
@@ -307,7 +313,7 @@ __device__ __forceinline__ uint32_t crc_batch(const uint32_t *tab, uint8_t *stag
                  : "=v"(v0), "=v"(v1), "=v"(v2), "=v"(v3)
                  : "v"(la)
                  : "memory");
-    if (next) crc_stage(stage, next);
+    if (next) crc_stage(stage, next, lastc);
 #pragma unroll
     for (int j = 0; j < 8; j++) {
         const uint4 x = j < 2 ? v0 : j < 4 ? v1 : j < 6 ? v2 : v3;
@@ -316,46 +322,51 @@ __device__ __forceinline__ uint32_t crc_batch(const uint32_t *tab, uint8_t *stag
     }
     return c;
 }
-// the rest (fewer than 64 bytes, from i, 16-byte aligned) from the cursor's
-// chunks: 8-byte steps, then one 4-byte step, then bytes
-__device__ __forceinline__ uint32_t crc_tail(uint32_t tabaddr, Cur &cur, const uint8_t *p, uint32_t n, uint32_t i,
-                                             uint32_t c) {
-    for (; i + 8 <= n; i += 8) {
-        const uintptr_t a = (uintptr_t)(p + i);
-        cur_fill(cur, a);
-        const uint32_t k = (uint32_t)(a & 15);
-        const uint32_t w0 = cur.w0, w1 = cur.w1, w2 = cur.w2, w3 = cur.w3;
-        c = crc_step8(tabaddr, (k ? w2 : w0) ^ c, k ? w3 : w1);
+// the staged last batch's rem (1 .. 63) bytes: 8-byte steps, then one
+// 4-byte step, then bytes, each word read back from the lane's staging slot
+__device__ __forceinline__ uint32_t lds_word_at(uint32_t la, uint32_t j) {  // bytes j .. j+3 (j % 4 == 0)
+    uint32_t x;
+    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(x) : "v"(la + ((j >> 4) << 10) + (j & 15)) : "memory");
+    return x;
+}
+__device__ __forceinline__ uint32_t crc_last(uint32_t tabaddr, uint8_t *stage, uint32_t rem, uint32_t c) {
+    const uint32_t la = (uint32_t)(uintptr_t)(stage + 16 * (threadIdx.x & 63));
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint32_t j = 0;
+    for (; j + 8 <= rem; j += 8) {
+        uint64_t x;
+        asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)"
+                     : "=v"(x)
+                     : "v"(la + ((j >> 4) << 10) + (j & 8))
+                     : "memory");
+        c = crc_step8(tabaddr, (uint32_t)x ^ c, (uint32_t)(x >> 32));
     }
-    if (i + 4 <= n) {
-        const uintptr_t a = (uintptr_t)(p + i);
-        cur_fill(cur, a);
-        c = crc_step4(tabaddr, cur_word_at(cur, (uint32_t)(a & 15)) ^ c);
-        i += 4;
+    if (j + 4 <= rem) {
+        c = crc_step4(tabaddr, lds_word_at(la, j) ^ c);
+        j += 4;
     }
-    if (i < n) {
-        const uintptr_t a = (uintptr_t)(p + i);
-        cur_fill(cur, a);
-        c = crc_bytes3(tabaddr, c, cur_word_at(cur, (uint32_t)(a & 15)), n - i);
-    }
+    if (j < rem) c = crc_bytes3(tabaddr, c, lds_word_at(la, j), rem - j);
     return c;
 }
+// Every byte after the head (crc_head) comes through the staging slot, the
+// last (short) batch included: a message's bytes cost one memory round trip
+// per 64, the next batch in flight while one is hashed.
 __device__ __forceinline__ uint32_t crc32_ieee_staged(const uint32_t *tab, Cur &cur, const uint8_t *p, uint32_t n,
-                                                      uint8_t *stage) {
+                                                      uint8_t *stage, uintptr_t lastc) {
     const uint32_t tabaddr = (uint32_t)(uintptr_t)tab;
     uint32_t c = 0xFFFFFFFFu;
     uint32_t i = crc_head(tabaddr, cur, p, n, c);
-    if (i + 64 <= n) {
+    if (i < n) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        crc_stage(stage, p + i);
-        for (;;) {
-            const bool more = i + 128 <= n;
-            c = crc_batch(tab, stage, c, more ? p + i + 64 : nullptr);
+        crc_stage(stage, p + i, lastc);
+        while (i + 64 <= n) {
+            const bool more = i + 64 < n;
+            c = crc_batch(tab, stage, c, more ? p + i + 64 : nullptr, lastc);
             i += 64;
-            if (!more) break;
         }
+        if (i < n) c = crc_last(tabaddr, stage, n - i, c);
     }
-    return ~crc_tail(tabaddr, cur, p, n, i, c);
+    return ~c;
 }
 
 }  // namespace
