@@ -336,6 +336,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # Rehearsal of the N-rank path on a one-GPU box (tests/test_gpu_dist_bench.py):
+    # L7G_DIST_BACKEND=gloo with L7G_DIST_ONE_DEVICE=1 puts every rank on cuda:0
+    # (RCCL refuses two ranks on one device).  The driver's runs set neither.
+    backend = os.environ.get("L7G_DIST_BACKEND", "nccl")
+    if os.environ.get("L7G_DIST_ONE_DEVICE") == "1":
+        local = 0
 
     import torch
     torch.cuda.set_device(local)
@@ -343,7 +349,10 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from cilium_amd import Engine, gen
     from cilium_amd import dist as l7dist
@@ -543,7 +552,9 @@ def main():
     dom = max((k for k in kernels if k != "partition"), key=lambda k: kernels[k]["ms"], default=None)
     traffic = None
     tpath = os.path.join(ROOT, "profiles", f"traffic_{args.workload}.json")
-    if dom and os.path.exists(tpath):
+    # the PMC passes behind the file ran the workload's default size on one GPU
+    measured_shape = world == 1 and args.requests in (0, dflt_n) and args.unique in (0, dflt_u)
+    if dom and measured_shape and os.path.exists(tpath):
         try:
             with open(tpath) as f:
                 tj = json.load(f)
@@ -580,7 +591,8 @@ def main():
                    "global_requests_per_step": n * world,
                    "mean_request_bytes": round(float(w.lengths.mean()), 1),
                    "protocol_mix": {k: v["requests"] for k, v in pbytes.items()},
-                   "parallelism": f"dp{world}" + (" (connection-sharded stream) + RCCL counter all-reduce"
+                   "parallelism": f"dp{world}" + (" (connection-sharded stream) + " +
+                                                  ("RCCL" if backend == "nccl" else backend) + " counter all-reduce"
                                                   if world > 1 else "")},
         "tables": {"rank0_compile_s": round(compile_s, 3), "rank0_rulesets_compiled": compiled if rank == 0 else None,
                    "rulesets_compiled_by_other_ranks": other_compiled},
