@@ -60,22 +60,36 @@ struct GRd {
     const uint8_t *b;
     uintptr_t lastc;  // the last 16-byte chunk holding a request byte (window loads never pass it)
     Cur cur;
+    uint8_t *stage;   // the lane's CRC staging slot (win9 stages the message window there)
     __device__ __forceinline__ uint32_t le4(uint32_t pos) { return le_load4(cur, b + pos); }
     __device__ __forceinline__ uint64_t be(uint32_t pos, int n) { return be_load(cur, b + pos, n); }
     // bytes [pos, pos + 36) as little-endian words: the four chunks that can
-    // hold them loaded together (one memory round trip), chunks past the
-    // request's last one clamped to it (their bytes are never used); the
-    // cursor is left on the chunk of byte pos + 16, where the message's CRC
-    // input starts
+    // hold them staged together into the lane's CRC slot (one memory round
+    // trip), chunks past the request's last one clamped to it (their bytes are
+    // never used), and read back.  The cursor is left on the chunk of byte
+    // pos + 16, where the message's CRC input starts, and the slot keeps the
+    // window for the CRC (crc32_ieee_window: its first 32-48 bytes cost no
+    // further round trip; cfg5 Kafka 16.06 -> 15.53 ms)
     __device__ __forceinline__ void win9(uint32_t pos, uint32_t (&x)[9]) {
         const uintptr_t a = (uintptr_t)(b + pos);
         const uintptr_t c0 = a & ~(uintptr_t)15;
         uint32_t w[16];
+        {
+            crc_stage(stage, reinterpret_cast<const uint8_t *>(c0), lastc);
+            const uint32_t la = (uint32_t)(uintptr_t)(stage + 16 * (threadIdx.x & 63));
+            uint4 v0, v1, v2, v3;
+            asm volatile("s_waitcnt vmcnt(0)\n\t"
+                         "ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:1024\n\t"
+                         "ds_read_b128 %2, %4 offset:2048\n\tds_read_b128 %3, %4 offset:3072\n\t"
+                         "s_waitcnt lgkmcnt(0)"
+                         : "=v"(v0), "=v"(v1), "=v"(v2), "=v"(v3)
+                         : "v"(la)
+                         : "memory");
+            const uint4 vv[4] = {v0, v1, v2, v3};
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const uintptr_t ck = c0 + 16 * k <= lastc ? c0 + 16 * k : lastc;
-            const uint4 v = gload16(ck);
-            w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+            for (int k = 0; k < 4; k++) {
+                w[4 * k] = vv[k].x; w[4 * k + 1] = vv[k].y; w[4 * k + 2] = vv[k].z; w[4 * k + 3] = vv[k].w;
+            }
         }
         const uint32_t s = (uint32_t)(a & 15), q = s >> 2;
 #pragma unroll
@@ -214,7 +228,7 @@ __device__ __forceinline__ int kd_message_set(R &r, uint32_t &pos, uint32_t end,
             // committed: the message is read whole
             dec.pos = at + msize;
             dec.limit -= (int32_t)(12 + msize);
-            if (!h.msg(at + 4, msize - 4, crc)) { pos = dec.pos; return 0; }  // stop, no drain
+            if (!h.msg_win(at + 4, msize - 4, crc)) { pos = dec.pos; return 0; }  // stop, no drain
             if ((attr & 3) == 3) { pos = dec.pos; return 0; }
             if (attr & 3) zflag = true;
         }
@@ -522,6 +536,10 @@ struct ExactHooks {
     __device__ __forceinline__ bool msg(uint32_t pos, uint32_t n, uint32_t stored) {
         return crc32_ieee_staged(crctab, r.cur, r.b + pos, n, stage, r.lastc) == stored;
     }
+    // the same, right after the walk's window read of this message (kd_message_set's fast path)
+    __device__ __forceinline__ bool msg_win(uint32_t pos, uint32_t n, uint32_t stored) {
+        return crc32_ieee_window(crctab, r.cur, r.b + pos, n, stage, r.lastc) == stored;
+    }
 };
 
 }  // namespace
@@ -596,7 +614,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) 
             if (verdict == V_UNSUPPORTED) break;
             if (!l7_in_arena(off, len, B.arena_len)) { verdict = V_UNSUPPORTED; break; }  // out of contract
             if (len < 4) { verdict = V_INCOMPLETE; break; }
-            GRd r{B.arena + off, ((uintptr_t)(B.arena + off) + len - 1) & ~(uintptr_t)15, {}};
+            GRd r{B.arena + off, ((uintptr_t)(B.arena + off) + len - 1) & ~(uintptr_t)15, {}, stage};
             r.cur.line = ~(uintptr_t)0;
             const int32_t size = (int32_t)r.be(0, 4);
             if (size <= 0) break;

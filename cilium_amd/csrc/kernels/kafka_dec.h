@@ -263,7 +263,9 @@ __device__ __forceinline__ uint32_t cur_word_at(const Cur &c, uint32_t k) {
 // Correct under any exec mask: each active lane stages and reads only its own
 // bytes, and a batch is waited for with vmcnt(0).  The last, short batch is
 // staged too (crc_last): its up to four chunks cost one round trip, where the
-// cursor took one per chunk (cfg5 Kafka 16.45 -> 16.10 ms).
+// cursor took one per chunk (cfg5 Kafka 16.45 -> 16.10 ms).  A message the walk
+// reads through its window starts from the window already in the slot
+// (crc32_ieee_window).
 
 // bytes before the first 16-byte boundary (at most 15, one chunk) in 8-, 4-
 // and 1-byte steps; returns how many were hashed into c
@@ -329,10 +331,12 @@ __device__ __forceinline__ uint32_t lds_word_at(uint32_t la, uint32_t j) {  // b
     asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(x) : "v"(la + ((j >> 4) << 10) + (j & 15)) : "memory");
     return x;
 }
-__device__ __forceinline__ uint32_t crc_last(uint32_t tabaddr, uint8_t *stage, uint32_t rem, uint32_t c) {
+// (bytes [j0, rem) of the slot: j0 a multiple of 8)
+__device__ __forceinline__ uint32_t crc_last(uint32_t tabaddr, uint8_t *stage, uint32_t rem, uint32_t c,
+                                             uint32_t j0 = 0) {
     const uint32_t la = (uint32_t)(uintptr_t)(stage + 16 * (threadIdx.x & 63));
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    uint32_t j = 0;
+    uint32_t j = j0;
     for (; j + 8 <= rem; j += 8) {
         uint64_t x;
         asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)"
@@ -359,6 +363,45 @@ __device__ __forceinline__ uint32_t crc32_ieee_staged(const uint32_t *tab, Cur &
     if (i < n) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         crc_stage(stage, p + i, lastc);
+        while (i + 64 <= n) {
+            const bool more = i + 64 < n;
+            c = crc_batch(tab, stage, c, more ? p + i + 64 : nullptr, lastc);
+            i += 64;
+        }
+        if (i < n) c = crc_last(tabaddr, stage, n - i, c);
+    }
+    return ~c;
+}
+// The same CRC for a message whose 64-byte window [c0, c0 + 64) the walk has
+// just staged into the slot (c0 = the chunk of the message's offset field,
+// p - 16): the CRC's bytes up to c0 + 64 are hashed from the slot, and the
+// first batch from memory is c0 + 64's, staged while they are hashed.
+__device__ __forceinline__ uint32_t crc32_ieee_window(const uint32_t *tab, Cur &cur, const uint8_t *p, uint32_t n,
+                                                      uint8_t *stage, uintptr_t lastc) {
+    const uint32_t tabaddr = (uint32_t)(uintptr_t)tab;
+    uint32_t c = 0xFFFFFFFFu;
+    uint32_t i = crc_head(tabaddr, cur, p, n, c);
+    if (i < n) {
+        const uint8_t *c0 = reinterpret_cast<const uint8_t *>((uintptr_t)(p - 16) & ~(uintptr_t)15);
+        const uint32_t o = (uint32_t)((p + i) - c0);  // 16 or 32
+        if (n - i <= 64 - o) return ~crc_last(tabaddr, stage, o + (n - i), c, o);
+        const uint32_t la = (uint32_t)(uintptr_t)(stage + 16 * (threadIdx.x & 63));
+        uint4 v1, v2, v3;
+        asm volatile("ds_read_b128 %0, %3 offset:1024\n\tds_read_b128 %1, %3 offset:2048\n\t"
+                     "ds_read_b128 %2, %3 offset:3072\n\ts_waitcnt lgkmcnt(0)"
+                     : "=v"(v1), "=v"(v2), "=v"(v3)
+                     : "v"(la)
+                     : "memory");
+        crc_stage(stage, c0 + 64, lastc);
+        const uint32_t j0 = o == 16 ? 0 : 2;
+#pragma unroll
+        for (uint32_t j = 0; j < 6; j++) {
+            if (j < j0) continue;
+            const uint4 x = j < 2 ? v1 : j < 4 ? v2 : v3;
+            const uint32_t lo = ((j & 1) ? x.z : x.x) ^ c, hi = (j & 1) ? x.w : x.y;
+            c = crc_slice8(tab, lo, hi);
+        }
+        i += 64 - o;
         while (i + 64 <= n) {
             const bool more = i + 64 < n;
             c = crc_batch(tab, stage, c, more ? p + i + 64 : nullptr, lastc);
