@@ -102,6 +102,18 @@ struct GRd {
         cur.line = c0 + 16 <= lastc ? c0 + 16 : ~(uintptr_t)0;
         cur.w0 = w[4]; cur.w1 = w[5]; cur.w2 = w[6]; cur.w3 = w[7];
     }
+    // big-endian 4 bytes at byte rel (rel + 4 <= 64) of the window win9 left in
+    // the slot: a field past the 36 bytes win9 returns, without a round trip
+    __device__ __forceinline__ uint32_t win_be4(uint32_t rel) {
+        const uint32_t la = (uint32_t)(uintptr_t)(stage + 16 * (threadIdx.x & 63));
+        const uint32_t w0 = rel >> 2, w1 = w0 < 15 ? w0 + 1 : 15;
+        uint32_t lo, hi;
+        asm volatile("ds_read_b32 %0, %2\n\tds_read_b32 %1, %3\n\ts_waitcnt lgkmcnt(0)"
+                     : "=&v"(lo), "=&v"(hi)
+                     : "v"(la + ((w0 >> 2) << 10) + ((w0 & 3) << 2)), "v"(la + ((w1 >> 2) << 10) + ((w1 & 3) << 2))
+                     : "memory");
+        return bswap32(__builtin_amdgcn_alignbyte(hi, lo, rel & 3));
+    }
 };
 
 // ---------------- io.ReadFull / LimitReader decoding over a byte source ----------------
@@ -218,11 +230,17 @@ __device__ __forceinline__ int kd_message_set(R &r, uint32_t &pos, uint32_t end,
             } else {
                 if ((uint32_t)klen > msize || vo + (uint32_t)klen + 4 > at + msize) break;
                 vo += (uint32_t)klen;
-                // the cursor kept on byte at + 4's chunk, where the CRC starts
-                // (crc_head hashes its bytes without another round trip)
-                const Cur keep = r.cur;
-                vlen = (int32_t)r.be(vo, 4);
-                r.cur = keep;
+                // from the window in the slot when it holds the field (short
+                // keys), else through the cursor, kept on byte at + 4's chunk
+                // where the CRC starts (crc_head hashes it without a round trip)
+                const uint32_t rel = vo - dec.pos + (uint32_t)((uintptr_t)(r.b + dec.pos) & 15);
+                if (rel + 4 <= 64) {
+                    vlen = (int32_t)r.win_be4(rel);
+                } else {
+                    const Cur keep = r.cur;
+                    vlen = (int32_t)r.be(vo, 4);
+                    r.cur = keep;
+                }
             }
             if (vlen >= 1 && ((uint32_t)vlen > msize || vo + 4 + (uint32_t)vlen > at + msize)) break;
             // committed: the message is read whole
