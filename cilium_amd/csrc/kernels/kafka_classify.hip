@@ -589,7 +589,12 @@ struct ExactHooks {
 // sel: this protocol's request indices from partition_kernel (mixed batches),
 // else requests 0..n-1.  answer_other: answer entries on connections that are
 // not Kafka (single-protocol engines, where partition_kernel does not run).
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) void kafka_classify_kernel(
+// kWaves: waves per SIMD it is built for -- 6 (80 VGPRs) when memcached runs
+// beside it in the workgroup slot it leaves per CU, 5 (96 VGPRs, almost no
+// spills) when it runs alone (cfg3 0.619 -> 0.601 ms; beside memcached the
+// 5-wave build loses: profiles/r6/ab6za_*).
+template <int kWaves>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves, 8))) void kafka_classify_kernel(
     Batch B, KafkaTables T, const uint32_t *__restrict__ sel, const uint32_t *__restrict__ sel_count,
     uint32_t answer_other, uint32_t *__restrict__ zlist, uint32_t *__restrict__ zcount, uint32_t *__restrict__ work) {
     const uint32_t n = B.n, nconns = B.nconns;
@@ -697,26 +702,33 @@ hipError_t LaunchKafkaClassify(const Batch &B, const KafkaTables &T, const uint3
                                hipStream_t stream, int leave_per_cu) {
     if (B.n == 0) return hipSuccess;
     uint32_t blocks = (B.n + kBlock - 1) / kBlock;
-    // persistent grid: as many workgroups as the CUs hold at once
-    static int cus = 0, per_cu = 0;
-    if (cus == 0) {
+    const bool beside = leave_per_cu > 0;
+    // persistent grid: as many workgroups as the CUs hold at once (per build)
+    static int cus[2] = {0, 0}, per_cu[2] = {0, 0};
+    if (cus[beside] == 0) {
         int dev = 0, c = 0, p = 0;
         if (hipGetDevice(&dev) == hipSuccess &&
             hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&p, kafka_classify_kernel, kBlock, 0) == hipSuccess && c > 0 &&
-            p > 0) {
-            per_cu = p;
-            cus = c;
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                &p, beside ? kafka_classify_kernel<6> : kafka_classify_kernel<5>, kBlock, 0) == hipSuccess &&
+            c > 0 && p > 0) {
+            per_cu[beside] = p;
+            cus[beside] = c;
         } else {
-            per_cu = 32;
-            cus = 256;
+            per_cu[beside] = 32;
+            cus[beside] = 256;
         }
     }
-    const int slots = leave_per_cu > 0 && per_cu > leave_per_cu ? per_cu - leave_per_cu : per_cu;
+    const int pc = per_cu[beside];
+    const int slots = beside && pc > leave_per_cu ? pc - leave_per_cu : pc;
     if (!work) blocks = blocks > 8192 ? 8192 : blocks;  // grid-stride beyond this
-    else if (blocks > (uint32_t)(cus * slots)) blocks = (uint32_t)(cus * slots);
-    hipLaunchKernelGGL(kafka_classify_kernel, dim3(blocks), dim3(kBlock), 0, stream, B, T, sel, sel_count,
-                       answer_other ? 1u : 0u, zlist, zcount, work);
+    else if (blocks > (uint32_t)(cus[beside] * slots)) blocks = (uint32_t)(cus[beside] * slots);
+    if (beside)
+        hipLaunchKernelGGL(kafka_classify_kernel<6>, dim3(blocks), dim3(kBlock), 0, stream, B, T, sel, sel_count,
+                           answer_other ? 1u : 0u, zlist, zcount, work);
+    else
+        hipLaunchKernelGGL(kafka_classify_kernel<5>, dim3(blocks), dim3(kBlock), 0, stream, B, T, sel, sel_count,
+                           answer_other ? 1u : 0u, zlist, zcount, work);
     return hipGetLastError();
 }
 
